@@ -1,0 +1,140 @@
+/*
+ * lo_icp.h — C ABI of the MI355X-native point-to-plane ICP registration core.
+ *
+ * Drop-in boundary for the reference's scan-to-map Gauss-Newton step:
+ *   bool IterativeClosestPointOptimizer::optimize(map::VoxelMap*, shared_ptr<LidarFrame>,
+ *                                                 const SE3f& initial, SE3f& optimized)
+ *   (reference src/optimization/IterativeClosestPointOptimizer.h:182-185, .cpp:255-463)
+ * and the map queries it makes:
+ *   VoxelMap::GetSurfelAtPoint       (src/database/VoxelMap.h:252-254, VoxelMap.cpp:368-386)
+ *   AdaptiveMEstimator::calculate_scale_factor (src/optimization/AdaptiveMEstimator.h:92, .cpp:63-79)
+ *
+ * Conventions (no exceptions cross this boundary; plain pointers and sizes only):
+ *  - A context = one GPU + one HIP stream + device-resident map, scan buffers and PKO tables.
+ *    Contexts are not thread-safe; distinct contexts may run concurrently (scan-parallel multi-GPU).
+ *  - The caller owns every host buffer; the library owns every device buffer.
+ *  - Poses are fp32 row-major 3x4 [R|t] (SE3f::Matrix() rows 0-2).
+ *  - Points are AoS float3 (util::Point3D, PointCloudUtils.h:34-38), local (sensor) frame.
+ *  - Return codes: LO_OK (0); LO_INSUFFICIENT (1) = a GN iteration found fewer than
+ *    min_correspondence_points correspondences (the reference's `return false`, T_out = T_init);
+ *    negative = argument / HIP errors (lo_last_error() has the text).
+ */
+#ifndef LO_ICP_H
+#define LO_ICP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LO_OK              0
+#define LO_INSUFFICIENT    1
+#define LO_ERR_ARG        -1
+#define LO_ERR_HIP        -2
+#define LO_ERR_CAPACITY   -3
+#define LO_ERR_STATE      -4
+
+#define LO_MAX_ITERS      64
+
+/* ICPConfig (IterativeClosestPointOptimizer.h:55-76, wired by Estimator.cpp:62-70) +
+ * AdaptiveMEstimatorConfig (AdaptiveMEstimator.h:24-41, built at Estimator.cpp:49-59) +
+ * the map geometry the surfel lookup needs (VoxelMap::GetVoxelSize/GetHierarchyFactor, VoxelMap.h:204-205). */
+typedef struct lo_config {
+    int    max_iterations;               /* config/kitti.yaml:35 -> 4 */
+    double translation_tolerance;        /* 0.005 m */
+    double rotation_tolerance;           /* 0.005 rad */
+    double max_correspondence_distance;  /* 1.0 m */
+    int    min_correspondence_points;    /* 10 (ICPConfig default; estimator.min_correspondence_points is not wired) */
+    int    use_robust_loss;              /* 1 */
+    double robust_loss_delta;            /* 0.1, used only when PKO is disabled */
+    int    loss_cauchy;                  /* 0: huber weight (SystemConfig.loss_type is never parsed -> "huber") */
+    int    use_adaptive_m_estimator;     /* 1: PKO */
+    double min_scale_factor;             /* 0.1 */
+    double max_scale_factor;             /* 10.0 */
+    int    num_alpha_segments;           /* 100 */
+    double truncated_threshold;          /* 10.0 */
+    int    gmm_components;               /* 3 (1..4 supported) */
+    int    gmm_sample_size;              /* 100 (1..256 supported) */
+    int    pko_kernel_cauchy;            /* 0: "huber" (kitti.yaml:51) */
+    float  voxel_size;                   /* map_voxel_size 0.5 */
+    int    hierarchy_factor;             /* 3 */
+    int    use_surfel_correspondence;    /* 1 */
+    int    max_points;                   /* scan capacity (points per optimize call) */
+} lo_config;
+
+/* One executed Gauss-Newton iteration (per-iteration parity log). */
+typedef struct lo_iter_log {
+    float  pose[12];   /* pose after this iteration's update */
+    int    n_corr;
+    double scale;      /* iteration-0 residual normalisation scale (std/6) */
+    double alpha;      /* PKO Huber delta used for the weights */
+    float  cost;       /* sum w r^2 */
+    float  H[21];      /* upper triangle of H, row-major */
+    float  g[6];
+    float  delta[6];   /* [dt, dw] */
+} lo_iter_log;
+
+typedef struct lo_stats {
+    int    iterations;
+    int    n_corr;         /* last iteration */
+    int    status;         /* LO_OK / LO_INSUFFICIENT */
+    int    converged;      /* reference always reports true (IterativeClosestPointOptimizer.cpp:456) */
+    double initial_cost;
+    double final_cost;
+    double gpu_ms;         /* device time of the whole optimize (HIP events) */
+} lo_stats;
+
+typedef struct lo_ctx lo_ctx;
+
+void        lo_config_default_kitti(lo_config* cfg);
+void        lo_config_default_mid360(lo_config* cfg);
+lo_ctx*     lo_create(const lo_config* cfg, int device, int* err);
+void        lo_destroy(lo_ctx* ctx);
+const char* lo_last_error(const lo_ctx* ctx);
+int         lo_device(const lo_ctx* ctx);
+
+/* ---- map side ----
+ * Replaces the map state read by VoxelMap::GetSurfelAtPoint: the L1 voxels with has_surfel == true.
+ * keys_xyz: int32 L1 voxel keys (VoxelKey, VoxelMap.h:152-164), |key| < 2^20 per axis.
+ * Full upload; call again after every VoxelMap::UpdateVoxelMap (Estimator.cpp:457). */
+int lo_map_set_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids, size_t m);
+size_t lo_map_surfel_count(const lo_ctx* ctx);
+
+/* ---- the optimize boundary ----
+ * Same contract as IterativeClosestPointOptimizer::optimize: GN to convergence / max_iterations.
+ * logs: nullable, room for cfg.max_iterations entries; stats: nullable. Synchronous. */
+int lo_icp_optimize(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T_init[12], float T_out[12],
+                    lo_iter_log* logs, lo_stats* stats);
+
+/* Device-resident variant: d_pts is a device pointer (AoS float3) on the context's device.
+ * Enqueues the whole GN loop on the context stream and returns immediately; the result is
+ * read (and the stream synchronised) by lo_icp_result(). */
+int lo_icp_optimize_async(lo_ctx* ctx, const float* d_pts, size_t n, const float T_init[12]);
+int lo_icp_result(lo_ctx* ctx, float T_out[12], lo_iter_log* logs, lo_stats* stats);
+int lo_sync(lo_ctx* ctx);
+void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
+
+/* ---- single-stage entry points (parity harness; each synchronous) ---- */
+/* find_correspondences (IterativeClosestPointOptimizer.cpp:587-645) at pose T:
+ * per-point valid flag and fp64 residual |n.(p_w - c)| (0 where invalid). Returns the count. */
+int lo_find_correspondences(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T[12],
+                            uint8_t* valid, double* residual);
+/* AdaptiveMEstimator::calculate_scale_factor on given normalised residuals (device PKO).
+ * gmm_out (nullable): weights, means, variances (3*gmm_components doubles). Returns alpha, NaN on error. */
+double lo_pko_scale_factor(lo_ctx* ctx, const double* residuals, size_t n, double* gmm_out);
+/* Weighted normal equations of one GN iteration (IterativeClosestPointOptimizer.cpp:345-410) at pose T
+ * with the given normalisation scale and Huber delta. H is 6x6 row-major (fp64 sums). Returns n_corr. */
+int lo_build_normal_equations(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T[12],
+                              double scale, double delta, double H[36], double g[6], double* cost);
+/* PKO sampling: first min(gmm_sample_size, n) entries of std::shuffle(iota(n), mt19937(42))
+ * as the device tables reproduce them (AdaptiveMEstimator.cpp:319-328). Host-side. */
+int lo_pko_sample_indices(lo_ctx* ctx, size_t n, int32_t* out);
+/* Context-free host variant (no GPU needed): sample_size = gmm_sample_size. */
+int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LO_ICP_H */

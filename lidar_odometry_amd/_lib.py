@@ -1,0 +1,91 @@
+"""ctypes binding of ``liblo_icp.so`` (the C ABI in ``include/lo_icp.h``).
+
+The shared library is built in-tree by ``make -C lidar_odometry_amd/csrc`` (``__graft_entry__.build()``).
+There is no CPU fallback: if the library or a HIP device is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblo_icp.so")
+
+LO_OK = 0
+LO_INSUFFICIENT = 1
+LO_ERR_ARG = -1
+LO_ERR_HIP = -2
+LO_ERR_CAPACITY = -3
+LO_ERR_STATE = -4
+LO_MAX_ITERS = 64
+
+# Every symbol include/lo_icp.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
+    "lo_device", "lo_map_set_surfels", "lo_map_surfel_count", "lo_icp_optimize", "lo_icp_optimize_async",
+    "lo_icp_result", "lo_sync", "lo_stream", "lo_find_correspondences", "lo_pko_scale_factor",
+    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host",
+)
+
+
+class LoConfig(C.Structure):
+    _fields_ = [
+        ("max_iterations", C.c_int), ("translation_tolerance", C.c_double), ("rotation_tolerance", C.c_double),
+        ("max_correspondence_distance", C.c_double), ("min_correspondence_points", C.c_int),
+        ("use_robust_loss", C.c_int), ("robust_loss_delta", C.c_double), ("loss_cauchy", C.c_int),
+        ("use_adaptive_m_estimator", C.c_int), ("min_scale_factor", C.c_double), ("max_scale_factor", C.c_double),
+        ("num_alpha_segments", C.c_int), ("truncated_threshold", C.c_double), ("gmm_components", C.c_int),
+        ("gmm_sample_size", C.c_int), ("pko_kernel_cauchy", C.c_int), ("voxel_size", C.c_float),
+        ("hierarchy_factor", C.c_int), ("use_surfel_correspondence", C.c_int), ("max_points", C.c_int),
+    ]
+
+
+class LoIterLog(C.Structure):
+    _fields_ = [("pose", C.c_float * 12), ("n_corr", C.c_int), ("scale", C.c_double), ("alpha", C.c_double),
+                ("cost", C.c_float), ("H", C.c_float * 21), ("g", C.c_float * 6), ("delta", C.c_float * 6)]
+
+
+class LoStats(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("n_corr", C.c_int), ("status", C.c_int), ("converged", C.c_int),
+                ("initial_cost", C.c_double), ("final_cost", C.c_double), ("gpu_ms", C.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    """Load liblo_icp.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP extension missing: {LIB_PATH}. Build it with `make -C lidar_odometry_amd/csrc` "
+                           "(there is no CPU fallback).")
+    L = C.CDLL(LIB_PATH)
+    fp, dp, ip, u8p, vp = (C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                           C.POINTER(C.c_uint8), C.c_void_p)
+    L.lo_config_default_kitti.argtypes = [C.POINTER(LoConfig)]
+    L.lo_config_default_mid360.argtypes = [C.POINTER(LoConfig)]
+    L.lo_create.restype = vp
+    L.lo_create.argtypes = [C.POINTER(LoConfig), C.c_int, C.POINTER(C.c_int)]
+    L.lo_destroy.argtypes = [vp]
+    L.lo_last_error.restype = C.c_char_p
+    L.lo_last_error.argtypes = [vp]
+    L.lo_device.argtypes = [vp]
+    L.lo_map_set_surfels.argtypes = [vp, ip, fp, fp, C.c_size_t]
+    L.lo_map_surfel_count.restype = C.c_size_t
+    L.lo_map_surfel_count.argtypes = [vp]
+    L.lo_icp_optimize.argtypes = [vp, fp, C.c_size_t, fp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]
+    L.lo_icp_optimize_async.argtypes = [vp, C.c_void_p, C.c_size_t, fp]
+    L.lo_icp_result.argtypes = [vp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]
+    L.lo_sync.argtypes = [vp]
+    L.lo_stream.restype = vp
+    L.lo_stream.argtypes = [vp]
+    L.lo_find_correspondences.argtypes = [vp, fp, C.c_size_t, fp, u8p, dp]
+    L.lo_pko_scale_factor.restype = C.c_double
+    L.lo_pko_scale_factor.argtypes = [vp, dp, C.c_size_t, dp]
+    L.lo_build_normal_equations.argtypes = [vp, fp, C.c_size_t, fp, C.c_double, C.c_double, dp, dp, dp]
+    L.lo_pko_sample_indices.argtypes = [vp, C.c_size_t, ip]
+    L.lo_pko_sample_indices_host.argtypes = [C.c_size_t, C.c_int, ip]
+    _lib = L
+    return L

@@ -1,0 +1,169 @@
+// lo_device.h — device-side data layout and numerics shared by the ICP kernels (gfx950 / CDNA4).
+//
+// HBM layout (one context):
+//   scan points       AoS float3, 12 B/pt (Point3D as the reference stores it; coalesced dwordx3 loads)
+//   surfel table      open-addressing hash, power-of-two capacity, load <= 0.5, linear probing;
+//                     one 32-B slot = {u64 Morton key, float normal[3], float centroid[3]} so a probe that
+//                     hits brings the payload in the same 32-B sector (no dependent second miss)
+//   per point         int32 slot index of the accepted correspondence (-1 = none)
+//   per 64 points     u64 validity ballot (rank -> point mapping for the PKO sampler)
+//   per 256-pt block  int count, fp64 residual sum and M2 (iteration-0 scale), 28 fp64 normal-eq partials
+//   DevState          pose, scale, alpha, n_corr, done flag, per-iteration logs (the GN loop state
+//                     lives on the device; the host never syncs inside optimize)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "../../include/lo_icp.h"
+
+namespace lo {
+
+constexpr int kBlock = 256;          // threads per block for the per-point kernels (4 waves)
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr int kNE = 28;              // 21 lower-triangular H + 6 g + cost
+constexpr int kPkoThreads = 1024;
+constexpr int kMaxBlocks = 16384;    // => max 4M points per scan
+constexpr int kMaxS = 256;
+constexpr int kMaxK = 4;
+constexpr int kMaxAlpha = 1000;
+
+struct __attribute__((aligned(32))) Slot {
+    uint64_t key;
+    float n[3];
+    float c[3];
+};
+static_assert(sizeof(Slot) == 32, "slot must be one 32-B sector");
+
+struct DevState {
+    float pose[12];
+    double scale;
+    double alpha;
+    int n_corr;
+    int iter;
+    int done;
+    int status;
+    double H_out[36];
+    double g_out[6];
+    double cost_out;
+    double gmm_out[3 * kMaxK];
+    lo_iter_log logs[LO_MAX_ITERS];
+};
+
+struct KParams {
+    // scan
+    const float* pts;
+    int n;
+    int nb;
+    // map
+    const Slot* tab;
+    uint32_t log2cap;
+    float l1scale;
+    // ICP config
+    int max_iters;
+    double tol_t, tol_r, maxd;
+    int min_corr;
+    int robust;
+    double robust_delta;
+    int cauchy_loss;
+    int use_pko;
+    // PKO config + tables
+    int S, K, NA, pko_cauchy;
+    double min_scale, trunc;
+    const double* alphas;
+    const double* Z;
+    const int32_t* small_off;
+    const int32_t* small_perm;
+    const int32_t* base;
+    const int32_t* ev_off;
+    const int32_t* ev_steps;
+    const int32_t* km_draws;
+    // work buffers
+    int32_t* slot;
+    uint64_t* wmask;
+    int32_t* blk_cnt;
+    double* blk_sum;
+    double* blk_m2;
+    double* blk_part;
+    double* res_dbg;          // nullable: per-point residual (parity entry point)
+    const double* direct_res; // nullable: PKO on given residuals (parity entry point)
+    DevState* st;
+};
+
+// ---------------------------------------------------------------------------------------------------
+// Bit-faithful scalar numerics (compiled with -ffp-contract=off; see DESIGN.md "fp order")
+// ---------------------------------------------------------------------------------------------------
+
+// transform_point_cloud: Matrix4f * Vector4f(x,y,z,1) (PointCloudUtils.cpp:119-121), Eigen packet order
+__device__ __forceinline__ void transform_pt(const float* T, float x, float y, float z, float& ox, float& oy, float& oz) {
+    float a;
+    a = T[0] * x; a = T[1] * y + a; a = T[2] * z + a; a = T[3] * 1.0f + a; ox = a;
+    a = T[4] * x; a = T[5] * y + a; a = T[6] * z + a; a = T[7] * 1.0f + a; oy = a;
+    a = T[8] * x; a = T[9] * y + a; a = T[10] * z + a; a = T[11] * 1.0f + a; oz = a;
+}
+
+// 3-term fp32 dot (Eigen redux_novec_unroller order)
+__device__ __forceinline__ float dot3f(float a0, float a1, float a2, float b0, float b1, float b2) {
+    float e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;
+    return e0 + (e1 + e2);
+}
+
+// VoxelKeyHash::ExpandBits (VoxelMap.h:168-177)
+__device__ __forceinline__ uint64_t expand21(int32_t v) {
+    uint64_t x = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffull;
+    x = (x | (x << 32)) & 0x1f00000000ffffull;
+    x = (x | (x << 16)) & 0x1f0000ff0000ffull;
+    x = (x | (x << 8)) & 0x100f00f00f00f00full;
+    x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+    x = (x | (x << 2)) & 0x1249249249249249ull;
+    return x;
+}
+
+__device__ __forceinline__ bool key_in_range(int v) { return v >= -(1 << 20) && v < (1 << 20); }
+
+__device__ __forceinline__ uint32_t hash_slot(uint64_t key, uint32_t log2cap) {
+    return static_cast<uint32_t>((key * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
+}
+
+// Surfel lookup: PointToVoxelKey(p, 1) (VoxelMap.cpp:50-58: fp32 division by voxel*factor, floor)
+// then the table probe.  Returns the slot index or -1.
+__device__ __forceinline__ int lookup_surfel(const Slot* __restrict__ tab, uint32_t log2cap, float l1scale,
+                                             float wx, float wy, float wz) {
+    if (!(isfinite(wx) && isfinite(wy) && isfinite(wz))) return -1;
+    const float fx = floorf(wx / l1scale), fy = floorf(wy / l1scale), fz = floorf(wz / l1scale);
+    if (!(fx >= -1048576.0f && fx < 1048576.0f && fy >= -1048576.0f && fy < 1048576.0f &&
+          fz >= -1048576.0f && fz < 1048576.0f)) return -1;
+    const int kx = static_cast<int>(fx), ky = static_cast<int>(fy), kz = static_cast<int>(fz);
+    const uint64_t key = expand21(kx) | (expand21(ky) << 1) | (expand21(kz) << 2);
+    const uint32_t mask = (1u << log2cap) - 1u;
+    uint32_t h = hash_slot(key, log2cap);
+    for (uint32_t p = 0; p <= mask; ++p) {
+        const uint64_t k = tab[h].key;
+        if (k == key) return static_cast<int>(h);
+        if (k == kEmptyKey) return -1;
+        h = (h + 1u) & mask;
+    }
+    return -1;
+}
+
+// fp64 point-to-plane residual |n.(p_w - c)| (IterativeClosestPointOptimizer.cpp:623-628);
+// Vector3d dot in Eigen's Packet2d order: (e0 + e1) + e2
+__device__ __forceinline__ double residual_f64(const Slot& s, float wx, float wy, float wz) {
+    const double d0 = static_cast<double>(wx) - static_cast<double>(s.c[0]);
+    const double d1 = static_cast<double>(wy) - static_cast<double>(s.c[1]);
+    const double d2 = static_cast<double>(wz) - static_cast<double>(s.c[2]);
+    const double e0 = static_cast<double>(s.n[0]) * d0;
+    const double e1 = static_cast<double>(s.n[1]) * d1;
+    const double e2 = static_cast<double>(s.n[2]) * d2;
+    return fabs((e0 + e1) + e2);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace lo

@@ -1,0 +1,492 @@
+// lo_icp.hip — host side of the C ABI declared in include/lo_icp.h.
+//
+// Owns one HIP stream per context, the device-resident surfel hash table, scan buffers, the PKO tables
+// and the DevState that carries the Gauss-Newton loop.  lo_icp_optimize enqueues the whole loop
+// (4 kernels x max_iterations) with no host synchronisation in between; the kernels read
+// DevState::done and fall through once the scan has converged or failed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lo_device.h"
+#include "lo_pko_tables.h"
+
+namespace lo {
+__global__ void k_correspond(KParams P, int with_stats);
+__global__ void k_pko(KParams P, int it);
+__global__ void k_accumulate(KParams P);
+__global__ void k_solve(KParams P, int it, int ne_only);
+}  // namespace lo
+
+using namespace lo;
+
+struct lo_ctx {
+    lo_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scan buffers
+    float* d_pts = nullptr;
+    int32_t* d_slot = nullptr;
+    uint64_t* d_wmask = nullptr;
+    int32_t* d_blk_cnt = nullptr;
+    double* d_blk_sum = nullptr;
+    double* d_blk_m2 = nullptr;
+    double* d_blk_part = nullptr;
+    double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
+    size_t res_cap = 0;
+    uint8_t* d_u8 = nullptr;
+    DevState* d_st = nullptr;
+    DevState* h_st = nullptr;       // pinned
+    // map
+    Slot* d_tab = nullptr;
+    size_t tab_cap = 0;             // allocated slots
+    uint32_t log2cap = 1;
+    size_t n_surfels = 0;
+    // PKO tables
+    PkoTables tables;
+    double* d_alphas = nullptr;
+    double* d_Z = nullptr;
+    int32_t* d_tabs_i = nullptr;    // small_off | small_perm | base | ev_off | ev_steps | km_draws
+    size_t off_small_off = 0, off_small_perm = 0, off_base = 0, off_ev_off = 0, off_ev_steps = 0, off_km = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float T_init[12];
+    size_t last_n = 0;
+    bool pending = false;
+};
+
+#define LO_HIP(ctx, call)                                                                  \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);               \
+            return LO_ERR_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
+    KParams P{};
+    const lo_config& g = c->cfg;
+    P.pts = d_pts;
+    P.n = n;
+    P.nb = (n + kBlock - 1) / kBlock;
+    P.tab = c->d_tab;
+    P.log2cap = c->log2cap;
+    P.l1scale = g.voxel_size * static_cast<float>(g.hierarchy_factor);   // PointToVoxelKey (VoxelMap.cpp:51-52)
+    P.max_iters = g.max_iterations;
+    P.tol_t = g.translation_tolerance;
+    P.tol_r = g.rotation_tolerance;
+    P.maxd = g.max_correspondence_distance;
+    P.min_corr = g.min_correspondence_points;
+    P.robust = g.use_robust_loss;
+    P.robust_delta = g.robust_loss_delta;
+    P.cauchy_loss = g.loss_cauchy;
+    P.use_pko = g.use_adaptive_m_estimator;
+    P.S = g.gmm_sample_size;
+    P.K = g.gmm_components;
+    P.NA = g.num_alpha_segments;
+    P.pko_cauchy = g.pko_kernel_cauchy;
+    P.min_scale = g.min_scale_factor;
+    P.trunc = g.truncated_threshold;
+    P.alphas = c->d_alphas;
+    P.Z = c->d_Z;
+    P.small_off = c->d_tabs_i + c->off_small_off;
+    P.small_perm = c->d_tabs_i + c->off_small_perm;
+    P.base = c->d_tabs_i + c->off_base;
+    P.ev_off = c->d_tabs_i + c->off_ev_off;
+    P.ev_steps = c->d_tabs_i + c->off_ev_steps;
+    P.km_draws = c->d_tabs_i + c->off_km;
+    P.slot = c->d_slot;
+    P.wmask = c->d_wmask;
+    P.blk_cnt = c->d_blk_cnt;
+    P.blk_sum = c->d_blk_sum;
+    P.blk_m2 = c->d_blk_m2;
+    P.blk_part = c->d_blk_part;
+    P.res_dbg = nullptr;
+    P.direct_res = nullptr;
+    P.st = c->d_st;
+    return P;
+}
+
+static int validate_config(const lo_config* g, std::string& err) {
+    if (!g) { err = "null config"; return LO_ERR_ARG; }
+    if (g->max_iterations < 1 || g->max_iterations > LO_MAX_ITERS) { err = "max_iterations out of [1, 64]"; return LO_ERR_ARG; }
+    if (g->gmm_sample_size < 1 || g->gmm_sample_size > kMaxS) { err = "gmm_sample_size out of [1, 256]"; return LO_ERR_ARG; }
+    if (g->gmm_components < 1 || g->gmm_components > kMaxK) { err = "gmm_components out of [1, 4]"; return LO_ERR_ARG; }
+    if (g->num_alpha_segments < 1 || g->num_alpha_segments > kMaxAlpha) { err = "num_alpha_segments out of [1, 1000]"; return LO_ERR_ARG; }
+    if (!(g->voxel_size > 0.0f)) { err = "voxel_size must be positive"; return LO_ERR_ARG; }   // VoxelMap.cpp:28-30
+    if (g->hierarchy_factor <= 0 || g->hierarchy_factor % 2 == 0) { err = "hierarchy_factor must be positive and odd"; return LO_ERR_ARG; }
+    if (g->max_points < 1 || g->max_points > kMaxBlocks * kBlock) { err = "max_points out of [1, 4194304]"; return LO_ERR_ARG; }
+    if (!g->use_surfel_correspondence) { err = "KDTree correspondence is not available in this build"; return LO_ERR_ARG; }
+    return LO_OK;
+}
+
+extern "C" {
+
+void lo_config_default_kitti(lo_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->max_iterations = 4;
+    c->translation_tolerance = 0.005;
+    c->rotation_tolerance = 0.005;
+    c->max_correspondence_distance = 1.0;
+    c->min_correspondence_points = 10;
+    c->use_robust_loss = 1;
+    c->robust_loss_delta = 0.1;
+    c->loss_cauchy = 0;
+    c->use_adaptive_m_estimator = 1;
+    c->min_scale_factor = 0.1;
+    c->max_scale_factor = 10.0;
+    c->num_alpha_segments = 100;
+    c->truncated_threshold = 10.0;
+    c->gmm_components = 3;
+    c->gmm_sample_size = 100;
+    c->pko_kernel_cauchy = 0;
+    c->voxel_size = 0.5f;
+    c->hierarchy_factor = 3;
+    c->use_surfel_correspondence = 1;
+    c->max_points = 1 << 17;
+}
+
+void lo_config_default_mid360(lo_config* c) {
+    lo_config_default_kitti(c);
+    c->voxel_size = 0.4f;   // config/mid360.yaml:19
+}
+
+const char* lo_last_error(const lo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+int lo_device(const lo_ctx* ctx) { return ctx ? ctx->device : -1; }
+void* lo_stream(lo_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+static int ctx_alloc(lo_ctx* c) {
+    const lo_config& g = c->cfg;
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const size_t N = static_cast<size_t>(g.max_points);
+    const size_t NB = (N + kBlock - 1) / kBlock;
+    LO_HIP(c, hipMalloc(&c->d_pts, N * 3 * sizeof(float)));
+    LO_HIP(c, hipMalloc(&c->d_slot, NB * kBlock * sizeof(int32_t)));
+    LO_HIP(c, hipMalloc(&c->d_wmask, NB * kWavesPerBlock * sizeof(uint64_t)));
+    LO_HIP(c, hipMalloc(&c->d_blk_cnt, NB * sizeof(int32_t)));
+    LO_HIP(c, hipMalloc(&c->d_blk_sum, NB * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_blk_m2, NB * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_blk_part, NB * kNE * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_st, sizeof(DevState)));
+    LO_HIP(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
+    std::memset(c->h_st, 0, sizeof(DevState));
+    LO_HIP(c, hipMemset(c->d_st, 0, sizeof(DevState)));
+    // empty table (capacity 2) so a scan before any map upload finds nothing
+    c->tab_cap = 2;
+    c->log2cap = 1;
+    LO_HIP(c, hipMalloc(&c->d_tab, c->tab_cap * sizeof(Slot)));
+    LO_HIP(c, hipMemset(c->d_tab, 0xff, c->tab_cap * sizeof(Slot)));
+    // PKO tables
+    build_pko_tables(c->tables, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
+                     g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel_cauchy != 0);
+    const PkoTables& t = c->tables;
+    LO_HIP(c, hipMalloc(&c->d_alphas, t.alphas.size() * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_Z, t.Z.size() * sizeof(double)));
+    LO_HIP(c, hipMemcpy(c->d_alphas, t.alphas.data(), t.alphas.size() * sizeof(double), hipMemcpyHostToDevice));
+    LO_HIP(c, hipMemcpy(c->d_Z, t.Z.data(), t.Z.size() * sizeof(double), hipMemcpyHostToDevice));
+    std::vector<int32_t> all;
+    auto append = [&](const std::vector<int32_t>& v, size_t& off) { off = all.size(); all.insert(all.end(), v.begin(), v.end()); all.push_back(0); };
+    append(t.small_off, c->off_small_off);
+    append(t.small_perm, c->off_small_perm);
+    append(t.base, c->off_base);
+    append(t.ev_off, c->off_ev_off);
+    append(t.ev_steps, c->off_ev_steps);
+    append(t.km_draws, c->off_km);
+    LO_HIP(c, hipMalloc(&c->d_tabs_i, all.size() * sizeof(int32_t)));
+    LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    LO_HIP(c, hipEventCreate(&c->ev0));
+    LO_HIP(c, hipEventCreate(&c->ev1));
+    return LO_OK;
+}
+
+lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
+    std::string e;
+    int rc = validate_config(cfg, e);
+    if (rc != LO_OK) { if (err) *err = rc; std::fprintf(stderr, "lo_create: %s\n", e.c_str()); return nullptr; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        if (err) *err = LO_ERR_HIP;
+        std::fprintf(stderr, "lo_create: no HIP device %d (count %d)\n", device, ndev);
+        return nullptr;
+    }
+    lo_ctx* c = new lo_ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    rc = ctx_alloc(c);
+    if (rc != LO_OK) {
+        std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
+        lo_destroy(c);
+        if (err) *err = rc;
+        return nullptr;
+    }
+    if (err) *err = LO_OK;
+    return c;
+}
+
+void lo_destroy(lo_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part,
+                    c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i};
+    for (void* b : bufs) if (b) (void)hipFree(b);
+    if (c->h_st) (void)hipHostFree(c->h_st);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ---------------------------------------------------------------- map
+static uint64_t morton_host(int32_t x, int32_t y, int32_t z) {
+    auto ex = [](int32_t v) {
+        uint64_t q = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffull;
+        q = (q | (q << 32)) & 0x1f00000000ffffull;
+        q = (q | (q << 16)) & 0x1f0000ff0000ffull;
+        q = (q | (q << 8)) & 0x100f00f00f00f00full;
+        q = (q | (q << 4)) & 0x10c30c30c30c30c3ull;
+        q = (q | (q << 2)) & 0x1249249249249249ull;
+        return q;
+    };
+    return ex(x) | (ex(y) << 1) | (ex(z) << 2);
+}
+
+int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, const float* centroids, size_t m) {
+    if (!c) return LO_ERR_ARG;
+    if (m > 0 && (!keys || !normals || !centroids)) { c->err = "null surfel arrays"; return LO_ERR_ARG; }
+    size_t cap = 2;
+    uint32_t l2 = 1;
+    while (cap < 2 * m) { cap <<= 1; ++l2; }            // load factor <= 0.5
+    std::vector<Slot> h(cap);
+    for (auto& s : h) { s.key = kEmptyKey; s.n[0] = s.n[1] = s.n[2] = 0.0f; s.c[0] = s.c[1] = s.c[2] = 0.0f; }
+    const uint64_t mask = cap - 1;
+    for (size_t i = 0; i < m; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            const int32_t v = keys[3 * i + a];
+            if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
+        }
+        const uint64_t key = morton_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        uint64_t b = (key * 0x9E3779B97F4A7C15ull) >> (64 - l2);
+        while (h[b].key != kEmptyKey && h[b].key != key) b = (b + 1) & mask;
+        h[b].key = key;                                    // duplicate keys: last one wins (map semantics)
+        for (int a = 0; a < 3; ++a) { h[b].n[a] = normals[3 * i + a]; h[b].c[a] = centroids[3 * i + a]; }
+    }
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (cap > c->tab_cap) {
+        LO_HIP(c, hipFree(c->d_tab));
+        c->d_tab = nullptr;
+        LO_HIP(c, hipMalloc(&c->d_tab, cap * sizeof(Slot)));
+        c->tab_cap = cap;
+    }
+    LO_HIP(c, hipMemcpy(c->d_tab, h.data(), cap * sizeof(Slot), hipMemcpyHostToDevice));
+    c->log2cap = l2;
+    c->n_surfels = m;
+    return LO_OK;
+}
+
+size_t lo_map_surfel_count(const lo_ctx* c) { return c ? c->n_surfels : 0; }
+
+// ---------------------------------------------------------------- optimize
+static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12]) {
+    const lo_config& g = c->cfg;
+    std::memcpy(c->T_init, T_init, sizeof(float) * 12);
+    c->last_n = n;
+    // reset the GN state: pose, done, status, iter
+    DevState* hs = c->h_st;
+    std::memcpy(hs->pose, T_init, sizeof(float) * 12);
+    hs->scale = 1.0;
+    hs->alpha = g.robust_loss_delta;
+    hs->n_corr = 0;
+    hs->iter = 0;
+    hs->done = 0;
+    hs->status = LO_OK;
+    LO_HIP(c, hipMemcpyAsync(c->d_st, hs, offsetof(DevState, H_out), hipMemcpyHostToDevice, c->stream));
+    LO_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if (n > 0) {
+        KParams P = make_params(c, d_pts, static_cast<int>(n));
+        const dim3 grid(P.nb), blk(kBlock);
+        for (int it = 0; it < g.max_iterations; ++it) {
+            hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, it == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_pko, dim3(1), dim3(kPkoThreads), 0, c->stream, P, it);
+            hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P);
+            hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, it, 0);
+        }
+        LO_HIP(c, hipGetLastError());
+    }
+    LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+    LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    c->pending = true;
+    return LO_OK;
+}
+
+int lo_icp_optimize_async(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12]) {
+    if (!c || !T_init || (n > 0 && !d_pts)) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    return enqueue_optimize(c, d_pts, n, T_init);
+}
+
+int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
+    if (!c) return LO_ERR_ARG;
+    if (!c->pending) { c->err = "no optimize in flight"; return LO_ERR_STATE; }
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    c->pending = false;
+    const DevState* hs = c->h_st;
+    int status = c->last_n == 0 ? LO_INSUFFICIENT : hs->status;
+    const int iters = hs->iter;
+    if (T_out) {
+        if (status == LO_OK) std::memcpy(T_out, hs->pose, sizeof(float) * 12);
+        else std::memcpy(T_out, c->T_init, sizeof(float) * 12);   // optimized_transform = initial (:266, :301)
+    }
+    if (logs) for (int i = 0; i < iters && i < c->cfg.max_iterations; ++i) logs[i] = hs->logs[i];
+    if (st) {
+        st->iterations = iters;
+        st->n_corr = hs->n_corr;
+        st->status = status;
+        st->converged = status == LO_OK ? 1 : 0;
+        st->initial_cost = iters > 0 ? hs->logs[0].cost : 0.0;
+        st->final_cost = iters > 0 ? hs->logs[iters - 1].cost : 0.0;
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.0f;
+        st->gpu_ms = ms;
+    }
+    return status;
+}
+
+int lo_sync(lo_ctx* c) {
+    if (!c) return LO_ERR_ARG;
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    return LO_OK;
+}
+
+int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12], float T_out[12],
+                    lo_iter_log* logs, lo_stats* st) {
+    if (!c || !T_init || !T_out || (n > 0 && !pts)) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    if (n > 0) LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    int rc = enqueue_optimize(c, c->d_pts, n, T_init);
+    if (rc != LO_OK) return rc;
+    return lo_icp_result(c, T_out, logs, st);
+}
+
+// ---------------------------------------------------------------- parity entry points
+static int ensure_res(lo_ctx* c, size_t n) {
+    if (c->res_cap >= n && c->d_res) return LO_OK;
+    if (c->d_res) { LO_HIP(c, hipFree(c->d_res)); c->d_res = nullptr; }
+    if (c->d_u8) { LO_HIP(c, hipFree(c->d_u8)); c->d_u8 = nullptr; }
+    const size_t cap = std::max<size_t>(n, 256);
+    LO_HIP(c, hipMalloc(&c->d_res, cap * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_u8, cap));
+    c->res_cap = cap;
+    return LO_OK;
+}
+
+static int reset_state(lo_ctx* c, const float T[12], double scale, double alpha) {
+    DevState* hs = c->h_st;
+    std::memcpy(hs->pose, T, sizeof(float) * 12);
+    hs->scale = scale;
+    hs->alpha = alpha;
+    hs->n_corr = 0;
+    hs->iter = 0;
+    hs->done = 0;
+    hs->status = LO_OK;
+    LO_HIP(c, hipMemcpyAsync(c->d_st, hs, offsetof(DevState, H_out), hipMemcpyHostToDevice, c->stream));
+    return LO_OK;
+}
+
+int lo_find_correspondences(lo_ctx* c, const float* pts, size_t n, const float T[12], uint8_t* valid, double* residual) {
+    if (!c || !T || (n > 0 && (!pts || !valid || !residual))) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    if (n == 0) return 0;
+    LO_HIP(c, hipSetDevice(c->device));
+    int rc = ensure_res(c, n);
+    if (rc != LO_OK) return rc;
+    rc = reset_state(c, T, 1.0, 0.1);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    KParams P = make_params(c, c->d_pts, static_cast<int>(n));
+    P.res_dbg = c->d_res;
+    hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 1);
+    LO_HIP(c, hipGetLastError());
+    std::vector<int32_t> slots(n);
+    LO_HIP(c, hipMemcpyAsync(slots.data(), c->d_slot, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipMemcpyAsync(residual, c->d_res, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    int cnt = 0;
+    for (size_t i = 0; i < n; ++i) { valid[i] = slots[i] >= 0 ? 1 : 0; cnt += valid[i]; }
+    return cnt;
+}
+
+double lo_pko_scale_factor(lo_ctx* c, const double* residuals, size_t n, double* gmm_out) {
+    if (!c || (n > 0 && !residuals)) return NAN;
+    if (n == 0) return 1.0;                                  // calculate_scale_factor, empty input (:66-69)
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return NAN; }
+    if (hipSetDevice(c->device) != hipSuccess) return NAN;
+    if (ensure_res(c, n) != LO_OK) return NAN;
+    const float I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    if (reset_state(c, I, 1.0, 0.1) != LO_OK) return NAN;
+    if (hipMemcpyAsync(c->d_res, residuals, n * sizeof(double), hipMemcpyHostToDevice, c->stream) != hipSuccess) return NAN;
+    KParams P = make_params(c, c->d_pts, static_cast<int>(n));
+    P.direct_res = c->d_res;
+    P.use_pko = 1;
+    hipLaunchKernelGGL(k_pko, dim3(1), dim3(kPkoThreads), 0, c->stream, P, 0);
+    if (hipGetLastError() != hipSuccess) return NAN;
+    if (hipMemcpyAsync(c->h_st, c->d_st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream) != hipSuccess) return NAN;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return NAN;
+    if (gmm_out) for (int j = 0; j < 3 * c->cfg.gmm_components; ++j) gmm_out[j] = c->h_st->gmm_out[j];
+    return c->h_st->alpha;
+}
+
+int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float T[12], double scale, double delta,
+                              double H[36], double g[6], double* cost) {
+    if (!c || !T || !H || !g || !cost || (n > 0 && !pts)) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    if (n == 0) { std::memset(H, 0, 36 * sizeof(double)); std::memset(g, 0, 6 * sizeof(double)); *cost = 0; return 0; }
+    LO_HIP(c, hipSetDevice(c->device));
+    int rc = reset_state(c, T, scale, delta);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    KParams P = make_params(c, c->d_pts, static_cast<int>(n));
+    hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
+    hipLaunchKernelGGL(k_accumulate, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
+    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, 0, 1);
+    LO_HIP(c, hipGetLastError());
+    std::vector<int32_t> cnt(P.nb);
+    LO_HIP(c, hipMemcpyAsync(cnt.data(), c->d_blk_cnt, P.nb * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    for (int q = 0; q < 36; ++q) H[q] = c->h_st->H_out[q];
+    for (int j = 0; j < 6; ++j) g[j] = c->h_st->g_out[j];
+    *cost = c->h_st->cost_out;
+    int total = 0;
+    for (int v : cnt) total += v;
+    return total;
+}
+
+int lo_pko_sample_indices(lo_ctx* c, size_t n, int32_t* out) {
+    if (!c || !out) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    const int k = static_cast<int>(std::min<size_t>(n, static_cast<size_t>(c->cfg.gmm_sample_size)));
+    for (int s = 0; s < k; ++s) out[s] = pko_sample_host(c->tables, static_cast<int>(n), s);
+    return k;
+}
+
+int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {
+    if (!out || sample_size < 1 || sample_size > kMaxS || n > static_cast<size_t>(kMaxBlocks) * kBlock) return LO_ERR_ARG;
+    PkoTables t;
+    build_pko_tables(t, sample_size, 1, static_cast<int>(std::max<size_t>(n, 1)), 0.1, 10.0, 1, 10.0, false);
+    const int k = static_cast<int>(std::min<size_t>(n, static_cast<size_t>(sample_size)));
+    for (int s = 0; s < k; ++s) out[s] = pko_sample_host(t, static_cast<int>(n), s);
+    return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,230 @@
+"""Host-side mirror of the reference's ICP interface over the HIP C ABI.
+
+``IterativeClosestPointOptimizer`` keeps the reference's names, argument meaning and error behaviour
+(src/optimization/IterativeClosestPointOptimizer.h:148-215):
+
+* ``optimize(voxel_map, points, initial_transform)`` -> ``(success, optimized_transform)``; on failure
+  (fewer than ``min_correspondence_points`` correspondences in some iteration) it returns ``False`` and the
+  initial transform, exactly like ``optimize`` (:298-302 with :266).
+* ``get_last_stats()`` mirrors ``OptimizationStats`` (:192-199) plus per-iteration logs.
+
+Every call runs on the GPU through ``liblo_icp.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import LoConfig, LoIterLog, LoStats, lib
+
+
+@dataclass
+class ICPConfig:
+    """ICPConfig (IterativeClosestPointOptimizer.h:55-76) as Estimator.cpp:62-70 wires it from kitti.yaml."""
+    max_iterations: int = 4
+    translation_tolerance: float = 0.005
+    rotation_tolerance: float = 0.005
+    max_correspondence_distance: float = 1.0
+    min_correspondence_points: int = 10
+    use_robust_loss: bool = True
+    robust_loss_delta: float = 0.1
+    use_surfel_correspondence: bool = True
+
+
+@dataclass
+class AdaptiveMEstimatorConfig:
+    """AdaptiveMEstimatorConfig (AdaptiveMEstimator.h:24-41) with config/kitti.yaml:41-51 values."""
+    use_adaptive_m_estimator: bool = True
+    loss_type: str = "huber"            # SystemConfig.loss_type is never parsed (ConfigUtils.h:65)
+    min_scale_factor: float = 0.1
+    max_scale_factor: float = 10.0
+    num_alpha_segments: int = 100
+    truncated_threshold: float = 10.0
+    gmm_components: int = 3
+    gmm_sample_size: int = 100
+    pko_kernel_type: str = "huber"
+
+
+@dataclass
+class MapGeometry:
+    voxel_size: float = 0.5              # map_voxel_size (kitti.yaml:19)
+    hierarchy_factor: int = 3            # Estimator.cpp:79
+
+
+def make_config(icp: ICPConfig, pko: AdaptiveMEstimatorConfig, geom: MapGeometry, max_points: int) -> LoConfig:
+    c = LoConfig()
+    lib().lo_config_default_kitti(C.byref(c))
+    c.max_iterations = icp.max_iterations
+    c.translation_tolerance = icp.translation_tolerance
+    c.rotation_tolerance = icp.rotation_tolerance
+    c.max_correspondence_distance = icp.max_correspondence_distance
+    c.min_correspondence_points = icp.min_correspondence_points
+    c.use_robust_loss = int(icp.use_robust_loss)
+    c.robust_loss_delta = icp.robust_loss_delta
+    c.loss_cauchy = int(pko.loss_type == "cauchy")
+    c.use_adaptive_m_estimator = int(pko.use_adaptive_m_estimator)
+    c.min_scale_factor = pko.min_scale_factor
+    c.max_scale_factor = pko.max_scale_factor
+    c.num_alpha_segments = pko.num_alpha_segments
+    c.truncated_threshold = pko.truncated_threshold
+    c.gmm_components = pko.gmm_components
+    c.gmm_sample_size = pko.gmm_sample_size
+    if pko.pko_kernel_type not in ("huber", "cauchy"):
+        raise ValueError(f"pko_kernel_type {pko.pko_kernel_type!r} not supported (huber, cauchy)")
+    c.pko_kernel_cauchy = int(pko.pko_kernel_type == "cauchy")
+    c.voxel_size = geom.voxel_size
+    c.hierarchy_factor = geom.hierarchy_factor
+    c.use_surfel_correspondence = int(icp.use_surfel_correspondence)
+    c.max_points = int(max_points)
+    return c
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _as_pts(points) -> np.ndarray:
+    p = np.ascontiguousarray(points, dtype=np.float32)
+    if p.ndim != 2 or p.shape[1] != 3:
+        raise ValueError("points must be an (N, 3) float32 array (Point3D AoS)")
+    return p
+
+
+def _as_pose(T) -> np.ndarray:
+    T = np.ascontiguousarray(np.asarray(T, dtype=np.float32))
+    if T.shape == (4, 4):
+        T = np.ascontiguousarray(T[:3, :])
+    return np.ascontiguousarray(T.reshape(12))
+
+
+def pose34(T12) -> np.ndarray:
+    return np.asarray(T12, dtype=np.float32).reshape(3, 4)
+
+
+@dataclass
+class OptimizationStats:
+    num_correspondences: int = 0
+    num_iterations: int = 0
+    initial_cost: float = 0.0
+    final_cost: float = 0.0
+    optimization_time_ms: float = 0.0
+    converged: bool = False
+    iterations: list = field(default_factory=list)
+
+
+class IterativeClosestPointOptimizer:
+    """GPU point-to-plane ICP with PKO robust weights (one HIP context = one device + stream)."""
+
+    def __init__(self, config: ICPConfig | None = None, adaptive: AdaptiveMEstimatorConfig | None = None,
+                 geometry: MapGeometry | None = None, device: int = 0, max_points: int = 1 << 17):
+        self.config = config or ICPConfig()
+        self.adaptive = adaptive or AdaptiveMEstimatorConfig()
+        self.geometry = geometry or MapGeometry()
+        self._cfg = make_config(self.config, self.adaptive, self.geometry, max_points)
+        err = C.c_int(0)
+        self._ctx = lib().lo_create(C.byref(self._cfg), device, C.byref(err))
+        if not self._ctx:
+            raise RuntimeError(f"lo_create failed (code {err.value}); is a HIP device present?")
+        self._map_token = None
+        self._last = OptimizationStats()
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().lo_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc < 0:
+            raise RuntimeError(f"liblo_icp error {rc}: {lib().lo_last_error(self._ctx).decode()}")
+        return rc
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    # ------------------------------------------------------------------ map
+    def set_surfels(self, keys, normals, centroids):
+        """Upload the L1 surfels (VoxelMap nodes with has_surfel) as the device hash table."""
+        k = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
+        n = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        c = np.ascontiguousarray(centroids, dtype=np.float32).reshape(-1, 3)
+        if not (len(k) == len(n) == len(c)):
+            raise ValueError("keys/normals/centroids length mismatch")
+        self._check(lib().lo_map_set_surfels(self._ctx, k.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(n), _fptr(c), len(k)))
+
+    def _sync_map(self, voxel_map):
+        if voxel_map is None:
+            return
+        token = (id(voxel_map), getattr(voxel_map, "revision", None))
+        if token == self._map_token and token[1] is not None:
+            return
+        s = voxel_map.surfels()
+        self.set_surfels(s[0], s[1], s[2])
+        self._map_token = token
+
+    # ------------------------------------------------------------------ optimize
+    def optimize(self, voxel_map, points, initial_transform):
+        """IterativeClosestPointOptimizer::optimize -> (success, optimized_transform[3x4])."""
+        self._sync_map(voxel_map)
+        p = _as_pts(points)
+        Ti = _as_pose(initial_transform)
+        To = np.zeros(12, np.float32)
+        logs = (LoIterLog * self._cfg.max_iterations)()
+        st = LoStats()
+        rc = self._check(lib().lo_icp_optimize(self._ctx, _fptr(p), len(p), _fptr(Ti), _fptr(To), logs, C.byref(st)))
+        its = []
+        for i in range(st.iterations):
+            L = logs[i]
+            its.append({"pose": np.array(L.pose[:], np.float32), "n_corr": L.n_corr, "scale": L.scale,
+                        "alpha": L.alpha, "cost": L.cost, "H": np.array(L.H[:], np.float32),
+                        "g": np.array(L.g[:], np.float32), "delta": np.array(L.delta[:], np.float32)})
+        self._last = OptimizationStats(st.n_corr, st.iterations, st.initial_cost, st.final_cost, st.gpu_ms,
+                                       bool(st.converged), its)
+        return rc == _lib.LO_OK, pose34(To)
+
+    def get_last_stats(self) -> OptimizationStats:
+        return self._last
+
+    # ------------------------------------------------------------------ single stages (parity harness)
+    def find_correspondences(self, points, T):
+        p = _as_pts(points)
+        t = _as_pose(T)
+        valid = np.zeros(len(p), np.uint8)
+        res = np.zeros(len(p), np.float64)
+        n = self._check(lib().lo_find_correspondences(self._ctx, _fptr(p), len(p), _fptr(t),
+                                                      valid.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                      res.ctypes.data_as(C.POINTER(C.c_double))))
+        return n, valid.astype(bool), res
+
+    def pko_scale_factor(self, residuals):
+        r = np.ascontiguousarray(residuals, dtype=np.float64)
+        K = self._cfg.gmm_components
+        gmm = np.zeros(3 * K, np.float64)
+        a = lib().lo_pko_scale_factor(self._ctx, r.ctypes.data_as(C.POINTER(C.c_double)), len(r),
+                                      gmm.ctypes.data_as(C.POINTER(C.c_double)))
+        if np.isnan(a):
+            raise RuntimeError(f"lo_pko_scale_factor failed: {lib().lo_last_error(self._ctx).decode()}")
+        return a, {"w": gmm[:K].copy(), "mu": gmm[K:2 * K].copy(), "var": gmm[2 * K:].copy()}
+
+    def build_normal_equations(self, points, T, scale, delta):
+        p = _as_pts(points)
+        t = _as_pose(T)
+        H = np.zeros(36, np.float64)
+        g = np.zeros(6, np.float64)
+        cost = C.c_double(0.0)
+        n = self._check(lib().lo_build_normal_equations(self._ctx, _fptr(p), len(p), _fptr(t), float(scale),
+                                                        float(delta), H.ctypes.data_as(C.POINTER(C.c_double)),
+                                                        g.ctypes.data_as(C.POINTER(C.c_double)), C.byref(cost)))
+        return n, H.reshape(6, 6), g, cost.value
+
+    def pko_sample_indices(self, n):
+        out = np.zeros(max(self._cfg.gmm_sample_size, 1), np.int32)
+        k = self._check(lib().lo_pko_sample_indices(self._ctx, n, out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out[:k]

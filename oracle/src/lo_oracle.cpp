@@ -1,0 +1,1188 @@
+/*
+ * lo_oracle.cpp — CPU ORACLE for the ICP hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * A single-threaded restatement of the reference (SiarheiHerasiuta/lidar_odometry) point-to-plane
+ * ICP step, written from the reference source without Eigen.  It is the checker for the HIP product
+ * (tests/), the `cpu_baseline` leg of bench.py and nothing else: the product never links or calls it.
+ *
+ * Faithfulness rules followed here:
+ *  - every floating-point expression keeps the reference's precision (fp32 vs fp64) and the
+ *    operation order that Eigen 3.4 produces for fixed-size objects on x86-64/SSE2 without FMA:
+ *      Matrix4f*Vector4f  (packet path)       : ((c0*x + c1*y) + c2*z) + c3*w
+ *      Matrix3f*Vector3f, Vector3f.dot/norm   : e0 + (e1 + e2)        (redux_novec_unroller)
+ *      Vector3d.dot                           : (e0 + e1) + e2         (Packet2d + tail)
+ *    The library is compiled with -O3 -ffp-contract=off and no -march (the reference's Release
+ *    flags have no -march, CMakeLists.txt:19-21, so no FMA is ever emitted there).
+ *  - unordered_dense containers are restated as "dense value vector in insertion order, erase moves the
+ *    last value into the hole" (unordered_dense.h do_erase) — the only property the reference's results
+ *    depend on (iteration order).
+ *  - PKO uses the real libstdc++ std::mt19937 / std::shuffle / std::uniform_int_distribution, exactly as
+ *    AdaptiveMEstimator.cpp does.
+ *
+ * Parity status: PKO pinned against reference golden vectors (tests/golden/pko_golden.json, produced by
+ * oracle/ref/pko_golden.cpp linked with the reference's own AdaptiveMEstimator.cpp).  Eigen-dependent
+ * pieces (JacobiSVD, LDLT, SE3, surfel PCA, correspondences) are parity UNPINNED against reference
+ * binaries (Eigen absent, reference unbuildable here).
+ */
+#include "lo_oracle.h"
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <random>
+#include <utility>
+#include <vector>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+namespace orc {
+
+/* ===================================================================================== */
+/*  Small fixed-size algebra with Eigen's evaluation order                                */
+/* ===================================================================================== */
+
+struct M3 { float a[3][3]; };   // a[row][col]
+
+static inline float dot3f(float a0, float a1, float a2, float b0, float b1, float b2) {
+    float e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;
+    return e0 + (e1 + e2);
+}
+static inline double dot3d(double a0, double a1, double a2, double b0, double b1, double b2) {
+    double e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;
+    return (e0 + e1) + e2;
+}
+static inline float norm3f(const float v[3]) { return std::sqrt(dot3f(v[0], v[1], v[2], v[0], v[1], v[2])); }
+
+static M3 eye3() { M3 m; for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) m.a[r][c] = (r == c) ? 1.0f : 0.0f; return m; }
+
+// Matrix3f * Matrix3f (lazy coeff-based product, MathUtils.h:81-83)
+static M3 mul33(const M3& A, const M3& B) {
+    M3 C;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            C.a[r][c] = dot3f(A.a[r][0], A.a[r][1], A.a[r][2], B.a[0][c], B.a[1][c], B.a[2][c]);
+    return C;
+}
+// Matrix3f * Vector3f
+static inline void mul3v(const M3& A, const float v[3], float out[3]) {
+    for (int r = 0; r < 3; ++r) out[r] = dot3f(A.a[r][0], A.a[r][1], A.a[r][2], v[0], v[1], v[2]);
+}
+
+/* ---- JacobiSVD<Matrix3f> (Eigen 3.4 JacobiSVD::compute, square case, no preconditioner) ---- */
+struct JRot { float c, s; };
+
+// makeJacobi(x, y, z) (Eigen/src/Jacobi/Jacobi.h)
+static JRot make_jacobi(float x, float y, float z) {
+    JRot j;
+    float deno = 2.0f * std::fabs(y);
+    if (deno < FLT_MIN) { j.c = 1.0f; j.s = 0.0f; return j; }
+    float tau = (x - z) / deno;
+    float w = std::sqrt(tau * tau + 1.0f);
+    float t = (tau > 0.0f) ? 1.0f / (tau + w) : 1.0f / (tau - w);
+    float sign_t = t > 0.0f ? 1.0f : -1.0f;
+    float n = 1.0f / std::sqrt(t * t + 1.0f);
+    j.s = ((-sign_t) * (y / std::fabs(y))) * std::fabs(t) * n;
+    j.c = n;
+    return j;
+}
+// rot1 * rot2 (JacobiRotation::operator*)
+static JRot jmul(JRot a, JRot b) { JRot r; r.c = a.c * b.c - a.s * b.s; r.s = a.c * b.s + a.s * b.c; return r; }
+static JRot jtrans(JRot a) { JRot r; r.c = a.c; r.s = -a.s; return r; }
+// apply_rotation_in_the_plane(x, y, j): x' = c x + s y ; y' = -s x + c y
+static inline void rot_pair(float& x, float& y, JRot j) {
+    float xi = x, yi = y;
+    x = j.c * xi + j.s * yi;
+    y = -j.s * xi + j.c * yi;
+}
+static void apply_left(M3& M, int p, int q, JRot j) { for (int i = 0; i < 3; ++i) rot_pair(M.a[p][i], M.a[q][i], j); }
+static void apply_right(M3& M, int p, int q, JRot j) { JRot t = jtrans(j); for (int i = 0; i < 3; ++i) rot_pair(M.a[i][p], M.a[i][q], t); }
+
+static void real_2x2_jacobi_svd(const M3& W, int p, int q, JRot* jl, JRot* jr) {
+    float m00 = W.a[p][p], m01 = W.a[p][q], m10 = W.a[q][p], m11 = W.a[q][q];
+    JRot rot1;
+    float t = m00 + m11;
+    float d = m10 - m01;
+    if (std::fabs(d) < FLT_MIN) { rot1.s = 0.0f; rot1.c = 1.0f; }
+    else {
+        float u = t / d;
+        float tmp = std::sqrt(1.0f + u * u);
+        rot1.s = 1.0f / tmp;
+        rot1.c = u / tmp;
+    }
+    // m.applyOnTheLeft(0,1,rot1)
+    rot_pair(m00, m10, rot1);
+    rot_pair(m01, m11, rot1);
+    *jr = make_jacobi(m00, m01, m11);
+    *jl = jmul(rot1, jtrans(*jr));
+}
+
+// Returns 0 on success, -1 on non-finite input.  U, V full; S descending.
+static int jacobi_svd3(const M3& A, M3& U, float S[3], M3& V) {
+    float scale = 0.0f;
+    bool nan = false;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
+        float v = std::fabs(A.a[r][c]);
+        if (std::isnan(v)) nan = true;
+        if (v > scale) scale = v;
+    }
+    if (nan || !std::isfinite(scale)) { U = eye3(); V = eye3(); S[0] = S[1] = S[2] = NAN; return -1; }
+    if (scale == 0.0f) scale = 1.0f;
+    M3 W;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) W.a[r][c] = A.a[r][c] / scale;
+    U = eye3(); V = eye3();
+    const float precision = 2.0f * FLT_EPSILON;
+    const float considerAsZero = FLT_MIN;
+    float maxDiag = std::max(std::fabs(W.a[0][0]), std::max(std::fabs(W.a[1][1]), std::fabs(W.a[2][2])));
+    // Eigen maxCoeff over |diag|: strict '>' visitor; with no NaN same as max.
+    bool finished = false;
+    int sweeps = 0;
+    while (!finished && sweeps < 1000) {
+        finished = true;
+        ++sweeps;
+        for (int p = 1; p < 3; ++p) {
+            for (int q = 0; q < p; ++q) {
+                float threshold = std::max(considerAsZero, precision * maxDiag);
+                if (std::fabs(W.a[p][q]) > threshold || std::fabs(W.a[q][p]) > threshold) {
+                    finished = false;
+                    JRot jl, jr;
+                    real_2x2_jacobi_svd(W, p, q, &jl, &jr);
+                    apply_left(W, p, q, jl);
+                    apply_right(U, p, q, jtrans(jl));
+                    apply_right(W, p, q, jr);
+                    apply_right(V, p, q, jr);
+                    maxDiag = std::max(maxDiag, std::max(std::fabs(W.a[p][p]), std::fabs(W.a[q][q])));
+                }
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        float a = W.a[i][i];
+        S[i] = std::fabs(a);
+        if (a < 0.0f) for (int r = 0; r < 3; ++r) U.a[r][i] = -U.a[r][i];
+    }
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    for (int i = 0; i < 3; ++i) {
+        int pos = i;
+        float mx = S[i];
+        for (int k = i + 1; k < 3; ++k) if (S[k] > mx) { mx = S[k]; pos = k; }
+        if (mx == 0.0f) break;
+        if (pos != i) {
+            std::swap(S[i], S[pos]);
+            for (int r = 0; r < 3; ++r) { std::swap(U.a[r][i], U.a[r][pos]); std::swap(V.a[r][i], V.a[r][pos]); }
+        }
+    }
+    return 0;
+}
+
+// Eigen 3x3 determinant (bruteforce_det3_helper order)
+static float det3(const M3& m) {
+    auto h = [&](int a, int b, int c) { return m.a[0][a] * (m.a[1][b] * m.a[2][c] - m.a[1][c] * m.a[2][b]); };
+    return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
+}
+
+// SO3(const Matrix3f&) — MathUtils.cpp:86-99
+static M3 so3_normalize(const M3& R) {
+    M3 U, V; float S[3];
+    jacobi_svd3(R, U, S, V);
+    M3 Vt; for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vt.a[r][c] = V.a[c][r];
+    M3 out = mul33(U, Vt);
+    if (det3(out) < 0.0f) {
+        for (int r = 0; r < 3; ++r) U.a[r][2] *= -1.0f;
+        out = mul33(U, Vt);
+    }
+    return out;
+}
+
+static M3 hat3(const float v[3]) {
+    M3 S;
+    S.a[0][0] = 0.0f;  S.a[0][1] = -v[2]; S.a[0][2] = v[1];
+    S.a[1][0] = v[2];  S.a[1][1] = 0.0f;  S.a[1][2] = -v[0];
+    S.a[2][0] = -v[1]; S.a[2][1] = v[0];  S.a[2][2] = 0.0f;
+    return S;
+}
+
+// SO3::Exp — MathUtils.cpp:23-39 (kEps = 1e-6f, MathUtils.h:40)
+static M3 so3_exp(const float w[3]) {
+    const float theta = norm3f(w);
+    if (theta < 1e-6f) {
+        M3 H = hat3(w), R = eye3();
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R.a[r][c] = R.a[r][c] + H.a[r][c];
+        return so3_normalize(R);
+    }
+    const float theta_inv = 1.0f / theta;
+    float k[3] = {w[0] * theta_inv, w[1] * theta_inv, w[2] * theta_inv};
+    M3 K = hat3(k);
+    float s = std::sin(theta), omc = 1.0f - std::cos(theta);
+    M3 sK;  for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) sK.a[r][c] = omc * K.a[r][c];
+    M3 KK = mul33(sK, K);   // ((1-cos)*K)*K, lazy product of the scaled expression
+    M3 R;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c)
+        R.a[r][c] = ((r == c ? 1.0f : 0.0f) + s * K.a[r][c]) + KK.a[r][c];
+    return so3_normalize(R);
+}
+
+struct SE3 { M3 R; float t[3]; };
+static SE3 se3_from12(const float T[12]) {
+    SE3 s;
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) s.R.a[r][c] = T[r * 4 + c]; s.t[r] = T[r * 4 + 3]; }
+    return s;
+}
+static void se3_to12(const SE3& s, float T[12]) {
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) T[r * 4 + c] = s.R.a[r][c]; T[r * 4 + 3] = s.t[r]; }
+}
+// SE3::operator* — MathUtils.h:144-147
+static SE3 se3_mul(const SE3& A, const SE3& B) {
+    SE3 o;
+    o.R = so3_normalize(mul33(A.R, B.R));
+    float Rt[3]; mul3v(A.R, B.t, Rt);
+    for (int i = 0; i < 3; ++i) o.t[i] = A.t[i] + Rt[i];
+    return o;
+}
+
+/* ---- LDLT (Eigen ldlt_inplace<Lower>::unblocked + LDLT::_solve_impl), fp32 6x6 ---- */
+static void ldlt6_solve(const float Hin[36], const float b[6], float x[6]) {
+    float m[6][6];
+    for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) m[r][c] = Hin[r * 6 + c];
+    int transp[6];
+    float temp[6];
+    const int size = 6;
+    bool zero_all = false;
+    for (int k = 0; k < size; ++k) {
+        int big = k; float bv = std::fabs(m[k][k]);
+        for (int i = k + 1; i < size; ++i) if (std::fabs(m[i][i]) > bv) { bv = std::fabs(m[i][i]); big = i; }
+        transp[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; ++j) std::swap(m[k][j], m[big][j]);
+            for (int i = big + 1; i < size; ++i) std::swap(m[i][k], m[i][big]);
+            std::swap(m[k][k], m[big][big]);
+            for (int i = k + 1; i < big; ++i) { float tmp = m[i][k]; m[i][k] = m[big][i]; m[big][i] = tmp; }
+        }
+        int rs = size - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
+            float acc = 0.0f; for (int j = 0; j < k; ++j) acc += m[k][j] * temp[j];
+            m[k][k] -= acc;
+            for (int i = k + 1; i < size; ++i) { float a = 0.0f; for (int j = 0; j < k; ++j) a += m[i][j] * temp[j]; m[i][k] -= a; }
+        }
+        float akk = m[k][k];
+        bool valid = std::fabs(akk) > 0.0f;
+        if (k == 0 && !valid) { zero_all = true; break; }
+        if (rs > 0 && valid) for (int i = k + 1; i < size; ++i) m[i][k] /= akk;
+    }
+    if (zero_all) { for (int i = 0; i < 6; ++i) x[i] = 0.0f; return; }
+    float d[6];
+    for (int i = 0; i < 6; ++i) d[i] = b[i];
+    for (int k = 0; k < size; ++k) if (transp[k] != k) std::swap(d[k], d[transp[k]]);
+    for (int i = 0; i < size; ++i) { float a = 0.0f; for (int j = 0; j < i; ++j) a += m[i][j] * d[j]; d[i] -= a; }
+    for (int i = 0; i < size; ++i) { if (std::fabs(m[i][i]) > FLT_MIN) d[i] /= m[i][i]; else d[i] = 0.0f; }
+    for (int i = size - 1; i >= 0; --i) { float a = 0.0f; for (int j = i + 1; j < size; ++j) a += m[j][i] * d[j]; d[i] -= a; }
+    for (int k = size - 1; k >= 0; --k) if (transp[k] != k) std::swap(d[k], d[transp[k]]);
+    for (int i = 0; i < 6; ++i) x[i] = d[i];
+}
+
+/* ===================================================================================== */
+/*  Dense hash containers (unordered_dense semantics: insertion-ordered values,          */
+/*  erase = move last value into the hole)                                                */
+/* ===================================================================================== */
+
+struct VKey { int x, y, z; bool operator==(const VKey& o) const { return x == o.x && y == o.y && z == o.z; } };
+
+static inline uint64_t expand_bits21(int32_t v) {
+    uint64_t x = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffULL;
+    x = (x | (x << 32)) & 0x1f00000000ffffULL;
+    x = (x | (x << 16)) & 0x1f0000ff0000ffULL;
+    x = (x | (x << 8)) & 0x100f00f00f00f00fULL;
+    x = (x | (x << 4)) & 0x10c30c30c30c30c3ULL;
+    x = (x | (x << 2)) & 0x1249249249249249ULL;
+    return x;
+}
+// VoxelKeyHash (VoxelMap.h:166-183) followed by unordered_dense's wyhash mix for non-avalanching hashes
+static inline uint64_t vkey_hash(const VKey& k) {
+    uint64_t morton = expand_bits21(k.x) | (expand_bits21(k.y) << 1) | (expand_bits21(k.z) << 2);
+    __uint128_t r = static_cast<__uint128_t>(morton) * 0x9E3779B97F4A7C15ULL;
+    return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
+}
+
+template <typename V>
+struct DenseMap {
+    std::vector<std::pair<VKey, V>> vals;
+    std::vector<uint32_t> buckets;   // 0 = empty, else value index + 1
+    uint64_t mask = 0;
+
+    DenseMap() { rehash(16); }
+    void rehash(size_t cap) {
+        buckets.assign(cap, 0u);
+        mask = cap - 1;
+        for (size_t i = 0; i < vals.size(); ++i) place(static_cast<uint32_t>(i));
+    }
+    void place(uint32_t vi) {
+        uint64_t b = vkey_hash(vals[vi].first) & mask;
+        while (buckets[b]) b = (b + 1) & mask;
+        buckets[b] = vi + 1;
+    }
+    int64_t find_bucket(const VKey& k) const {
+        uint64_t b = vkey_hash(k) & mask;
+        while (buckets[b]) {
+            if (vals[buckets[b] - 1].first == k) return static_cast<int64_t>(b);
+            b = (b + 1) & mask;
+        }
+        return -1;
+    }
+    V* find(const VKey& k) { int64_t b = find_bucket(k); return b < 0 ? nullptr : &vals[buckets[b] - 1].second; }
+    const V* find(const VKey& k) const { int64_t b = find_bucket(k); return b < 0 ? nullptr : &vals[buckets[b] - 1].second; }
+    V& operator[](const VKey& k) {
+        int64_t b = find_bucket(k);
+        if (b >= 0) return vals[buckets[b] - 1].second;
+        if ((vals.size() + 1) * 5 > buckets.size() * 4) rehash(buckets.size() * 2);   // max load 0.8
+        vals.emplace_back(k, V());
+        place(static_cast<uint32_t>(vals.size() - 1));
+        return vals.back().second;
+    }
+    bool insert_key(const VKey& k) {   // set semantics
+        if (find_bucket(k) >= 0) return false;
+        (*this)[k];
+        return true;
+    }
+    bool erase(const VKey& k) {
+        int64_t bi = find_bucket(k);
+        if (bi < 0) return false;
+        uint64_t b = static_cast<uint64_t>(bi);
+        uint32_t vi = buckets[b] - 1;
+        // backward-shift deletion (linear probing)
+        buckets[b] = 0;
+        uint64_t j = (b + 1) & mask;
+        while (buckets[j]) {
+            uint64_t home = vkey_hash(vals[buckets[j] - 1].first) & mask;
+            bool move = ((j - home) & mask) >= ((j - b) & mask) ? true : false;
+            // move if the hole lies cyclically in [home, j)
+            if (((j - home) & mask) >= ((j - b) & mask)) { buckets[b] = buckets[j]; buckets[j] = 0; b = j; }
+            (void)move;
+            j = (j + 1) & mask;
+        }
+        uint32_t last = static_cast<uint32_t>(vals.size() - 1);
+        if (vi != last) {
+            int64_t lb = find_bucket(vals[last].first);
+            vals[vi] = std::move(vals[last]);
+            buckets[lb] = vi + 1;
+        }
+        vals.pop_back();
+        return true;
+    }
+    size_t size() const { return vals.size(); }
+    bool empty() const { return vals.empty(); }
+    void clear() { vals.clear(); rehash(16); }
+};
+
+struct Empty {};
+using KeySet = DenseMap<Empty>;
+
+/* ===================================================================================== */
+/*  VoxelMap (VoxelMap.cpp)                                                               */
+/* ===================================================================================== */
+
+struct L0Node { float c[3] = {0.0f, 0.0f, 0.0f}; int hit_count = 1; int point_count = 0; };
+struct L1Node {
+    KeySet children;
+    bool has_surfel = false;
+    float normal[3] = {0.0f, 0.0f, 0.0f};
+    float centroid[3] = {0.0f, 0.0f, 0.0f};
+    float planarity = 1.0f;
+    int last_child_count = 0;
+};
+
+struct VoxelMap {
+    float voxel_size = 0.5f;
+    int factor = 3;
+    float planarity_threshold = 0.1f;
+    bool compute_surfels = true;
+    int init_hit_count = 1;
+    DenseMap<L0Node> L0;
+    DenseMap<L1Node> L1;
+
+    // PointToVoxelKey — VoxelMap.cpp:50-58
+    VKey key_of(const float p[3], int level) const {
+        float scale = voxel_size;
+        if (level == 1) scale *= static_cast<float>(factor);
+        VKey k;
+        k.x = static_cast<int>(std::floor(p[0] / scale));
+        k.y = static_cast<int>(std::floor(p[1] / scale));
+        k.z = static_cast<int>(std::floor(p[2] / scale));
+        return k;
+    }
+    // GetParentKey — :60-67
+    VKey parent_of(const VKey& k) const {
+        int f = factor;
+        VKey p;
+        p.x = k.x >= 0 ? k.x / f : (k.x - (f - 1)) / f;
+        p.y = k.y >= 0 ? k.y / f : (k.y - (f - 1)) / f;
+        p.z = k.z >= 0 ? k.z / f : (k.z - (f - 1)) / f;
+        return p;
+    }
+    void register_to_parent(const VKey& k) { L1[parent_of(k)].children.insert_key(k); }   // :77-80
+    void unregister_from_parent(const VKey& k) {                                        // :82-97
+        VKey p = parent_of(k);
+        L1Node* n = L1.find(p);
+        if (!n) return;
+        n->children.erase(k);
+        if (n->children.size() < 5) n->has_surfel = false;
+        if (n->children.empty()) L1.erase(p);
+    }
+    void add_point(const float p[3]) {                                                    // :99-120
+        VKey key = key_of(p, 0);
+        bool was_empty = L0.find(key) == nullptr;
+        L0Node& v = L0[key];
+        int n = v.point_count;
+        if (n == 0) {
+            v.c[0] = p[0]; v.c[1] = p[1]; v.c[2] = p[2];
+            v.hit_count = init_hit_count;
+            v.point_count = 1;
+        } else {
+            float nf = static_cast<float>(n), n1 = static_cast<float>(n + 1);
+            for (int i = 0; i < 3; ++i) v.c[i] = (v.c[i] * nf + p[i]) / n1;
+            v.point_count++;
+        }
+        if (was_empty) register_to_parent(key);
+    }
+    // surfel PCA shared by UpdateVoxelMap (:187-261) and RecomputeAllSurfels (:304-366)
+    // returns planarity; fills normal/centroid
+    float fit_surfel(const std::vector<std::array<float, 3>>& cs, float normal[3], float centroid[3]) {
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        for (auto& p : cs) for (int i = 0; i < 3; ++i) c[i] += p[i];
+        float nf = static_cast<float>(cs.size());
+        for (int i = 0; i < 3; ++i) c[i] /= nf;
+        M3 cov; for (int r = 0; r < 3; ++r) for (int q = 0; q < 3; ++q) cov.a[r][q] = 0.0f;
+        for (auto& p : cs) {
+            float d[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
+            for (int q = 0; q < 3; ++q) for (int r = 0; r < 3; ++r) cov.a[r][q] += d[q] * d[r];
+        }
+        for (int r = 0; r < 3; ++r) for (int q = 0; q < 3; ++q) cov.a[r][q] /= nf;
+        M3 U, V; float S[3];
+        jacobi_svd3(cov, U, S, V);
+        for (int i = 0; i < 3; ++i) { normal[i] = U.a[i][2]; centroid[i] = c[i]; }
+        return S[2] / (S[0] + 1e-6f);
+    }
+
+    void update(const float* xyz, int n, const double sensor[3], double max_distance, bool is_keyframe) {
+        if (!xyz || n <= 0) return;
+        if (!is_keyframe) return;
+        float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
+        float radius_sq = static_cast<float>(max_distance * max_distance);
+        std::vector<VKey> rm;
+        for (auto& kv : L0.vals) {
+            float d0 = kv.second.c[0] - sp[0], d1 = kv.second.c[1] - sp[1], d2 = kv.second.c[2] - sp[2];
+            float dsq = dot3f(d0, d1, d2, d0, d1, d2);
+            if (dsq > radius_sq) rm.push_back(kv.first);
+        }
+        for (auto& k : rm) { unregister_from_parent(k); L0.erase(k); }
+        std::vector<VKey> rm1;
+        for (auto& kv : L1.vals) if (kv.second.children.empty()) rm1.push_back(kv.first);
+        for (auto& k : rm1) L1.erase(k);
+
+        KeySet affected;
+        for (int i = 0; i < n; ++i) {
+            const float* p = xyz + 3 * i;
+            add_point(p);
+            affected.insert_key(key_of(p, 1));
+        }
+        if (!compute_surfels) return;
+        const int MIN_CHILDREN = 5;
+        for (auto& akv : affected.vals) {
+            const VKey key1 = akv.first;
+            L1Node* node = L1.find(key1);
+            if (!node) continue;
+            int cnt = static_cast<int>(node->children.size());
+            if (cnt < MIN_CHILDREN) { node->has_surfel = false; continue; }
+            if (node->has_surfel && node->last_child_count == cnt) continue;
+            std::vector<std::array<float, 3>> cs;
+            cs.reserve(cnt);
+            for (auto& ck : node->children.vals) {
+                const L0Node* l0 = L0.find(ck.first);
+                if (l0) cs.push_back({l0->c[0], l0->c[1], l0->c[2]});
+            }
+            if (cs.size() < 3) { node->has_surfel = false; continue; }
+            float nrm[3], cen[3];
+            float planarity = fit_surfel(cs, nrm, cen);
+            if (planarity > planarity_threshold) {
+                node->has_surfel = false;
+                std::vector<VKey> kids;
+                for (auto& ck : node->children.vals) kids.push_back(ck.first);
+                for (auto& k : kids) L0.erase(k);
+                L1.erase(key1);
+                continue;
+            }
+            node->has_surfel = true;
+            for (int i = 0; i < 3; ++i) { node->normal[i] = nrm[i]; node->centroid[i] = cen[i]; }
+            node->planarity = planarity;
+            node->last_child_count = cnt;
+        }
+    }
+
+    void recompute_all_surfels() {   // :304-366
+        const int MIN_CHILDREN = 5;
+        for (auto& kv : L1.vals) {
+            L1Node& node = kv.second;
+            int cnt = static_cast<int>(node.children.size());
+            if (cnt < MIN_CHILDREN) { node.has_surfel = false; continue; }
+            std::vector<std::array<float, 3>> cs;
+            for (auto& ck : node.children.vals) {
+                const L0Node* l0 = L0.find(ck.first);
+                if (l0) cs.push_back({l0->c[0], l0->c[1], l0->c[2]});
+            }
+            if (cs.size() < static_cast<size_t>(MIN_CHILDREN)) { node.has_surfel = false; continue; }
+            float nrm[3], cen[3];
+            float planarity = fit_surfel(cs, nrm, cen);
+            if (planarity > planarity_threshold) { node.has_surfel = false; continue; }
+            node.has_surfel = true;
+            for (int i = 0; i < 3; ++i) { node.normal[i] = nrm[i]; node.centroid[i] = cen[i]; }
+            node.planarity = planarity;
+            node.last_child_count = cnt;
+        }
+    }
+
+    void apply_transform(const float T[12]) {   // ApplyTransformAndRehash :264-302
+        SE3 s = se3_from12(T);
+        std::vector<std::pair<VKey, L0Node>> tr;
+        tr.reserve(L0.size());
+        for (auto& kv : L0.vals) {
+            L0Node nn = kv.second;
+            float rc[3]; mul3v(s.R, kv.second.c, rc);
+            for (int i = 0; i < 3; ++i) nn.c[i] = rc[i] + s.t[i];
+            tr.emplace_back(key_of(nn.c, 0), nn);
+        }
+        L0.clear(); L1.clear();
+        for (auto& kn : tr) {
+            L0Node& ex = L0[kn.first];
+            if (ex.point_count == 0) ex = kn.second;
+            else {
+                float n1 = static_cast<float>(ex.point_count), n2 = static_cast<float>(kn.second.point_count);
+                for (int i = 0; i < 3; ++i) ex.c[i] = (ex.c[i] * n1 + kn.second.c[i] * n2) / (n1 + n2);
+                ex.point_count += kn.second.point_count;
+            }
+            register_to_parent(kn.first);
+        }
+        recompute_all_surfels();
+    }
+
+    // GetSurfelAtPoint — :368-386
+    bool lookup(const float p[3], float n[3], float c[3]) const {
+        VKey k = key_of(p, 1);
+        const L1Node* node = L1.find(k);
+        if (!node || !node->has_surfel) return false;
+        for (int i = 0; i < 3; ++i) { n[i] = node->normal[i]; c[i] = node->centroid[i]; }
+        return true;
+    }
+};
+
+/* ===================================================================================== */
+/*  PKO — AdaptiveMEstimator.cpp                                                          */
+/* ===================================================================================== */
+
+struct PKO {
+    or_pko_cfg cfg;
+    std::vector<double> alphas, Z;
+    std::vector<double> w, mu, var;
+
+    double kernel(double r, double delta) const {   // pko_kernel_weight :128-156
+        if (cfg.kernel == 0) {
+            double a = std::fabs(r);
+            return a <= delta ? 1.0 : delta / a;
+        }
+        double e2 = r * r, d2 = delta * delta;
+        return d2 / (d2 + e2);
+    }
+    double partition(double alpha) const {          // :692-708
+        const double bound = cfg.truncated_threshold, step = 0.01;
+        double integral = 0.0;
+        for (double x = 0.0; x <= bound; x += step) integral += kernel(x, alpha) * step;
+        return std::max(integral, 1e-10);
+    }
+    void init_tables() {                             // initialize_pko :218-241
+        int S = cfg.num_alpha_segments;
+        alphas.assign(S + 1, 0.0); Z.assign(S + 1, 0.0);
+        alphas[0] = cfg.min_scale_factor;
+        Z[0] = partition(cfg.min_scale_factor);
+        for (int i = 1; i <= S; ++i) {
+            double t = static_cast<double>(i) / static_cast<double>(S);
+            double ls = (std::pow(100.0, t) - 1.0) / 99.0;
+            double a = cfg.min_scale_factor + (cfg.max_scale_factor - cfg.min_scale_factor) * ls;
+            alphas[i] = a; Z[i] = partition(a);
+        }
+    }
+    static double gpdf(double x, double mean, double variance) {   // :675-685
+        if (variance <= 0.0) return 0.0;
+        double diff = x - mean;
+        double expo = -0.5 * (diff * diff) / variance;
+        double norm = 1.0 / std::sqrt(2.0 * M_PI * variance);
+        return norm * std::exp(expo);
+    }
+    void fit_gmm(const std::vector<double>& res) {   // :294-485
+        int n = static_cast<int>(res.size());
+        int sample_size = cfg.gmm_sample_size > 0 ? cfg.gmm_sample_size
+                                                  : std::min(std::max(100, static_cast<int>(n * 0.1)), 10000);
+        if (sample_size > n) sample_size = n;
+        std::vector<int> idx(n);
+        std::iota(idx.begin(), idx.end(), 0);
+        std::mt19937 g(42);
+        std::shuffle(idx.begin(), idx.end(), g);
+        std::vector<double> sd(sample_size);
+        for (int i = 0; i < sample_size; ++i) sd[i] = res[idx[i]];
+        n = sample_size;
+        const int K = cfg.gmm_components;
+        std::mt19937 gen(42);
+        std::uniform_int_distribution<> dis(0, static_cast<int>(sd.size()) - 1);
+        mu.assign(K, 0.0);
+        mu[0] = 0.0;
+        for (int i = 1; i < K; ++i) mu[i] = sd[dis(gen)];
+        std::vector<int> clusters(sd.size());
+        std::vector<double> nm(K);
+        while (true) {
+            for (size_t i = 0; i < sd.size(); ++i) {
+                double md = std::numeric_limits<double>::max();
+                int ci = 0;
+                for (int j = 0; j < K; ++j) {
+                    double d = std::fabs(sd[i] - mu[j]);
+                    if (d < md) { md = d; ci = j; }
+                }
+                clusters[i] = ci;
+            }
+            std::fill(nm.begin(), nm.end(), 0.0);
+            std::vector<int> counts(K, 0);
+            for (size_t i = 0; i < sd.size(); ++i) { nm[clusters[i]] += sd[i]; counts[clusters[i]]++; }
+            for (int j = 0; j < K; ++j) {
+                if (j == 0) nm[j] = 0.0;
+                else if (counts[j] > 0) nm[j] /= static_cast<double>(counts[j]);
+            }
+            if (mu == nm) break;
+            nm[0] = 0.0;
+            mu = nm;
+        }
+        double mean = std::accumulate(sd.begin(), sd.end(), 0.0) / sd.size();
+        double iv = 0.0;
+        for (double x : sd) iv += std::pow(x - mean, 2);
+        iv /= sd.size();
+        var.assign(K, iv);
+        std::vector<int> cc(K, 0);
+        for (size_t i = 0; i < sd.size(); ++i) cc[clusters[i]]++;
+        w.resize(K);
+        for (int j = 0; j < K; ++j) w[j] = static_cast<double>(cc[j]) / static_cast<double>(sd.size());
+
+        std::vector<std::vector<double>> resp(n, std::vector<double>(K));
+        for (int it = 0; it < 100; ++it) {
+            std::vector<double> sr(n, 0.0);
+            for (int i = 0; i < n; ++i) {
+                for (int j = 0; j < K; ++j) { resp[i][j] = w[j] * gpdf(sd[i], mu[j], var[j]); sr[i] += resp[i][j]; }
+                for (int j = 0; j < K; ++j) resp[i][j] /= sr[i];
+            }
+            std::vector<double> Nk(K, 0.0);
+            for (int j = 0; j < K; ++j) for (int i = 0; i < n; ++i) Nk[j] += resp[i][j];
+            std::vector<double> nw(K), nmu(K, 0.0), nv(K, 0.0);
+            for (int j = 0; j < K; ++j) {
+                nw[j] = Nk[j] / static_cast<double>(n);
+                if (j == 0) nmu[j] = 0.0;
+                else { for (int i = 0; i < n; ++i) nmu[j] += resp[i][j] * sd[i]; nmu[j] /= Nk[j]; }
+                for (int i = 0; i < n; ++i) { double d = sd[i] - nmu[j]; nv[j] += resp[i][j] * d * d; }
+                nv[j] /= Nk[j];
+                nv[j] = std::max(nv[j], 1e-6);
+            }
+            double change = 0.0;
+            for (int j = 1; j < K; ++j) change += std::fabs(nmu[j] - mu[j]);
+            w = nw; nmu[0] = 0.0; mu = nmu; var = nv;
+            if (change < 1e-6) break;
+        }
+    }
+    double js(double alpha) const {                 // calculate_js_divergence :710-787
+        const int segs = 100;
+        double dr = cfg.truncated_threshold / static_cast<double>(segs);
+        double pf = 0.0;
+        for (size_t j = 0; j < alphas.size(); ++j) if (std::fabs(alphas[j] - alpha) < 1e-10) { pf = Z[j]; break; }
+        if (pf == 0.0) pf = partition(alpha);
+        if (pf < 1e-10) return std::numeric_limits<double>::max();
+        double cost = 0.0, cnt = 0.0;
+        for (int i = 0; i < segs; ++i) {
+            double r = dr * (1 + static_cast<double>(i));
+            double Pr = 0.0;
+            if (!w.empty() && !mu.empty() && !var.empty())
+                for (int m = 0; m < cfg.gmm_components && m < static_cast<int>(w.size()); ++m) Pr += w[m] * gpdf(r, mu[m], var[m]);
+            Pr += 1e-10;
+            double kv = kernel(r, alpha);
+            double Q = kv / (pf + 1e-10) + 1e-10;
+            double M = 0.5 * (Pr + Q);
+            double jsd = 0.5 * (Pr * std::log(Pr / M) + Q * std::log(Q / M));
+            if (std::isnan(jsd)) continue;
+            cost += jsd; cnt += 1.0;
+        }
+        if (cnt == 0) return std::numeric_limits<double>::max();
+        return cost / cnt;
+    }
+    double scale_factor(const std::vector<double>& res) {   // calculate_scale_factor :63-79 + :243-291
+        if (res.empty()) return 1.0;
+        if (alphas.empty()) init_tables();
+        fit_gmm(res);
+        double best_a = cfg.min_scale_factor, best_c = std::numeric_limits<double>::max();
+        for (size_t i = 1; i < alphas.size(); ++i) {
+            double c = js(alphas[i]);
+            if (c < best_c) { best_c = c; best_a = alphas[i]; }
+        }
+        return best_a;
+    }
+};
+
+/* ===================================================================================== */
+/*  Point cloud utilities                                                                 */
+/* ===================================================================================== */
+
+// transform_point_cloud (PointCloudUtils.cpp:102-125): Matrix4f * Vector4f(x,y,z,1), packet order
+static inline void transform_pt(const SE3& T, const float p[3], float o[3]) {
+    for (int r = 0; r < 3; ++r) {
+        float acc = T.R.a[r][0] * p[0];
+        acc = T.R.a[r][1] * p[1] + acc;
+        acc = T.R.a[r][2] * p[2] + acc;
+        acc = T.t[r] * 1.0f + acc;
+        o[r] = acc;
+    }
+}
+
+// FastVoxelFilter::filter (VoxelMap.h:73-104)
+struct FilterAcc { float sx = 0.0f, sy = 0.0f, sz = 0.0f; uint32_t count = 0; };
+static inline uint64_t expand_bits_filter(uint64_t v) {
+    v = v & 0x1FFFFF;
+    v = (v | (v << 32)) & 0x1F00000000FFFFULL;
+    v = (v | (v << 16)) & 0x1F0000FF0000FFULL;
+    v = (v | (v << 8)) & 0x100F00F00F00F00FULL;
+    v = (v | (v << 4)) & 0x10C30C30C30C30C3ULL;
+    v = (v | (v << 2)) & 0x1249249249249249ULL;
+    return v;
+}
+
+/* ===================================================================================== */
+/*  ICP — IterativeClosestPointOptimizer.cpp                                              */
+/* ===================================================================================== */
+
+struct Corr {   // DualFrameCorrespondences (IterativeClosestPointOptimizer.h:128-144)
+    std::vector<std::array<double, 3>> last, curr, normals;
+    std::vector<double> residuals;
+    void clear() { last.clear(); curr.clear(); normals.clear(); residuals.clear(); }
+    size_t size() const { return last.size(); }
+};
+
+static size_t find_corr(const VoxelMap& map, const float* pts, int n, const SE3& T, double maxd, Corr& c,
+                        uint8_t* valid_out, double* res_out) {
+    c.clear();
+    if (map.L0.empty()) return 0;
+    if (n <= 0) return 0;
+    std::vector<float> world(static_cast<size_t>(n) * 3);
+    for (int i = 0; i < n; ++i) transform_pt(T, pts + 3 * i, &world[3 * i]);
+    for (int i = 0; i < n; ++i) {
+        const float* q = &world[3 * i];
+        if (valid_out) { valid_out[i] = 0; res_out[i] = 0.0; }
+        float nf[3], cf[3];
+        if (!map.lookup(q, nf, cf)) continue;
+        double d0 = static_cast<double>(q[0]) - static_cast<double>(cf[0]);
+        double d1 = static_cast<double>(q[1]) - static_cast<double>(cf[1]);
+        double d2 = static_cast<double>(q[2]) - static_cast<double>(cf[2]);
+        double r = std::fabs(dot3d(nf[0], nf[1], nf[2], d0, d1, d2));
+        if (r > maxd) continue;
+        c.last.push_back({static_cast<double>(cf[0]), static_cast<double>(cf[1]), static_cast<double>(cf[2])});
+        c.curr.push_back({static_cast<double>(pts[3 * i]), static_cast<double>(pts[3 * i + 1]), static_cast<double>(pts[3 * i + 2])});
+        c.normals.push_back({static_cast<double>(nf[0]), static_cast<double>(nf[1]), static_cast<double>(nf[2])});
+        c.residuals.push_back(r);
+        if (valid_out) { valid_out[i] = 1; res_out[i] = r; }
+    }
+    return c.size();
+}
+
+/* ---- KDTree variant (find_correspondences_kdtree :647-767), brute-force exact 5-NN ----
+ * nanoflann KNNResultSet keeps the K smallest squared L2 distances (fp32 accumulate
+ * d0*d0 + d1*d1 + d2*d2) sorted ascending; equal distances keep the first-inserted
+ * (insertion sort shifts only strictly larger entries).  The tree visit order only matters
+ * for exact ties, which this brute force resolves by smaller index (parity unpinned there). */
+static void knn5(const std::vector<float>& cloud, const float q[3], int idx[5], float dist[5], int& found) {
+    found = 0;
+    size_t m = cloud.size() / 3;
+    for (size_t i = 0; i < m; ++i) {
+        float d0 = q[0] - cloud[3 * i], d1 = q[1] - cloud[3 * i + 1], d2 = q[2] - cloud[3 * i + 2];
+        float d = d0 * d0 + d1 * d1 + d2 * d2;
+        if (found == 5 && !(d < dist[4])) continue;
+        int j = found < 5 ? found : 4;
+        if (found < 5) found++;
+        while (j > 0 && dist[j - 1] > d) { dist[j] = dist[j - 1]; idx[j] = idx[j - 1]; --j; }
+        dist[j] = d; idx[j] = static_cast<int>(i);
+    }
+}
+
+// symmetric 3x3 eigen decomposition in double (cyclic Jacobi); returns eigenvector of smallest eigenvalue
+static void smallest_eigvec3d(const double A_in[3][3], double v_out[3]) {
+    double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    std::memcpy(A, A_in, sizeof(A));
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
+        if (off < 1e-300) break;
+        for (int p = 0; p < 2; ++p) for (int q = p + 1; q < 3; ++q) {
+            if (A[p][q] == 0.0) continue;
+            double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+            double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+            double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+            for (int k = 0; k < 3; ++k) {
+                double akp = A[k][p], akq = A[k][q];
+                A[k][p] = c * akp - s * akq; A[k][q] = s * akp + c * akq;
+            }
+            for (int k = 0; k < 3; ++k) {
+                double apk = A[p][k], aqk = A[q][k];
+                A[p][k] = c * apk - s * aqk; A[q][k] = s * apk + c * aqk;
+            }
+            for (int k = 0; k < 3; ++k) {
+                double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = c * vkp - s * vkq; V[k][q] = s * vkp + c * vkq;
+            }
+        }
+    }
+    int mi = 0;
+    for (int i = 1; i < 3; ++i) if (A[i][i] < A[mi][mi]) mi = i;
+    for (int k = 0; k < 3; ++k) v_out[k] = V[k][mi];
+}
+
+static size_t find_corr_kdtree(const VoxelMap& map, const float* pts, int n, const SE3& T, double maxd, Corr& c,
+                               uint8_t* valid_out, double* res_out, float* nout, float* tout) {
+    c.clear();
+    if (map.L0.empty() || n <= 0) return 0;
+    std::vector<float> cloud;   // GetPointCloud (:388-403), L0 iteration order
+    cloud.reserve(map.L0.size() * 3);
+    for (auto& kv : map.L0.vals) { cloud.push_back(kv.second.c[0]); cloud.push_back(kv.second.c[1]); cloud.push_back(kv.second.c[2]); }
+    for (int i = 0; i < n; ++i) {
+        if (valid_out) { valid_out[i] = 0; res_out[i] = 0.0; }
+        float q[3]; transform_pt(T, pts + 3 * i, q);
+        int idx[5]; float dist[5]; int found;
+        knn5(cloud, q, idx, dist, found);
+        if (found < 5) continue;
+        double P[5][3];
+        for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) P[k][d] = cloud[3 * idx[k] + d];
+        // is_collinear(p0,p1,p2,0.5) :785-792
+        double v1[3], v2[3];
+        for (int d = 0; d < 3; ++d) { v1[d] = P[1][d] - P[0][d]; v2[d] = P[2][d] - P[0][d]; }
+        double n1 = std::sqrt(dot3d(v1[0], v1[1], v1[2], v1[0], v1[1], v1[2]));
+        double n2 = std::sqrt(dot3d(v2[0], v2[1], v2[2], v2[0], v2[1], v2[2]));
+        if (n1 > 0) for (int d = 0; d < 3; ++d) v1[d] /= n1;
+        if (n2 > 0) for (int d = 0; d < 3; ++d) v2[d] /= n2;
+        double cr[3] = {v1[1] * v2[2] - v1[2] * v2[1], v1[2] * v2[0] - v1[0] * v2[2], v1[0] * v2[1] - v1[1] * v2[0]};
+        if (std::sqrt(dot3d(cr[0], cr[1], cr[2], cr[0], cr[1], cr[2])) < 0.5) continue;
+        double cen[3] = {0, 0, 0};
+        for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) cen[d] += P[k][d];
+        for (int d = 0; d < 3; ++d) cen[d] /= 5.0;
+        double S[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        for (int k = 0; k < 5; ++k) {
+            double a[3] = {P[k][0] - cen[0], P[k][1] - cen[1], P[k][2] - cen[2]};
+            for (int r = 0; r < 3; ++r) for (int s = 0; s < 3; ++s) S[r][s] += a[r] * a[s];
+        }
+        double nrm[3];
+        smallest_eigvec3d(S, nrm);
+        double pd = -dot3d(nrm[0], nrm[1], nrm[2], cen[0], cen[1], cen[2]);
+        double dist_pl = std::fabs(dot3d(nrm[0], nrm[1], nrm[2], q[0], q[1], q[2]) + pd);
+        if (dist_pl > maxd) continue;
+        c.last.push_back({cen[0], cen[1], cen[2]});
+        c.curr.push_back({static_cast<double>(pts[3 * i]), static_cast<double>(pts[3 * i + 1]), static_cast<double>(pts[3 * i + 2])});
+        c.normals.push_back({nrm[0], nrm[1], nrm[2]});
+        c.residuals.push_back(dist_pl);
+        if (valid_out) { valid_out[i] = 1; res_out[i] = dist_pl; }
+        if (nout) for (int d = 0; d < 3; ++d) { nout[3 * i + d] = static_cast<float>(nrm[d]); tout[3 * i + d] = static_cast<float>(cen[d]); }
+    }
+    return c.size();
+}
+
+// Weighted normal equations (:345-410)
+static void build_ne(const Corr& c, const SE3& T, const or_icp_cfg& cfg, double scale, double delta_a,
+                     float H[6][6], float g[6], float& cost) {
+    for (int r = 0; r < 6; ++r) { g[r] = 0.0f; for (int q = 0; q < 6; ++q) H[r][q] = 0.0f; }
+    cost = 0.0f;
+    const M3& R = T.R;
+    const double sden = std::max(scale, 1e-6);
+    for (size_t i = 0; i < c.size(); ++i) {
+        float p[3], q[3], n[3];
+        for (int d = 0; d < 3; ++d) {
+            p[d] = static_cast<float>(c.curr[i][d]);
+            q[d] = static_cast<float>(c.last[i][d]);
+            n[d] = static_cast<float>(c.normals[i][d]);
+        }
+        float Rp[3]; mul3v(R, p, Rp);
+        float pw[3] = {Rp[0] + T.t[0], Rp[1] + T.t[1], Rp[2] + T.t[2]};
+        float residual = dot3f(n[0], n[1], n[2], pw[0] - q[0], pw[1] - q[1], pw[2] - q[2]);
+        float nres = static_cast<float>(c.residuals[i] / sden);
+        float J[6];
+        for (int j = 0; j < 3; ++j) J[j] = dot3f(n[0], n[1], n[2], R.a[0][j], R.a[1][j], R.a[2][j]);
+        float nn[3] = {-n[0], -n[1], -n[2]};
+        float a[3];
+        for (int j = 0; j < 3; ++j) a[j] = dot3f(nn[0], nn[1], nn[2], R.a[0][j], R.a[1][j], R.a[2][j]);
+        M3 S = hat3(p);
+        for (int j = 0; j < 3; ++j) J[3 + j] = dot3f(a[0], a[1], a[2], S.a[0][j], S.a[1][j], S.a[2][j]);
+        float w = 1.0f;
+        if (cfg.use_robust_loss) {
+            float an = std::fabs(nres);
+            float dl = static_cast<float>(delta_a);
+            if (cfg.loss_cauchy) { float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
+            else if (an > dl) w = dl / an;
+        }
+        float wJ[6];
+        for (int j = 0; j < 6; ++j) wJ[j] = w * J[j];
+        for (int col = 0; col < 6; ++col) for (int row = 0; row < 6; ++row) H[row][col] += J[col] * wJ[row];
+        float wr = w * residual;
+        for (int j = 0; j < 6; ++j) g[j] += wr * J[j];
+        cost += wr * residual;
+    }
+}
+
+static double iter0_scale(const std::vector<double>& res_in) {   // :304-316
+    std::vector<double> r = res_in;
+    std::sort(r.begin(), r.end());
+    double mean = std::accumulate(r.begin(), r.end(), 0.0) / r.size();
+    double var = 0.0;
+    for (double v : r) var += (v - mean) * (v - mean);
+    var /= r.size();
+    return std::sqrt(var) / 6.0;
+}
+
+static int icp_optimize(const VoxelMap& map, const float* pts, int n, const float Ti[12], float To[12],
+                        const or_icp_cfg& cfg, bool kdtree, or_iter_log* logs, int* iters_out) {
+    SE3 cur = se3_from12(Ti);
+    std::memcpy(To, Ti, sizeof(float) * 12);
+    PKO pko; pko.cfg = cfg.pko;
+    double scale = 1.0;
+    int iters = 0;
+    Corr c;
+    for (int it = 0; it < cfg.max_iterations; ++it) {
+        size_t nc = kdtree ? find_corr_kdtree(map, pts, n, cur, cfg.max_correspondence_distance, c, nullptr, nullptr, nullptr, nullptr)
+                           : find_corr(map, pts, n, cur, cfg.max_correspondence_distance, c, nullptr, nullptr);
+        if (nc < static_cast<size_t>(cfg.min_correspondence_points)) {
+            if (iters_out) *iters_out = iters;
+            return 0;
+        }
+        if (it == 0 && !c.residuals.empty()) scale = iter0_scale(c.residuals);
+        double delta_a = cfg.robust_loss_delta;
+        if (cfg.use_pko) {
+            std::vector<double> nr;
+            nr.reserve(c.residuals.size());
+            for (double r : c.residuals) nr.push_back(r / std::max(scale, 1e-6));
+            if (!nr.empty()) delta_a = pko.scale_factor(nr);
+        }
+        float H[6][6], g[6], cost;
+        build_ne(c, cur, cfg, scale, delta_a, H, g, cost);
+        float Hf[36], mg[6], delta[6];
+        for (int r = 0; r < 6; ++r) for (int q = 0; q < 6; ++q) Hf[r * 6 + q] = H[r][q];
+        for (int j = 0; j < 6; ++j) mg[j] = -g[j];
+        ldlt6_solve(Hf, mg, delta);
+        float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
+        SE3 dT;
+        if (norm3f(dw) < 1e-10f) dT.R = so3_normalize(eye3());
+        else dT.R = so3_exp(dw);
+        for (int d = 0; d < 3; ++d) dT.t[d] = dt[d];
+        cur = se3_mul(cur, dT);
+        float tdel = norm3f(dt), rdel = norm3f(dw);
+        ++iters;
+        if (logs) {
+            or_iter_log& L = logs[it];
+            se3_to12(cur, L.pose);
+            L.n_corr = static_cast<int>(nc);
+            L.scale = scale;
+            L.alpha = delta_a;
+            L.cost = cost;
+            int k = 0;
+            for (int r = 0; r < 6; ++r) for (int q = r; q < 6; ++q) L.H[k++] = H[r][q];
+            for (int j = 0; j < 6; ++j) { L.g[j] = g[j]; L.delta[j] = delta[j]; }
+        }
+        bool conv = (tdel < cfg.translation_tolerance) && (rdel < cfg.rotation_tolerance);
+        if (conv) break;
+    }
+    se3_to12(cur, To);
+    if (iters_out) *iters_out = iters;
+    return 1;
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+/* ===================================================================================== */
+/*  C ABI                                                                                 */
+/* ===================================================================================== */
+
+extern "C" {
+
+double or_pko_scale_factor(const or_pko_cfg* cfg, const double* residuals, int n, double* gmm_out) {
+    PKO p; p.cfg = *cfg;
+    std::vector<double> r(residuals, residuals + n);
+    double a = p.scale_factor(r);
+    if (gmm_out && n > 0) {
+        int K = cfg->gmm_components;
+        for (int j = 0; j < K; ++j) { gmm_out[j] = p.w[j]; gmm_out[K + j] = p.mu[j]; gmm_out[2 * K + j] = p.var[j]; }
+    }
+    return a;
+}
+
+void or_shuffle_prefix(int n, int k, int* out) {
+    std::vector<int> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::mt19937 g(42);
+    std::shuffle(idx.begin(), idx.end(), g);
+    for (int i = 0; i < k && i < n; ++i) out[i] = idx[i];
+}
+
+void or_kmeans_seed_draws(int m, int count, int* out) {
+    std::mt19937 gen(42);
+    std::uniform_int_distribution<> dis(0, m - 1);
+    for (int i = 0; i < count; ++i) out[i] = dis(gen);
+}
+
+void or_pko_tables(const or_pko_cfg* cfg, double* alphas, double* Z) {
+    PKO p; p.cfg = *cfg;
+    p.init_tables();
+    for (size_t i = 0; i < p.alphas.size(); ++i) { alphas[i] = p.alphas[i]; Z[i] = p.Z[i]; }
+}
+
+void or_se3_compose(const float A[12], const float B[12], float out[12]) {
+    se3_to12(se3_mul(se3_from12(A), se3_from12(B)), out);
+}
+void or_so3_exp(const float w[3], float R[9]) {
+    M3 m = so3_exp(w);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R[r * 3 + c] = m.a[r][c];
+}
+void or_so3_normalize(const float Rin[9], float Rout[9]) {
+    M3 m; for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) m.a[r][c] = Rin[r * 3 + c];
+    M3 o = so3_normalize(m);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rout[r * 3 + c] = o.a[r][c];
+}
+int or_jacobi_svd3(const float A[9], float U[9], float S[3], float V[9]) {
+    M3 a; for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) a.a[r][c] = A[r * 3 + c];
+    M3 u, v;
+    int rc = jacobi_svd3(a, u, S, v);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) { U[r * 3 + c] = u.a[r][c]; V[r * 3 + c] = v.a[r][c]; }
+    return rc;
+}
+void or_ldlt6_solve(const float H[36], const float b[6], float x[6]) { ldlt6_solve(H, b, x); }
+
+void* or_map_create(float voxel_size, int hierarchy_factor, float planarity_threshold, int compute_surfels) {
+    VoxelMap* m = new VoxelMap();
+    m->voxel_size = voxel_size;
+    m->factor = hierarchy_factor;
+    m->planarity_threshold = planarity_threshold;
+    m->compute_surfels = compute_surfels != 0;
+    return m;
+}
+void or_map_destroy(void* m) { delete static_cast<VoxelMap*>(m); }
+void or_map_update(void* m, const float* xyz, int n, const double sensor[3], double max_distance, int is_keyframe) {
+    static_cast<VoxelMap*>(m)->update(xyz, n, sensor, max_distance, is_keyframe != 0);
+}
+void or_map_apply_transform(void* m, const float T[12]) { static_cast<VoxelMap*>(m)->apply_transform(T); }
+int or_map_l0_count(void* m) { return static_cast<int>(static_cast<VoxelMap*>(m)->L0.size()); }
+int or_map_l1_count(void* m) { return static_cast<int>(static_cast<VoxelMap*>(m)->L1.size()); }
+int or_map_surfel_count(void* m) {
+    int c = 0;
+    for (auto& kv : static_cast<VoxelMap*>(m)->L1.vals) if (kv.second.has_surfel) ++c;
+    return c;
+}
+int or_map_get_surfels(void* m, int32_t* keys, float* normals, float* centroids, float* planarity, int cap) {
+    int c = 0;
+    for (auto& kv : static_cast<VoxelMap*>(m)->L1.vals) {
+        if (!kv.second.has_surfel) continue;
+        if (c >= cap) break;
+        keys[3 * c] = kv.first.x; keys[3 * c + 1] = kv.first.y; keys[3 * c + 2] = kv.first.z;
+        for (int i = 0; i < 3; ++i) { normals[3 * c + i] = kv.second.normal[i]; centroids[3 * c + i] = kv.second.centroid[i]; }
+        if (planarity) planarity[c] = kv.second.planarity;
+        ++c;
+    }
+    return c;
+}
+int or_map_get_l0(void* m, float* xyz, int cap) {
+    int c = 0;
+    for (auto& kv : static_cast<VoxelMap*>(m)->L0.vals) {
+        if (c >= cap) break;
+        for (int i = 0; i < 3; ++i) xyz[3 * c + i] = kv.second.c[i];
+        ++c;
+    }
+    return c;
+}
+int or_map_lookup(void* m, const float p[3], float n[3], float c[3]) { return static_cast<VoxelMap*>(m)->lookup(p, n, c) ? 1 : 0; }
+
+int or_voxel_filter(const float* in, int n, float voxel_size, int stride, float* out) {
+    if (n <= 0 || stride < 1) return 0;
+    const float inv = 1.0f / voxel_size;
+    std::vector<uint64_t> keys_order;
+    struct KV { uint64_t k; FilterAcc a; };
+    std::vector<KV> vals;
+    std::vector<uint32_t> buckets(1024, 0u);
+    uint64_t mask = 1023;
+    auto hk = [](uint64_t k) { __uint128_t r = static_cast<__uint128_t>(k) * 0x9E3779B97F4A7C15ULL; return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64); };
+    for (int i = 0; i < n; i += stride) {
+        const float* p = in + 3 * i;
+        if (!std::isfinite(p[0]) || !std::isfinite(p[1]) || !std::isfinite(p[2])) continue;
+        const int64_t OFF = (1 << 20);
+        int64_t ix = static_cast<int64_t>(std::floor(p[0] * inv)) + OFF;
+        int64_t iy = static_cast<int64_t>(std::floor(p[1] * inv)) + OFF;
+        int64_t iz = static_cast<int64_t>(std::floor(p[2] * inv)) + OFF;
+        ix = std::max<int64_t>(0, std::min<int64_t>(ix, (1 << 21) - 1));
+        iy = std::max<int64_t>(0, std::min<int64_t>(iy, (1 << 21) - 1));
+        iz = std::max<int64_t>(0, std::min<int64_t>(iz, (1 << 21) - 1));
+        uint64_t key = expand_bits_filter(static_cast<uint64_t>(ix)) | (expand_bits_filter(static_cast<uint64_t>(iy)) << 1) |
+                       (expand_bits_filter(static_cast<uint64_t>(iz)) << 2);
+        uint64_t b = hk(key) & mask;
+        int64_t vi = -1;
+        while (buckets[b]) { if (vals[buckets[b] - 1].k == key) { vi = buckets[b] - 1; break; } b = (b + 1) & mask; }
+        if (vi < 0) {
+            vals.push_back({key, FilterAcc()});
+            vi = static_cast<int64_t>(vals.size() - 1);
+            buckets[b] = static_cast<uint32_t>(vi + 1);
+            if (vals.size() * 5 > buckets.size() * 4) {
+                buckets.assign(buckets.size() * 2, 0u); mask = buckets.size() - 1;
+                for (size_t j = 0; j < vals.size(); ++j) { uint64_t bb = hk(vals[j].k) & mask; while (buckets[bb]) bb = (bb + 1) & mask; buckets[bb] = static_cast<uint32_t>(j + 1); }
+            }
+        }
+        FilterAcc& a = vals[vi].a;
+        a.sx += p[0]; a.sy += p[1]; a.sz += p[2]; a.count++;
+    }
+    int c = 0;
+    for (auto& kv : vals) {
+        float ic = 1.0f / static_cast<float>(kv.a.count);
+        out[3 * c] = kv.a.sx * ic; out[3 * c + 1] = kv.a.sy * ic; out[3 * c + 2] = kv.a.sz * ic;
+        ++c;
+    }
+    return c;
+}
+
+void or_transform_points(const float* in, int n, const float T[12], float* out) {
+    SE3 s = se3_from12(T);
+    for (int i = 0; i < n; ++i) transform_pt(s, in + 3 * i, out + 3 * i);
+}
+
+int or_find_correspondences(void* map, const float* pts, int n, const float T[12], double maxd, uint8_t* valid, double* residual) {
+    Corr c;
+    return static_cast<int>(find_corr(*static_cast<VoxelMap*>(map), pts, n, se3_from12(T), maxd, c, valid, residual));
+}
+
+int or_find_correspondences_kdtree(void* map, const float* pts, int n, const float T[12], double maxd, uint8_t* valid,
+                                   double* residual, float* normal_out, float* target_out) {
+    Corr c;
+    return static_cast<int>(find_corr_kdtree(*static_cast<VoxelMap*>(map), pts, n, se3_from12(T), maxd, c, valid, residual,
+                                             normal_out, target_out));
+}
+
+int or_icp_optimize(void* map, const float* pts, int n, const float T_init[12], float T_out[12], const or_icp_cfg* cfg,
+                    int use_kdtree, or_iter_log* logs, int* iterations) {
+    return icp_optimize(*static_cast<VoxelMap*>(map), pts, n, T_init, T_out, *cfg, use_kdtree != 0, logs, iterations);
+}
+
+int or_build_normal_equations(void* map, const float* pts, int n, const float T[12], const or_icp_cfg* cfg, double scale,
+                              double delta, float H[36], float g[6], float* cost) {
+    Corr c;
+    SE3 s = se3_from12(T);
+    size_t nc = find_corr(*static_cast<VoxelMap*>(map), pts, n, s, cfg->max_correspondence_distance, c, nullptr, nullptr);
+    float Hm[6][6];
+    build_ne(c, s, *cfg, scale, delta, Hm, g, *cost);
+    for (int r = 0; r < 6; ++r) for (int q = 0; q < 6; ++q) H[r * 6 + q] = Hm[r][q];
+    return static_cast<int>(nc);
+}
+
+}  // extern "C"

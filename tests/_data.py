@@ -1,0 +1,87 @@
+"""Shared, cached synthetic parity inputs (test infrastructure).
+
+Maps are built with the ORACLE VoxelMap (the checker), then handed to both the oracle ICP and the HIP
+product through the same surfel arrays, so the two sides see identical map contents.
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+
+import oracle
+from lidar_odometry_amd import synth
+
+
+def pose12(T) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(T, dtype=np.float64)[:3, :].astype(np.float32).reshape(12))
+
+
+@functools.lru_cache(maxsize=None)
+def kitti_seq(n_frames: int = 40):
+    return synth.KittiLikeSequence(seed=7, n_frames=n_frames)
+
+
+@functools.lru_cache(maxsize=None)
+def kitti_scan(i: int, n_frames: int = 40):
+    return kitti_seq(n_frames).scan(i)
+
+
+@functools.lru_cache(maxsize=None)
+def kitti_map(last_kf: int = 20, n_frames: int = 40, voxel: float = 0.5, stride: int = 8):
+    """Oracle VoxelMap fed with keyframes 0, 2, ..., last_kf at ground-truth poses (kitti.yaml params)."""
+    seq = kitti_seq(n_frames)
+    m = oracle.VoxelMap(voxel, 3, 0.1, True)
+    for k in range(0, last_kf + 1, 2):
+        pts = oracle.voxel_filter(kitti_scan(k, n_frames), voxel, stride)
+        T = seq.poses[k]
+        m.update(synth.transform(T, pts), T[:3, 3], 120.0, True)
+    return m
+
+
+def kitti_case(frame: int, seed: int = 42, last_kf: int = 20, n_frames: int = 40, sigma_t=0.05, sigma_r=0.01):
+    """(map, filtered scan points, perturbed initial pose 12, ground-truth pose 12)."""
+    seq = kitti_seq(n_frames)
+    m = kitti_map(last_kf, n_frames)
+    pts = oracle.voxel_filter(kitti_scan(frame, n_frames), 0.5, 8)
+    rng = np.random.default_rng(seed + frame)
+    Ti = synth.perturb(seq.poses[frame], rng, sigma_t, sigma_r)
+    return m, pts, pose12(Ti), pose12(seq.poses[frame])
+
+
+@functools.lru_cache(maxsize=None)
+def mid360_case(frame: int = 3):
+    """MID360-like (C3): voxel 0.4 (L1 = fp32(0.4f*3)), stride 4, surfel correspondence forced on."""
+    sc = synth.mid360_scene()
+    m = oracle.VoxelMap(0.4, 3, 0.1, True)
+    poses = [synth.se3(synth.rot_z(0.05 * k), [0.3 * k, 0.1 * k, 1.0]) for k in range(8)]
+    for k in range(0, 6, 2):
+        p = oracle.voxel_filter(synth.mid360_like_scan(sc, poses[k], k), 0.4, 4)
+        m.update(synth.transform(poses[k], p), poses[k][:3, 3], 48.0, True)
+    pts = oracle.voxel_filter(synth.mid360_like_scan(sc, poses[frame], frame), 0.4, 4)
+    Ti = synth.perturb(poses[frame], np.random.default_rng(142 + frame))
+    return m, pts, pose12(Ti), pose12(poses[frame])
+
+
+@functools.lru_cache(maxsize=None)
+def patch_case(n_points: int = 1_000_000, seed: int = 1000):
+    """C5: 1M-point scan of 1000 planar patches + 10 % outliers; map from a second noisy sampling."""
+    sc = synth.patch_scene(1000, seed)
+    m = oracle.VoxelMap(0.5, 3, 0.1, True)
+    mp = synth.sample_patches(sc, 1_500_000, seed + 7, sigma=0.01, outlier_frac=0.0)
+    m.update(mp, np.zeros(3), 1e4, True)
+    T = synth.se3(synth.rot_z(0.3), [1.0, -2.0, 0.5])
+    world = synth.sample_patches(sc, n_points, seed + 11)
+    local = synth.transform(np.linalg.inv(T), world)
+    Ti = synth.perturb(T, np.random.default_rng(seed), 0.05, 0.01)
+    return m, local, pose12(Ti), pose12(T)
+
+
+def surfels(m):
+    k, n, c, _ = m.surfels()
+    return k, n, c
+
+
+def rot_angle(Ra, Rb) -> float:
+    Rd = np.asarray(Ra, np.float64).T @ np.asarray(Rb, np.float64)
+    return float(np.arccos(np.clip((np.trace(Rd) - 1) / 2, -1.0, 1.0)))

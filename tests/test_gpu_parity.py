@@ -1,0 +1,218 @@
+"""GPU parity tests: the HIP product (through the C ABI) against the CPU oracle on identical inputs.
+
+Bars (BASELINE.json north_star):
+  * correspondences at a given pose: identical valid set and bit-identical fp64 residuals;
+  * PKO alpha: identical to the reference golden vectors (GMM parameters within 1e-9 relative);
+  * normal equations: |dH|/|H| <= 1e-5 (fp32 sequential sum in the reference vs fixed-order tree here);
+  * optimize: per executed GN iteration pose within 1e-4 m / 1e-4 rad, same iteration count.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+
+TOL_T = 1e-4      # m   (north_star)
+TOL_R = 1e-4      # rad
+
+
+@pytest.fixture(scope="module")
+def icp():
+    from lidar_odometry_amd import IterativeClosestPointOptimizer
+    o = IterativeClosestPointOptimizer(max_points=1 << 20)
+    yield o
+    o.close()
+
+
+def _load_map(icp, m):
+    k, n, c = _data.surfels(m)
+    icp.set_surfels(k, n, c)
+
+
+def _pose_err(Ta, Tb):
+    A = np.asarray(Ta, np.float64).reshape(3, 4)
+    B = np.asarray(Tb, np.float64).reshape(3, 4)
+    return float(np.linalg.norm(A[:, 3] - B[:, 3])), _data.rot_angle(A[:, :3], B[:, :3])
+
+
+# ------------------------------------------------------------------------------------------- K1
+@pytest.mark.parametrize("frame", [11, 17, 25])
+def test_correspondences_bitwise(icp, frame):
+    m, pts, Ti, _ = _data.kitti_case(frame)
+    _load_map(icp, m)
+    for T in (Ti, _data.kitti_case(frame, seed=7)[2]):
+        n_o, v_o, r_o = oracle.find_correspondences(m, pts, T)
+        n_g, v_g, r_g = icp.find_correspondences(pts, T)
+        assert n_g == n_o
+        np.testing.assert_array_equal(v_g, v_o)
+        np.testing.assert_array_equal(r_g.view(np.uint64), r_o.view(np.uint64))
+
+
+def test_correspondences_mid360_voxel04(icp):
+    m, pts, Ti, _ = _data.mid360_case()
+    from lidar_odometry_amd import IterativeClosestPointOptimizer, MapGeometry
+    o = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=0.4), max_points=1 << 16)
+    try:
+        k, n, c = _data.surfels(m)
+        o.set_surfels(k, n, c)
+        n_o, v_o, r_o = oracle.find_correspondences(m, pts, Ti)
+        n_g, v_g, r_g = o.find_correspondences(pts, Ti)
+        assert n_g == n_o > 0
+        np.testing.assert_array_equal(v_g, v_o)
+        np.testing.assert_array_equal(r_g, r_o)
+    finally:
+        o.close()
+
+
+def test_correspondences_edge_cases(icp):
+    m, pts, Ti, _ = _data.kitti_case(11)
+    _load_map(icp, m)
+    bad = pts[:300].copy()
+    bad[0] = [np.nan, 0, 0]
+    bad[1] = [np.inf, 1, 1]
+    bad[2] = [1e9, 1e9, 1e9]          # key outside +-2^20 -> miss
+    n_o, v_o, r_o = oracle.find_correspondences(m, bad[3:], Ti)
+    n_g, v_g, r_g = icp.find_correspondences(bad, Ti)
+    assert not v_g[:3].any()
+    np.testing.assert_array_equal(v_g[3:], v_o)
+    # single point, ragged sizes around block boundaries
+    for n in (1, 63, 64, 65, 255, 256, 257, 1023):
+        sub = pts[:n]
+        n_o, v_o, r_o = oracle.find_correspondences(m, sub, Ti)
+        n_g, v_g, r_g = icp.find_correspondences(sub, Ti)
+        assert n_g == n_o
+        np.testing.assert_array_equal(v_g, v_o)
+        np.testing.assert_array_equal(r_g, r_o)
+
+
+# ------------------------------------------------------------------------------------------- PKO
+def _golden():
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    z = np.load(os.path.join(g, "pko_inputs.npz"))
+    out = []
+    with open(os.path.join(g, "pko_golden.jsonl")) as f:
+        for line in f:
+            d = json.loads(line)
+            out.append((d, z[f"case_{d['case']}"]))
+    return out
+
+
+def test_pko_alpha_matches_reference_golden(icp):
+    mism = []
+    for d, r in _golden():
+        a, gmm = icp.pko_scale_factor(r)
+        if a != d["alpha"]:
+            mism.append((d["case"], d["n"], a, d["alpha"]))
+            continue
+        for k in ("w", "mu", "var"):
+            ref = np.array(d[k], np.float64)
+            np.testing.assert_allclose(gmm[k], ref, rtol=1e-9, atol=1e-12, equal_nan=True, err_msg=f"case {d['case']} {k}")
+    assert not mism, f"alpha mismatches: {mism}"
+
+
+def test_pko_sample_indices_device_tables(icp):
+    for n in (1, 5, 99, 100, 101, 4000, 65535, 65536, 100001):
+        np.testing.assert_array_equal(icp.pko_sample_indices(n), oracle.shuffle_prefix(n, 100))
+
+
+# ------------------------------------------------------------------------------------------- K3
+@pytest.mark.parametrize("frame", [11, 25])
+def test_normal_equations(icp, frame):
+    m, pts, Ti, _ = _data.kitti_case(frame)
+    _load_map(icp, m)
+    for scale, delta in ((0.01, 0.5), (0.004, 3.0), (0.02, 10.0)):
+        n_o, H_o, g_o, c_o = oracle.build_normal_equations(m, pts, Ti, scale, delta)
+        n_g, H_g, g_g, c_g = icp.build_normal_equations(pts, Ti, scale, delta)
+        assert n_g == n_o
+        H_o = 0.5 * (H_o + H_o.T).astype(np.float64)     # reference H is symmetric up to fp32 rounding
+        assert np.linalg.norm(H_g - H_o) / np.linalg.norm(H_o) <= 1e-5
+        assert np.linalg.norm(g_g - g_o) / max(np.linalg.norm(g_o), 1e-12) <= 1e-4
+        assert abs(c_g - c_o) / max(abs(c_o), 1e-12) <= 1e-4
+
+
+# ------------------------------------------------------------------------------------------- optimize
+def _compare_optimize(icp, m, pts, Ti, tol_t=TOL_T, tol_r=TOL_R):
+    ok_o, To_o, it_o, logs_o = oracle.icp_optimize(m, pts, Ti)
+    ok_g, To_g = icp.optimize(None, pts, Ti)
+    st = icp.get_last_stats()
+    assert ok_g == ok_o
+    assert st.num_iterations == it_o, f"iteration count {st.num_iterations} vs oracle {it_o}"
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        assert lg["n_corr"] == lo["n_corr"], f"iter {k}: n_corr {lg['n_corr']} vs {lo['n_corr']}"
+        assert lg["alpha"] == lo["alpha"], f"iter {k}: alpha {lg['alpha']} vs {lo['alpha']}"
+        et, er = _pose_err(lg["pose"], lo["pose"])
+        assert et <= tol_t and er <= tol_r, f"iter {k}: dt {et:.2e} m, dr {er:.2e} rad"
+    et, er = _pose_err(To_g, To_o)
+    assert et <= tol_t and er <= tol_r
+    return st
+
+
+@pytest.mark.parametrize("frame", [11, 13, 17, 21, 25, 31])
+def test_optimize_kitti_like_per_iteration(icp, frame):
+    m, pts, Ti, Tgt = _data.kitti_case(frame)
+    _load_map(icp, m)
+    _compare_optimize(icp, m, pts, Ti)
+
+
+def test_optimize_large_perturbation(icp):
+    m, pts, Ti, Tgt = _data.kitti_case(15, seed=5, sigma_t=0.3, sigma_r=0.03)
+    _load_map(icp, m)
+    _compare_optimize(icp, m, pts, Ti)
+
+
+def test_optimize_mid360_like():
+    from lidar_odometry_amd import IterativeClosestPointOptimizer, MapGeometry
+    m, pts, Ti, _ = _data.mid360_case()
+    o = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=0.4), max_points=1 << 16)
+    try:
+        k, n, c = _data.surfels(m)
+        o.set_surfels(k, n, c)
+        _compare_optimize(o, m, pts, Ti)
+    finally:
+        o.close()
+
+
+def test_optimize_insufficient_correspondences(icp):
+    m, pts, Ti, _ = _data.kitti_case(11)
+    _load_map(icp, m)
+    far = pts + np.float32(5000.0)        # nothing maps onto a surfel
+    ok, To = icp.optimize(None, far, Ti)
+    assert not ok
+    np.testing.assert_array_equal(To.reshape(12), Ti)
+    ok, To = icp.optimize(None, pts[:0], Ti)   # empty cloud
+    assert not ok
+    ok_o, _, it_o, _ = oracle.icp_optimize(m, far, Ti)
+    assert not ok_o
+
+
+def test_optimize_empty_map():
+    from lidar_odometry_amd import IterativeClosestPointOptimizer
+    o = IterativeClosestPointOptimizer(max_points=4096)
+    try:
+        pts = np.random.default_rng(0).normal(size=(500, 3)).astype(np.float32)
+        ok, To = o.optimize(None, pts, np.eye(3, 4, dtype=np.float32))
+        assert not ok
+    finally:
+        o.close()
+
+
+def test_optimize_repeatable(icp):
+    m, pts, Ti, _ = _data.kitti_case(21)
+    _load_map(icp, m)
+    _, A = icp.optimize(None, pts, Ti)
+    _, B = icp.optimize(None, pts, Ti)
+    np.testing.assert_array_equal(A, B)     # fixed-order reductions: bitwise run-to-run
+
+
+@pytest.mark.slow
+def test_optimize_1m_point_scan(icp):
+    """C5 size: 1M-point scan.  Oracle run once (~seconds); poses per iteration within tolerance."""
+    m, pts, Ti, Tgt = _data.patch_case()
+    _load_map(icp, m)
+    st = _compare_optimize(icp, m, pts, Ti)
+    assert st.iterations[0]["n_corr"] > 500_000

@@ -1,0 +1,135 @@
+"""CPU tests: the oracle against the reference's own golden vectors and against known-answer properties."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _golden():
+    z = np.load(os.path.join(GOLD, "pko_inputs.npz"))
+    with open(os.path.join(GOLD, "pko_golden.jsonl")) as f:
+        for line in f:
+            d = json.loads(line)
+            yield d, z[f"case_{d['case']}"]
+
+
+@pytest.mark.parametrize("case", list(range(26)))
+def test_pko_matches_reference_golden_bitwise(case):
+    d, r = [x for x in _golden()][case]
+    assert len(r) == d["n"]
+    a, g = oracle.pko_scale_factor(r)
+    assert a == d["alpha"]
+    for k in ("w", "mu", "var"):
+        np.testing.assert_array_equal(g[k], np.array(d[k], dtype=np.float64))
+
+
+def test_pko_tables_match_reference():
+    d, _ = next(iter(_golden()))
+    a, z = oracle.pko_tables()
+    np.testing.assert_array_equal(a, np.array(d["alphas"]))
+    np.testing.assert_array_equal(z, np.array(d["Z"]))
+
+
+def test_shuffle_prefix_matches_reference():
+    for d, r in _golden():
+        np.testing.assert_array_equal(oracle.shuffle_prefix(len(r), 100), np.array(d["perm"], dtype=np.int32))
+        if d["n"] > 0:
+            np.testing.assert_array_equal(oracle.kmeans_seed_draws(min(100, d["n"])), np.array(d["kmeans_draws"], dtype=np.int32))
+
+
+def test_jacobi_svd_reconstructs_and_sorts():
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        A = rng.normal(size=(3, 3)).astype(np.float32)
+        A = (A @ A.T).astype(np.float32)          # covariance-like (symmetric PSD)
+        rc, U, S, V = oracle.jacobi_svd3(A)
+        assert rc == 0
+        assert S[0] >= S[1] >= S[2] >= 0
+        np.testing.assert_allclose(U @ np.diag(S) @ V.T, A, atol=2e-5 * np.abs(A).max())
+        np.testing.assert_allclose(U.T @ U, np.eye(3), atol=2e-6)
+
+
+def test_jacobi_svd_degenerate():
+    rc, U, S, V = oracle.jacobi_svd3(np.zeros((3, 3), np.float32))
+    assert rc == 0 and np.all(S == 0)
+    np.testing.assert_array_equal(U, np.eye(3, dtype=np.float32))
+    rc, U, S, V = oracle.jacobi_svd3(np.diag([1.0, 4.0, 2.0]).astype(np.float32))
+    np.testing.assert_array_equal(S, np.array([4, 2, 1], np.float32))
+
+
+def test_so3_exp_matches_rodrigues():
+    rng = np.random.default_rng(1)
+    for _ in range(100):
+        w = rng.normal(0, 0.3, 3).astype(np.float32)
+        R = oracle.so3_exp(w)
+        th = np.linalg.norm(w.astype(np.float64))
+        k = w / th
+        K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        Rr = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        np.testing.assert_allclose(R, Rr, atol=1e-6)
+        np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-6)
+    assert np.array_equal(oracle.so3_normalize(np.eye(3)), np.eye(3, dtype=np.float32))
+
+
+def test_ldlt_solve():
+    rng = np.random.default_rng(2)
+    for _ in range(50):
+        J = rng.normal(size=(200, 6))
+        H = (J.T @ J).astype(np.float32)
+        b = rng.normal(size=6).astype(np.float32)
+        x = oracle.ldlt6_solve(H, b)
+        np.testing.assert_allclose(H.astype(np.float64) @ x, b, rtol=1e-3, atol=1e-3)
+    # zero matrix -> zero solution (pivot handling of LDLT::compute / _solve_impl)
+    np.testing.assert_array_equal(oracle.ldlt6_solve(np.zeros((6, 6), np.float32), np.ones(6, np.float32)), np.zeros(6))
+
+
+def test_voxel_filter_first_occurrence_order():
+    pts = np.array([[0.1, 0.1, 0.1], [5, 5, 5], [0.2, 0.2, 0.2], [np.nan, 0, 0], [5.1, 5.1, 5.1]], np.float32)
+    out = oracle.voxel_filter(pts, 0.5, 1)
+    assert out.shape == (2, 3)
+    s = np.float32(0.1) + np.float32(0.2)
+    np.testing.assert_array_equal(out[0], np.float32(s) * (np.float32(1.0) / np.float32(2.0)))
+    out2 = oracle.voxel_filter(pts, 0.5, 2)     # stride picks 0, 2, 4
+    assert out2.shape == (2, 3)
+
+
+def test_voxelmap_surfels_and_lookup():
+    rng = np.random.default_rng(3)
+    # a dense horizontal plane z=0.2 over [0,6]^2 -> planar L1 voxels with normal +-z
+    xy = rng.uniform(0, 6, (20000, 2))
+    pts = np.concatenate([xy, np.full((20000, 1), 0.2)], axis=1).astype(np.float32)
+    m = oracle.VoxelMap(0.5, 3, 0.1, True)
+    m.update(pts, np.zeros(3), 100.0, True)
+    k, n, c, pl = m.surfels()
+    assert len(k) >= 9
+    assert np.all(np.abs(np.abs(n[:, 2]) - 1) < 1e-5)
+    ok, nn, cc = m.lookup(np.array([1.0, 1.0, 0.3], np.float32))
+    assert ok and abs(cc[2] - 0.2) < 1e-5
+    ok, _, _ = m.lookup(np.array([1.0, 1.0, 5.0], np.float32))
+    assert not ok
+    # radius pruning removes everything far from a distant sensor
+    m.update(pts[:10], np.array([1000.0, 0, 0]), 10.0, True)
+    assert m.l0_count() <= 10
+
+
+def test_oracle_icp_converges_on_kitti_like():
+    from tests import _data
+    m, pts, Ti, Tgt = _data.kitti_case(11)
+    ok, To, iters, logs = oracle.icp_optimize(m, pts, Ti)
+    assert ok and 1 <= iters <= 4
+    assert np.linalg.norm(To.reshape(3, 4)[:, 3] - Tgt.reshape(3, 4)[:, 3]) < 0.02
+    assert logs[0]["n_corr"] > 1000
+
+
+def test_oracle_icp_insufficient_on_empty_map():
+    m = oracle.VoxelMap(0.5, 3, 0.1, True)
+    pts = np.random.default_rng(0).normal(size=(100, 3)).astype(np.float32)
+    Ti = np.eye(3, 4, dtype=np.float32).reshape(12)
+    ok, To, iters, logs = oracle.icp_optimize(m, pts, Ti)
+    assert not ok and iters == 0
+    np.testing.assert_array_equal(To, Ti)
