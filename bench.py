@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""Benchmark: scan-to-map point-to-plane ICP (GN to convergence) on MI355X.
+
+One *step* = one scan's IterativeClosestPointOptimizer::optimize (<= max_iterations GN iterations with PKO)
+per GPU, against a frozen device-resident surfel map, scan points already resident in HBM.
+Multi-GPU is scan-parallel (weak scaling): every rank owns its own map and scan stream; after each step the
+ranks all-gather their 16-float pose/status records over RCCL (the only collective; no map sharding).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config kitti|mid360|patch1m]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (driver contract).  The CPU baseline is the oracle restatement of the
+reference ICP (single thread) timed on a bounded sample of the same scans.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "ICP GN-iterations/sec and scans/sec on KITTI-07 @ 1/2/4/8 GPU; % HBM BW"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# --------------------------------------------------------------------------------------------------
+# workloads (product-side data path only: synth + lo_voxelmap + lo_voxel_filter)
+# --------------------------------------------------------------------------------------------------
+def build_kitti(rank: int):
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    kf = []
+    for k in range(0, 41, 2):                       # keyframes ~1.2 m apart (kitti.yaml keyframe_distance 1.0)
+        pts = voxel_filter(seq.scan(k), 0.5, 8)     # FastVoxelFilter, point_stride 8, voxel 0.5
+        T = seq.poses[k]
+        w = synth.transform(T, pts)
+        vm.update(w, T[:3, 3], 120.0, True)         # UpdateVoxelMap(.., 1.2 * max_range)
+        kf.append((w, T[:3, 3].copy()))
+    rng = np.random.default_rng(42 + rank)
+    scans, inits, gts = [], [], []
+    for f in range(1, 40, 2):                       # the frames between keyframes
+        scans.append(voxel_filter(seq.scan(f), 0.5, 8))
+        inits.append(synth.perturb(seq.poses[f], rng, 0.05, 0.01))
+        gts.append(seq.poses[f])
+    return {"name": "KITTI-07-like HDL-64 scan (stride 8, 0.5 m voxels) surfel ICP, config/kitti.yaml",
+            "voxel": 0.5, "max_dist": 120.0, "vm": vm, "scans": scans, "inits": inits, "gts": gts, "keyframes": kf}
+
+
+def build_mid360(rank: int):
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    sc = synth.mid360_scene()
+    poses = [synth.se3(synth.rot_z(0.05 * k), [0.3 * k, 0.1 * k, 1.0]) for k in range(42)]
+    vm = VoxelMap(0.4, 3, 0.1, True)
+    kf = []
+    for k in range(0, 41, 2):
+        p = voxel_filter(synth.mid360_like_scan(sc, poses[k], k), 0.4, 4)
+        w = synth.transform(poses[k], p)
+        vm.update(w, poses[k][:3, 3], 48.0, True)
+        kf.append((w, poses[k][:3, 3].copy()))
+    rng = np.random.default_rng(142 + rank)
+    scans, inits, gts = [], [], []
+    for f in range(1, 40, 2):
+        scans.append(voxel_filter(synth.mid360_like_scan(sc, poses[f], f), 0.4, 4))
+        inits.append(synth.perturb(poses[f], rng, 0.05, 0.01))
+        gts.append(poses[f])
+    return {"name": "MID360-like rosette scan (stride 4, 0.4 m voxels) surfel ICP, config/mid360.yaml (surfel forced)",
+            "voxel": 0.4, "max_dist": 48.0, "vm": vm, "scans": scans, "inits": inits, "gts": gts, "keyframes": kf}
+
+
+def build_patch1m(rank: int):
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.voxelmap import VoxelMap
+    sc = synth.patch_scene(1000, 1000 + rank)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    mp = synth.sample_patches(sc, 1_500_000, 1007 + rank, sigma=0.01, outlier_frac=0.0)
+    vm.update(mp, np.zeros(3), 1e4, True)
+    rng = np.random.default_rng(1000 + rank)
+    scans, inits, gts = [], [], []
+    for f in range(4):
+        T = synth.se3(synth.rot_z(0.3 + 0.1 * f), [1.0 + f, -2.0, 0.5])
+        world = synth.sample_patches(sc, 1_000_000, 1011 + 10 * f + rank)
+        scans.append(synth.transform(np.linalg.inv(T), world))
+        inits.append(synth.perturb(T, rng, 0.05, 0.01))
+        gts.append(T)
+    return {"name": "synthetic 1M-pt scan, 1000 planar patches + 10% outliers, surfel ICP",
+            "voxel": 0.5, "max_dist": 1e4, "vm": vm, "scans": scans, "inits": inits, "gts": gts,
+            "keyframes": [(mp, np.zeros(3))]}
+
+
+WORKLOADS = {"kitti": build_kitti, "mid360": build_mid360, "patch1m": build_patch1m}
+
+
+def pose12(T):
+    return np.ascontiguousarray(np.asarray(T, np.float64)[:3, :].astype(np.float32).reshape(12))
+
+
+# --------------------------------------------------------------------------------------------------
+# CPU baseline: oracle restatement of the reference ICP, 1 thread, bounded sample
+# --------------------------------------------------------------------------------------------------
+def cpu_baseline(wl, budget_s: float):
+    import oracle
+    m = oracle.VoxelMap(wl["voxel"], 3, 0.1, True)
+    for w, s in wl["keyframes"]:
+        m.update(w, s, wl["max_dist"], True)
+    scans, inits = wl["scans"], [pose12(T) for T in wl["inits"]]
+    n_scans = n_iters = 0
+    t0 = time.perf_counter()
+    while True:
+        i = n_scans % len(scans)
+        ok, To, it, _ = oracle.icp_optimize(m, scans[i], inits[i])
+        n_scans += 1
+        n_iters += it
+        el = time.perf_counter() - t0
+        if el >= budget_s and n_scans >= len(scans):
+            break
+    return {"value": n_scans / el, "unit": "scans/s", "cores": 1, "kind": "port",
+            "gn_iters_per_sec": n_iters / el,
+            "sample": f"{n_scans} optimize() calls over {len(scans)} distinct scans in {el:.1f} s "
+                      f"(oracle/liblo_oracle.so, single thread, g++ -O3, same synthetic inputs)"}
+
+
+def read_pmc_traffic(workload_key: str):
+    """HBM bytes per k_correspond launch from a committed rocprofv3 PMC summary (profiles/), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(workload_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+# --------------------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from lidar_odometry_amd import lib
+    from lidar_odometry_amd.icp import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
+
+    t_data = time.perf_counter()
+    wl = WORKLOADS[args.config](rank)
+    log(f"[rank {rank}] data built in {time.perf_counter() - t_data:.1f} s: {len(wl['scans'])} scans, "
+        f"avg {np.mean([len(s) for s in wl['scans']]):.0f} pts, {wl['vm'].surfel_count()} surfels")
+    max_pts = max(len(s) for s in wl["scans"])
+    icp = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
+                                         device=local, max_points=max_pts)
+    L = lib()
+    stream = torch.cuda.current_stream(dev)
+    L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
+    rc = L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle)
+    assert rc == 0, rc
+    d_scans = [torch.from_numpy(s).to(dev) for s in wl["scans"]]
+    inits = [pose12(T) for T in wl["inits"]]
+    fptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))   # noqa: E731
+    pose_rec = torch.zeros(16, dtype=torch.float32, device=dev)
+    gathered = torch.zeros(16 * world, dtype=torch.float32, device=dev)
+
+    def step(k):
+        i = k % len(d_scans)
+        rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]))
+        if rc != 0:
+            raise RuntimeError(f"lo_icp_optimize_async rc={rc}: {L.lo_last_error(icp.ctx).decode()}")
+        if world > 1:
+            L.lo_icp_export_pose(icp.ctx, C.c_void_p(pose_rec.data_ptr()))
+            dist.all_gather_into_tensor(gathered, pose_rec)
+
+    # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them)
+    iters, errs = [], []
+    for i in range(len(d_scans)):
+        ok, To = icp.optimize(None, wl["scans"][i], inits[i])
+        st = icp.get_last_stats()
+        iters.append(st.num_iterations)
+        errs.append(float(np.linalg.norm(To[:, 3] - wl["gts"][i][:3, 3])))
+    L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_scans = args.steps * world
+    total_iters = sum(iters[k % len(iters)] for k in range(args.steps)) * world
+
+    # live per-kernel device times (HIP events around back-to-back launches on this context's stream)
+    i0 = int(np.argmax([len(s) for s in wl["scans"]]))
+    kern_us = {}
+    for kid, name in enumerate(("k_correspond", "k_accumulate", "k_pko", "k_solve")):
+        ms = C.c_float(0.0)
+        reps = 200 if kid != 2 else 50
+        rc = L.lo_bench_kernel(icp.ctx, C.c_void_p(d_scans[i0].data_ptr()), d_scans[i0].shape[0], fptr(inits[i0]),
+                               C.c_double(0.01), C.c_double(1.0), kid, reps, C.byref(ms))
+        assert rc == 0, rc
+        kern_us[name] = ms.value * 1e3
+    n0 = d_scans[i0].shape[0]
+    n_valid, valid, _ = icp.find_correspondences(wl["scans"][i0], inits[i0])
+    v = n_valid / n0
+    # algorithmic bytes per k_correspond launch: per point 12 B point + 8 B key probe + 24 B payload on a hit
+    # (lower-bounded by the accepted fraction v) + 4 B slot index written + 1/8 B validity ballot
+    alg_bytes = n0 * (12 + 8 + 24 * v + 4 + 0.125)
+    t_corr = kern_us["k_correspond"] * 1e-6
+    achieved = alg_bytes / t_corr / 1e9
+    traffic = read_pmc_traffic(args.config)
+
+    result = {
+        "metric": METRIC,
+        "value": total_scans / el,
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (pose, J, H) + f64 (residuals, PKO)",
+        "data": "synthetic (deterministic raycast scenes; no dataset reachable offline)",
+        "config": {"workload": wl["name"], "points_per_scan_avg": float(np.mean([len(s) for s in wl["scans"]])),
+                   "distinct_scans": len(wl["scans"]), "map_surfels": wl["vm"].surfel_count(),
+                   "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),
+                   "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step)" if world > 1
+                   else "single GPU, one HIP stream"},
+        "gn_iters_per_sec": total_iters / el,
+        "translation_error_vs_gt_m_median": float(np.median(errs)),
+        "kernel_us": kern_us,
+        "roofline": {"kernel": "k_correspond", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes, "points_per_launch": int(n0), "valid_fraction": v},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
+        result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
+    icp.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -55,7 +55,7 @@ typedef struct lo_config {
     double max_scale_factor;             /* 10.0 */
     int    num_alpha_segments;           /* 100 */
     double truncated_threshold;          /* 10.0 */
-    int    gmm_components;               /* 3 (1..4 supported) */
+    int    gmm_components;               /* 3 (1..3 supported) */
     int    gmm_sample_size;              /* 100 (1..256 supported) */
     int    pko_kernel_cauchy;            /* 0: "huber" (kitti.yaml:51) */
     float  voxel_size;                   /* map_voxel_size 0.5 */
@@ -115,6 +115,15 @@ int lo_icp_optimize_async(lo_ctx* ctx, const float* d_pts, size_t n, const float
 int lo_icp_result(lo_ctx* ctx, float T_out[12], lo_iter_log* logs, lo_stats* stats);
 int lo_sync(lo_ctx* ctx);
 void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
+/* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again. */
+int lo_set_stream(lo_ctx* ctx, void* hip_stream);
+/* Enqueue a copy of the current GN state into device memory: 16 floats = pose[12], status, iterations,
+ * n_corr, 0.  For the scan-parallel pose gather (RCCL all-gather of these 16 floats per rank). */
+int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);
+/* Timing harness: reps back-to-back launches of one kernel (0 correspond, 1 accumulate, 2 pko, 3 solve)
+ * on a device-resident scan at pose T; writes the average device time per launch (HIP events). */
+int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
+                    int kernel_id, int reps, float* avg_ms);
 
 /* ---- single-stage entry points (parity harness; each synchronous) ---- */
 /* find_correspondences (IterativeClosestPointOptimizer.cpp:587-645) at pose T:
@@ -131,6 +140,8 @@ int lo_build_normal_equations(lo_ctx* ctx, const float* pts_xyz, size_t n, const
 /* PKO sampling: first min(gmm_sample_size, n) entries of std::shuffle(iota(n), mt19937(42))
  * as the device tables reproduce them (AdaptiveMEstimator.cpp:319-328). Host-side. */
 int lo_pko_sample_indices(lo_ctx* ctx, size_t n, int32_t* out);
+/* Diagnostic: 16 device counters (phase timestamps of the -DLO_PKO_STAMPS build; zeros otherwise). */
+int lo_debug_counters(lo_ctx* ctx, unsigned long long out[16]);
 /* Context-free host variant (no GPU needed): sample_size = gmm_sample_size. */
 int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out);
 

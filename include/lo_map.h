@@ -1,0 +1,48 @@
+/*
+ * lo_map.h — map-side C ABI: the 2-level voxel/surfel map that feeds the ICP's surfel table, and the
+ * scan downsampler that feeds its point cloud.  Host C++ (host form).
+ *
+ *   lo_voxelmap_*   replaces map::VoxelMap's build side: UpdateVoxelMap (src/database/VoxelMap.cpp:128-262),
+ *                   AddPoint (:99-120), surfel PCA + planarity erase (:187-261), GetPointCloud (:388-403).
+ *   lo_voxel_filter replaces map::FastVoxelFilter::filter (src/database/VoxelMap.h:73-104).
+ *
+ * Results are bit-identical to the reference's fp32 arithmetic (insertion-ordered containers with
+ * unordered_dense's swap-with-last erase, Eigen JacobiSVD<Matrix3f> restated), checked against the oracle.
+ */
+#ifndef LO_MAP_H
+#define LO_MAP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lo_icp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lo_voxelmap lo_voxelmap;
+
+lo_voxelmap* lo_voxelmap_create(float voxel_size, int hierarchy_factor, float planarity_threshold, int compute_surfels);
+void         lo_voxelmap_destroy(lo_voxelmap* m);
+/* UpdateVoxelMap(new_cloud (world frame), sensor_position, max_distance, is_keyframe) */
+int          lo_voxelmap_update(lo_voxelmap* m, const float* world_xyz, size_t n, const double sensor[3],
+                                double max_distance, int is_keyframe);
+size_t       lo_voxelmap_l0_count(const lo_voxelmap* m);
+size_t       lo_voxelmap_l1_count(const lo_voxelmap* m);
+size_t       lo_voxelmap_surfel_count(const lo_voxelmap* m);
+/* L1 voxels with has_surfel, in L1 iteration order. Returns the number written. */
+size_t       lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys_xyz, float* normals, float* centroids,
+                                     float* planarity, size_t cap);
+/* GetPointCloud: L0 centroids in L0 iteration order. */
+size_t       lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap);
+/* Upload the map's surfels to an ICP context (lo_map_set_surfels). */
+int          lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m);
+
+/* FastVoxelFilter::filter(input, output, stride): returns the number of output points (<= n). */
+size_t       lo_voxel_filter(const float* in_xyz, size_t n, float voxel_size, int stride, float* out_xyz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LO_MAP_H */

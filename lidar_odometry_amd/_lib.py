@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblo_icp.so")
+LIB_PATH = os.environ.get("LO_ICP_LIB") or os.path.join(_HERE, "liblo_icp.so")
 
 LO_OK = 0
 LO_INSUFFICIENT = 1
@@ -23,8 +23,12 @@ LO_MAX_ITERS = 64
 EXPORTED_SYMBOLS = (
     "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
     "lo_device", "lo_map_set_surfels", "lo_map_surfel_count", "lo_icp_optimize", "lo_icp_optimize_async",
-    "lo_icp_result", "lo_sync", "lo_stream", "lo_find_correspondences", "lo_pko_scale_factor",
-    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host",
+    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
+    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
+    # include/lo_map.h
+    "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
+    "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
+    "lo_map_set_from_voxelmap", "lo_voxel_filter",
 )
 
 
@@ -81,11 +85,29 @@ def lib():
     L.lo_sync.argtypes = [vp]
     L.lo_stream.restype = vp
     L.lo_stream.argtypes = [vp]
+    L.lo_set_stream.argtypes = [vp, vp]
+    L.lo_icp_export_pose.argtypes = [vp, vp]
+    L.lo_bench_kernel.argtypes = [vp, vp, C.c_size_t, fp, C.c_double, C.c_double, C.c_int, C.c_int, fp]
     L.lo_find_correspondences.argtypes = [vp, fp, C.c_size_t, fp, u8p, dp]
     L.lo_pko_scale_factor.restype = C.c_double
     L.lo_pko_scale_factor.argtypes = [vp, dp, C.c_size_t, dp]
     L.lo_build_normal_equations.argtypes = [vp, fp, C.c_size_t, fp, C.c_double, C.c_double, dp, dp, dp]
     L.lo_pko_sample_indices.argtypes = [vp, C.c_size_t, ip]
     L.lo_pko_sample_indices_host.argtypes = [C.c_size_t, C.c_int, ip]
+    L.lo_debug_counters.argtypes = [vp, C.POINTER(C.c_ulonglong)]
+    L.lo_voxelmap_create.restype = vp
+    L.lo_voxelmap_create.argtypes = [C.c_float, C.c_int, C.c_float, C.c_int]
+    L.lo_voxelmap_destroy.argtypes = [vp]
+    L.lo_voxelmap_update.argtypes = [vp, fp, C.c_size_t, dp, C.c_double, C.c_int]
+    for f in ("lo_voxelmap_l0_count", "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count"):
+        getattr(L, f).restype = C.c_size_t
+        getattr(L, f).argtypes = [vp]
+    L.lo_voxelmap_get_surfels.restype = C.c_size_t
+    L.lo_voxelmap_get_surfels.argtypes = [vp, ip, fp, fp, fp, C.c_size_t]
+    L.lo_voxelmap_get_l0.restype = C.c_size_t
+    L.lo_voxelmap_get_l0.argtypes = [vp, fp, C.c_size_t]
+    L.lo_map_set_from_voxelmap.argtypes = [vp, vp]
+    L.lo_voxel_filter.restype = C.c_size_t
+    L.lo_voxel_filter.argtypes = [fp, C.c_size_t, C.c_float, C.c_int, fp]
     _lib = L
     return L

@@ -23,7 +23,9 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kNE = 28;              // 21 lower-triangular H + 6 g + cost
-constexpr int kPkoThreads = 1024;
+constexpr int kPkoBlock = 256;       // PKO workgroup: one GMM sample per thread (S <= 256)
+constexpr int kPkoMaxWGs = 64;       // PKO workgroups per launch (each evaluates a slice of the alpha grid)
+constexpr int kPkoAlphaPerWG = 4;    // alphas per JS pass of one workgroup
 constexpr int kMaxBlocks = 16384;    // => max 4M points per scan
 constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
@@ -48,6 +50,7 @@ struct DevState {
     double g_out[6];
     double cost_out;
     double gmm_out[3 * kMaxK];
+    unsigned long long dbg[16];     // diagnostic build only (-DLO_PKO_STAMPS): phase timestamps / counters
     lo_iter_log logs[LO_MAX_ITERS];
 };
 
@@ -68,6 +71,7 @@ struct KParams {
     double robust_delta;
     int cauchy_loss;
     int use_pko;
+    int alpha_given;          // 1: take the Huber delta from DevState::alpha (normal-equation entry point)
     // PKO config + tables
     int S, K, NA, pko_cauchy;
     double min_scale, trunc;
@@ -86,6 +90,7 @@ struct KParams {
     double* blk_sum;
     double* blk_m2;
     double* blk_part;
+    double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     DevState* st;
@@ -157,6 +162,90 @@ __device__ __forceinline__ double residual_f64(const Slot& s, float wx, float wy
     const double e1 = static_cast<double>(s.n[1]) * d1;
     const double e2 = static_cast<double>(s.n[2]) * d2;
     return fabs((e0 + e1) + e2);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Wave-wide sums with DPP (quad_perm, row_half_mirror, row_mirror, row_bcast:15/31): 6 VALU steps and
+// no LDS round trip (a __shfl_xor is a ds_bpermute through the LDS crossbar).  All 64 lanes must be
+// active.  The total ends in lane 63 and is broadcast with v_readlane.
+// ---------------------------------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u)));
+    const int hi = dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u >> 32)));
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+}
+
+__device__ __forceinline__ double wave_total(double v) {
+    v += dpp64<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+    v += dpp64<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+    v += dpp64<0x141, 0xf>(v);   // row_half_mirror
+    v += dpp64<0x140, 0xf>(v);   // row_mirror        -> every lane holds its 16-lane row sum
+    v += dpp64<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+    v += dpp64<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3 -> lane 63 holds the total
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u)), 63));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u >> 32)), 63));
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ float wave_total(float v) {
+#define LO_DPPF(CTRL, RM) __builtin_bit_cast(float, dpp32<CTRL, RM>(__builtin_bit_cast(int, v)))
+    v += LO_DPPF(0xB1, 0xf);
+    v += LO_DPPF(0x4E, 0xf);
+    v += LO_DPPF(0x141, 0xf);
+    v += LO_DPPF(0x140, 0xf);
+    v += LO_DPPF(0x142, 0xa);
+    v += LO_DPPF(0x143, 0xc);
+#undef LO_DPPF
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+// fp64 reciprocal / reciprocal square root: v_rcp_f64 / v_rsq_f64 + two Newton steps (~1 ulp; ~5 VALU
+// instead of the ~10 of a correctly rounded v_div_scale/v_div_fmas/v_div_fixup division).  A zero divisor
+// gives NaN (0*inf in the Newton step) where IEEE division gives inf; every such use in the PKO feeds a
+// quantity the reference also turns into NaN (0/0 responsibilities, empty components).
+__device__ __forceinline__ double rcp64(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double rsq64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double e = fma(-x * y, y, 1.0);
+    y = fma(0.5 * y, e, y);
+    e = fma(-x * y, y, 1.0);
+    return fma(0.5 * y, e, y);
+}
+
+// std::max(a, b) for doubles (returns a when the comparison is false, so a NaN first argument survives)
+__device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
+
+// calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the FIRST alpha with the
+// strictly smallest JS cost, min_scale_factor if none is below DBL_MAX.  Every wave computes it
+// redundantly from P.js (lexicographic (cost, index) minimum == first strict minimum).
+__device__ __forceinline__ double pko_select_alpha(const KParams& P) {
+    const int lane = threadIdx.x & 63;
+    double bv = 1.7976931348623157e308;
+    int bi = 0x7fffffff;
+    for (int i = 1 + lane; i <= P.NA; i += 64) {
+        const double v = P.js[i];
+        if (v < bv) { bv = v; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    return (bv < 1.7976931348623157e308) ? P.alphas[bi] : P.min_scale;
 }
 
 template <typename T>

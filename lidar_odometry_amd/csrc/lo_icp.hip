@@ -18,9 +18,13 @@
 
 namespace lo {
 __global__ void k_correspond(KParams P, int with_stats);
-__global__ void k_pko(KParams P, int it);
+template <int NW> __global__ void k_pko_t(KParams P, int it);
+__global__ void k_pko_finish(KParams P);
 __global__ void k_accumulate(KParams P);
 __global__ void k_solve(KParams P, int it, int ne_only);
+struct Pose12 { float v[12]; };
+__global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
+__global__ void k_export_pose(const DevState* st, float* out);
 }  // namespace lo
 
 using namespace lo;
@@ -29,6 +33,7 @@ struct lo_ctx {
     lo_config cfg{};
     int device = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;
     std::string err;
     // scan buffers
     float* d_pts = nullptr;
@@ -38,6 +43,7 @@ struct lo_ctx {
     double* d_blk_sum = nullptr;
     double* d_blk_m2 = nullptr;
     double* d_blk_part = nullptr;
+    double* d_js = nullptr;
     double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
     size_t res_cap = 0;
     uint8_t* d_u8 = nullptr;
@@ -68,6 +74,17 @@ struct lo_ctx {
             return LO_ERR_HIP;                                                             \
         }                                                                                  \
     } while (0)
+
+// PKO workgroups: enough to give every workgroup <= 2 alphas of the JS grid, capped at kPkoMaxWGs
+static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs, (g.num_alpha_segments + 1) / 2)); }
+
+static void launch_pko(lo_ctx* c, const KParams& P, int it) {
+    // one GMM sample per thread: 2 waves cover the reference's 100 samples, 4 waves up to 256
+    if (c->cfg.gmm_sample_size <= 128)
+        hipLaunchKernelGGL(k_pko_t<2>, dim3(pko_grid(c->cfg)), dim3(128), 0, c->stream, P, it);
+    else
+        hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), 0, c->stream, P, it);
+}
 
 static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     KParams P{};
@@ -107,6 +124,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.blk_sum = c->d_blk_sum;
     P.blk_m2 = c->d_blk_m2;
     P.blk_part = c->d_blk_part;
+    P.js = c->d_js;
     P.res_dbg = nullptr;
     P.direct_res = nullptr;
     P.st = c->d_st;
@@ -117,7 +135,7 @@ static int validate_config(const lo_config* g, std::string& err) {
     if (!g) { err = "null config"; return LO_ERR_ARG; }
     if (g->max_iterations < 1 || g->max_iterations > LO_MAX_ITERS) { err = "max_iterations out of [1, 64]"; return LO_ERR_ARG; }
     if (g->gmm_sample_size < 1 || g->gmm_sample_size > kMaxS) { err = "gmm_sample_size out of [1, 256]"; return LO_ERR_ARG; }
-    if (g->gmm_components < 1 || g->gmm_components > kMaxK) { err = "gmm_components out of [1, 4]"; return LO_ERR_ARG; }
+    if (g->gmm_components < 1 || g->gmm_components > 3) { err = "gmm_components out of [1, 3]"; return LO_ERR_ARG; }
     if (g->num_alpha_segments < 1 || g->num_alpha_segments > kMaxAlpha) { err = "num_alpha_segments out of [1, 1000]"; return LO_ERR_ARG; }
     if (!(g->voxel_size > 0.0f)) { err = "voxel_size must be positive"; return LO_ERR_ARG; }   // VoxelMap.cpp:28-30
     if (g->hierarchy_factor <= 0 || g->hierarchy_factor % 2 == 0) { err = "hierarchy_factor must be positive and odd"; return LO_ERR_ARG; }
@@ -174,6 +192,7 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_blk_sum, NB * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_blk_m2, NB * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_blk_part, NB * kNE * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_js, (kMaxAlpha + 1) * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_st, sizeof(DevState)));
     LO_HIP(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
     std::memset(c->h_st, 0, sizeof(DevState));
@@ -235,12 +254,12 @@ void lo_destroy(lo_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part,
-                    c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i};
+                    c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -299,30 +318,23 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
     c->last_n = n;
-    // reset the GN state: pose, done, status, iter
-    DevState* hs = c->h_st;
-    std::memcpy(hs->pose, T_init, sizeof(float) * 12);
-    hs->scale = 1.0;
-    hs->alpha = g.robust_loss_delta;
-    hs->n_corr = 0;
-    hs->iter = 0;
-    hs->done = 0;
-    hs->status = LO_OK;
-    LO_HIP(c, hipMemcpyAsync(c->d_st, hs, offsetof(DevState, H_out), hipMemcpyHostToDevice, c->stream));
+    // reset the GN state (pose by kernel argument: no host staging buffer, scans can queue back to back)
+    Pose12 T0;
+    std::memcpy(T0.v, T_init, sizeof(float) * 12);
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
+    hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
     if (n > 0) {
         KParams P = make_params(c, d_pts, static_cast<int>(n));
         const dim3 grid(P.nb), blk(kBlock);
         for (int it = 0; it < g.max_iterations; ++it) {
             hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, it == 0 ? 1 : 0);
-            hipLaunchKernelGGL(k_pko, dim3(1), dim3(kPkoThreads), 0, c->stream, P, it);
+            launch_pko(c, P, it);
             hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P);
             hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, it, 0);
         }
         LO_HIP(c, hipGetLastError());
     }
     LO_HIP(c, hipEventRecord(c->ev1, c->stream));
-    LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     c->pending = true;
     return LO_OK;
 }
@@ -337,6 +349,9 @@ int lo_icp_optimize_async(lo_ctx* c, const float* d_pts, size_t n, const float T
 int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     if (!c) return LO_ERR_ARG;
     if (!c->pending) { c->err = "no optimize in flight"; return LO_ERR_STATE; }
+    // state header + the executed iterations' logs only
+    const size_t bytes = offsetof(DevState, logs) + sizeof(lo_iter_log) * static_cast<size_t>(c->cfg.max_iterations);
+    LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
     LO_HIP(c, hipStreamSynchronize(c->stream));
     c->pending = false;
     const DevState* hs = c->h_st;
@@ -391,15 +406,10 @@ static int ensure_res(lo_ctx* c, size_t n) {
 }
 
 static int reset_state(lo_ctx* c, const float T[12], double scale, double alpha) {
-    DevState* hs = c->h_st;
-    std::memcpy(hs->pose, T, sizeof(float) * 12);
-    hs->scale = scale;
-    hs->alpha = alpha;
-    hs->n_corr = 0;
-    hs->iter = 0;
-    hs->done = 0;
-    hs->status = LO_OK;
-    LO_HIP(c, hipMemcpyAsync(c->d_st, hs, offsetof(DevState, H_out), hipMemcpyHostToDevice, c->stream));
+    Pose12 T0;
+    std::memcpy(T0.v, T, sizeof(float) * 12);
+    hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, scale, alpha);
+    LO_HIP(c, hipGetLastError());
     return LO_OK;
 }
 
@@ -438,7 +448,8 @@ double lo_pko_scale_factor(lo_ctx* c, const double* residuals, size_t n, double*
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.direct_res = c->d_res;
     P.use_pko = 1;
-    hipLaunchKernelGGL(k_pko, dim3(1), dim3(kPkoThreads), 0, c->stream, P, 0);
+    launch_pko(c, P, 0);
+    hipLaunchKernelGGL(k_pko_finish, dim3(1), dim3(64), 0, c->stream, P);
     if (hipGetLastError() != hipSuccess) return NAN;
     if (hipMemcpyAsync(c->h_st, c->d_st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream) != hipSuccess) return NAN;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return NAN;
@@ -456,6 +467,7 @@ int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float
     if (rc != LO_OK) return rc;
     LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
+    P.alpha_given = 1;
     hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
     hipLaunchKernelGGL(k_accumulate, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, 0, 1);
@@ -478,6 +490,63 @@ int lo_pko_sample_indices(lo_ctx* c, size_t n, int32_t* out) {
     const int k = static_cast<int>(std::min<size_t>(n, static_cast<size_t>(c->cfg.gmm_sample_size)));
     for (int s = 0; s < k; ++s) out[s] = pko_sample_host(c->tables, static_cast<int>(n), s);
     return k;
+}
+
+int lo_set_stream(lo_ctx* c, void* stream) {
+    if (!c) return LO_ERR_ARG;
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->own_stream) { LO_HIP(c, hipStreamDestroy(c->stream)); c->own_stream = false; }
+    if (stream) c->stream = static_cast<hipStream_t>(stream);
+    else { LO_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
+    return LO_OK;
+}
+
+int lo_icp_export_pose(lo_ctx* c, float* d_out16) {
+    if (!c || !d_out16) return LO_ERR_ARG;
+    hipLaunchKernelGGL(k_export_pose, dim3(1), dim3(64), 0, c->stream, c->d_st, d_out16);
+    LO_HIP(c, hipGetLastError());
+    return LO_OK;
+}
+
+int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
+                    int kernel_id, int reps, float* avg_ms) {
+    if (!c || !d_pts || !T || !avg_ms || n == 0 || reps < 1 || kernel_id < 0 || kernel_id > 3) return LO_ERR_ARG;
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    int rc = reset_state(c, T, scale, alpha);
+    if (rc != LO_OK) return rc;
+    KParams P = make_params(c, d_pts, static_cast<int>(n));
+    P.alpha_given = 1;
+    const dim3 grid(P.nb), blk(kBlock);
+    // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials
+    hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 1);
+    hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P);
+    LO_HIP(c, hipGetLastError());
+    LO_HIP(c, hipEventRecord(c->ev0, c->stream));
+    for (int r = 0; r < reps; ++r) {
+        switch (kernel_id) {
+            case 0: hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 0); break;
+            case 1: hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P); break;
+            case 2: launch_pko(c, P, 1); break;
+            default: hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, 0, 1); break;
+        }
+    }
+    LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+    LO_HIP(c, hipGetLastError());
+    LO_HIP(c, hipEventSynchronize(c->ev1));
+    float ms = 0.0f;
+    LO_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *avg_ms = ms / reps;
+    return LO_OK;
+}
+
+int lo_debug_counters(lo_ctx* c, unsigned long long out[16]) {
+    if (!c || !out) return LO_ERR_ARG;
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(c->d_st) + offsetof(DevState, dbg), 16 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost));
+    return LO_OK;
 }
 
 int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {

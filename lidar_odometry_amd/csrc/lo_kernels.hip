@@ -5,9 +5,8 @@
 //   k_correspond  per point: transform, L1 surfel probe, fp64 residual, accept r <= max_corr
 //                 (find_correspondences :587-645); per-wave validity ballots; iteration 0 also the
 //                 per-block residual sum / M2 for the normalisation scale (:304-316)
-//   k_pko         one workgroup: correspondence count, scale, the reference's PKO sample selection
-//                 (std::shuffle(mt19937(42)) reproduced from host tables), k-means + EM GMM fit and the
-//                 JS-divergence alpha grid (AdaptiveMEstimator.cpp:243-485, :710-787)
+//   k_pko         (lo_pko.hip) correspondence count, scale, the reference's PKO sample selection, GMM fit
+//                 and the JS-divergence alpha grid (AdaptiveMEstimator.cpp:243-485, :710-787)
 //   k_accumulate  per correspondence: Huber weight, residual, Jacobian, 21+6+1 partial sums; wave shuffle
 //                 + LDS tree to one 28-double partial per block (:345-410)
 //   k_solve       one workgroup: fixed-order fp64 sum of block partials, pivoted LDLT (:418),
@@ -71,7 +70,7 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
         return;
     }
     // iteration 0: per-block (count, sum, M2) for a stable fp64 merge of the residual variance
-    double v = wave_sum(valid ? r : 0.0);
+    double v = wave_total(valid ? r : 0.0);
     if (lane == 0) s_red[wid] = v;
     __syncthreads();
     if (tid == 0) {
@@ -85,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
     __syncthreads();
     const double mb = s_mean;
     const double d = valid ? (r - mb) : 0.0;
-    v = wave_sum(d * d);
+    v = wave_total(d * d);
     __syncthreads();
     if (lane == 0) s_red[wid] = v;
     __syncthreads();
@@ -97,305 +96,23 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
 }
 
 // ====================================================================================================
-// k_pko
-// ====================================================================================================
-__device__ __forceinline__ int pko_sample(const KParams& P, int n, int s) {
-    if (n < P.S) return P.small_perm[P.small_off[n] + s];
-    const int mode = (n <= 65535) ? ((n & 1) ? 0 : 1) : 2;
-    const int lo0 = P.ev_off[mode * (P.S + 1) + s], hi0 = P.ev_off[mode * (P.S + 1) + s + 1];
-    // last event step <= n-1
-    int lo = lo0, hi = hi0;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (P.ev_steps[mid] <= n - 1) lo = mid + 1; else hi = mid;
-    }
-    return lo == lo0 ? P.base[mode * P.S + s] : P.ev_steps[lo - 1];
-}
-
-// gaussian_pdf (AdaptiveMEstimator.cpp:675-685)
-__device__ __forceinline__ double gpdf(double x, double mean, double variance) {
-    if (variance <= 0.0) return 0.0;
-    const double diff = x - mean;
-    const double expo = -0.5 * (diff * diff) / variance;
-    const double norm = 1.0 / sqrt(2.0 * M_PI * variance);
-    return norm * exp(expo);
-}
-
-__device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {   // :128-156
-    if (!cauchy) { const double a = fabs(r); return a <= d ? 1.0 : d / a; }
-    const double e2 = r * r, d2 = d * d;
-    return d2 / (d2 + e2);
-}
-
-__device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
-
-__global__ __launch_bounds__(kPkoThreads) void k_pko(KParams P, int it) {
-    DevState* st = P.st;
-    if (st->done) return;
-    __shared__ double sh[10240];                 // 80 KB: block prefix (as int) / JS chunk table
-    __shared__ double s_sd[kMaxS];
-    __shared__ double s_P[100];
-    __shared__ double s_js[kMaxAlpha + 1];
-    __shared__ double s_red[kPkoThreads / 64];
-    __shared__ int s_ired[kPkoThreads / 64];
-    __shared__ double s_gmm[3 * kMaxK];
-    __shared__ int s_nc;
-    __shared__ double s_scale, s_mean;
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    constexpr int NW = kPkoThreads / 64;
-    int* pre = reinterpret_cast<int*>(sh);
-
-    if (P.direct_res) {
-        if (tid == 0) { s_nc = P.n; s_scale = 1.0; }
-        __syncthreads();
-    } else {
-        // ---- 1. exclusive prefix of per-block correspondence counts (rank -> block) + stats merge ----
-        const int nb = P.nb;
-        const int per = (nb + kPkoThreads - 1) / kPkoThreads;
-        const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
-        int loc = 0;
-        double lsum = 0.0;
-        for (int b = b0; b < b1; ++b) { loc += P.blk_cnt[b]; if (it == 0) lsum += P.blk_sum[b]; }
-        int inc = loc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
-        if (lane == 63) s_ired[wid] = inc;
-        const double ws = wave_sum(lsum);
-        if (lane == 0) s_red[wid] = ws;
-        __syncthreads();
-        if (tid == 0) {
-            int run = 0;
-            double tot = 0.0;
-            for (int w = 0; w < NW; ++w) { const int c = s_ired[w]; s_ired[w] = run; run += c; tot += s_red[w]; }
-            s_nc = run;
-            s_mean = run > 0 ? tot / run : 0.0;
-        }
-        __syncthreads();
-        int excl = s_ired[wid] + inc - loc;
-        for (int b = b0; b < b1; ++b) { pre[b] = excl; excl += P.blk_cnt[b]; }
-        if (it == 0) {
-            const double mean = s_mean;
-            double m2 = 0.0;
-            for (int b = b0; b < b1; ++b) {
-                const int c = P.blk_cnt[b];
-                if (c > 0) { const double dm = P.blk_sum[b] / c - mean; m2 += P.blk_m2[b] + c * (dm * dm); }
-            }
-            m2 = wave_sum(m2);
-            __syncthreads();
-            if (lane == 0) s_red[wid] = m2;
-            __syncthreads();
-            if (tid == 0) {
-                double M2 = 0.0;
-                for (int w = 0; w < NW; ++w) M2 += s_red[w];
-                const double var = s_nc > 0 ? M2 / s_nc : 0.0;
-                s_scale = sqrt(var) / 6.0;            // IterativeClosestPointOptimizer.cpp:314-315
-                st->scale = s_scale;
-            }
-        } else if (tid == 0) {
-            s_scale = st->scale;
-        }
-        __syncthreads();
-    }
-    const int nc = s_nc;
-    if (nc < P.min_corr && !P.direct_res) {               // :298-302
-        if (tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
-        return;
-    }
-    if (!P.use_pko || nc == 0) {
-        if (tid == 0) { st->alpha = nc == 0 ? 1.0 : P.robust_delta; st->n_corr = nc; }
-        return;
-    }
-    const double scale = s_scale;
-    const double sden = std_max(scale, 1e-6);
-
-    // ---- 2. the reference's GMM sample: r_hat[perm_nc[s]], s < min(S, nc) ----
-    const int S = min(P.S, nc);
-    if (tid < S) {
-        const int rank = pko_sample(P, nc, tid);
-        double v;
-        if (P.direct_res) {
-            v = P.direct_res[rank];
-        } else {
-            int lo = 0, hi = P.nb - 1;                     // last block with pre[b] <= rank
-            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (pre[mid] <= rank) lo = mid; else hi = mid - 1; }
-            const int b = lo;
-            int k = rank - pre[b];
-            int w = 0;
-            uint64_t mk = 0;
-            for (; w < kWavesPerBlock; ++w) {
-                mk = P.wmask[b * kWavesPerBlock + w];
-                const int c = __popcll(mk);
-                if (k < c) break;
-                k -= c;
-            }
-            for (int q = 0; q < k; ++q) mk &= mk - 1;
-            const int bit = __ffsll(static_cast<unsigned long long>(mk)) - 1;
-            const int pidx = b * kBlock + w * kWave + bit;
-            float T[12];
-            for (int q = 0; q < 12; ++q) T[q] = st->pose[q];
-            float wx, wy, wz;
-            transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
-            const double r = residual_f64(P.tab[P.slot[pidx]], wx, wy, wz);
-            v = r / sden;                                   // :321-326
-        }
-        s_sd[tid] = v;
-    }
-    __syncthreads();
-
-    // ---- 3. GMM: k-means init + EM (fit_gmm, AdaptiveMEstimator.cpp:294-485), wave 0 ----
-    // Loops run to the compile-time kMaxK with `j < K` guards so every per-component array stays in VGPRs.
-    const int K = P.K;
-    if (wid == 0) {
-        double x[4];
-        bool have[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { const int idx = lane + 64 * q; have[q] = idx < S; x[q] = have[q] ? s_sd[idx] : 0.0; }
-        double mu[kMaxK], var[kMaxK], w[kMaxK], cntd[kMaxK];
-        const int D = K > 1 ? K - 1 : 1;
-#pragma unroll
-        for (int j = 0; j < kMaxK; ++j) { mu[j] = (j > 0 && j < K) ? s_sd[P.km_draws[S * D + (j - 1)]] : 0.0; cntd[j] = 0.0; }
-        for (int guard = 0; guard < 100000; ++guard) {
-            double sums[kMaxK];
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) { sums[j] = 0.0; cntd[j] = 0.0; }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (!have[q]) continue;
-                double md = DBL_MAX;
-                int ci = 0;
-#pragma unroll
-                for (int j = 0; j < kMaxK; ++j) if (j < K) { const double d = fabs(x[q] - mu[j]); if (d < md) { md = d; ci = j; } }
-#pragma unroll
-                for (int j = 0; j < kMaxK; ++j) if (j == ci) { sums[j] += x[q]; cntd[j] += 1.0; }
-            }
-            bool eq = true;
-            double nm[kMaxK];
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) {
-                if (j < K) {
-                    sums[j] = wave_sum(sums[j]);
-                    cntd[j] = wave_sum(cntd[j]);
-                }
-                nm[j] = (j == 0 || j >= K) ? 0.0 : (cntd[j] > 0.0 ? sums[j] / cntd[j] : 0.0);
-                eq = eq && (nm[j] == mu[j]);
-            }
-            if (eq) break;
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) mu[j] = nm[j];
-        }
-        double sx = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) if (have[q]) sx += x[q];
-        const double mean_of_data = wave_sum(sx) / S;
-        double sv = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) if (have[q]) { const double d = x[q] - mean_of_data; sv += d * d; }
-        const double iv = wave_sum(sv) / S;
-#pragma unroll
-        for (int j = 0; j < kMaxK; ++j) { var[j] = iv; w[j] = cntd[j] / static_cast<double>(S); }
-
-        for (int em = 0; em < 100; ++em) {
-            double Nk[kMaxK], Sx[kMaxK], resp[4][kMaxK], nrm[kMaxK];
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) { Nk[j] = 0.0; Sx[j] = 0.0; nrm[j] = var[j] <= 0.0 ? 0.0 : 1.0 / sqrt(2.0 * M_PI * var[j]); }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                double sr = 0.0;
-#pragma unroll
-                for (int j = 0; j < kMaxK; ++j) {
-                    double pdf = 0.0;
-                    if (var[j] > 0.0) { const double diff = x[q] - mu[j]; pdf = nrm[j] * exp(-0.5 * (diff * diff) / var[j]); }
-                    resp[q][j] = w[j] * pdf;
-                    if (j < K) sr += resp[q][j];
-                }
-#pragma unroll
-                for (int j = 0; j < kMaxK; ++j) {
-                    resp[q][j] /= sr;
-                    if (have[q] && j < K) { Nk[j] += resp[q][j]; Sx[j] += resp[q][j] * x[q]; }
-                }
-            }
-            double nmu[kMaxK], nv[kMaxK], nw[kMaxK];
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) {
-                if (j < K) { Nk[j] = wave_sum(Nk[j]); Sx[j] = wave_sum(Sx[j]); }
-                nw[j] = Nk[j] / static_cast<double>(S);
-                nmu[j] = (j == 0 || j >= K) ? 0.0 : Sx[j] / Nk[j];
-            }
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) {
-                double vv = 0.0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) if (have[q]) { const double d = x[q] - nmu[j]; vv += resp[q][j] * d * d; }
-                if (j < K) vv = wave_sum(vv);
-                nv[j] = std_max(vv / Nk[j], 1e-6);
-            }
-            double change = 0.0;
-#pragma unroll
-            for (int j = 1; j < kMaxK; ++j) if (j < K) change += fabs(nmu[j] - mu[j]);
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) { w[j] = nw[j]; mu[j] = nmu[j]; var[j] = nv[j]; }
-            if (change < 1e-6) break;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < kMaxK; ++j) if (j < K) { s_gmm[j] = w[j]; s_gmm[K + j] = mu[j]; s_gmm[2 * K + j] = var[j]; }
-        }
-    }
-    __syncthreads();
-
-    // ---- 4. JS divergence over the alpha grid (calculate_js_divergence :710-787) ----
-    const double dr = P.trunc / 100.0;
-    if (tid < 100) {
-        const double r = dr * (1 + static_cast<double>(tid));
-        double Pr = 0.0;
-        for (int m = 0; m < K; ++m) Pr += s_gmm[m] * gpdf(r, s_gmm[K + m], s_gmm[2 * K + m]);
-        s_P[tid] = Pr + 1e-10;
-    }
-    __syncthreads();
-    const int NA = P.NA;
-    for (int c0 = 1; c0 <= NA; c0 += 100) {
-        const int na = min(100, NA - c0 + 1);
-        for (int idx = tid; idx < na * 100; idx += kPkoThreads) {
-            const int a = idx / 100, b = idx - a * 100;
-            const double alpha = P.alphas[c0 + a];
-            const double pf = P.Z[c0 + a];
-            const double r = dr * (1 + static_cast<double>(b));
-            const double Pr = s_P[b];
-            const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
-            const double M = 0.5 * (Pr + Q);
-            sh[idx] = 0.5 * (Pr * log(Pr / M) + Q * log(Q / M));
-        }
-        __syncthreads();
-        if (tid < na) {
-            double cost = 0.0, cnt = 0.0;
-            for (int b = 0; b < 100; ++b) {
-                const double v = sh[tid * 100 + b];
-                if (isnan(v)) continue;
-                cost += v;
-                cnt += 1.0;
-            }
-            s_js[c0 + tid] = cnt == 0.0 ? DBL_MAX : cost / cnt;
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        double best_a = P.min_scale, best_c = DBL_MAX;       // calculate_pko_scale_factor :256-275
-        for (int i = 1; i <= NA; ++i) if (s_js[i] < best_c) { best_c = s_js[i]; best_a = P.alphas[i]; }
-        st->alpha = best_a;
-        st->n_corr = nc;
-        for (int j = 0; j < 3 * K; ++j) st->gmm_out[j] = s_gmm[j];
-    }
-}
-
-// ====================================================================================================
 // k_accumulate
 // ====================================================================================================
 __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
     const DevState* st = P.st;
     if (st->done) return;
     __shared__ float s_acc[kWavesPerBlock][kNE];
+    __shared__ double s_alpha;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // Huber delta of this iteration: argmin of the JS grid k_pko wrote (PKO), else robust_loss_delta
+    if (wid == 0) {
+        const double a = P.alpha_given ? P.st->alpha : (P.use_pko ? pko_select_alpha(P) : P.robust_delta);
+        if (lane == 0) {
+            s_alpha = a;
+            if (blockIdx.x == 0 && !P.alpha_given) P.st->alpha = a;
+        }
+    }
+    __syncthreads();
     const int i = blockIdx.x * kBlock + tid;
     float acc[kNE];
 #pragma unroll
@@ -406,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
         const double scale = st->scale;
-        const float dl = static_cast<float>(st->alpha);
+        const float dl = static_cast<float>(s_alpha);
         const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
         const Slot sl = P.tab[s];
         float wx, wy, wz;
@@ -450,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
     }
 #pragma unroll
     for (int k = 0; k < kNE; ++k) {
-        const float v = wave_sum(acc[k]);
+        const float v = wave_total(acc[k]);
         if (lane == 0) s_acc[wid][k] = v;
     }
     __syncthreads();
@@ -511,46 +228,94 @@ __device__ void so3_exp(const float* w, float* R) {
     so3_project(M, R);
 }
 
-// H.ldlt().solve(b): Eigen's pivoted LDLT (LDLT.h ldlt_inplace<Lower>::unblocked / _solve_impl) in fp64
+// H.ldlt().solve(b): Eigen's pivoted LDLT (LDLT.h ldlt_inplace<Lower>::unblocked / _solve_impl) in fp64.
+// Fully unrolled; the data-dependent pivot swaps are unrolled selects so the matrix stays in VGPRs.
+__device__ __forceinline__ void dswap(double& a, double& b) { const double t = a; a = b; b = t; }
+
 __device__ void ldlt6_solve(const double* Hin, const double* b, double* x) {
-    double m[36];
-    for (int k = 0; k < 36; ++k) m[k] = Hin[k];
+    double m[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) m[r][c] = Hin[r * 6 + c];
     int tr[6];
-    double temp[6];
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         int big = k;
-        double bv = fabs(m[k * 7]);
-        for (int i = k + 1; i < 6; ++i) if (fabs(m[i * 7]) > bv) { bv = fabs(m[i * 7]); big = i; }
+        double bv = fabs(m[k][k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) if (fabs(m[i][i]) > bv) { bv = fabs(m[i][i]); big = i; }
         tr[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; ++j) { const double t = m[k * 6 + j]; m[k * 6 + j] = m[big * 6 + j]; m[big * 6 + j] = t; }
-            for (int i = big + 1; i < 6; ++i) { const double t = m[i * 6 + k]; m[i * 6 + k] = m[i * 6 + big]; m[i * 6 + big] = t; }
-            { const double t = m[k * 7]; m[k * 7] = m[big * 7]; m[big * 7] = t; }
-            for (int i = k + 1; i < big; ++i) { const double t = m[i * 6 + k]; m[i * 6 + k] = m[big * 6 + i]; m[big * 6 + i] = t; }
-        }
-        if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = m[j * 7] * m[k * 6 + j];
-            double acc = 0.0;
-            for (int j = 0; j < k; ++j) acc += m[k * 6 + j] * temp[j];
-            m[k * 7] -= acc;
-            for (int i = k + 1; i < 6; ++i) {
-                double a = 0.0;
-                for (int j = 0; j < k; ++j) a += m[i * 6 + j] * temp[j];
-                m[i * 6 + k] -= a;
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            if (big == i) {
+#pragma unroll
+                for (int j = 0; j < k; ++j) dswap(m[k][j], m[i][j]);
+#pragma unroll
+                for (int r = i + 1; r < 6; ++r) dswap(m[r][k], m[r][i]);
+                dswap(m[k][k], m[i][i]);
+#pragma unroll
+                for (int r = k + 1; r < i; ++r) { const double t = m[r][k]; m[r][k] = m[i][r]; m[i][r] = t; }
             }
         }
-        const double akk = m[k * 7];
+        if (k > 0) {
+            double temp[6];
+#pragma unroll
+            for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < k; ++j) acc += m[k][j] * temp[j];
+            m[k][k] -= acc;
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) {
+                double a = 0.0;
+#pragma unroll
+                for (int j = 0; j < k; ++j) a += m[i][j] * temp[j];
+                m[i][k] -= a;
+            }
+        }
+        const double akk = m[k][k];
         const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) { for (int i = 0; i < 6; ++i) x[i] = 0.0; return; }
-        if (valid) for (int i = k + 1; i < 6; ++i) m[i * 6 + k] /= akk;
+        if (k == 0 && !valid) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) x[i] = 0.0;
+            return;
+        }
+        if (valid) {
+#pragma unroll
+            for (int i = k + 1; i < 6; ++i) m[i][k] /= akk;
+        }
     }
     double d[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) d[i] = b[i];
-    for (int k = 0; k < 6; ++k) if (tr[k] != k) { const double t = d[k]; d[k] = d[tr[k]]; d[tr[k]] = t; }
-    for (int i = 0; i < 6; ++i) { double a = 0.0; for (int j = 0; j < i; ++j) a += m[i * 6 + j] * d[j]; d[i] -= a; }
-    for (int i = 0; i < 6; ++i) { if (fabs(m[i * 7]) > DBL_MIN) d[i] /= m[i * 7]; else d[i] = 0.0; }
-    for (int i = 5; i >= 0; --i) { double a = 0.0; for (int j = i + 1; j < 6; ++j) a += m[j * 6 + i] * d[j]; d[i] -= a; }
-    for (int k = 5; k >= 0; --k) if (tr[k] != k) { const double t = d[k]; d[k] = d[tr[k]]; d[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) if (tr[k] == i) dswap(d[k], d[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double a = 0.0;
+#pragma unroll
+        for (int j = 0; j < i; ++j) a += m[i][j] * d[j];
+        d[i] -= a;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) d[i] = (fabs(m[i][i]) > DBL_MIN) ? d[i] / m[i][i] : 0.0;
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double a = 0.0;
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) a += m[j][i] * d[j];
+        d[i] -= a;
+    }
+#pragma unroll
+    for (int k = 5; k >= 0; --k) {
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) if (tr[k] == i) dswap(d[k], d[i]);
+    }
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
@@ -624,4 +389,33 @@ __global__ __launch_bounds__(256) void k_solve(KParams P, int it, int ne_only) {
     if (tdel < P.tol_t && rdel < P.tol_r) st->done = 1;               // :443-448
 }
 
+// ====================================================================================================
+// k_init: reset the GN state for a new scan.  The initial pose travels as a kernel argument, so any
+// number of scans can be enqueued back to back without a host staging buffer.
+// ====================================================================================================
+struct Pose12 { float v[12]; };
+
+__global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
+    if (threadIdx.x < 12) st->pose[threadIdx.x] = T.v[threadIdx.x];
+    if (threadIdx.x == 0) {
+        st->scale = scale;
+        st->alpha = alpha;
+        st->n_corr = 0;
+        st->iter = 0;
+        st->done = 0;
+        st->status = LO_OK;
+    }
+}
+
+// Copy the current pose + status into a caller buffer (16 floats: pose[12], status, iterations, n_corr, 0).
+__global__ void k_export_pose(const DevState* st, float* out) {
+    const int t = threadIdx.x;
+    if (t < 12) out[t] = st->pose[t];
+    if (t == 12) out[12] = static_cast<float>(st->status);
+    if (t == 13) out[13] = static_cast<float>(st->iter);
+    if (t == 14) out[14] = static_cast<float>(st->n_corr);
+    if (t == 15) out[15] = 0.0f;
+}
+
 }  // namespace lo
+

@@ -1,0 +1,459 @@
+// lo_voxelmap.cpp — host C++ map side (include/lo_map.h).
+//
+// The ICP kernels only read the surfel table; this file builds it the way the reference does so the
+// product runs a full odometry loop without the reference: map::VoxelMap::UpdateVoxelMap
+// (src/database/VoxelMap.cpp:128-262) and map::FastVoxelFilter::filter (src/database/VoxelMap.h:73-104).
+//
+// Result-defining details kept from the reference:
+//  * containers iterate in insertion order and erase by moving the last element into the hole
+//    (ankerl::unordered_dense do_erase) — this fixes the child order used in the fp32 centroid/covariance
+//    sums and the order of L0 pruning;
+//  * keys: PointToVoxelKey = floor(p / scale) with scale = voxel * factor in fp32 (:50-58); the L0->L1
+//    parent is integer floor division (:60-67);
+//  * the surfel normal is U.col(2) of Eigen's 2-sided Jacobi SVD of the fp32 covariance (restated below),
+//    planarity = s2 / (s0 + 1e-6f) (:239-243).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/lo_map.h"
+
+namespace lo {
+namespace {
+
+struct Key3 {
+    int32_t x, y, z;
+};
+inline bool operator==(const Key3& a, const Key3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+
+inline uint64_t spread21(int32_t v) {
+    uint64_t q = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffull;
+    q = (q | (q << 32)) & 0x1f00000000ffffull;
+    q = (q | (q << 16)) & 0x1f0000ff0000ffull;
+    q = (q | (q << 8)) & 0x100f00f00f00f00full;
+    q = (q | (q << 4)) & 0x10c30c30c30c30c3ull;
+    q = (q | (q << 2)) & 0x1249249249249249ull;
+    return q;
+}
+inline uint64_t mix64(uint64_t h) {
+    __uint128_t r = static_cast<__uint128_t>(h) * 0x9E3779B97F4A7C15ull;
+    return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
+}
+struct HashKey3 {
+    uint64_t operator()(const Key3& k) const { return mix64(spread21(k.x) | (spread21(k.y) << 1) | (spread21(k.z) << 2)); }
+};
+struct HashU64 {
+    uint64_t operator()(uint64_t k) const { return mix64(k); }
+};
+struct NoValue {};
+
+// Insertion-ordered open-addressing map; erase moves the last entry into the hole.
+template <class K, class V, class H>
+class OrderedMap {
+  public:
+    OrderedMap() { reindex(16); }
+    size_t size() const { return keys_.size(); }
+    bool empty() const { return keys_.empty(); }
+    const K& key_at(size_t i) const { return keys_[i]; }
+    V& val_at(size_t i) { return vals_[i]; }
+    const V& val_at(size_t i) const { return vals_[i]; }
+
+    int64_t find(const K& k) const {
+        uint64_t b = H()(k) & mask_;
+        for (;;) {
+            const int32_t e = slots_[b];
+            if (e < 0) return -1;
+            if (keys_[e] == k) return e;
+            b = (b + 1) & mask_;
+        }
+    }
+    // returns index; *inserted set when new (value default-constructed)
+    size_t upsert(const K& k, bool* inserted) {
+        const int64_t f = find(k);
+        if (f >= 0) { if (inserted) *inserted = false; return static_cast<size_t>(f); }
+        if ((keys_.size() + 1) * 5 > slots_.size() * 4) reindex(slots_.size() * 2);
+        keys_.push_back(k);
+        vals_.emplace_back();
+        place(static_cast<int32_t>(keys_.size() - 1));
+        if (inserted) *inserted = true;
+        return keys_.size() - 1;
+    }
+    bool erase(const K& k) {
+        uint64_t b = H()(k) & mask_;
+        for (;;) {
+            const int32_t e = slots_[b];
+            if (e < 0) return false;
+            if (keys_[e] == k) break;
+            b = (b + 1) & mask_;
+        }
+        const int32_t victim = slots_[b];
+        slots_[b] = -1;
+        for (uint64_t j = (b + 1) & mask_; slots_[j] >= 0; j = (j + 1) & mask_) {   // backward shift
+            const uint64_t home = H()(keys_[slots_[j]]) & mask_;
+            if (((j - home) & mask_) >= ((j - b) & mask_)) { slots_[b] = slots_[j]; slots_[j] = -1; b = j; }
+        }
+        const int32_t last = static_cast<int32_t>(keys_.size() - 1);
+        if (victim != last) {
+            uint64_t s = H()(keys_[last]) & mask_;
+            while (slots_[s] != last) s = (s + 1) & mask_;
+            keys_[victim] = keys_[last];
+            vals_[victim] = std::move(vals_[last]);
+            slots_[s] = victim;
+        }
+        keys_.pop_back();
+        vals_.pop_back();
+        return true;
+    }
+    void clear() { keys_.clear(); vals_.clear(); reindex(16); }
+
+  private:
+    void place(int32_t i) {
+        uint64_t b = H()(keys_[i]) & mask_;
+        while (slots_[b] >= 0) b = (b + 1) & mask_;
+        slots_[b] = i;
+    }
+    void reindex(size_t cap) {
+        slots_.assign(cap, -1);
+        mask_ = cap - 1;
+        for (size_t i = 0; i < keys_.size(); ++i) place(static_cast<int32_t>(i));
+    }
+    std::vector<K> keys_;
+    std::vector<V> vals_;
+    std::vector<int32_t> slots_;
+    uint64_t mask_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Eigen JacobiSVD<Matrix3f>, square case (JacobiSVD.h compute(), real_2x2_jacobi_svd, makeJacobi)
+// ---------------------------------------------------------------------------------------------
+struct Rot { float c, s; };
+inline Rot rot_t(Rot r) { return {r.c, -r.s}; }
+inline Rot rot_mul(Rot a, Rot b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
+inline void rotate(float& x, float& y, Rot r) {
+    const float xi = x, yi = y;
+    x = r.c * xi + r.s * yi;
+    y = -r.s * xi + r.c * yi;
+}
+inline Rot make_jacobi(float x, float y, float z) {
+    const float deno = 2.0f * std::fabs(y);
+    if (deno < FLT_MIN) return {1.0f, 0.0f};
+    const float tau = (x - z) / deno;
+    const float w = std::sqrt(tau * tau + 1.0f);
+    const float t = tau > 0.0f ? 1.0f / (tau + w) : 1.0f / (tau - w);
+    const float sgn = t > 0.0f ? 1.0f : -1.0f;
+    const float n = 1.0f / std::sqrt(t * t + 1.0f);
+    return {n, ((-sgn) * (y / std::fabs(y))) * std::fabs(t) * n};
+}
+
+// A row-major a[r][c]; U columns = left singular vectors, S descending.
+void jacobi_svd3(const float A[3][3], float U[3][3], float S[3]) {
+    float scale = 0.0f;                                               // maxCoeff<PropagateNaN>
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
+        const float v = std::fabs(A[r][c]);
+        scale = (std::isnan(v) || std::isnan(scale)) ? NAN : std::max(scale, v);
+    }
+    float W[3][3], V[3][3];
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) { U[r][c] = V[r][c] = (r == c) ? 1.0f : 0.0f; }
+    if (!std::isfinite(scale)) { S[0] = S[1] = S[2] = NAN; return; }
+    if (scale == 0.0f) scale = 1.0f;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) W[r][c] = A[r][c] / scale;
+    float maxDiag = std::max(std::fabs(W[0][0]), std::max(std::fabs(W[1][1]), std::fabs(W[2][2])));
+    const float prec = 2.0f * FLT_EPSILON;
+    bool done = false;
+    for (int sweep = 0; !done && sweep < 1000; ++sweep) {
+        done = true;
+        for (int p = 1; p < 3; ++p) {
+            for (int q = 0; q < p; ++q) {
+                const float thr = std::max(FLT_MIN, prec * maxDiag);
+                if (!(std::fabs(W[p][q]) > thr || std::fabs(W[q][p]) > thr)) continue;
+                done = false;
+                // real_2x2_jacobi_svd
+                float m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+                Rot r1;
+                const float t = m00 + m11, d = m10 - m01;
+                if (std::fabs(d) < FLT_MIN) r1 = {1.0f, 0.0f};
+                else {
+                    const float u = t / d;
+                    const float tmp = std::sqrt(1.0f + u * u);
+                    r1 = {u / tmp, 1.0f / tmp};
+                }
+                rotate(m00, m10, r1);
+                rotate(m01, m11, r1);
+                const Rot jr = make_jacobi(m00, m01, m11);
+                const Rot jl = rot_mul(r1, rot_t(jr));
+                for (int i = 0; i < 3; ++i) rotate(W[p][i], W[q][i], jl);       // W.applyOnTheLeft(p,q,jl)
+                for (int i = 0; i < 3; ++i) rotate(U[i][p], U[i][q], jl);       // U.applyOnTheRight(p,q,jl^T)
+                const Rot jrt = rot_t(jr);
+                for (int i = 0; i < 3; ++i) rotate(W[i][p], W[i][q], jrt);      // W.applyOnTheRight(p,q,jr)
+                for (int i = 0; i < 3; ++i) rotate(V[i][p], V[i][q], jrt);
+                maxDiag = std::max(maxDiag, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = W[i][i];
+        S[i] = std::fabs(a);
+        if (a < 0.0f) for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
+    }
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    for (int i = 0; i < 3; ++i) {                                         // descending sort (first max)
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k) if (S[k] > S[pos]) pos = k;
+        if (S[pos] == 0.0f) break;
+        if (pos != i) {
+            std::swap(S[i], S[pos]);
+            for (int r = 0; r < 3; ++r) { std::swap(U[r][i], U[r][pos]); std::swap(V[r][i], V[r][pos]); }
+        }
+    }
+}
+
+struct L0 {
+    float c[3] = {0.0f, 0.0f, 0.0f};
+    int hit_count = 1;
+    int point_count = 0;
+};
+using ChildSet = OrderedMap<Key3, NoValue, HashKey3>;
+struct L1 {
+    ChildSet children;
+    bool has_surfel = false;
+    float normal[3] = {0.0f, 0.0f, 0.0f};
+    float centroid[3] = {0.0f, 0.0f, 0.0f};
+    float planarity = 1.0f;
+    int last_child_count = 0;
+};
+
+}  // namespace
+
+struct HostVoxelMap {
+    float voxel = 0.5f;
+    int factor = 3;
+    float planarity_thr = 0.1f;
+    bool compute_surfels = true;
+    OrderedMap<Key3, L0, HashKey3> l0;
+    OrderedMap<Key3, L1, HashKey3> l1;
+
+    Key3 key(const float* p, int level) const {
+        float s = voxel;
+        if (level == 1) s *= static_cast<float>(factor);
+        return {static_cast<int32_t>(std::floor(p[0] / s)), static_cast<int32_t>(std::floor(p[1] / s)),
+                static_cast<int32_t>(std::floor(p[2] / s))};
+    }
+    Key3 parent(const Key3& k) const {
+        const int f = factor;
+        auto d = [f](int v) { return v >= 0 ? v / f : (v - (f - 1)) / f; };
+        return {d(k.x), d(k.y), d(k.z)};
+    }
+    void unregister(const Key3& k) {
+        const Key3 p = parent(k);
+        const int64_t i = l1.find(p);
+        if (i < 0) return;
+        L1& n = l1.val_at(i);
+        n.children.erase(k);
+        if (n.children.size() < 5) n.has_surfel = false;
+        if (n.children.empty()) l1.erase(p);
+    }
+    void add_point(const float* p) {
+        const Key3 k = key(p, 0);
+        bool fresh = false;
+        const size_t i = l0.upsert(k, &fresh);
+        L0& v = l0.val_at(i);
+        const int n = v.point_count;
+        if (n == 0) {
+            std::memcpy(v.c, p, sizeof(float) * 3);
+            v.hit_count = 1;
+            v.point_count = 1;
+        } else {
+            const float nf = static_cast<float>(n), n1 = static_cast<float>(n + 1);
+            for (int a = 0; a < 3; ++a) v.c[a] = (v.c[a] * nf + p[a]) / n1;
+            v.point_count++;
+        }
+        if (fresh) {
+            const size_t j = l1.upsert(parent(k), nullptr);
+            l1.val_at(j).children.upsert(k, nullptr);
+        }
+    }
+
+    void update(const float* xyz, size_t n, const double sensor[3], double max_distance, bool keyframe) {
+        if (!xyz || n == 0 || !keyframe) return;
+        const float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
+        const float rsq = static_cast<float>(max_distance * max_distance);
+        std::vector<Key3> doomed;
+        for (size_t i = 0; i < l0.size(); ++i) {
+            const float* c = l0.val_at(i).c;
+            const float d0 = c[0] - sp[0], d1 = c[1] - sp[1], d2 = c[2] - sp[2];
+            const float e0 = d0 * d0, e1 = d1 * d1, e2 = d2 * d2;
+            if (e0 + (e1 + e2) > rsq) doomed.push_back(l0.key_at(i));
+        }
+        for (const Key3& k : doomed) { unregister(k); l0.erase(k); }
+        std::vector<Key3> empty1;
+        for (size_t i = 0; i < l1.size(); ++i) if (l1.val_at(i).children.empty()) empty1.push_back(l1.key_at(i));
+        for (const Key3& k : empty1) l1.erase(k);
+
+        OrderedMap<Key3, NoValue, HashKey3> touched;
+        for (size_t i = 0; i < n; ++i) {
+            add_point(xyz + 3 * i);
+            touched.upsert(key(xyz + 3 * i, 1), nullptr);
+        }
+        if (!compute_surfels) return;
+        std::vector<float> cs;
+        for (size_t t = 0; t < touched.size(); ++t) {
+            const Key3 k1 = touched.key_at(t);
+            const int64_t li = l1.find(k1);
+            if (li < 0) continue;
+            L1& node = l1.val_at(li);
+            const int cnt = static_cast<int>(node.children.size());
+            if (cnt < 5) { node.has_surfel = false; continue; }
+            if (node.has_surfel && node.last_child_count == cnt) continue;
+            cs.clear();
+            for (size_t q = 0; q < node.children.size(); ++q) {
+                const int64_t c0 = l0.find(node.children.key_at(q));
+                if (c0 >= 0) cs.insert(cs.end(), l0.val_at(c0).c, l0.val_at(c0).c + 3);
+            }
+            const size_t m = cs.size() / 3;
+            if (m < 3) { node.has_surfel = false; continue; }
+            float cen[3] = {0.0f, 0.0f, 0.0f};
+            for (size_t q = 0; q < m; ++q) for (int a = 0; a < 3; ++a) cen[a] += cs[3 * q + a];
+            const float mf = static_cast<float>(m);
+            for (int a = 0; a < 3; ++a) cen[a] /= mf;
+            float cov[3][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+            for (size_t q = 0; q < m; ++q) {
+                const float d[3] = {cs[3 * q] - cen[0], cs[3 * q + 1] - cen[1], cs[3 * q + 2] - cen[2]};
+                for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) cov[r][c] += d[c] * d[r];
+            }
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) cov[r][c] /= mf;
+            float U[3][3], S[3];
+            jacobi_svd3(cov, U, S);
+            const float planarity = S[2] / (S[0] + 1e-6f);
+            if (planarity > planarity_thr) {
+                node.has_surfel = false;
+                std::vector<Key3> kids;
+                for (size_t q = 0; q < node.children.size(); ++q) kids.push_back(node.children.key_at(q));
+                for (const Key3& k : kids) l0.erase(k);
+                l1.erase(k1);
+                continue;
+            }
+            node.has_surfel = true;
+            for (int a = 0; a < 3; ++a) { node.normal[a] = U[a][2]; node.centroid[a] = cen[a]; }
+            node.planarity = planarity;
+            node.last_child_count = cnt;
+        }
+    }
+};
+
+}  // namespace lo
+
+using lo::HostVoxelMap;
+
+struct lo_voxelmap {
+    HostVoxelMap m;
+};
+
+extern "C" {
+
+lo_voxelmap* lo_voxelmap_create(float voxel_size, int hierarchy_factor, float planarity_threshold, int compute_surfels) {
+    if (!(voxel_size > 0.0f) || hierarchy_factor <= 0 || hierarchy_factor % 2 == 0) return nullptr;
+    lo_voxelmap* v = new lo_voxelmap();
+    v->m.voxel = voxel_size;
+    v->m.factor = hierarchy_factor;
+    v->m.planarity_thr = planarity_threshold;
+    v->m.compute_surfels = compute_surfels != 0;
+    return v;
+}
+
+void lo_voxelmap_destroy(lo_voxelmap* m) { delete m; }
+
+int lo_voxelmap_update(lo_voxelmap* m, const float* xyz, size_t n, const double sensor[3], double max_distance, int is_keyframe) {
+    if (!m || !sensor || (n > 0 && !xyz)) return LO_ERR_ARG;
+    m->m.update(xyz, n, sensor, max_distance, is_keyframe != 0);
+    return LO_OK;
+}
+
+size_t lo_voxelmap_l0_count(const lo_voxelmap* m) { return m ? m->m.l0.size() : 0; }
+size_t lo_voxelmap_l1_count(const lo_voxelmap* m) { return m ? m->m.l1.size() : 0; }
+size_t lo_voxelmap_surfel_count(const lo_voxelmap* m) {
+    if (!m) return 0;
+    size_t c = 0;
+    for (size_t i = 0; i < m->m.l1.size(); ++i) c += m->m.l1.val_at(i).has_surfel ? 1 : 0;
+    return c;
+}
+
+size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* normals, float* centroids, float* planarity, size_t cap) {
+    if (!m) return 0;
+    size_t c = 0;
+    for (size_t i = 0; i < m->m.l1.size() && c < cap; ++i) {
+        const auto& n = m->m.l1.val_at(i);
+        if (!n.has_surfel) continue;
+        const auto& k = m->m.l1.key_at(i);
+        if (keys) { keys[3 * c] = k.x; keys[3 * c + 1] = k.y; keys[3 * c + 2] = k.z; }
+        for (int a = 0; a < 3; ++a) {
+            if (normals) normals[3 * c + a] = n.normal[a];
+            if (centroids) centroids[3 * c + a] = n.centroid[a];
+        }
+        if (planarity) planarity[c] = n.planarity;
+        ++c;
+    }
+    return c;
+}
+
+size_t lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap) {
+    if (!m || !xyz) return 0;
+    size_t c = 0;
+    for (; c < m->m.l0.size() && c < cap; ++c) std::memcpy(xyz + 3 * c, m->m.l0.val_at(c).c, sizeof(float) * 3);
+    return c;
+}
+
+int lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m) {
+    if (!ctx || !m) return LO_ERR_ARG;
+    const size_t s = lo_voxelmap_surfel_count(m);
+    std::vector<int32_t> k(3 * std::max<size_t>(s, 1));
+    std::vector<float> n(3 * std::max<size_t>(s, 1)), c(3 * std::max<size_t>(s, 1));
+    lo_voxelmap_get_surfels(m, k.data(), n.data(), c.data(), nullptr, s);
+    return lo_map_set_surfels(ctx, k.data(), n.data(), c.data(), s);
+}
+
+// FastVoxelFilter::filter (VoxelMap.h:73-104): Morton key of floor(p * (1/voxel)) + 2^20 clamped to 21 bits,
+// running fp32 sums in input order, centroid = sum * (1/count); output in first-occurrence order.
+size_t lo_voxel_filter(const float* in, size_t n, float voxel_size, int stride, float* out) {
+    if (!in || !out || n == 0 || stride < 1) return 0;
+    struct Acc { float sx = 0.0f, sy = 0.0f, sz = 0.0f; uint32_t count = 0; };
+    lo::OrderedMap<uint64_t, Acc, lo::HashU64> acc;
+    const float inv = 1.0f / voxel_size;
+    auto expand = [](uint64_t v) {
+        v &= 0x1FFFFF;
+        v = (v | (v << 32)) & 0x1F00000000FFFFull;
+        v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+        v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+        v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+        v = (v | (v << 2)) & 0x1249249249249249ull;
+        return v;
+    };
+    for (size_t i = 0; i < n; i += static_cast<size_t>(stride)) {
+        const float* p = in + 3 * i;
+        if (!std::isfinite(p[0]) || !std::isfinite(p[1]) || !std::isfinite(p[2])) continue;
+        int64_t q[3];
+        for (int a = 0; a < 3; ++a) {
+            q[a] = static_cast<int64_t>(std::floor(p[a] * inv)) + (1 << 20);
+            q[a] = std::max<int64_t>(0, std::min<int64_t>(q[a], (1 << 21) - 1));
+        }
+        const uint64_t key = expand(static_cast<uint64_t>(q[0])) | (expand(static_cast<uint64_t>(q[1])) << 1) |
+                             (expand(static_cast<uint64_t>(q[2])) << 2);
+        Acc& a = acc.val_at(acc.upsert(key, nullptr));
+        a.sx += p[0];
+        a.sy += p[1];
+        a.sz += p[2];
+        a.count++;
+    }
+    for (size_t i = 0; i < acc.size(); ++i) {
+        const Acc& a = acc.val_at(i);
+        const float ic = 1.0f / static_cast<float>(a.count);
+        out[3 * i] = a.sx * ic;
+        out[3 * i + 1] = a.sy * ic;
+        out[3 * i + 2] = a.sz * ic;
+    }
+    return acc.size();
+}
+
+}  // extern "C"

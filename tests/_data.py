@@ -83,5 +83,7 @@ def surfels(m):
 
 
 def rot_angle(Ra, Rb) -> float:
-    Rd = np.asarray(Ra, np.float64).T @ np.asarray(Rb, np.float64)
-    return float(np.arccos(np.clip((np.trace(Rd) - 1) / 2, -1.0, 1.0)))
+    """Rotation difference in rad.  ||Ra - Rb||_F / sqrt(2) = 2 sin(theta/2) ~ theta; unlike the arccos-of-trace
+    form it does not turn a 1e-7 fp32 orthonormality error into a 4e-4 rad reading."""
+    d = np.asarray(Ra, np.float64) - np.asarray(Rb, np.float64)
+    return float(np.linalg.norm(d) / np.sqrt(2.0))

@@ -1,0 +1,85 @@
+"""CPU tests: the product's host map side (lo_voxelmap_*, lo_voxel_filter) is bit-identical to the oracle
+restatement of VoxelMap::UpdateVoxelMap / FastVoxelFilter::filter on the same inputs (no GPU needed)."""
+import numpy as np
+import pytest
+
+import oracle
+from lidar_odometry_amd import synth
+from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+from tests import _data
+
+
+@pytest.mark.parametrize("frame,stride,voxel", [(0, 8, 0.5), (5, 1, 0.5), (9, 4, 0.4), (13, 3, 0.25)])
+def test_voxel_filter_bitwise(frame, stride, voxel):
+    raw = _data.kitti_scan(frame)
+    a = voxel_filter(raw, voxel, stride)
+    b = oracle.voxel_filter(raw, voxel, stride)
+    assert a.shape == b.shape
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_voxel_filter_edge_cases():
+    assert voxel_filter(np.zeros((0, 3), np.float32), 0.5, 1).shape == (0, 3)
+    p = np.array([[np.nan, 0, 0], [np.inf, 0, 0], [1e30, 1e30, 1e30], [-1e30, 0, 0], [0.1, 0.2, 0.3]], np.float32)
+    np.testing.assert_array_equal(voxel_filter(p, 0.5, 1), oracle.voxel_filter(p, 0.5, 1))
+
+
+def _compare_maps(a: VoxelMap, b: "oracle.VoxelMap"):
+    assert a.l0_count() == b.l0_count()
+    assert a.l1_count() == b.l1_count()
+    np.testing.assert_array_equal(a.l0_cloud(), b.l0_cloud())
+    ka, na, ca, pa = a.surfels()
+    kb, nb, cb, pb = b.surfels()
+    np.testing.assert_array_equal(ka, kb)
+    np.testing.assert_array_equal(na.view(np.uint32), nb.view(np.uint32))
+    np.testing.assert_array_equal(ca.view(np.uint32), cb.view(np.uint32))
+    np.testing.assert_array_equal(pa.view(np.uint32), pb.view(np.uint32))
+
+
+def test_voxelmap_keyframe_sequence_bitwise():
+    seq = _data.kitti_seq()
+    a = VoxelMap(0.5, 3, 0.1, True)
+    b = oracle.VoxelMap(0.5, 3, 0.1, True)
+    for k in range(0, 21, 2):
+        pts = voxel_filter(_data.kitti_scan(k), 0.5, 8)
+        T = seq.poses[k]
+        w = synth.transform(T, pts)
+        a.update(w, T[:3, 3], 120.0, True)
+        b.update(w, T[:3, 3], 120.0, True)
+        _compare_maps(a, b)
+    assert a.surfel_count() > 500
+
+
+def test_voxelmap_pruning_and_planarity_erase():
+    rng = np.random.default_rng(11)
+    a = VoxelMap(0.5, 3, 0.1, True)
+    b = oracle.VoxelMap(0.5, 3, 0.1, True)
+    # planar + volumetric clutter (planarity erase path), then move the sensor so pruning erases voxels
+    for step in range(6):
+        plane = np.concatenate([rng.uniform(-20, 20, (4000, 2)), rng.normal(0, 0.01, (4000, 1))], 1)
+        blob = rng.normal(0, 1.0, (2000, 3)) + np.array([5.0 * step, 0, 3])
+        pts = np.concatenate([plane, blob]).astype(np.float32)
+        sensor = np.array([8.0 * step, 0.0, 0.0])
+        a.update(pts, sensor, 25.0, True)
+        b.update(pts, sensor, 25.0, True)
+        _compare_maps(a, b)
+    a.update(pts, sensor, 25.0, False)   # non-keyframe: no-op
+    _compare_maps(a, b)
+
+
+def test_voxelmap_mid360_voxel04():
+    m_o, _, _, _ = _data.mid360_case()
+    sc = synth.mid360_scene()
+    a = VoxelMap(0.4, 3, 0.1, True)
+    poses = [synth.se3(synth.rot_z(0.05 * k), [0.3 * k, 0.1 * k, 1.0]) for k in range(8)]
+    for k in range(0, 6, 2):
+        p = voxel_filter(synth.mid360_like_scan(sc, poses[k], k), 0.4, 4)
+        a.update(synth.transform(poses[k], p), poses[k][:3, 3], 48.0, True)
+    _compare_maps(a, m_o)
+
+
+def test_voxelmap_invalid_params():
+    with pytest.raises(ValueError):
+        VoxelMap(0.0, 3)
+    with pytest.raises(ValueError):
+        VoxelMap(0.5, 2)
