@@ -27,6 +27,8 @@ constexpr int kPkoBlock = 256;       // PKO workgroup: one GMM sample per thread
 constexpr int kPkoMaxWGs = 64;       // PKO workgroups per launch (each evaluates a slice of the alpha grid)
 constexpr int kPkoAlphaPerWG = 4;    // alphas per JS pass of one workgroup
 constexpr int kMaxBlocks = 16384;    // => max 4M points per scan
+constexpr int kAccBlocks = 1024;     // k_accumulate grid cap (grid-stride beyond): bounds the k_solve partial sum
+constexpr int kSolveThreads = 1024;  // k_solve: 36 x 28 threads sum the block partials, coalesced
 constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
@@ -59,6 +61,7 @@ struct KParams {
     const float* pts;
     int n;
     int nb;
+    int nb_acc;                       // k_accumulate blocks = min(nb, kAccBlocks)
     // map
     const Slot* tab;
     uint32_t log2cap;

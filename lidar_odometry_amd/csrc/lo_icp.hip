@@ -92,6 +92,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.pts = d_pts;
     P.n = n;
     P.nb = (n + kBlock - 1) / kBlock;
+    P.nb_acc = P.nb < kAccBlocks ? (P.nb > 0 ? P.nb : 1) : kAccBlocks;
     P.tab = c->d_tab;
     P.log2cap = c->log2cap;
     P.l1scale = g.voxel_size * static_cast<float>(g.hierarchy_factor);   // PointToVoxelKey (VoxelMap.cpp:51-52)
@@ -329,8 +330,8 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         for (int it = 0; it < g.max_iterations; ++it) {
             hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, it == 0 ? 1 : 0);
             launch_pko(c, P, it);
-            hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P);
-            hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, it, 0);
+            hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P);
+            hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
         }
         LO_HIP(c, hipGetLastError());
     }
@@ -469,8 +470,8 @@ int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.alpha_given = 1;
     hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
-    hipLaunchKernelGGL(k_accumulate, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
-    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, 0, 1);
+    hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P);
+    hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1);
     LO_HIP(c, hipGetLastError());
     std::vector<int32_t> cnt(P.nb);
     LO_HIP(c, hipMemcpyAsync(cnt.data(), c->d_blk_cnt, P.nb * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -521,15 +522,15 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     const dim3 grid(P.nb), blk(kBlock);
     // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials
     hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 1);
-    hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P);
+    hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P);
     LO_HIP(c, hipGetLastError());
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int r = 0; r < reps; ++r) {
         switch (kernel_id) {
             case 0: hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 0); break;
-            case 1: hipLaunchKernelGGL(k_accumulate, grid, blk, 0, c->stream, P); break;
+            case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P); break;
             case 2: launch_pko(c, P, 1); break;
-            default: hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, c->stream, P, 0, 1); break;
+            default: hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1); break;
         }
     }
     LO_HIP(c, hipEventRecord(c->ev1, c->stream));

@@ -113,17 +113,19 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
         }
     }
     __syncthreads();
-    const int i = blockIdx.x * kBlock + tid;
     float acc[kNE];
 #pragma unroll
     for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
-    const int s = (i < P.n) ? P.slot[i] : -1;
-    if (s >= 0) {
-        float T[12];
+    float T[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
-        const double scale = st->scale;
-        const float dl = static_cast<float>(s_alpha);
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    const double scale = st->scale;
+    const float dl = static_cast<float>(s_alpha);
+    // grid-stride (at most kAccBlocks blocks): per-thread fp32 sums of <= 4 points at 1M, then the same
+    // wave / block trees; the partial count k_solve reduces stays <= kAccBlocks
+    for (int i = blockIdx.x * kBlock + tid; i < P.n; i += P.nb_acc * kBlock) {
+        const int s = P.slot[i];
+        if (s < 0) continue;
         const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
         const Slot sl = P.tab[s];
         float wx, wy, wz;
@@ -319,22 +321,28 @@ __device__ void ldlt6_solve(const double* Hin, const double* b, double* x) {
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
-__global__ __launch_bounds__(256) void k_solve(KParams P, int it, int ne_only) {
+__global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int ne_only) {
     DevState* st = P.st;
     if (st->done) return;
-    __shared__ double part[8][kNE];
+    constexpr int kQ = kSolveThreads / kNE;          // 36 partial rows per entry
+    __shared__ double part[kQ][kNE];
     __shared__ double tot[kNE];
     const int tid = threadIdx.x;
-    if (tid < 8 * kNE) {
+    if (tid < kQ * kNE) {
+        // thread t sums flat entries t, t + kQ*kNE, ... of blk_part[nb_acc][kNE]: coalesced, entry = t % kNE
         const int k = tid % kNE, q = tid / kNE;
-        double s = 0.0;
-        for (int b = q; b < P.nb; b += 8) s += P.blk_part[static_cast<size_t>(b) * kNE + k];
-        part[q][k] = s;
+        const double* src = P.blk_part + tid;
+        const int nrow = (P.nb_acc - q + kQ - 1) / kQ;
+        double s0 = 0.0, s1 = 0.0;
+        int j = 0;
+        for (; j + 1 < nrow; j += 2) { s0 += src[static_cast<size_t>(j) * kQ * kNE]; s1 += src[static_cast<size_t>(j + 1) * kQ * kNE]; }
+        if (j < nrow) s0 += src[static_cast<size_t>(j) * kQ * kNE];
+        part[q][k] = s0 + s1;
     }
     __syncthreads();
     if (tid < kNE) {
         double s = 0.0;
-        for (int q = 0; q < 8; ++q) s += part[q][tid];
+        for (int q = 0; q < kQ; ++q) s += part[q][tid];
         tot[tid] = s;
     }
     __syncthreads();

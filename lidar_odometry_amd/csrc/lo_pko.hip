@@ -244,50 +244,66 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
         __syncthreads();
     } else {
         const int nb = P.nb;
-        const int per = (nb + NT - 1) / NT;
-        const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
-        int loc = 0;
+        // (a) coalesced pass: block counts -> LDS, total count / residual sum
+        int cnt = 0;
         double lsum = 0.0;
-        for (int b = b0; b < b1; ++b) { loc += P.blk_cnt[b]; if (it == 0) lsum += P.blk_sum[b]; }
-        int inc = loc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
-        const double ws = wave_total(lsum);
-        if (lane == 63) s_iscan[wid] = inc;
-        if (lane == 0) s_dscan[wid] = ws;
+#pragma unroll 4
+        for (int b = tid; b < nb; b += NT) {
+            const int c = P.blk_cnt[b];
+            s_pre[b] = c;
+            cnt += c;
+            if (it == 0) lsum += P.blk_sum[b];
+        }
+        cnt = wave_sum(cnt);
+        lsum = wave_total(lsum);
+        if (lane == 0) { s_iscan[wid] = cnt; s_dscan[wid] = lsum; }
         __syncthreads();
         if (tid == 0) {
             int run = 0;
             double tot = 0.0;
-            for (int w = 0; w < NW; ++w) { const int c = s_iscan[w]; s_iscan[w] = run; run += c; tot += s_dscan[w]; }
+            for (int w = 0; w < NW; ++w) { run += s_iscan[w]; tot += s_dscan[w]; }
             s_nc = run;
             s_mean = run > 0 ? tot / run : 0.0;
         }
         __syncthreads();
-        int excl = s_iscan[wid] + inc - loc;
-        for (int b = b0; b < b1; ++b) { s_pre[b] = excl; excl += P.blk_cnt[b]; }
+        // (b) contiguous ranges of the counts (LDS) for the exclusive prefix; iteration 0: Chan merge of the
+        //     per-block (count, sum, M2) about the global mean, coalesced
+        const int per = (nb + NT - 1) / NT;
+        const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+        int loc = 0;
+        for (int b = b0; b < b1; ++b) loc += s_pre[b];
+        int inc = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
+        double m2 = 0.0;
         if (it == 0) {
-            // Chan merge of per-block (count, sum, M2): variance about the global mean
             const double mean = s_mean;
-            double m2 = 0.0;
-            for (int b = b0; b < b1; ++b) {
-                const int c = P.blk_cnt[b];
+#pragma unroll 4
+            for (int b = tid; b < nb; b += NT) {
+                const int c = s_pre[b];
                 if (c > 0) { const double dm = P.blk_sum[b] / c - mean; m2 += P.blk_m2[b] + c * (dm * dm); }
             }
             m2 = wave_total(m2);
-            __syncthreads();
-            if (lane == 0) s_dscan[wid] = m2;
-            __syncthreads();
-            if (tid == 0) {
-                double M2 = 0.0;
-                for (int w = 0; w < NW; ++w) M2 += s_dscan[w];
-                const double var = s_nc > 0 ? M2 / s_nc : 0.0;
-                s_scale = sqrt(var) / 6.0;                  // IterativeClosestPointOptimizer.cpp:314-315
-                if (lead) st->scale = s_scale;
-            }
-        } else if (tid == 0) {
-            s_scale = st->scale;
         }
+        __syncthreads();                                         // s_iscan / s_dscan reuse
+        if (lane == 63) s_iscan[wid] = inc;
+        if (lane == 0) s_dscan[wid] = m2;
+        __syncthreads();
+        if (tid == 0) {
+            int run = 0;
+            double M2 = 0.0;
+            for (int w = 0; w < NW; ++w) { const int c = s_iscan[w]; s_iscan[w] = run; run += c; M2 += s_dscan[w]; }
+            if (it == 0) {
+                const double var = s_nc > 0 ? M2 / s_nc : 0.0;
+                s_scale = sqrt(var) / 6.0;                      // IterativeClosestPointOptimizer.cpp:314-315
+                if (lead) st->scale = s_scale;
+            } else {
+                s_scale = st->scale;
+            }
+        }
+        __syncthreads();
+        int excl = s_iscan[wid] + inc - loc;
+        for (int b = b0; b < b1; ++b) { const int c = s_pre[b]; s_pre[b] = excl; excl += c; }
         __syncthreads();
     }
     const int nc = s_nc;

@@ -25,4 +25,5 @@ for line in open(os.path.join(ROOT, "tests", "golden", "pko_golden.jsonl")):
     t = [out[i] for i in range(7)]
     dt = [t[i + 1] - t[i] for i in range(6)]
     print(f"case {d['case']:2d} n={d['n']:6d} alpha_ok={a == d['alpha']} em_iters={out[8]:3d} km_iters={out[9]:3d} "
-          + " ".join(f"{n}={v}" for n, v in zip(names, dt)) + f" total={t[6] - t[0]}")
+          + " ".join(f"{n}={v}" for n, v in zip(names, dt)) + f" total={t[6] - t[0]}"
+          + (f" | em50: E={out[11] - out[10]} reduce={out[12] - out[11]} M={out[13] - out[12]}" if out[13] else ""))
