@@ -11,9 +11,11 @@
 //
 // Layout on the chip: the EM is a strictly sequential chain of (usually all) 100 iterations, so its latency
 // sets the kernel time.  Every workgroup of the launch fits the same GMM redundantly (identical, deterministic
-// results, no inter-workgroup traffic) with one sample per lane over NW = ceil(S/64) waves and ONE LDS
-// exchange + barrier per EM / k-means iteration; afterwards workgroup g evaluates the JS divergence for
-// alphas g+1, g+1+G, ... and writes them to global memory.  The argmin over the grid (first strict minimum,
+// results, no inter-workgroup traffic) on ONE wave holding ceil(S/64) samples per lane: each EM / k-means
+// iteration is pure VALU (permlane/DPP butterfly sums, no LDS round trip, no barrier) -- measured faster than
+// splitting the samples over two waves with one LDS exchange + barrier per iteration (scripts/pko_stamps.py).
+// Afterwards workgroup g evaluates the JS divergence for alphas g+1, g+1+G, ... and writes them to global
+// memory.  The argmin over the grid (first strict minimum,
 // as the reference loop) is taken by the consumers (k_accumulate / k_pko_finish) after the kernel boundary,
 // so no in-launch hand-off is needed.
 #include "lo_device.h"
@@ -59,60 +61,93 @@ __device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {
 #define LO_COUNT(dbg, i, v) do { } while (0)
 #endif
 
-// Block-wide sums of NV <= 8 values per thread.  Intra-wave step is a transposed reduction: every lane
-// stores its NV values to its wave's LDS tile, lane l then adds the 8 entries [l>>3][8*(l&7) .. +7] and
-// three DPP steps finish each 8-lane group, so value q's wave total sits in lanes 8q..8q+7 (~45
-// instructions instead of NV x 6 DPP rounds).  Per-wave totals go through one more LDS tile and ONE
-// __syncthreads; the sum over waves is in fixed order.  part[] is double-buffered by the parity bit.
-template <int NW>
-struct PkoScratch {
-    double tile[NW][8][64];
-    double part[2][NW][8];
-};
-
-template <int NW, int NV>
-__device__ __forceinline__ void block_totals(double (&v)[NV], PkoScratch<NW>* sc, int& buf) {
-    static_assert(NV <= 8, "transposed reduction handles up to 8 values");
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < NV; ++q) sc->tile[wid][q][lane] = v[q];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int q = lane >> 3, c = (lane & 7) * 8;
-    double t = 0.0;
-    if (q < NV) {
-        const double* row = &sc->tile[wid][q][c];
-        const double a0 = row[0] + row[1], a1 = row[2] + row[3], a2 = row[4] + row[5], a3 = row[6] + row[7];
-        t = (a0 + a1) + (a2 + a3);
-    }
-    t += dpp64<0xB1, 0xf>(t);    // quad_perm [1,0,3,2]
-    t += dpp64<0x4E, 0xf>(t);    // quad_perm [2,3,0,1]
-    t += dpp64<0x141, 0xf>(t);   // row_half_mirror: 8-lane group total in every lane of the group
-    if (lane < NV * 8 && (lane & 7) == 0) sc->part[buf][wid][lane >> 3] = t;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        double u = sc->part[buf][0][k];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) u += sc->part[buf][w][k];
-        v[k] = u;
-    }
-    buf ^= 1;
+// exp(y) for y <= 0 or NaN (the E-step exponent -(d^2) * 0.5 / var): Cody-Waite reduction by ln2 and a
+// degree-12 Taylor polynomial on |r| <= ln2/2; <= 2 ulp from glibc exp over [-745, 0] (checked on 2e7 points).
+// No overflow branch is needed for y <= 0, and the underflow to 0 falls out of v_ldexp_f64.
+__device__ __forceinline__ double exp_nonpos(double y) {
+    const double n = rint(y * 0x1.71547652b82fep+0);
+    double r = fma(-n, 0x1.62e42fefa39efp-1, y);
+    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
+    double p = 0x1.1eed8eff8d898p-29;
+    p = fma(p, r, 0x1.ae64567f544e4p-26);
+    p = fma(p, r, 0x1.27e4fb7789f5cp-22);
+    p = fma(p, r, 0x1.71de3a556c734p-19);
+    p = fma(p, r, 0x1.a01a01a01a01ap-16);
+    p = fma(p, r, 0x1.a01a01a01a01ap-13);
+    p = fma(p, r, 0x1.6c16c16c16c17p-10);
+    p = fma(p, r, 0x1.1111111111111p-7);
+    p = fma(p, r, 0x1.5555555555555p-5);
+    p = fma(p, r, 0x1.5555555555555p-3);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, static_cast<int>(n));
 }
 
-// fit_gmm (AdaptiveMEstimator.cpp:294-485) on S <= 64*NW samples held one per thread.
-// The E-step constants w_j / sqrt(2 pi var_j) and 0.5 / var_j are formed once per EM iteration, reciprocals
-// are Newton-refined hardware estimates and sums are trees: results move by a few ulp against the
-// reference's sequential evaluation.  The device PKO is checked for identical alpha against the reference's
-// golden vectors (tests/test_gpu_parity.py::test_pko_alpha_matches_reference_golden).
-template <int NW, int K>
-__device__ void gmm_fit(const double* s_sd, int S, const int32_t* draws, PkoScratch<NW>* sc, double* gmm,
-                        unsigned long long* dbg) {
-    static_assert(3 * K - 1 <= 8 && 2 * K - 1 <= 8, "partials");
-    const int tid = threadIdx.x;
-    const bool have = tid < S;
-    const double x = have ? s_sd[tid] : 0.0;
-    int buf = 0;
+// ---- single-wave reductions ------------------------------------------------------------------------
+// Sum of 8 fp64 values over the 64 lanes of a wave without LDS: a butterfly that halves the values per lane
+// while halving the lane group (v_permlane32_swap: lanes 32-63 <-> 0-31, v_permlane16_swap: odd <-> even
+// 16-lane rows, DPP row_ror:8), after which value q sits in lanes 8q..8q+7; three DPP steps finish each
+// 8-lane group and v_readlane broadcasts the totals (wave-uniform results).  ~50 VALU ops, no waits.
+__device__ __forceinline__ void pl32_swap(double& a, double& b) {   // a <- [a_lo | b_lo], b <- [a_hi | b_hi]
+    const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(__double2loint(a)),
+                                                     static_cast<unsigned>(__double2loint(b)), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(__double2hiint(a)),
+                                                     static_cast<unsigned>(__double2hiint(b)), false, false);
+    a = __hiloint2double(static_cast<int>(hi[0]), static_cast<int>(lo[0]));
+    b = __hiloint2double(static_cast<int>(hi[1]), static_cast<int>(lo[1]));
+}
+__device__ __forceinline__ void pl16_swap(double& a, double& b) {   // a <- [a0 b0 a2 b2], b <- [a1 b1 a3 b3] (rows)
+    const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(__double2loint(a)),
+                                                     static_cast<unsigned>(__double2loint(b)), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(__double2hiint(a)),
+                                                     static_cast<unsigned>(__double2hiint(b)), false, false);
+    a = __hiloint2double(static_cast<int>(hi[0]), static_cast<int>(lo[0]));
+    b = __hiloint2double(static_cast<int>(hi[1]), static_cast<int>(lo[1]));
+}
+__device__ __forceinline__ double readlane64(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+template <int NV>
+__device__ __forceinline__ void wave_totals8(double (&v)[NV]) {
+    static_assert(NV >= 1 && NV <= 8, "butterfly handles up to 8 values");
+    double u[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) u[q] = q < NV ? v[q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { pl32_swap(u[q], u[q + 4]); u[q] += u[q + 4]; }   // lo: v_q, hi: v_{q+4}
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { pl16_swap(u[q], u[q + 2]); u[q] += u[q + 2]; }   // rows: v_q v_{q+2} v_{q+4} v_{q+6}
+    const bool up = (threadIdx.x & 8) != 0;
+    double t = up ? u[1] : u[0];
+    const double o = up ? u[0] : u[1];
+    t += dpp64<0x128, 0xf>(o);      // row_ror:8 = lane ^ 8 inside a row -> value q in lanes 8q..8q+7
+    t += dpp64<0xB1, 0xf>(t);       // quad_perm [1,0,3,2]
+    t += dpp64<0x4E, 0xf>(t);       // quad_perm [2,3,0,1]
+    t += dpp64<0x141, 0xf>(t);      // row_half_mirror: 8-lane group total
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 8 * q);
+}
+
+// fit_gmm (AdaptiveMEstimator.cpp:294-485) by ONE wave holding SPL samples per lane (sample s*64 + lane).
+// The EM is a strictly sequential chain, so it runs where the chain is shortest: a single wave with no
+// LDS round trip and no barrier per iteration (wave_totals8), SPL independent exp chains per component for
+// ILP.  The E-step constants w_j / sqrt(2 pi var_j) and 0.5 / var_j come from one Newton-refined rsq per
+// component; reciprocals are Newton-refined hardware estimates and sums are trees, so results move by a
+// few ulp against the reference's sequential evaluation.  The device PKO is checked for identical alpha
+// against the reference's golden vectors (tests/test_gpu_parity.py::test_pko_alpha_matches_reference_golden).
+template <int K, int SPL>
+__device__ __forceinline__ void gmm_fit_w(const double* s_sd, int S, const int32_t* draws, double* gmm, unsigned long long* dbg) {
+    static_assert(3 * K - 1 <= 8, "partials");
+    const int lane = threadIdx.x & 63;
+    double x[SPL];
+    bool have[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        have[s] = lane + 64 * s < S;
+        x[s] = have[s] ? s_sd[lane + 64 * s] : 0.0;
+    }
     double mu[K], cnt[K];
     mu[0] = 0.0;
 #pragma unroll
@@ -122,18 +157,23 @@ __device__ void gmm_fit(const double* s_sd, int S, const int32_t* draws, PkoScra
 
     // ---- k-means until the means repeat exactly (:351-389) ----
     for (int guard = 0; guard < 100000; ++guard) {
-        double md = DBL_MAX;
-        int ci = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) { const double d = fabs(x - mu[j]); if (d < md) { md = d; ci = j; } }
         double v[2 * K - 1];                               // counts 0..K-1, sums 1..K-1
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool mine = have && ci == j;
-            v[j] = mine ? 1.0 : 0.0;
-            if (j > 0) v[K + j - 1] = mine ? x : 0.0;
+        for (int q = 0; q < 2 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double md = DBL_MAX;
+            int ci = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) { const double d = fabs(x[s] - mu[j]); if (d < md) { md = d; ci = j; } }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const bool mine = have[s] && ci == j;
+                v[j] += mine ? 1.0 : 0.0;
+                if (j > 0) v[K + j - 1] += mine ? x[s] : 0.0;
+            }
         }
-        block_totals<NW, 2 * K - 1>(v, sc, buf);
+        wave_totals8<2 * K - 1>(v);
         bool eq = true;
         double nm[K];
 #pragma unroll
@@ -149,45 +189,55 @@ __device__ void gmm_fit(const double* s_sd, int S, const int32_t* draws, PkoScra
     }
     LO_STAMP(dbg, 3);
     // ---- initial variance of the sample (:392-399), weights from cluster sizes (:402-410) ----
-    double m1[1] = {have ? x : 0.0};
-    block_totals<NW, 1>(m1, sc, buf);
-    const double mean = m1[0] / S;
-    double m2[1] = {have ? (x - mean) * (x - mean) : 0.0};
-    block_totals<NW, 1>(m2, sc, buf);
-    const double iv = m2[0] / S;
+    double m1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m1 += have[s] ? x[s] : 0.0;
+    const double mean = wave_total(m1) / S;
+    double m2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m2 += have[s] ? (x[s] - mean) * (x[s] - mean) : 0.0;
+    const double iv = wave_total(m2) / S;
     const double invS = 1.0 / static_cast<double>(S);
+    constexpr double kInvSqrt2Pi = 0.3989422804014327;     // 1 / sqrt(2 pi)
     double w[K], var[K], ca[K], cb[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         var[j] = iv;
         w[j] = cnt[j] / static_cast<double>(S);
-        ca[j] = w[j] * rsq64(2.0 * M_PI * iv);
-        cb[j] = 0.5 * rcp64(iv);
+        const double rs = rsq64(iv);
+        // gaussian_pdf returns 0 for var <= 0 (:677): ca = 0, cb = 0 gives exactly 0 for every sample
+        ca[j] = (iv <= 0.0) ? 0.0 : w[j] * (rs * kInvSqrt2Pi);
+        cb[j] = (iv <= 0.0) ? 0.0 : 0.5 * (rs * rs);
     }
     LO_STAMP(dbg, 4);
 
     // ---- EM, <= 100 iterations, tolerance 1e-6 on the summed |d mean| of components >= 1 (:413-484) ----
-    // One reduction round per iteration: N_j, sum r x (j >= 1) and sum r (x - c_j)^2 about the previous
-    // mean c_j; var_j = sum r (x - c_j)^2 / N_j - (mu_j - c_j)^2 (the two-pass sum up to rounding).
+    // One reduction per iteration: N_j, sum r x (j >= 1) and sum r (x - c_j)^2 about the previous mean c_j;
+    // var_j = sum r (x - c_j)^2 / N_j - (mu_j - c_j)^2 (the two-pass sum up to rounding).  var_j >= 1e-6 (or
+    // NaN) after the first M-step, so the var <= 0 branch of gaussian_pdf only matters before it.
     for (int em = 0; em < 100; ++em) {
-        double p[K], d[K], sr = 0.0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            d[j] = x - mu[j];
-            const double e = exp(-((d[j] * d[j]) * cb[j]));
-            p[j] = (var[j] <= 0.0) ? 0.0 : ca[j] * e;      // gaussian_pdf returns 0 for var <= 0
-            sr += p[j];
-        }
-        const double isr = rcp64(sr);
         double v[3 * K - 1];                               // N_j | sum r x (j>=1) | sum r d^2
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const double r = p[j] * isr;
-            v[j] = have ? r : 0.0;
-            if (j > 0) v[K + j - 1] = have ? r * x : 0.0;
-            v[2 * K - 1 + j] = have ? (r * d[j]) * d[j] : 0.0;
+        for (int q = 0; q < 3 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double p[K], d[K], sr = 0.0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                d[j] = x[s] - mu[j];
+                p[j] = ca[j] * exp_nonpos(-((d[j] * d[j]) * cb[j]));
+                sr += p[j];
+            }
+            const double isr = have[s] ? rcp64(sr) : 0.0;  // empty slots contribute exactly 0
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const double r = p[j] * isr;
+                v[j] += r;
+                if (j > 0) v[K + j - 1] += r * x[s];
+                v[2 * K - 1 + j] += (r * d[j]) * d[j];
+            }
         }
-        block_totals<NW, 3 * K - 1>(v, sc, buf);
+        wave_totals8<3 * K - 1>(v);
         double change = 0.0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -201,17 +251,25 @@ __device__ void gmm_fit(const double* s_sd, int S, const int32_t* draws, PkoScra
             w[j] = Nk * invS;
             mu[j] = nmu;
             var[j] = nv;
-            ca[j] = w[j] * rsq64(2.0 * M_PI * nv);
-            cb[j] = 0.5 * rcp64(nv);
+            const double rs = rsq64(nv);
+            ca[j] = w[j] * (rs * kInvSqrt2Pi);
+            cb[j] = 0.5 * (rs * rs);
         }
         LO_COUNT(dbg, 8, em + 1);
         if (change < 1e-6) break;
     }
     LO_STAMP(dbg, 5);
-    if (tid == 0) {
+    if (lane == 0) {
 #pragma unroll
         for (int j = 0; j < K; ++j) { gmm[j] = w[j]; gmm[K + j] = mu[j]; gmm[2 * K + j] = var[j]; }
     }
+}
+
+template <int K>
+__device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm, unsigned long long* dbg) {
+    if (S <= 64) gmm_fit_w<K, 1>(s_sd, S, draws, gmm, dbg);
+    else if (S <= 128) gmm_fit_w<K, 2>(s_sd, S, draws, gmm, dbg);
+    else gmm_fit_w<K, 4>(s_sd, S, draws, gmm, dbg);
 }
 
 template <int NW>
@@ -226,7 +284,6 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     LO_STAMP(dbg, 0);
     __shared__ int s_pre[kMaxBlocks];                // 64 KB: exclusive prefix of block counts
     __shared__ double s_sd[64 * NW];
-    __shared__ PkoScratch<NW> s_scratch;
     __shared__ double s_gmm[3 * kMaxK];
     __shared__ double s_P[100];
     __shared__ double s_jsd[kPkoAlphaPerWG][100];
@@ -355,10 +412,12 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     // ---- 3. GMM ----
     const int D = P.K > 1 ? P.K - 1 : 1;
     const int32_t* draws = P.km_draws + S * D;
-    switch (P.K) {
-        case 1: gmm_fit<NW, 1>(s_sd, S, draws, &s_scratch, s_gmm, dbg); break;
-        case 2: gmm_fit<NW, 2>(s_sd, S, draws, &s_scratch, s_gmm, dbg); break;
-        default: gmm_fit<NW, 3>(s_sd, S, draws, &s_scratch, s_gmm, dbg); break;
+    if (wid == 0) {                                             // one wave: see gmm_fit_w
+        switch (P.K) {
+            case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, dbg); break;
+            case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, dbg); break;
+            default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, dbg); break;
+        }
     }
     __syncthreads();
     if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
@@ -392,11 +451,16 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
             const int ai = a0 + tid * G;
             if (ai <= P.NA) {
                 double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
-                for (int b = 0; b < 100; ++b) {
-                    const double v = s_jsd[tid][b];
-                    if (isnan(v)) continue;
-                    cost += v;
-                    cnt += 1.0;
+                for (int b0 = 0; b0 < 100; b0 += 10) {           // batched LDS reads, then the serial adds
+                    double vb[10];
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) vb[q] = s_jsd[tid][b0 + q];
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) {
+                        const bool ok = !isnan(vb[q]);
+                        cost += ok ? vb[q] : 0.0;                // cost starts at +0: adding +0 == skipping
+                        cnt += ok ? 1.0 : 0.0;
+                    }
                 }
                 P.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }

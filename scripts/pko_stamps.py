@@ -8,7 +8,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LO_ICP_LIB"] = os.path.join(ROOT, "lidar_odometry_amd", "liblo_icp_diag.so")
+os.environ["LO_ICP_LIB"] = os.environ.get("LO_DIAG_LIB", os.path.join(ROOT, "lidar_odometry_amd", "liblo_icp_diag.so"))
 sys.path.insert(0, ROOT)
 from lidar_odometry_amd import IterativeClosestPointOptimizer, lib  # noqa: E402
 
