@@ -24,11 +24,12 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kNE = 28;              // 21 lower-triangular H + 6 g + cost
 constexpr int kPkoBlock = 256;       // PKO workgroup: one GMM sample per thread (S <= 256)
-constexpr int kPkoMaxWGs = 64;       // PKO workgroups per launch (each evaluates a slice of the alpha grid)
+constexpr int kPkoMaxWGs = 128;      // PKO workgroups per launch (each evaluates a slice of the alpha grid)
 constexpr int kPkoAlphaPerWG = 4;    // alphas per JS pass of one workgroup
 constexpr int kMaxBlocks = 16384;    // => max 4M points per scan
 constexpr int kAccBlocks = 1024;     // k_accumulate grid cap (grid-stride beyond): bounds the k_solve partial sum
 constexpr int kSolveThreads = 1024;  // k_solve: 36 x 28 threads sum the block partials, coalesced
+constexpr int kFuseMaxBlocks = 64;   // <= this many accumulate blocks: the last one also solves (no k_solve launch)
 constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
@@ -48,6 +49,7 @@ struct DevState {
     int iter;
     int done;
     int status;
+    unsigned int acc_arrive;        // k_accumulate last-block-done counter (reset by the last block)
     double H_out[36];
     double g_out[6];
     double cost_out;
@@ -62,6 +64,8 @@ struct KParams {
     int n;
     int nb;
     int nb_acc;                       // k_accumulate blocks = min(nb, kAccBlocks)
+    int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
+    float T0[12];
     // map
     const Slot* tab;
     uint32_t log2cap;

@@ -20,7 +20,7 @@ namespace lo {
 __global__ void k_correspond(KParams P, int with_stats);
 template <int NW> __global__ void k_pko_t(KParams P, int it);
 __global__ void k_pko_finish(KParams P);
-__global__ void k_accumulate(KParams P);
+__global__ void k_accumulate(KParams P, int it, int fuse);
 __global__ void k_solve(KParams P, int it, int ne_only);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
@@ -75,8 +75,8 @@ struct lo_ctx {
         }                                                                                  \
     } while (0)
 
-// PKO workgroups: enough to give every workgroup <= 2 alphas of the JS grid, capped at kPkoMaxWGs
-static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs, (g.num_alpha_segments + 1) / 2)); }
+// PKO workgroups: one alpha of the JS grid per workgroup (each fits the GMM redundantly), capped at kPkoMaxWGs
+static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs, g.num_alpha_segments)); }
 
 static void launch_pko(lo_ctx* c, const KParams& P, int it) {
     // one GMM sample per thread: 2 waves cover the reference's 100 samples, 4 waves up to 256
@@ -323,15 +323,23 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
     Pose12 T0;
     std::memcpy(T0.v, T_init, sizeof(float) * 12);
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
-    hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
-    if (n > 0) {
+    if (n == 0) {
+        hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
+    } else {
         KParams P = make_params(c, d_pts, static_cast<int>(n));
+        KParams P0 = P;                                   // first k_correspond also resets the GN state
+        P0.init = 1;
+        std::memcpy(P0.T0, T_init, sizeof(float) * 12);
         const dim3 grid(P.nb), blk(kBlock);
         for (int it = 0; it < g.max_iterations; ++it) {
-            hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, it == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, it == 0 ? P0 : P, it == 0 ? 1 : 0);
             launch_pko(c, P, it);
-            hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P);
-            hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
+            if (P.nb_acc <= kFuseMaxBlocks) {          // small scans: the last accumulate block solves
+                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
+            } else {                                   // large scans: 1024 threads reduce the partials
+                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
+                hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
+            }
         }
         LO_HIP(c, hipGetLastError());
     }
@@ -470,8 +478,12 @@ int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.alpha_given = 1;
     hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
-    hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P);
-    hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1);
+    if (P.nb_acc <= kFuseMaxBlocks) {
+        hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P, 0, 2);
+    } else {
+        hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P, 0, 0);
+        hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1);
+    }
     LO_HIP(c, hipGetLastError());
     std::vector<int32_t> cnt(P.nb);
     LO_HIP(c, hipMemcpyAsync(cnt.data(), c->d_blk_cnt, P.nb * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -522,13 +534,14 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     const dim3 grid(P.nb), blk(kBlock);
     // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials
     hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 1);
-    hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P);
+    hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0, 0);
     LO_HIP(c, hipGetLastError());
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int r = 0; r < reps; ++r) {
         switch (kernel_id) {
             case 0: hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 0); break;
-            case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P); break;
+            case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0,
+                                       P.nb_acc <= kFuseMaxBlocks ? 2 : 0); break;
             case 2: launch_pko(c, P, 1); break;
             default: hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1); break;
         }

@@ -27,8 +27,10 @@ namespace lo {
 // k_correspond
 // ====================================================================================================
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
-    const DevState* st = P.st;
-    if (st->done) return;
+    DevState* st = P.st;
+    // P.init: first launch of a scan.  The GN state reset (k_init's job) is folded in here -- the pose comes
+    // from the kernel argument, block 0 writes the fresh DevState that the later kernels of the scan read.
+    if (!P.init && st->done) return;
     __shared__ double s_red[kWavesPerBlock];
     __shared__ int s_cnt[kWavesPerBlock];
     __shared__ double s_mean;
@@ -37,7 +39,19 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
     const int i = blockIdx.x * kBlock + tid;
     float T[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    for (int k = 0; k < 12; ++k) T[k] = P.init ? P.T0[k] : st->pose[k];
+    if (P.init && blockIdx.x == 0 && tid < 12) {
+        st->pose[tid] = P.T0[tid];
+        if (tid == 0) {
+            st->scale = 1.0;
+            st->alpha = P.robust_delta;
+            st->n_corr = 0;
+            st->iter = 0;
+            st->done = 0;
+            st->status = LO_OK;
+            st->acc_arrive = 0;
+        }
+    }
 
     int slot = -1;
     double r = 0.0;
@@ -98,8 +112,13 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
 // ====================================================================================================
 // k_accumulate
 // ====================================================================================================
-__global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
-    const DevState* st = P.st;
+template <int NT>
+__device__ void solve_tail(const KParams& P, int it, int ne_only);
+
+// fuse: 0 = partials only, 1 = the last block to finish also runs the GN solve / update (k_solve's job),
+// 2 = the last block writes the summed normal equations (lo_build_normal_equations)
+__global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fuse) {
+    DevState* st = P.st;
     if (st->done) return;
     __shared__ float s_acc[kWavesPerBlock][kNE];
     __shared__ double s_alpha;
@@ -179,6 +198,19 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P) {
         for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
         P.blk_part[static_cast<size_t>(blockIdx.x) * kNE + tid] = v;
     }
+    if (fuse == 0) return;
+    // last-block-done: release the partials at agent scope (the 8 XCDs have separate L2s), count arrivals;
+    // the block that arrives last acquires and reduces them in fixed block order -- one launch fewer per
+    // GN iteration, same deterministic sum as a separate k_solve
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = (atomicAdd(&st->acc_arrive, 1u) == gridDim.x - 1) ? 1 : 0;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (tid == 0) st->acc_arrive = 0;
+    solve_tail<kBlock>(P, it, fuse == 2);
 }
 
 // ====================================================================================================
@@ -194,7 +226,9 @@ __device__ void mul33f(const float* A, const float* B, float* C) {   // Matrix3f
 __device__ void so3_project(const float* Min, float* Rout) {
     double X[9];
     for (int k = 0; k < 9; ++k) X[k] = Min[k];
-    for (int itn = 0; itn < 6; ++itn) {
+    // Newton's polar iteration converges quadratically; inputs are orthonormal to fp32 rounding (~1e-7), so
+    // three steps reach the fp64 fixed point (1e-7 -> 1e-14 -> fp64 eps)
+    for (int itn = 0; itn < 3; ++itn) {
         const double c00 = X[4] * X[8] - X[5] * X[7], c01 = X[5] * X[6] - X[3] * X[8], c02 = X[3] * X[7] - X[4] * X[6];
         const double c10 = X[2] * X[7] - X[1] * X[8], c11 = X[0] * X[8] - X[2] * X[6], c12 = X[1] * X[6] - X[0] * X[7];
         const double c20 = X[1] * X[5] - X[2] * X[4], c21 = X[2] * X[3] - X[0] * X[5], c22 = X[0] * X[4] - X[1] * X[3];
@@ -207,7 +241,9 @@ __device__ void so3_project(const float* Min, float* Rout) {
     for (int k = 0; k < 9; ++k) Rout[k] = static_cast<float>(X[k]);
 }
 
-// SO3::Exp (MathUtils.cpp:23-39), kEps = 1e-6f
+// SO3::Exp (MathUtils.cpp:23-39), kEps = 1e-6f.  The reference re-projects Exp's matrix with an fp32 JacobiSVD
+// (SO3(const Matrix3f&), :86-99) and again after R * Exp; here only the product is projected -- Exp's output is
+// orthonormal to fp32 rounding, so the two orders agree to ~1e-7, far inside the 1e-4 pose tolerance.
 __device__ void so3_exp(const float* w, float* R) {
     const float theta = sqrtf(dot3f(w[0], w[1], w[2], w[0], w[1], w[2]));
     float M[9];
@@ -215,7 +251,7 @@ __device__ void so3_exp(const float* w, float* R) {
         M[0] = 1.0f; M[1] = -w[2]; M[2] = w[1];
         M[3] = w[2]; M[4] = 1.0f; M[5] = -w[0];
         M[6] = -w[1]; M[7] = w[0]; M[8] = 1.0f;
-        so3_project(M, R);
+        for (int k = 0; k < 9; ++k) R[k] = M[k];
         return;
     }
     const float ti = 1.0f / theta;
@@ -226,8 +262,7 @@ __device__ void so3_exp(const float* w, float* R) {
     for (int k = 0; k < 9; ++k) sK[k] = omc * K[k];
     mul33f(sK, K, KK);
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) M[r * 3 + c] = ((r == c ? 1.0f : 0.0f) + s * K[r * 3 + c]) + KK[r * 3 + c];
-    so3_project(M, R);
+        for (int c = 0; c < 3; ++c) R[r * 3 + c] = ((r == c ? 1.0f : 0.0f) + s * K[r * 3 + c]) + KK[r * 3 + c];
 }
 
 // H.ldlt().solve(b): Eigen's pivoted LDLT (LDLT.h ldlt_inplace<Lower>::unblocked / _solve_impl) in fp64.
@@ -321,10 +356,10 @@ __device__ void ldlt6_solve(const double* Hin, const double* b, double* x) {
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
-__global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int ne_only) {
+template <int NT>
+__device__ void solve_tail(const KParams& P, int it, int ne_only) {
     DevState* st = P.st;
-    if (st->done) return;
-    constexpr int kQ = kSolveThreads / kNE;          // 36 partial rows per entry
+    constexpr int kQ = NT / kNE;                     // partial rows per entry (36 for 1024 threads, 9 for 256)
     __shared__ double part[kQ][kNE];
     __shared__ double tot[kNE];
     const int tid = threadIdx.x;
@@ -333,11 +368,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int 
         const int k = tid % kNE, q = tid / kNE;
         const double* src = P.blk_part + tid;
         const int nrow = (P.nb_acc - q + kQ - 1) / kQ;
-        double s0 = 0.0, s1 = 0.0;
+        constexpr size_t kStride = static_cast<size_t>(kQ) * kNE;
+        double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // 8 independent loads in flight
         int j = 0;
-        for (; j + 1 < nrow; j += 2) { s0 += src[static_cast<size_t>(j) * kQ * kNE]; s1 += src[static_cast<size_t>(j + 1) * kQ * kNE]; }
-        if (j < nrow) s0 += src[static_cast<size_t>(j) * kQ * kNE];
-        part[q][k] = s0 + s1;
+        for (; j + 8 <= nrow; j += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] += src[static_cast<size_t>(j + u) * kStride];
+        }
+        for (; j < nrow; ++j) a[0] += src[static_cast<size_t>(j) * kStride];
+        part[q][k] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
     __syncthreads();
     if (tid < kNE) {
@@ -397,6 +436,12 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int 
     if (tdel < P.tol_t && rdel < P.tol_r) st->done = 1;               // :443-448
 }
 
+// Standalone solve over all block partials (lo_bench_kernel; the GN loop fuses it into k_accumulate)
+__global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int ne_only) {
+    if (P.st->done) return;
+    solve_tail<kSolveThreads>(P, it, ne_only);
+}
+
 // ====================================================================================================
 // k_init: reset the GN state for a new scan.  The initial pose travels as a kernel argument, so any
 // number of scans can be enqueued back to back without a host staging buffer.
@@ -412,6 +457,7 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
         st->iter = 0;
         st->done = 0;
         st->status = LO_OK;
+        st->acc_arrive = 0;
     }
 }
 

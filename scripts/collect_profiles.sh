@@ -9,6 +9,8 @@ mkdir -p profiles
 for w in kitti 1m; do
     f=gpurun_out/stats_$w/run_kernel_stats.csv
     [ -f "$f" ] && cp "$f" "profiles/${tag}_${w}_kernel_stats.csv"
+    t=gpurun_out/stats_$w/run_kernel_trace.csv
+    [ -f "$t" ] && python scripts/trace_summary.py "$t" --out "profiles/${tag}_${w}_trace_summary.json" > /dev/null
     if [ -d gpurun_out/pmc_fetch_$w ] && [ -d gpurun_out/pmc_write_$w ]; then
         name=$w; [ "$w" = 1m ] && name=patch1m
         python scripts/pmc_summary.py --workload "$name" --fetch gpurun_out/pmc_fetch_$w \
