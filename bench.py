@@ -101,7 +101,15 @@ def build_patch1m(rank: int):
             "keyframes": [(mp, np.zeros(3))]}
 
 
-WORKLOADS = {"kitti": build_kitti, "mid360": build_mid360, "patch1m": build_patch1m}
+def build_kitti_kdtree(rank: int):
+    wl = build_kitti(rank)
+    wl["name"] = "KITTI-07-like HDL-64 scan, KDTree correspondence variant (5-NN plane fit), config/kitti.yaml"
+    wl["kdtree"] = True
+    return wl
+
+
+WORKLOADS = {"kitti": build_kitti, "kitti_kdtree": build_kitti_kdtree, "mid360": build_mid360,
+             "patch1m": build_patch1m}
 
 
 def pose12(T):
@@ -121,7 +129,7 @@ def cpu_baseline(wl, budget_s: float):
     t0 = time.perf_counter()
     while True:
         i = n_scans % len(scans)
-        ok, To, it, _ = oracle.icp_optimize(m, scans[i], inits[i])
+        ok, To, it, _ = oracle.icp_optimize(m, scans[i], inits[i], kdtree=wl.get("kdtree", False))
         n_scans += 1
         n_iters += it
         el = time.perf_counter() - t0
@@ -174,8 +182,9 @@ def main():
     log(f"[rank {rank}] data built in {time.perf_counter() - t_data:.1f} s: {len(wl['scans'])} scans, "
         f"avg {np.mean([len(s) for s in wl['scans']]):.0f} pts, {wl['vm'].surfel_count()} surfels")
     max_pts = max(len(s) for s in wl["scans"])
-    icp = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
-                                         device=local, max_points=max_pts)
+    kd = bool(wl.get("kdtree", False))
+    icp = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not kd), AdaptiveMEstimatorConfig(),
+                                         MapGeometry(voxel_size=wl["voxel"]), device=local, max_points=max_pts)
     L = lib()
     stream = torch.cuda.current_stream(dev)
     L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
@@ -229,7 +238,8 @@ def main():
     # live per-kernel device times (HIP events around back-to-back launches on this context's stream)
     i0 = int(np.argmax([len(s) for s in wl["scans"]]))
     kern_us = {}
-    for kid, name in enumerate(("k_correspond", "k_accumulate", "k_pko", "k_solve")):
+    stage0 = "k_knn+k_knn_brute+k_plane" if kd else "k_correspond"
+    for kid, name in enumerate((stage0, "k_accumulate", "k_pko", "k_solve")):
         ms = C.c_float(0.0)
         reps = 200 if kid != 2 else 50
         rc = L.lo_bench_kernel(icp.ctx, C.c_void_p(d_scans[i0].data_ptr()), d_scans[i0].shape[0], fptr(inits[i0]),
@@ -242,7 +252,13 @@ def main():
     # algorithmic bytes per k_correspond launch: per point 12 B point + 8 B key probe + 24 B payload on a hit
     # (lower-bounded by the accepted fraction v) + 4 B slot index written + 1/8 B validity ballot
     alg_bytes = n0 * (12 + 8 + 24 * v + 4 + 0.125)
-    t_corr = kern_us["k_correspond"] * 1e-6
+    corr_kernel = "k_correspond"
+    if kd:
+        # KDTree stage (k_knn + k_knn_brute + k_plane): per point 12 B point + 5 x 16 B neighbour centroids +
+        # 20 B neighbour list written and re-read + 4 B slot; per accepted point 32 B plane + 8 B residual
+        alg_bytes = n0 * (12 + 80 + 40 + 4 + 0.125 + 40 * v)
+        corr_kernel = stage0
+    t_corr = kern_us[stage0] * 1e-6
     achieved = alg_bytes / t_corr / 1e9
     traffic = read_pmc_traffic(args.config)
     # where a step's device time goes: isolated kernel time x launches per scan (working launches only)
@@ -274,6 +290,7 @@ def main():
         "data": "synthetic (deterministic raycast scenes; no dataset reachable offline)",
         "config": {"workload": wl["name"], "points_per_scan_avg": float(np.mean([len(s) for s in wl["scans"]])),
                    "distinct_scans": len(wl["scans"]), "map_surfels": wl["vm"].surfel_count(),
+                   "map_l0_points": wl["vm"].l0_count(), "correspondence": "kdtree 5-NN" if kd else "L1 surfel",
                    "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),
                    "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step)" if world > 1
                    else "single GPU, one HIP stream"},
@@ -286,7 +303,7 @@ def main():
                                        "(sequential 100-iteration EM), not HBM/MFMA-bound (DESIGN.md)"},
         "pcie_inclusive": {"value": pcie_rate, "unit": "scans/s", "scans": n_pc,
                            "path": "lo_icp_optimize on host buffers (H2D points, D2H pose+logs, sync per scan)"},
-        "roofline": {"kernel": "k_correspond", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": corr_kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes, "points_per_launch": int(n0), "valid_fraction": v},

@@ -60,7 +60,7 @@ typedef struct lo_config {
     int    pko_kernel_cauchy;            /* 0: "huber" (kitti.yaml:51) */
     float  voxel_size;                   /* map_voxel_size 0.5 */
     int    hierarchy_factor;             /* 3 */
-    int    use_surfel_correspondence;    /* 1 */
+    int    use_surfel_correspondence;    /* 1: L1 surfel lookup; 0: KDTree variant (5-NN plane fit, :647-767) */
     int    max_points;                   /* scan capacity (points per optimize call) */
 } lo_config;
 
@@ -94,6 +94,7 @@ lo_ctx*     lo_create(const lo_config* cfg, int device, int* err);
 void        lo_destroy(lo_ctx* ctx);
 const char* lo_last_error(const lo_ctx* ctx);
 int         lo_device(const lo_ctx* ctx);
+int         lo_get_config(const lo_ctx* ctx, lo_config* out);   /* the configuration the context was built with */
 
 /* ---- map side ----
  * Replaces the map state read by VoxelMap::GetSurfelAtPoint: the L1 voxels with has_surfel == true.
@@ -101,6 +102,13 @@ int         lo_device(const lo_ctx* ctx);
  * Full upload; call again after every VoxelMap::UpdateVoxelMap (Estimator.cpp:457). */
 int lo_map_set_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids, size_t m);
 size_t lo_map_surfel_count(const lo_ctx* ctx);
+
+/* KDTree variant (use_surfel_correspondence = 0): the map point cloud the reference's kd-tree indexes,
+ * VoxelMap::GetPointCloud (VoxelMap.cpp:388-403) = L0 centroids in L0 order.  Replaces
+ * VoxelMap::RebuildKdTree (:420-438, called at Estimator.cpp:461) with a device grid built from it.
+ * Neighbour ties are broken by this order (index).  LO_ERR_STATE on a surfel-mode context. */
+int lo_map_set_points(lo_ctx* ctx, const float* xyz, size_t m);
+size_t lo_map_point_count(const lo_ctx* ctx);
 
 /* ---- the optimize boundary ----
  * Same contract as IterativeClosestPointOptimizer::optimize: GN to convergence / max_iterations.

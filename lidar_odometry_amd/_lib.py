@@ -22,7 +22,8 @@ LO_MAX_ITERS = 64
 # Every symbol include/lo_icp.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
-    "lo_device", "lo_map_set_surfels", "lo_map_surfel_count", "lo_icp_optimize", "lo_icp_optimize_async",
+    "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
+    "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_async",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
     # include/lo_map.h
@@ -79,6 +80,12 @@ def lib():
     L.lo_map_set_surfels.argtypes = [vp, ip, fp, fp, C.c_size_t]
     L.lo_map_surfel_count.restype = C.c_size_t
     L.lo_map_surfel_count.argtypes = [vp]
+    L.lo_map_set_points.restype = C.c_int
+    L.lo_map_set_points.argtypes = [vp, C.POINTER(C.c_float), C.c_size_t]
+    L.lo_map_point_count.restype = C.c_size_t
+    L.lo_map_point_count.argtypes = [vp]
+    L.lo_get_config.restype = C.c_int
+    L.lo_get_config.argtypes = [vp, C.POINTER(LoConfig)]
     L.lo_icp_optimize.argtypes = [vp, fp, C.c_size_t, fp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]
     L.lo_icp_optimize_async.argtypes = [vp, C.c_void_p, C.c_size_t, fp]
     L.lo_icp_result.argtypes = [vp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]

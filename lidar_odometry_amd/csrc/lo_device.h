@@ -50,6 +50,7 @@ struct DevState {
     int done;
     int status;
     unsigned int acc_arrive;        // k_accumulate last-block-done counter (reset by the last block)
+    unsigned int kd_unres_n;        // KDTree path: queries the grid search could not certify (k_knn_brute)
     double H_out[36];
     double g_out[6];
     double cost_out;
@@ -66,6 +67,16 @@ struct KParams {
     int nb_acc;                       // k_accumulate blocks = min(nb, kAccBlocks)
     int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
     float T0[12];
+    // KDTree correspondence path (use_surfel_correspondence = 0; lo_kdtree.hip)
+    const float4* kd_pts;             // L0 centroids sorted by grid cell: x, y, z, original index (int bits)
+    const uint32_t* kd_start;         // cell -> first point (dense grid, ncell + 1 entries)
+    int kd_m;                         // map points
+    int kd_org[3], kd_dim[3];         // grid origin (cell coords) and extent
+    float kd_h;                       // grid cell edge
+    int32_t* kd_nbr;                  // per point: 5 neighbour positions into kd_pts (-1: fewer than 5)
+    int32_t* kd_unres;                // queries left to the brute-force pass
+    double* kd_res;                   // per point fp64 point-to-plane distance (the reference's residual)
+    Slot* kd_plane;                   // per point plane: normal / centroid rounded to fp32 (.cast<float>())
     // map
     const Slot* tab;
     uint32_t log2cap;
@@ -260,6 +271,77 @@ __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Correspondence-kernel helpers shared by the surfel (k_correspond) and KDTree (lo_kdtree.hip) paths.
+// ---------------------------------------------------------------------------------------------------
+// Pose of the current GN iteration.  With P.init (first launch of a scan) it is the kernel argument T0 and
+// block 0 writes the fresh GN state that the later kernels of the scan read (k_init folded in).
+__device__ __forceinline__ void scan_pose(const KParams& P, float (&T)[12]) {
+    DevState* st = P.st;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.init ? P.T0[k] : st->pose[k];
+    if (P.init && blockIdx.x == 0 && threadIdx.x < 12) {
+        st->pose[threadIdx.x] = P.T0[threadIdx.x];
+        if (threadIdx.x == 0) {
+            st->scale = 1.0;
+            st->alpha = P.robust_delta;
+            st->n_corr = 0;
+            st->iter = 0;
+            st->done = 0;
+            st->status = LO_OK;
+            st->acc_arrive = 0;
+            // kd_unres_n is NOT reset here: other blocks of the same k_knn launch may already be appending
+            // (k_plane zeroes it after every use; k_init / lo_create start it at 0)
+        }
+    }
+}
+
+// Per-wave validity ballots, per-block accepted count and (iteration 0, with_stats) the per-block
+// (count, sum, M2) of the accepted fp64 residuals for the stable merge of the residual variance.
+__device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, double r, int with_stats) {
+    __shared__ double s_red[kWavesPerBlock];
+    __shared__ int s_cnt[kWavesPerBlock];
+    __shared__ double s_mean;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t m = __ballot(valid);
+    if (lane == 0) {
+        P.wmask[blockIdx.x * kWavesPerBlock + wid] = m;
+        s_cnt[wid] = __popcll(m);
+    }
+    if (!with_stats) {
+        __syncthreads();
+        if (tid == 0) {
+            int c = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) c += s_cnt[w];
+            P.blk_cnt[blockIdx.x] = c;
+        }
+        return;
+    }
+    double v = wave_total(valid ? r : 0.0);
+    if (lane == 0) s_red[wid] = v;
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0;
+        double sum = 0.0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { c += s_cnt[w]; sum += s_red[w]; }
+        P.blk_cnt[blockIdx.x] = c;
+        P.blk_sum[blockIdx.x] = sum;
+        s_mean = c > 0 ? sum / c : 0.0;
+    }
+    __syncthreads();
+    const double mb = s_mean;
+    const double d = valid ? (r - mb) : 0.0;
+    v = wave_total(d * d);
+    __syncthreads();
+    if (lane == 0) s_red[wid] = v;
+    __syncthreads();
+    if (tid == 0) {
+        double m2 = 0.0;
+        for (int w = 0; w < kWavesPerBlock; ++w) m2 += s_red[w];
+        P.blk_m2[blockIdx.x] = m2;
+    }
 }
 
 }  // namespace lo

@@ -25,6 +25,9 @@ __global__ void k_solve(KParams P, int it, int ne_only);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
+__global__ void k_knn(KParams P);
+__global__ void k_knn_brute(KParams P);
+__global__ void k_plane(KParams P, int with_stats);
 }  // namespace lo
 
 using namespace lo;
@@ -54,6 +57,19 @@ struct lo_ctx {
     size_t tab_cap = 0;             // allocated slots
     uint32_t log2cap = 1;
     size_t n_surfels = 0;
+    // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
+    bool kd = false;
+    float4* d_kd_pts = nullptr;
+    size_t kd_pts_cap = 0;
+    uint32_t* d_kd_start = nullptr;
+    size_t kd_start_cap = 0;
+    int kd_m = 0;
+    int kd_org[3] = {0, 0, 0}, kd_dim[3] = {1, 1, 1};
+    float kd_h = 1.0f;
+    int32_t* d_kd_nbr = nullptr;
+    int32_t* d_kd_unres = nullptr;
+    double* d_kd_res = nullptr;
+    Slot* d_kd_plane = nullptr;
     // PKO tables
     PkoTables tables;
     double* d_alphas = nullptr;
@@ -129,6 +145,18 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.res_dbg = nullptr;
     P.direct_res = nullptr;
     P.st = c->d_st;
+    if (c->kd) {                                         // KDTree path: downstream kernels read per-point planes
+        P.tab = c->d_kd_plane;
+        P.kd_pts = c->d_kd_pts;
+        P.kd_start = c->d_kd_start;
+        P.kd_m = c->kd_m;
+        for (int a = 0; a < 3; ++a) { P.kd_org[a] = c->kd_org[a]; P.kd_dim[a] = c->kd_dim[a]; }
+        P.kd_h = c->kd_h;
+        P.kd_nbr = c->d_kd_nbr;
+        P.kd_unres = c->d_kd_unres;
+        P.kd_res = c->d_kd_res;
+        P.kd_plane = c->d_kd_plane;
+    }
     return P;
 }
 
@@ -141,7 +169,6 @@ static int validate_config(const lo_config* g, std::string& err) {
     if (!(g->voxel_size > 0.0f)) { err = "voxel_size must be positive"; return LO_ERR_ARG; }   // VoxelMap.cpp:28-30
     if (g->hierarchy_factor <= 0 || g->hierarchy_factor % 2 == 0) { err = "hierarchy_factor must be positive and odd"; return LO_ERR_ARG; }
     if (g->max_points < 1 || g->max_points > kMaxBlocks * kBlock) { err = "max_points out of [1, 4194304]"; return LO_ERR_ARG; }
-    if (!g->use_surfel_correspondence) { err = "KDTree correspondence is not available in this build"; return LO_ERR_ARG; }
     return LO_OK;
 }
 
@@ -177,6 +204,11 @@ void lo_config_default_mid360(lo_config* c) {
 }
 
 const char* lo_last_error(const lo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+int lo_get_config(const lo_ctx* ctx, lo_config* out) {
+    if (!ctx || !out) return LO_ERR_ARG;
+    *out = ctx->cfg;
+    return LO_OK;
+}
 int lo_device(const lo_ctx* ctx) { return ctx ? ctx->device : -1; }
 void* lo_stream(lo_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
@@ -223,6 +255,17 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
+    c->kd = g.use_surfel_correspondence == 0;
+    if (c->kd) {
+        LO_HIP(c, hipMalloc(&c->d_kd_nbr, NB * kBlock * 5 * sizeof(int32_t)));
+        LO_HIP(c, hipMalloc(&c->d_kd_unres, NB * kBlock * sizeof(int32_t)));
+        LO_HIP(c, hipMalloc(&c->d_kd_res, NB * kBlock * sizeof(double)));
+        LO_HIP(c, hipMalloc(&c->d_kd_plane, NB * kBlock * sizeof(Slot)));
+        LO_HIP(c, hipMalloc(&c->d_kd_start, 2 * sizeof(uint32_t)));     // empty grid until lo_map_set_points
+        LO_HIP(c, hipMemset(c->d_kd_start, 0, 2 * sizeof(uint32_t)));
+        c->kd_start_cap = 2;
+        c->kd_h = 2.0f * g.voxel_size;
+    }
     return LO_OK;
 }
 
@@ -255,7 +298,8 @@ void lo_destroy(lo_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part,
-                    c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i};
+                    c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
+                    c->d_kd_pts, c->d_kd_start, c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -314,7 +358,97 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
 
 size_t lo_map_surfel_count(const lo_ctx* c) { return c ? c->n_surfels : 0; }
 
+// VoxelMap::RebuildKdTree (VoxelMap.cpp:420-438) equivalent: a dense uniform grid (cell = 2 x voxel, doubled
+// until it fits kKdMaxCells) over the L0 centroids in GetPointCloud order; points sorted by cell (x fastest),
+// index order inside a cell; kd_start[cell] = first point, kd_start[ncell] = m.
+static constexpr size_t kKdMaxCells = size_t(1) << 26;
+
+int lo_map_set_points(lo_ctx* c, const float* xyz, size_t m) {
+    if (!c) return LO_ERR_ARG;
+    if (!c->kd) { c->err = "lo_map_set_points needs use_surfel_correspondence = 0"; return LO_ERR_STATE; }
+    if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
+    if (m > static_cast<size_t>(INT32_MAX / 2)) { c->err = "too many map points"; return LO_ERR_CAPACITY; }
+    for (size_t i = 0; i < 3 * m; ++i)
+        if (!std::isfinite(xyz[i])) { c->err = "non-finite map point"; return LO_ERR_ARG; }
+    float h = 2.0f * c->cfg.voxel_size;
+    int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
+    auto cell = [&](float v) { return static_cast<int64_t>(std::floor(v / h)); };
+    for (;;) {
+        int64_t lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, hi[3] = {INT64_MIN, INT64_MIN, INT64_MIN};
+        for (size_t i = 0; i < m; ++i)
+            for (int a = 0; a < 3; ++a) { const int64_t k = cell(xyz[3 * i + a]); lo[a] = std::min(lo[a], k); hi[a] = std::max(hi[a], k); }
+        if (m == 0) { for (int a = 0; a < 3; ++a) { lo[a] = 0; hi[a] = 0; } }
+        size_t ncell = 1;
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) {
+            const int64_t d = hi[a] - lo[a] + 1;
+            if (d > static_cast<int64_t>(kKdMaxCells) || lo[a] < INT32_MIN / 2 || hi[a] > INT32_MAX / 2) { ok = false; break; }
+            ncell *= static_cast<size_t>(d);
+            if (ncell > kKdMaxCells) { ok = false; break; }
+        }
+        if (ok) { for (int a = 0; a < 3; ++a) { org[a] = static_cast<int>(lo[a]); dim[a] = static_cast<int>(hi[a] - lo[a] + 1); } break; }
+        h *= 2.0f;
+    }
+    const size_t ncell = static_cast<size_t>(dim[0]) * dim[1] * dim[2];
+    std::vector<uint32_t> start(ncell + 1, 0);
+    std::vector<uint32_t> lin(m);
+    for (size_t i = 0; i < m; ++i) {
+        const int64_t x = cell(xyz[3 * i]) - org[0], y = cell(xyz[3 * i + 1]) - org[1], z = cell(xyz[3 * i + 2]) - org[2];
+        lin[i] = static_cast<uint32_t>((static_cast<size_t>(z) * dim[1] + y) * dim[0] + x);
+        start[lin[i] + 1]++;
+    }
+    for (size_t k = 0; k < ncell; ++k) start[k + 1] += start[k];
+    std::vector<float4> pts(std::max<size_t>(m, 1));
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    for (size_t i = 0; i < m; ++i) {                     // stable: index order inside a cell
+        float4 v;
+        v.x = xyz[3 * i]; v.y = xyz[3 * i + 1]; v.z = xyz[3 * i + 2];
+        int32_t id = static_cast<int32_t>(i);
+        std::memcpy(&v.w, &id, sizeof(float));
+        pts[fill[lin[i]]++] = v;
+    }
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (pts.size() > c->kd_pts_cap) {
+        if (c->d_kd_pts) LO_HIP(c, hipFree(c->d_kd_pts));
+        c->d_kd_pts = nullptr;
+        LO_HIP(c, hipMalloc(&c->d_kd_pts, pts.size() * sizeof(float4)));
+        c->kd_pts_cap = pts.size();
+    }
+    if (start.size() > c->kd_start_cap) {
+        if (c->d_kd_start) LO_HIP(c, hipFree(c->d_kd_start));
+        c->d_kd_start = nullptr;
+        LO_HIP(c, hipMalloc(&c->d_kd_start, start.size() * sizeof(uint32_t)));
+        c->kd_start_cap = start.size();
+    }
+    LO_HIP(c, hipMemcpy(c->d_kd_pts, pts.data(), pts.size() * sizeof(float4), hipMemcpyHostToDevice));
+    LO_HIP(c, hipMemcpy(c->d_kd_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->kd_m = static_cast<int>(m);
+    c->kd_h = h;
+    for (int a = 0; a < 3; ++a) { c->kd_org[a] = org[a]; c->kd_dim[a] = dim[a]; }
+    return LO_OK;
+}
+
+size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->kd_m) : 0; }
+
 // ---------------------------------------------------------------- optimize
+// Correspondence stage of one GN iteration: surfel lookup, or (KDTree variant) grid kNN + brute-force
+// fallback + plane fit.  P0 carries init = 1 on a scan's first iteration.
+static constexpr int kBruteBlocks = 256;
+
+static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats) {
+    const dim3 grid(P.nb), blk(kBlock);
+    if (!c->kd) {
+        hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, with_stats);
+        return;
+    }
+    KParams Pn = P;
+    Pn.init = 0;
+    hipLaunchKernelGGL(k_knn, dim3((static_cast<size_t>(P.n) * 8 + kBlock - 1) / kBlock), blk, 0, c->stream, P);   // 8 lanes / query
+    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(256), 0, c->stream, Pn);
+    hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
+}
+
 static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12]) {
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
@@ -330,9 +464,9 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         KParams P0 = P;                                   // first k_correspond also resets the GN state
         P0.init = 1;
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
-        const dim3 grid(P.nb), blk(kBlock);
+        const dim3 blk(kBlock);
         for (int it = 0; it < g.max_iterations; ++it) {
-            hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, it == 0 ? P0 : P, it == 0 ? 1 : 0);
+            launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0);
             launch_pko(c, P, it);
             if (P.nb_acc <= kFuseMaxBlocks) {          // small scans: the last accumulate block solves
                 hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
@@ -434,7 +568,7 @@ int lo_find_correspondences(lo_ctx* c, const float* pts, size_t n, const float T
     LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.res_dbg = c->d_res;
-    hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 1);
+    launch_correspond(c, P, 1);
     LO_HIP(c, hipGetLastError());
     std::vector<int32_t> slots(n);
     LO_HIP(c, hipMemcpyAsync(slots.data(), c->d_slot, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -477,7 +611,7 @@ int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float
     LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.alpha_given = 1;
-    hipLaunchKernelGGL(k_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
+    launch_correspond(c, P, 0);
     if (P.nb_acc <= kFuseMaxBlocks) {
         hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P, 0, 2);
     } else {
@@ -533,13 +667,13 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     P.alpha_given = 1;
     const dim3 grid(P.nb), blk(kBlock);
     // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials
-    hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 1);
+    launch_correspond(c, P, 1);
     hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0, 0);
     LO_HIP(c, hipGetLastError());
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int r = 0; r < reps; ++r) {
         switch (kernel_id) {
-            case 0: hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, 0); break;
+            case 0: launch_correspond(c, P, 0); break;                 // KDTree: kNN + fallback + plane fit
             case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0,
                                        P.nb_acc <= kFuseMaxBlocks ? 2 : 0); break;
             case 2: launch_pko(c, P, 1); break;

@@ -1,0 +1,370 @@
+// lo_kdtree.hip — KDTree correspondence variant (use_surfel_correspondence = false) on the device.
+//
+// Reference: IterativeClosestPointOptimizer::find_correspondences_kdtree (IterativeClosestPointOptimizer.cpp:
+// 647-767), is_collinear (:785-792), KdTree::nearestKSearch (PointCloudUtils.h:398-423) over nanoflann 1.7.1
+// (L2_Simple_Adaptor, KNNResultSet; thirdparty/nanoflann/nanoflann.hpp:199-282, :1885-1905) built on the
+// map's L0 centroids (VoxelMap::GetPointCloud :388-403, RebuildKdTree :420-438).
+//
+// The kd-tree is an ordering device; what the reference consumes is the exact 5-NN set by fp32 squared L2
+// distance ((0 + dx^2) + dy^2) + dz^2, sorted ascending.  MI355X-first, the search runs on a dense uniform
+// grid over the centroids (built on the host at map upload, lo_map_set_points), 8 lanes per query:
+//   k_knn        shells of cells around the query cell, rows split over the query's lanes (batched loads,
+//                butterfly merge of per-lane top-5 lists); after shell r the result is certified once the 5th
+//                distance is below the distance from the query to the scanned cube (minus a margin that
+//                covers fp32 binning); otherwise the query goes to
+//   k_knn_brute  one workgroup per unresolved query: lane-strided brute force + LDS tree merge of top-5 lists;
+//   k_plane      collinearity gate, 5-point centroid / covariance, smallest eigenvector (fp64 cyclic Jacobi,
+//                the oracle's restatement of JacobiSVD<MatrixXd>(5x3).matrixV().col(2)), point-to-plane
+//                distance <= max_correspondence_distance; writes the per-point plane (fp32-rounded normal and
+//                centroid, as .cast<float>() at :361-365), the fp64 distance (residuals[i]) and the same ballots /
+//                block statistics as the surfel path, so k_pko_t / k_accumulate run unchanged.
+// Ties in distance are broken by the centroid's original index (an index-ordered brute force); nanoflann
+// breaks them by tree-visit order (NANOFLANN_FIRST_MATCH is not defined), so exact ties are parity-unpinned.
+// Non-finite queries find nothing (nanoflann only adds points with dist < worstDist = FLT_MAX).
+#include "lo_device.h"
+
+#include <cfloat>
+
+namespace lo {
+
+constexpr int kKnnRMax = 3;            // grid shells before a query falls back to brute force
+constexpr double kKnnMargin = 1e-2;    // m: covers fp32 binning of centroids near cell faces
+
+struct Top5 {
+    float d[5];
+    int id[5];      // original centroid index (tie-break)
+    int pos[5];     // position in kd_pts
+    int n;
+};
+
+__device__ __forceinline__ bool lex_less(float da, int ia, float db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+__device__ __forceinline__ void top5_init(Top5& t) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { t.d[k] = __builtin_inff(); t.id[k] = 0x7fffffff; t.pos[k] = -1; }
+    t.n = 0;
+}
+
+// KNNResultSet::addPoint behind searchLevel's `dist < worstDist` (worstDist = FLT_MAX until 5 are held),
+// with (dist, index) order; unrolled compare-swaps keep the list in VGPRs.
+__device__ __forceinline__ void top5_insert(Top5& t, float d, int id, int pos) {
+    if (t.n < 5) {
+        if (!(d < FLT_MAX)) return;
+        ++t.n;
+    } else if (!lex_less(d, id, t.d[4], t.id[4])) {
+        return;
+    }
+    t.d[4] = d; t.id[4] = id; t.pos[4] = pos;
+#pragma unroll
+    for (int k = 4; k > 0; --k) {
+        if (lex_less(t.d[k], t.id[k], t.d[k - 1], t.id[k - 1])) {
+            const float fd = t.d[k]; t.d[k] = t.d[k - 1]; t.d[k - 1] = fd;
+            const int fi = t.id[k]; t.id[k] = t.id[k - 1]; t.id[k - 1] = fi;
+            const int fp = t.pos[k]; t.pos[k] = t.pos[k - 1]; t.pos[k - 1] = fp;
+        }
+    }
+}
+
+__device__ __forceinline__ float l2sq(float qx, float qy, float qz, const float4& v) {
+    const float dx = qx - v.x, dy = qy - v.y, dz = qz - v.z;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+__device__ __forceinline__ void scan_range(const KParams& P, uint32_t s, uint32_t e, float qx, float qy, float qz, Top5& t) {
+    uint32_t p = s;
+    for (; p + 4 <= e; p += 4) {                 // 4 independent loads in flight per lane
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = P.kd_pts[p + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
+    }
+    for (; p < e; ++p) {
+        const float4 v = P.kd_pts[p];
+        top5_insert(t, l2sq(qx, qy, qz, v), __float_as_int(v.w), static_cast<int>(p));
+    }
+}
+
+// Merge of disjoint top-5 lists across the kKnnGroup lanes of a query (butterfly over __shfl_xor):
+// every lane of the group ends with the group's (dist, index)-smallest five.
+constexpr int kKnnGroup = 8;
+
+__device__ __forceinline__ Top5 group_merge(const Top5& own) {
+    Top5 t = own;
+#pragma unroll
+    for (int o = 1; o < kKnnGroup; o <<= 1) {
+        Top5 u;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            u.d[k] = __shfl_xor(t.d[k], o, 64);
+            u.id[k] = __shfl_xor(t.id[k], o, 64);
+            u.pos[k] = __shfl_xor(t.pos[k], o, 64);
+        }
+        u.n = __shfl_xor(t.n, o, 64);
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
+    }
+    return t;
+}
+
+// ====================================================================================================
+// k_knn: grid shells.  kd_nbr[5i] = positions of the 5-NN, -1 = fewer than 5 (rejected), -2 = unresolved
+// ====================================================================================================
+__global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
+    if (!P.init && P.st->done) return;
+    // kKnnGroup consecutive lanes share one query: lane g scans rows g, g + G, ... of each shell, so a query's
+    // candidate loads are spread over G lanes (the scan has only ~N/64 waves: latency, not bandwidth, bounds it)
+    const int gi = blockIdx.x * kBlock + threadIdx.x;
+    const int i = gi / kKnnGroup, g = gi % kKnnGroup;
+    float T[12];
+    scan_pose(P, T);
+    if (i >= P.n) return;                                    // whole groups leave together
+    int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+    float qx, qy, qz;
+    transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+    if (!(isfinite(qx) && isfinite(qy) && isfinite(qz)) || P.kd_m < 5) { if (g == 0) out[0] = -1; return; }
+    const float h = P.kd_h;
+    const float fx = floorf(qx / h), fy = floorf(qy / h), fz = floorf(qz / h);
+    if (!(fabsf(fx) < 1e9f && fabsf(fy) < 1e9f && fabsf(fz) < 1e9f)) {
+        if (g == 0) { out[0] = -2; P.kd_unres[atomicAdd(&P.st->kd_unres_n, 1u)] = i; }
+        return;
+    }
+    const int c[3] = {static_cast<int>(fx), static_cast<int>(fy), static_cast<int>(fz)};
+    const int dimx = P.kd_dim[0], dimy = P.kd_dim[1], dimz = P.kd_dim[2];
+    const int ox = P.kd_org[0], oy = P.kd_org[1], oz = P.kd_org[2];
+    const double q[3] = {qx, qy, qz};
+    Top5 own, grp;
+    top5_init(own);
+    bool done = false;
+    for (int r = 0; r <= kKnnRMax && !done; ++r) {
+        const int side = 2 * r + 1;
+        for (int k = g; k < side * side; k += kKnnGroup) {
+            const int dz = k / side - r, dy = k % side - r;
+            const int z = c[2] + dz - oz, y = c[1] + dy - oy;
+            if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
+            const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
+            if (dz == -r || dz == r || dy == -r || dy == r) {               // whole row of the shell
+                const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
+                if (x0 <= x1) scan_range(P, P.kd_start[row + x0], P.kd_start[row + x1 + 1], qx, qy, qz, own);
+            } else {                                                        // the two end cells
+                const int xa = c[0] - r - ox, xb = c[0] + r - ox;
+                if (xa >= 0 && xa < dimx) scan_range(P, P.kd_start[row + xa], P.kd_start[row + xa + 1], qx, qy, qz, own);
+                if (xb >= 0 && xb < dimx) scan_range(P, P.kd_start[row + xb], P.kd_start[row + xb + 1], qx, qy, qz, own);
+            }
+        }
+        grp = group_merge(own);
+        // every unscanned centroid lies outside the cube of cells [c - r, c + r]
+        bool all = true;
+        double b = DBL_MAX;
+        const int org[3] = {ox, oy, oz}, dim[3] = {dimx, dimy, dimz};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            all = all && (c[a] - r <= org[a]) && (c[a] + r >= org[a] + dim[a] - 1);
+            b = fmin(b, q[a] - static_cast<double>(c[a] - r) * h);
+            b = fmin(b, static_cast<double>(c[a] + r + 1) * h - q[a]);
+        }
+        if (all) {
+            done = true;
+        } else if (grp.n == 5) {
+            const double e = b - kKnnMargin;
+            done = e > 0.0 && static_cast<double>(grp.d[4]) < e * e * (1.0 - 1e-6);
+        }
+    }
+    if (g != 0) return;
+    if (!done) {
+        out[0] = -2;
+        P.kd_unres[atomicAdd(&P.st->kd_unres_n, 1u)] = i;
+        return;
+    }
+    if (grp.n < 5) { out[0] = -1; return; }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) out[k] = grp.pos[k];
+}
+
+// ====================================================================================================
+// k_knn_brute: unresolved queries, one workgroup each (grid-strided over the device-side list)
+// ====================================================================================================
+constexpr int kBruteThreads = 256;
+
+__global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
+    DevState* st = P.st;
+    if (st->done) return;
+    const unsigned nu = st->kd_unres_n;
+    if (blockIdx.x >= nu) return;
+    __shared__ float s_d[kBruteThreads][5];
+    __shared__ int s_id[kBruteThreads][5];
+    __shared__ int s_pos[kBruteThreads][5];
+    __shared__ int s_n[kBruteThreads];
+    const int tid = threadIdx.x;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    for (unsigned u = blockIdx.x; u < nu; u += gridDim.x) {
+        const int i = P.kd_unres[u];
+        float qx, qy, qz;
+        transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+        Top5 t;
+        top5_init(t);
+        int p = tid;
+        for (; p + 3 * kBruteThreads < P.kd_m; p += 4 * kBruteThreads) {   // 4 loads in flight per lane
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = P.kd_pts[p + u * kBruteThreads];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), p + u * kBruteThreads);
+        }
+        for (; p < P.kd_m; p += kBruteThreads) {
+            const float4 v = P.kd_pts[p];
+            top5_insert(t, l2sq(qx, qy, qz, v), __float_as_int(v.w), p);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { s_d[tid][k] = t.d[k]; s_id[tid][k] = t.id[k]; s_pos[tid][k] = t.pos[k]; }
+        s_n[tid] = t.n;
+        __syncthreads();
+        for (int s = kBruteThreads / 2; s > 0; s >>= 1) {
+            if (tid < s) {
+                Top5 a;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) { a.d[k] = s_d[tid][k]; a.id[k] = s_id[tid][k]; a.pos[k] = s_pos[tid][k]; }
+                a.n = s_n[tid];
+                const int nb = s_n[tid + s];
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    if (k < nb) top5_insert(a, s_d[tid + s][k], s_id[tid + s][k], s_pos[tid + s][k]);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) { s_d[tid][k] = a.d[k]; s_id[tid][k] = a.id[k]; s_pos[tid][k] = a.pos[k]; }
+                s_n[tid] = a.n;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+            if (s_n[0] < 5) out[0] = -1;
+            else for (int k = 0; k < 5; ++k) out[k] = s_pos[0][k];
+        }
+        __syncthreads();
+    }
+}
+
+// ====================================================================================================
+// k_plane: plane fit + residual + the correspondence epilogue
+// ====================================================================================================
+__device__ __forceinline__ double dot3d(double a0, double a1, double a2, double b0, double b1, double b2) {
+    const double e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;       // Vector3d dot: (e0 + e1) + e2
+    return (e0 + e1) + e2;
+}
+
+// Smallest-eigenvalue eigenvector of a symmetric 3x3 (cyclic Jacobi, fp64) -- the same sweep as the oracle's
+// smallest_eigvec3d (oracle/src/lo_oracle.cpp), so normals agree bit for bit under -ffp-contract=off.
+// Fully unrolled (p, q) rotations keep A and V in registers.
+__device__ __forceinline__ void jrot(double (&A)[3][3], double (&V)[3][3], int p, int q) {
+    if (A[p][q] == 0.0) return;
+    const double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+    const double cc = 1.0 / sqrt(t * t + 1.0), s = t * cc;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double akp = A[k][p], akq = A[k][q];
+        A[k][p] = cc * akp - s * akq; A[k][q] = s * akp + cc * akq;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double apk = A[p][k], aqk = A[q][k];
+        A[p][k] = cc * apk - s * aqk; A[q][k] = s * apk + cc * aqk;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double vkp = V[k][p], vkq = V[k][q];
+        V[k][p] = cc * vkp - s * vkq; V[k][q] = s * vkp + cc * vkq;
+    }
+}
+
+__device__ __forceinline__ void smallest_eigvec3d(double (&A)[3][3], double (&v)[3]) {
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
+        if (off < 1e-300) break;
+        jrot(A, V, 0, 1);
+        jrot(A, V, 0, 2);
+        jrot(A, V, 1, 2);
+    }
+    int mi = 0;
+    if (A[1][1] < A[0][0]) mi = 1;
+    if (A[2][2] < (mi == 0 ? A[0][0] : A[1][1])) mi = 2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v[k] = (mi == 0) ? V[k][0] : (mi == 1 ? V[k][1] : V[k][2]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
+    DevState* st = P.st;
+    if (st->done) return;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                        // k_knn_brute has drained the list
+        st->dbg[15] = st->kd_unres_n;                                 // last unresolved count (lo_debug_counters)
+        st->kd_unres_n = 0;
+    }
+    bool valid = false;
+    double dist = 0.0;
+    if (i < P.n) {
+        const int32_t* nb = P.kd_nbr + 5 * static_cast<size_t>(i);
+        if (nb[0] >= 0) {
+            double Pm[5][3];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const float4 v = P.kd_pts[nb[k]];
+                Pm[k][0] = v.x; Pm[k][1] = v.y; Pm[k][2] = v.z;
+            }
+            // is_collinear(p0, p1, p2, 0.5) (:785-792): |normalize(p1-p0) x normalize(p2-p0)| < 0.5 rejects
+            double v1[3], v2[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { v1[d] = Pm[1][d] - Pm[0][d]; v2[d] = Pm[2][d] - Pm[0][d]; }
+            const double n1 = sqrt(dot3d(v1[0], v1[1], v1[2], v1[0], v1[1], v1[2]));
+            const double n2 = sqrt(dot3d(v2[0], v2[1], v2[2], v2[0], v2[1], v2[2]));
+            if (n1 > 0) { v1[0] /= n1; v1[1] /= n1; v1[2] /= n1; }
+            if (n2 > 0) { v2[0] /= n2; v2[1] /= n2; v2[2] /= n2; }
+            const double cr0 = v1[1] * v2[2] - v1[2] * v2[1], cr1 = v1[2] * v2[0] - v1[0] * v2[2],
+                         cr2 = v1[0] * v2[1] - v1[1] * v2[0];
+            if (!(sqrt(dot3d(cr0, cr1, cr2, cr0, cr1, cr2)) < 0.5)) {
+                double cen[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < 5; ++k) { cen[0] += Pm[k][0]; cen[1] += Pm[k][1]; cen[2] += Pm[k][2]; }
+                cen[0] /= 5.0; cen[1] /= 5.0; cen[2] /= 5.0;
+                double S[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const double a[3] = {Pm[k][0] - cen[0], Pm[k][1] - cen[1], Pm[k][2] - cen[2]};
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                        for (int s = 0; s < 3; ++s) S[r][s] += a[r] * a[s];
+                }
+                double nrm[3];
+                smallest_eigvec3d(S, nrm);
+                float T[12];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+                float qx, qy, qz;
+                transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+                const double pd = -dot3d(nrm[0], nrm[1], nrm[2], cen[0], cen[1], cen[2]);
+                dist = fabs(dot3d(nrm[0], nrm[1], nrm[2], qx, qy, qz) + pd);
+                valid = !(dist > P.maxd);                       // :746-748 (NaN kept)
+                if (valid) {
+                    Slot sl;
+                    sl.key = 0;
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) { sl.n[d] = static_cast<float>(nrm[d]); sl.c[d] = static_cast<float>(cen[d]); }
+                    P.kd_plane[i] = sl;
+                    P.kd_res[i] = dist;
+                }
+            }
+        }
+        P.slot[i] = valid ? i : -1;
+        if (P.res_dbg) P.res_dbg[i] = valid ? dist : 0.0;
+    }
+    corr_epilogue(P, valid, dist, with_stats);
+}
+
+}  // namespace lo

@@ -27,31 +27,12 @@ namespace lo {
 // k_correspond
 // ====================================================================================================
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
-    DevState* st = P.st;
     // P.init: first launch of a scan.  The GN state reset (k_init's job) is folded in here -- the pose comes
     // from the kernel argument, block 0 writes the fresh DevState that the later kernels of the scan read.
-    if (!P.init && st->done) return;
-    __shared__ double s_red[kWavesPerBlock];
-    __shared__ int s_cnt[kWavesPerBlock];
-    __shared__ double s_mean;
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int i = blockIdx.x * kBlock + tid;
+    if (!P.init && P.st->done) return;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
     float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = P.init ? P.T0[k] : st->pose[k];
-    if (P.init && blockIdx.x == 0 && tid < 12) {
-        st->pose[tid] = P.T0[tid];
-        if (tid == 0) {
-            st->scale = 1.0;
-            st->alpha = P.robust_delta;
-            st->n_corr = 0;
-            st->iter = 0;
-            st->done = 0;
-            st->status = LO_OK;
-            st->acc_arrive = 0;
-        }
-    }
+    scan_pose(P, T);
 
     int slot = -1;
     double r = 0.0;
@@ -68,45 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
         P.slot[i] = slot;
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
     }
-    const bool valid = slot >= 0;
-    const uint64_t m = __ballot(valid);
-    if (lane == 0) {
-        P.wmask[blockIdx.x * kWavesPerBlock + wid] = m;
-        s_cnt[wid] = __popcll(m);
-    }
-    if (!with_stats) {
-        __syncthreads();
-        if (tid == 0) {
-            int c = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) c += s_cnt[w];
-            P.blk_cnt[blockIdx.x] = c;
-        }
-        return;
-    }
-    // iteration 0: per-block (count, sum, M2) for a stable fp64 merge of the residual variance
-    double v = wave_total(valid ? r : 0.0);
-    if (lane == 0) s_red[wid] = v;
-    __syncthreads();
-    if (tid == 0) {
-        int c = 0;
-        double sum = 0.0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { c += s_cnt[w]; sum += s_red[w]; }
-        P.blk_cnt[blockIdx.x] = c;
-        P.blk_sum[blockIdx.x] = sum;
-        s_mean = c > 0 ? sum / c : 0.0;
-    }
-    __syncthreads();
-    const double mb = s_mean;
-    const double d = valid ? (r - mb) : 0.0;
-    v = wave_total(d * d);
-    __syncthreads();
-    if (lane == 0) s_red[wid] = v;
-    __syncthreads();
-    if (tid == 0) {
-        double m2 = 0.0;
-        for (int w = 0; w < kWavesPerBlock; ++w) m2 += s_red[w];
-        P.blk_m2[blockIdx.x] = m2;
-    }
+    corr_epilogue(P, slot >= 0, r, with_stats);
 }
 
 // ====================================================================================================
@@ -146,10 +89,15 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
         const int s = P.slot[i];
         if (s < 0) continue;
         const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
-        const Slot sl = P.tab[s];
-        float wx, wy, wz;
-        transform_pt(T, px, py, pz, wx, wy, wz);
-        const double r = residual_f64(sl, wx, wy, wz);
+        const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
+        double r;
+        if (P.kd_res) {
+            r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
+        } else {
+            float wx, wy, wz;
+            transform_pt(T, px, py, pz, wx, wy, wz);
+            r = residual_f64(sl, wx, wy, wz);
+        }
         const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
         // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
         const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
@@ -458,6 +406,7 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
         st->done = 0;
         st->status = LO_OK;
         st->acc_arrive = 0;
+        st->kd_unres_n = 0;
     }
 }
 

@@ -397,12 +397,16 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
             for (int q = 0; q < k; ++q) mk &= mk - 1;
             const int bit = __ffsll(static_cast<unsigned long long>(mk)) - 1;
             const int pidx = b * kBlock + w * kWave + bit;
-            float T[12];
+            if (P.kd_res) {
+                v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
+            } else {
+                float T[12];
 #pragma unroll
-            for (int q = 0; q < 12; ++q) T[q] = st->pose[q];
-            float wx, wy, wz;
-            transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
-            v = residual_f64(P.tab[P.slot[pidx]], wx, wy, wz) / sden;   // :321-326
+                for (int q = 0; q < 12; ++q) T[q] = st->pose[q];
+                float wx, wy, wz;
+                transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
+                v = residual_f64(P.tab[P.slot[pidx]], wx, wy, wz) / sden;   // :321-326
+            }
         }
         s_sd[tid] = v;
     }

@@ -411,7 +411,17 @@ int lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m) {
     std::vector<int32_t> k(3 * std::max<size_t>(s, 1));
     std::vector<float> n(3 * std::max<size_t>(s, 1)), c(3 * std::max<size_t>(s, 1));
     lo_voxelmap_get_surfels(m, k.data(), n.data(), c.data(), nullptr, s);
-    return lo_map_set_surfels(ctx, k.data(), n.data(), c.data(), s);
+    int rc = lo_map_set_surfels(ctx, k.data(), n.data(), c.data(), s);
+    if (rc != LO_OK) return rc;
+    lo_config cfg;
+    if (lo_get_config(ctx, &cfg) == LO_OK && !cfg.use_surfel_correspondence) {
+        // KDTree variant: GetPointCloud (VoxelMap.cpp:388-403) in L0 order, then RebuildKdTree's grid
+        const size_t l0 = lo_voxelmap_l0_count(m);
+        std::vector<float> xyz(3 * std::max<size_t>(l0, 1));
+        lo_voxelmap_get_l0(m, xyz.data(), l0);
+        rc = lo_map_set_points(ctx, xyz.data(), l0);
+    }
+    return rc;
 }
 
 // FastVoxelFilter::filter (VoxelMap.h:73-104): Morton key of floor(p * (1/voxel)) + 2^20 clamped to 21 bits,

@@ -159,14 +159,22 @@ class IterativeClosestPointOptimizer:
             raise ValueError("keys/normals/centroids length mismatch")
         self._check(lib().lo_map_set_surfels(self._ctx, k.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(n), _fptr(c), len(k)))
 
+    def set_map_points(self, points):
+        """KDTree variant: upload VoxelMap::GetPointCloud (L0 centroids, L0 order) -- RebuildKdTree's input."""
+        p = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        self._check(lib().lo_map_set_points(self._ctx, _fptr(p), len(p)))
+
     def _sync_map(self, voxel_map):
         if voxel_map is None:
             return
         token = (id(voxel_map), getattr(voxel_map, "revision", None))
         if token == self._map_token and token[1] is not None:
             return
-        s = voxel_map.surfels()
-        self.set_surfels(s[0], s[1], s[2])
+        if self.config.use_surfel_correspondence:
+            s = voxel_map.surfels()
+            self.set_surfels(s[0], s[1], s[2])
+        else:
+            self.set_map_points(voxel_map.l0_cloud())
         self._map_token = token
 
     # ------------------------------------------------------------------ optimize

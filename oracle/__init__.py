@@ -91,6 +91,8 @@ def lib():
         L.or_find_correspondences.restype = C.c_int
         L.or_find_correspondences_kdtree.argtypes = [vp, fp, C.c_int, fp, C.c_double, u8p, dp, fp, fp]
         L.or_find_correspondences_kdtree.restype = C.c_int
+        L.or_set_kdtree_search.argtypes = [C.c_int]
+        L.or_set_kdtree_search.restype = None
         L.or_icp_optimize.argtypes = [vp, fp, C.c_int, fp, fp, C.POINTER(IcpCfg), C.c_int,
                                       C.POINTER(IterLog), ip]
         L.or_icp_optimize.restype = C.c_int
@@ -252,6 +254,11 @@ class VoxelMap:
 
 
 # ---------------------------------------------------------------- ICP
+def set_kdtree_search(use_tree: bool):
+    """KDTree-variant neighbour search: kd-tree (default) or the index-ordered brute force (same results)."""
+    lib().or_set_kdtree_search(int(bool(use_tree)))
+
+
 def find_correspondences(vmap: VoxelMap, pts, T, max_corr=1.0, kdtree=False):
     p, pp = _f32(pts)
     t, tp = _f32(np.asarray(T).reshape(12))

@@ -397,7 +397,90 @@ struct L1Node {
     int last_child_count = 0;
 };
 
+
+/* ---- static kd-tree over the map cloud (VoxelMap::RebuildKdTree :420-438 role, nanoflann leaf size 10) ----
+ * Exact 5-NN by the fp32 squared L2 of nanoflann's L2_Simple_Adaptor; the result set keeps the (dist, index)
+ * lexicographic smallest, i.e. exactly what an index-ordered brute force returns (tests check this).  A node is
+ * skipped only when its box lower bound, shrunk by 1e-6 relative against fp32 rounding of point distances, is
+ * strictly above the current 5th distance, so equal-distance lower-index points are never pruned. */
+struct KdTree3 {
+    struct Node { float lo[3], hi[3]; int left = -1, right = -1, begin = 0, end = 0; };
+    std::vector<float> pts;     // xyz by original index
+    std::vector<int> perm;
+    std::vector<Node> nodes;
+    void build(const std::vector<float>& cloud) {
+        pts = cloud;
+        const int m = static_cast<int>(cloud.size() / 3);
+        perm.resize(m);
+        for (int i = 0; i < m; ++i) perm[i] = i;
+        nodes.clear();
+        if (m > 0) build_rec(0, m);
+    }
+    int build_rec(int b, int e) {
+        Node nd;
+        for (int a = 0; a < 3; ++a) { nd.lo[a] = FLT_MAX; nd.hi[a] = -FLT_MAX; }
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[a] = std::min(nd.lo[a], pts[3 * perm[i] + a]);
+                nd.hi[a] = std::max(nd.hi[a], pts[3 * perm[i] + a]);
+            }
+        nd.begin = b; nd.end = e;
+        const int id = static_cast<int>(nodes.size());
+        nodes.push_back(nd);
+        if (e - b > 10) {
+            int ax = 0;
+            for (int a = 1; a < 3; ++a) if (nd.hi[a] - nd.lo[a] > nd.hi[ax] - nd.lo[ax]) ax = a;
+            const int mid = (b + e) / 2;
+            std::nth_element(perm.begin() + b, perm.begin() + mid, perm.begin() + e,
+                             [&](int x, int y) { return pts[3 * x + ax] < pts[3 * y + ax]; });
+            const int l = build_rec(b, mid), r = build_rec(mid, e);
+            nodes[id].left = l; nodes[id].right = r;
+        }
+        return id;
+    }
+    static bool lex_less(float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); }
+    void insert(const float q[3], int i, int idx[5], float dist[5], int& found) const {
+        const float d0 = q[0] - pts[3 * i], d1 = q[1] - pts[3 * i + 1], d2 = q[2] - pts[3 * i + 2];
+        const float d = d0 * d0 + d1 * d1 + d2 * d2;
+        if (found < 5) { if (!(d < FLT_MAX)) return; }
+        else if (!lex_less(d, i, dist[4], idx[4])) return;
+        int j = found < 5 ? found : 4;
+        if (found < 5) ++found;
+        while (j > 0 && lex_less(d, i, dist[j - 1], idx[j - 1])) { dist[j] = dist[j - 1]; idx[j] = idx[j - 1]; --j; }
+        dist[j] = d; idx[j] = i;
+    }
+    double box_d2(const Node& nd, const float q[3]) const {
+        double s = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            double g = 0.0;
+            if (q[a] < nd.lo[a]) g = static_cast<double>(nd.lo[a]) - q[a];
+            else if (q[a] > nd.hi[a]) g = static_cast<double>(q[a]) - nd.hi[a];
+            s += g * g;
+        }
+        return s;
+    }
+    void search(int ni, const float q[3], int idx[5], float dist[5], int& found) const {
+        const Node& nd = nodes[ni];
+        if (found == 5 && box_d2(nd, q) * (1.0 - 1e-6) > static_cast<double>(dist[4])) return;
+        if (nd.left < 0) {
+            for (int k = nd.begin; k < nd.end; ++k) insert(q, perm[k], idx, dist, found);
+            return;
+        }
+        const double dl = box_d2(nodes[nd.left], q), dr = box_d2(nodes[nd.right], q);
+        if (dl <= dr) { search(nd.left, q, idx, dist, found); search(nd.right, q, idx, dist, found); }
+        else { search(nd.right, q, idx, dist, found); search(nd.left, q, idx, dist, found); }
+    }
+    void knn5(const float q[3], int idx[5], float dist[5], int& found) const {
+        found = 0;
+        if (nodes.empty() || !(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) return;
+        search(0, q, idx, dist, found);
+    }
+};
+
 struct VoxelMap {
+    uint64_t revision = 0;                 // bumped by update / apply_transform (kd-tree cache key)
+    mutable KdTree3 kd;
+    mutable uint64_t kd_rev = ~0ull;
     float voxel_size = 0.5f;
     int factor = 3;
     float planarity_threshold = 0.1f;
@@ -470,6 +553,7 @@ struct VoxelMap {
     }
 
     void update(const float* xyz, int n, const double sensor[3], double max_distance, bool is_keyframe) {
+        ++revision;
         if (!xyz || n <= 0) return;
         if (!is_keyframe) return;
         float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
@@ -547,6 +631,7 @@ struct VoxelMap {
     }
 
     void apply_transform(const float T[12]) {   // ApplyTransformAndRehash :264-302
+        ++revision;
         SE3 s = se3_from12(T);
         std::vector<std::pair<VKey, L0Node>> tr;
         tr.reserve(L0.size());
@@ -798,7 +883,9 @@ static size_t find_corr(const VoxelMap& map, const float* pts, int n, const SE3&
     return c.size();
 }
 
-/* ---- KDTree variant (find_correspondences_kdtree :647-767), brute-force exact 5-NN ----
+static bool g_kd_use_tree = true;      // or_set_kdtree_search(0) -> index-ordered brute force
+
+/* ---- KDTree variant (find_correspondences_kdtree :647-767), exact 5-NN (kd-tree or brute force) ----
  * nanoflann KNNResultSet keeps the K smallest squared L2 distances (fp32 accumulate
  * d0*d0 + d1*d1 + d2*d2) sorted ascending; equal distances keep the first-inserted
  * (insertion sort shifts only strictly larger entries).  The tree visit order only matters
@@ -809,7 +896,10 @@ static void knn5(const std::vector<float>& cloud, const float q[3], int idx[5], 
     for (size_t i = 0; i < m; ++i) {
         float d0 = q[0] - cloud[3 * i], d1 = q[1] - cloud[3 * i + 1], d2 = q[2] - cloud[3 * i + 2];
         float d = d0 * d0 + d1 * d1 + d2 * d2;
-        if (found == 5 && !(d < dist[4])) continue;
+        // searchLevel adds a leaf point only if dist < worstDist, and worstDist is FLT_MAX until K are held
+        // (nanoflann.hpp:1893-1900, KNNResultSet): NaN / inf distances are never added
+        const float worst = found < 5 ? FLT_MAX : dist[4];
+        if (!(d < worst)) continue;
         int j = found < 5 ? found : 4;
         if (found < 5) found++;
         while (j > 0 && dist[j - 1] > d) { dist[j] = dist[j - 1]; idx[j] = idx[j - 1]; --j; }
@@ -855,11 +945,14 @@ static size_t find_corr_kdtree(const VoxelMap& map, const float* pts, int n, con
     std::vector<float> cloud;   // GetPointCloud (:388-403), L0 iteration order
     cloud.reserve(map.L0.size() * 3);
     for (auto& kv : map.L0.vals) { cloud.push_back(kv.second.c[0]); cloud.push_back(kv.second.c[1]); cloud.push_back(kv.second.c[2]); }
+    const bool use_tree = g_kd_use_tree;
+    if (use_tree && map.kd_rev != map.revision) { map.kd.build(cloud); map.kd_rev = map.revision; }   // RebuildKdTree
     for (int i = 0; i < n; ++i) {
         if (valid_out) { valid_out[i] = 0; res_out[i] = 0.0; }
         float q[3]; transform_pt(T, pts + 3 * i, q);
         int idx[5]; float dist[5]; int found;
-        knn5(cloud, q, idx, dist, found);
+        if (use_tree) map.kd.knn5(q, idx, dist, found);
+        else knn5(cloud, q, idx, dist, found);
         if (found < 5) continue;
         double P[5][3];
         for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) P[k][d] = cloud[3 * idx[k] + d];
@@ -1161,6 +1254,8 @@ int or_find_correspondences(void* map, const float* pts, int n, const float T[12
     Corr c;
     return static_cast<int>(find_corr(*static_cast<VoxelMap*>(map), pts, n, se3_from12(T), maxd, c, valid, residual));
 }
+
+void or_set_kdtree_search(int use_tree) { g_kd_use_tree = use_tree != 0; }
 
 int or_find_correspondences_kdtree(void* map, const float* pts, int n, const float T[12], double maxd, uint8_t* valid,
                                    double* residual, float* normal_out, float* target_out) {

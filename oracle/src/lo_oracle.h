@@ -102,6 +102,7 @@ void   or_transform_points(const float* in, int n, const float T[12], float* out
 int    or_find_correspondences(void* map, const float* pts, int n, const float T[12],
                                double max_corr_dist, uint8_t* valid, double* residual);
 /* find_correspondences_kdtree at pose T (brute-force exact 5-NN over L0 centroids). */
+void   or_set_kdtree_search(int use_tree);   /* 1: kd-tree (default), 0: index-ordered brute force */
 int    or_find_correspondences_kdtree(void* map, const float* pts, int n, const float T[12],
                                       double max_corr_dist, uint8_t* valid, double* residual,
                                       float* normal_out /* nullable, n*3 */, float* target_out /* nullable */);

@@ -1,0 +1,159 @@
+"""GPU parity of the KDTree correspondence variant (use_surfel_correspondence = false).
+
+The oracle is an index-ordered brute-force 5-NN (nanoflann's result set, ties by index) + the same fp64
+collinearity gate / 5-point plane fit; the device runs a grid search with a brute-force fallback.  Bars:
+identical valid set and bit-identical fp64 plane distances at a given pose; optimize per GN iteration within
+1e-4 m / 1e-4 rad (north_star).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def kd_icp():
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), max_points=1 << 17)
+    yield o
+    o.close()
+
+
+def _pose_err(Ta, Tb):
+    A = np.asarray(Ta, np.float64).reshape(3, 4)
+    B = np.asarray(Tb, np.float64).reshape(3, 4)
+    return float(np.linalg.norm(A[:, 3] - B[:, 3])), _data.rot_angle(A[:, :3], B[:, :3])
+
+
+@pytest.mark.parametrize("frame", [11, 21])
+def test_kdtree_correspondences_bitwise(kd_icp, frame):
+    m, pts, Ti, _ = _data.kitti_case(frame)
+    kd_icp.set_map_points(m.l0_cloud())
+    n_o, v_o, r_o = oracle.find_correspondences(m, pts, Ti, kdtree=True)
+    n_g, v_g, r_g = kd_icp.find_correspondences(pts, Ti)
+    assert n_o > 0.5 * len(pts)
+    assert n_g == n_o
+    np.testing.assert_array_equal(v_g, v_o)
+    np.testing.assert_array_equal(r_g.view(np.uint64), r_o.view(np.uint64))
+
+
+def test_kdtree_fallback_and_edge_queries(kd_icp):
+    """Far queries exceed the grid shells (brute-force pass); NaN/inf queries find nothing."""
+    m, pts, Ti, _ = _data.kitti_case(13)
+    kd_icp.set_map_points(m.l0_cloud())
+    q = pts[:700].copy()
+    q[:200] += np.float32(25.0)            # beyond the shell radius of the grid search
+    q[200] = [np.nan, 0, 0]
+    q[201] = [np.inf, 1, 1]
+    n_o, v_o, r_o = oracle.find_correspondences(m, q, Ti, kdtree=True)
+    n_g, v_g, r_g = kd_icp.find_correspondences(q, Ti)
+    assert not v_g[200] and not v_g[201]
+    assert n_g == n_o
+    np.testing.assert_array_equal(v_g, v_o)
+    np.testing.assert_array_equal(r_g.view(np.uint64), r_o.view(np.uint64))
+
+
+def test_kdtree_tiny_maps():
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), max_points=4096)
+    try:
+        rng = np.random.default_rng(3)
+        pts = rng.normal(size=(300, 3)).astype(np.float32)
+        I = np.eye(3, 4, dtype=np.float32)
+        o.set_map_points(rng.normal(size=(4, 3)).astype(np.float32))      # fewer than K = 5 points
+        n, v, _ = o.find_correspondences(pts, I)
+        assert n == 0 and not v.any()
+        five = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0.01], [0.5, 0.5, 0]], np.float32)
+        o.set_map_points(five)                                             # every query sees the same plane
+        n, v, r = o.find_correspondences(pts, I)
+        assert n > 0
+        ok = v.astype(bool)
+        assert np.all(np.abs(r[ok]) <= 1.0)
+        ok_opt, To = o.optimize(None, pts[:0], I)                         # empty scan -> failure
+        assert not ok_opt
+    finally:
+        o.close()
+
+
+@pytest.mark.parametrize("frame", [11, 17, 25])
+def test_kdtree_optimize_per_iteration(kd_icp, frame):
+    m, pts, Ti, _ = _data.kitti_case(frame)
+    kd_icp.set_map_points(m.l0_cloud())
+    ok_o, To_o, it_o, logs_o = oracle.icp_optimize(m, pts, Ti, kdtree=True)
+    ok_g, To_g = kd_icp.optimize(None, pts, Ti)
+    st = kd_icp.get_last_stats()
+    assert ok_g == ok_o
+    assert st.num_iterations == it_o
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        if k == 0:
+            assert lg["n_corr"] == lo["n_corr"]
+            assert lg["scale"] == pytest.approx(lo["scale"], rel=1e-12)
+            assert lg["alpha"] == lo["alpha"]
+        else:
+            assert abs(lg["n_corr"] - lo["n_corr"]) <= max(2, 1e-4 * lo["n_corr"])
+        et, er = _pose_err(lg["pose"], lo["pose"])
+        assert et <= 1e-4 and er <= 1e-4, f"iter {k}: dt {et:.2e} m, dr {er:.2e} rad"
+
+
+def test_kdtree_voxelmap_sync():
+    """optimize(voxel_map, ...) uploads GetPointCloud from the product VoxelMap in KDTree mode."""
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = _data.kitti_seq()
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    om = oracle.VoxelMap(0.5, 3, 0.1, True)
+    for k in (0, 2, 4):
+        p = voxel_filter(_data.kitti_scan(k), 0.5, 8)
+        w = synth.transform(seq.poses[k], p)
+        vm.update(w, seq.poses[k][:3, 3], 120.0, True)
+        om.update(w, seq.poses[k][:3, 3], 120.0, True)
+    np.testing.assert_array_equal(vm.l0_cloud(), om.l0_cloud())
+    pts = voxel_filter(_data.kitti_scan(3), 0.5, 8)
+    Ti = _data.pose12(seq.poses[3])
+    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), max_points=1 << 16)
+    try:
+        ok, T = o.optimize(vm, pts, Ti)
+        ok_o, To, _, _ = oracle.icp_optimize(om, pts, Ti, kdtree=True)
+        assert ok == ok_o
+        et, er = _pose_err(T, To)
+        assert et <= 1e-4 and er <= 1e-4
+    finally:
+        o.close()
+
+
+def test_kdtree_exact_ties_lattice():
+    """Lattice map: many exactly equal neighbour distances; the device must break ties by index like the
+    oracle (grid shells and the brute-force pass both)."""
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer, MapGeometry
+    g = np.stack(np.meshgrid(np.arange(12), np.arange(12), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
+    lattice = (g * 0.5).astype(np.float32)
+    m = oracle.VoxelMap(0.25, 3, 0.1, False)
+    m.update(lattice, np.zeros(3), 1e3, True)
+    rng = np.random.default_rng(5)
+    q = (rng.integers(0, 22, size=(600, 3)) * 0.25).astype(np.float32)
+    q[500:] += np.float32(9.0)                       # some far queries -> brute-force pass
+    I = np.eye(3, 4, dtype=np.float32).reshape(12)
+    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), geometry=MapGeometry(voxel_size=0.25),
+                                       max_points=4096)
+    try:
+        o.set_map_points(m.l0_cloud())
+        n_o, v_o, r_o = oracle.find_correspondences(m, q, I, kdtree=True)
+        n_g, v_g, r_g = o.find_correspondences(q, I)
+        assert n_g == n_o
+        np.testing.assert_array_equal(v_g, v_o)
+        np.testing.assert_array_equal(r_g.view(np.uint64), r_o.view(np.uint64))
+    finally:
+        o.close()
+
+
+def test_kdtree_optimize_repeatable(kd_icp):
+    """Atomics only build the unresolved-query list; results must be bitwise run-to-run."""
+    m, pts, Ti, _ = _data.kitti_case(21)
+    kd_icp.set_map_points(m.l0_cloud())
+    outs = [kd_icp.optimize(None, pts, Ti)[1] for _ in range(3)]
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])

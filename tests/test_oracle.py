@@ -133,3 +133,41 @@ def test_oracle_icp_insufficient_on_empty_map():
     ok, To, iters, logs = oracle.icp_optimize(m, pts, Ti)
     assert not ok and iters == 0
     np.testing.assert_array_equal(To, Ti)
+
+
+# ------------------------------------------------------------------ KDTree variant: kd-tree == brute force
+def _kd_both(m, pts, T):
+    oracle.set_kdtree_search(False)
+    try:
+        b = oracle.find_correspondences(m, pts, T, kdtree=True)
+    finally:
+        oracle.set_kdtree_search(True)
+    t = oracle.find_correspondences(m, pts, T, kdtree=True)
+    return b, t
+
+
+def test_oracle_kdtree_matches_bruteforce_kitti():
+    from tests import _data
+    m, pts, Ti, _ = _data.kitti_case(11)
+    (nb, vb, rb), (nt, vt, rt) = _kd_both(m, pts, Ti)
+    assert nb == nt > 0
+    np.testing.assert_array_equal(vb, vt)
+    np.testing.assert_array_equal(rb.view(np.uint64), rt.view(np.uint64))
+
+
+def test_oracle_kdtree_ties_and_nonfinite():
+    """A lattice map makes many neighbour distances exactly equal: ties must resolve by index like the brute
+    force; NaN / inf queries find nothing."""
+    g = np.stack(np.meshgrid(np.arange(12), np.arange(12), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
+    lattice = (g * 0.5).astype(np.float32)
+    m = oracle.VoxelMap(0.25, 3, 0.1, False)
+    m.update(lattice, np.zeros(3), 1e3, True)
+    rng = np.random.default_rng(5)
+    q = (rng.integers(0, 22, size=(400, 3)) * 0.25).astype(np.float32)   # on-lattice / mid-cell: exact ties
+    q[:5] = [[np.nan, 0, 0], [np.inf, 0, 0], [0, -np.inf, 0], [1, 1, np.nan], [1e30, 0, 0]]
+    I = np.eye(3, 4, dtype=np.float32).reshape(12)
+    (nb, vb, rb), (nt, vt, rt) = _kd_both(m, q, I)
+    assert nb == nt
+    np.testing.assert_array_equal(vb, vt)
+    np.testing.assert_array_equal(rb.view(np.uint64), rt.view(np.uint64))
+    assert not vb[:4].any()
