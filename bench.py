@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "ICP GN-iterations/sec and scans/sec on KITTI-07 @ 1/2/4/8 GPU; % HBM BW"
+ORDER = "azimuth"          # patch1m point order (--order)
 
 
 def log(*a):
@@ -93,10 +94,12 @@ def build_patch1m(rank: int):
     for f in range(4):
         T = synth.se3(synth.rot_z(0.3 + 0.1 * f), [1.0 + f, -2.0, 0.5])
         world = synth.sample_patches(sc, 1_000_000, 1011 + 10 * f + rank)
-        scans.append(synth.transform(np.linalg.inv(T), world))
+        local = synth.transform(np.linalg.inv(T), world)
+        # acquisition order of a spinning sensor (azimuth); --order random keeps the generator's permutation
+        scans.append(local if ORDER == "random" else synth.azimuth_order(local))
         inits.append(synth.perturb(T, rng, 0.05, 0.01))
         gts.append(T)
-    return {"name": "synthetic 1M-pt scan, 1000 planar patches + 10% outliers, surfel ICP",
+    return {"name": f"synthetic 1M-pt scan, 1000 planar patches + 10% outliers, surfel ICP, {ORDER} point order",
             "voxel": 0.5, "max_dist": 1e4, "vm": vm, "scans": scans, "inits": inits, "gts": gts,
             "keyframes": [(mp, np.zeros(3))]}
 
@@ -162,7 +165,10 @@ def main():
     ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--order", default="azimuth", choices=["azimuth", "random"], help="patch1m scan point order")
     args = ap.parse_args()
+    global ORDER
+    ORDER = args.order
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -260,7 +266,7 @@ def main():
         corr_kernel = stage0
     t_corr = kern_us[stage0] * 1e-6
     achieved = alg_bytes / t_corr / 1e9
-    traffic = read_pmc_traffic(args.config)
+    traffic = read_pmc_traffic(args.config + ("_random" if args.config == "patch1m" and ORDER == "random" else ""))
     # where a step's device time goes: isolated kernel time x launches per scan (working launches only)
     gi = float(np.mean(iters))
     per_scan = {k: v * gi for k, v in kern_us.items()}

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -309,17 +310,11 @@ void lo_destroy(lo_ctx* c) {
 }
 
 // ---------------------------------------------------------------- map
-static uint64_t morton_host(int32_t x, int32_t y, int32_t z) {
-    auto ex = [](int32_t v) {
-        uint64_t q = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffull;
-        q = (q | (q << 32)) & 0x1f00000000ffffull;
-        q = (q | (q << 16)) & 0x1f0000ff0000ffull;
-        q = (q | (q << 8)) & 0x100f00f00f00f00full;
-        q = (q | (q << 4)) & 0x10c30c30c30c30c3ull;
-        q = (q | (q << 2)) & 0x1249249249249249ull;
-        return q;
-    };
-    return ex(x) | (ex(y) << 1) | (ex(z) << 2);
+// pack_key (lo_device.h): three 21-bit fields key + 2^20
+static uint64_t pack_key_host(int32_t x, int32_t y, int32_t z) {
+    return static_cast<uint64_t>(static_cast<uint32_t>(x + (1 << 20))) |
+           (static_cast<uint64_t>(static_cast<uint32_t>(y + (1 << 20))) << 21) |
+           (static_cast<uint64_t>(static_cast<uint32_t>(z + (1 << 20))) << 42);
 }
 
 int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, const float* centroids, size_t m) {
@@ -336,7 +331,7 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
             const int32_t v = keys[3 * i + a];
             if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
         }
-        const uint64_t key = morton_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
         uint64_t b = (key * 0x9E3779B97F4A7C15ull) >> (64 - l2);
         while (h[b].key != kEmptyKey && h[b].key != key) b = (b + 1) & mask;
         h[b].key = key;                                    // duplicate keys: last one wins (map semantics)

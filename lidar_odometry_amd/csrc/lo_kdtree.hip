@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
         P.slot[i] = valid ? i : -1;
         if (P.res_dbg) P.res_dbg[i] = valid ? dist : 0.0;
     }
-    corr_epilogue(P, valid, dist, with_stats);
+    corr_epilogue(P, valid, dist, with_stats, blockIdx.x);
 }
 
 }  // namespace lo

@@ -29,27 +29,32 @@ namespace lo {
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
     // P.init: first launch of a scan.  The GN state reset (k_init's job) is folded in here -- the pose comes
     // from the kernel argument, block 0 writes the fresh DevState that the later kernels of the scan read.
-    if (!P.init && P.st->done) return;
+    // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
+    // instead of serialising at the start of every wave.
     const int i = blockIdx.x * kBlock + threadIdx.x;
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    if (i < P.n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    const DevState* cst = P.st;
+    const int done = cst->done;
     float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
+    if (!P.init && done) return;
     scan_pose(P, T);
-
     int slot = -1;
     double r = 0.0;
     if (i < P.n) {
-        const float x = P.pts[3 * i], y = P.pts[3 * i + 1], z = P.pts[3 * i + 2];
         float wx, wy, wz;
-        transform_pt(T, x, y, z, wx, wy, wz);
+        transform_pt(T, px, py, pz, wx, wy, wz);
         const int s = lookup_surfel(P.tab, P.log2cap, P.l1scale, wx, wy, wz);
         if (s >= 0) {
-            const Slot sl = P.tab[s];
-            r = residual_f64(sl, wx, wy, wz);
-            if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, as :630)
+            r = residual_f64(P.tab[s], wx, wy, wz);
+            if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, :630)
         }
         P.slot[i] = slot;
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
     }
-    corr_epilogue(P, slot >= 0, r, with_stats);
+    corr_epilogue(P, slot >= 0, r, with_stats, blockIdx.x);
 }
 
 // ====================================================================================================

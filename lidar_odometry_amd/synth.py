@@ -264,6 +264,14 @@ def patch_scene(n_patches: int = 1000, seed: int = 1000, extent: float = 100.0):
     return {"c": centers, "n": normals, "a": a, "b": b, "size": size, "extent": extent}
 
 
+def azimuth_order(local_pts) -> np.ndarray:
+    """Reorder sensor-frame points by azimuth (then range), the acquisition order of a spinning LiDAR."""
+    p = np.asarray(local_pts)
+    az = np.arctan2(p[:, 1], p[:, 0])
+    rg = np.einsum("ij,ij->i", p[:, :2], p[:, :2])
+    return np.ascontiguousarray(p[np.lexsort((rg, az))])
+
+
 def sample_patches(sc, n_points: int, seed: int, sigma: float = 0.01, outlier_frac: float = 0.1) -> np.ndarray:
     """World-frame samples: (1 - outlier_frac) on patches (area-weighted), the rest uniform in the volume."""
     rng = np.random.default_rng(seed)

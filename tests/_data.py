@@ -72,7 +72,7 @@ def patch_case(n_points: int = 1_000_000, seed: int = 1000):
     m.update(mp, np.zeros(3), 1e4, True)
     T = synth.se3(synth.rot_z(0.3), [1.0, -2.0, 0.5])
     world = synth.sample_patches(sc, n_points, seed + 11)
-    local = synth.transform(np.linalg.inv(T), world)
+    local = synth.azimuth_order(synth.transform(np.linalg.inv(T), world))   # spinning-sensor acquisition order
     Ti = synth.perturb(T, np.random.default_rng(seed), 0.05, 0.01)
     return m, local, pose12(Ti), pose12(T)
 
