@@ -243,13 +243,19 @@ def main():
 
     # live per-kernel device times (HIP events around back-to-back launches on this context's stream)
     i0 = int(np.argmax([len(s) for s in wl["scans"]]))
+    # the scan's own iteration-0 normalisation scale and PKO alpha, so the isolated launches see the real
+    # residual distribution (EM iteration count) and weights
+    icp.optimize(None, wl["scans"][i0], inits[i0])
+    it0 = icp.get_last_stats().iterations
+    scale0 = float(it0[0]["scale"]) if it0 else 0.01
+    alpha0 = float(it0[0]["alpha"]) if it0 else 1.0
     kern_us = {}
     stage0 = "k_knn+k_knn_brute+k_plane" if kd else "k_correspond"
     for kid, name in enumerate((stage0, "k_accumulate", "k_pko", "k_solve")):
         ms = C.c_float(0.0)
         reps = 200 if kid != 2 else 50
         rc = L.lo_bench_kernel(icp.ctx, C.c_void_p(d_scans[i0].data_ptr()), d_scans[i0].shape[0], fptr(inits[i0]),
-                               C.c_double(0.01), C.c_double(1.0), kid, reps, C.byref(ms))
+                               C.c_double(scale0), C.c_double(alpha0), kid, reps, C.byref(ms))
         assert rc == 0, rc
         kern_us[name] = ms.value * 1e3
     n0 = d_scans[i0].shape[0]
@@ -304,9 +310,9 @@ def main():
         "translation_error_vs_gt_m_median": float(np.median(errs)),
         "kernel_us": kern_us,
         "step_device_us_est": {"per_kernel": per_scan, "dominant_kernel": dom,
-                               "dominant_share": per_scan[dom] / (el / args.steps * 1e6),
-                               "note": "isolated kernel time x GN iterations per scan; k_pko is latency-bound "
-                                       "(sequential 100-iteration EM), not HBM/MFMA-bound (DESIGN.md)"},
+                               "dominant_share_of_kernel_time": per_scan[dom] / sum(per_scan.values()),
+                               "note": "isolated kernel time (scan's own iteration-0 scale/alpha) x GN iterations per "
+                                       "scan; k_pko is latency-bound (sequential <=100-iteration EM), not HBM/MFMA-bound"},
         "pcie_inclusive": {"value": pcie_rate, "unit": "scans/s", "scans": n_pc,
                            "path": "lo_icp_optimize on host buffers (H2D points, D2H pose+logs, sync per scan)"},
         "roofline": {"kernel": corr_kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

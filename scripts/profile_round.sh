@@ -12,6 +12,10 @@ fi
 steps+=(
   "bench_kitti:600:python bench.py > gpurun_out/bench_kitti.json"
   "bench_1m:900:python bench.py --config patch1m --steps 40 --warmup 4 --cpu-budget 10 > gpurun_out/bench_patch1m.json"
+  "bench_1m_rand:600:python bench.py --config patch1m --order random --steps 40 --warmup 4 --no-cpu-baseline > gpurun_out/bench_patch1m_random.json"
+  "bench_kd:600:python bench.py --config kitti_kdtree --cpu-budget 10 > gpurun_out/bench_kitti_kdtree.json"
+  "bench_mid360:600:python bench.py --config mid360 --cpu-budget 10 > gpurun_out/bench_mid360.json"
+  "stats_kd:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kd -o run --output-format csv -- python bench.py --config kitti_kdtree --steps 200 --warmup 10 --no-cpu-baseline"
   "stats_kitti:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline"
   "stats_1m:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline"
   "pmcf_kitti:600:rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline"
