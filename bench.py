@@ -104,6 +104,17 @@ def build_patch1m(rank: int):
             "keyframes": [(mp, np.zeros(3))]}
 
 
+def build_kitti_raw(rank: int):
+    """Raw HDL-64 scans: the step is Estimator::preprocess_frame (device FastVoxelFilter, stride 8, 0.5 m) + optimize."""
+    from lidar_odometry_amd import synth
+    wl = build_kitti(rank)
+    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
+    wl["raw_scans"] = [seq.scan(f) for f in range(1, 40, 2)]
+    wl["name"] = "KITTI-07-like raw HDL-64 scan -> device voxel filter (stride 8, 0.5 m) -> surfel ICP, config/kitti.yaml"
+    wl["raw"] = True
+    return wl
+
+
 def build_kitti_kdtree(rank: int):
     wl = build_kitti(rank)
     wl["name"] = "KITTI-07-like HDL-64 scan, KDTree correspondence variant (5-NN plane fit), config/kitti.yaml"
@@ -111,7 +122,7 @@ def build_kitti_kdtree(rank: int):
     return wl
 
 
-WORKLOADS = {"kitti": build_kitti, "kitti_kdtree": build_kitti_kdtree, "mid360": build_mid360,
+WORKLOADS = {"kitti": build_kitti, "kitti_raw": build_kitti_raw, "kitti_kdtree": build_kitti_kdtree, "mid360": build_mid360,
              "patch1m": build_patch1m}
 
 
@@ -132,7 +143,8 @@ def cpu_baseline(wl, budget_s: float):
     t0 = time.perf_counter()
     while True:
         i = n_scans % len(scans)
-        ok, To, it, _ = oracle.icp_optimize(m, scans[i], inits[i], kdtree=wl.get("kdtree", False))
+        pts_i = oracle.voxel_filter(wl["raw_scans"][i], 0.5, 8) if wl.get("raw") else scans[i]
+        ok, To, it, _ = oracle.icp_optimize(m, pts_i, inits[i], kdtree=wl.get("kdtree", False))
         n_scans += 1
         n_iters += it
         el = time.perf_counter() - t0
@@ -188,6 +200,9 @@ def main():
     log(f"[rank {rank}] data built in {time.perf_counter() - t_data:.1f} s: {len(wl['scans'])} scans, "
         f"avg {np.mean([len(s) for s in wl['scans']]):.0f} pts, {wl['vm'].surfel_count()} surfels")
     max_pts = max(len(s) for s in wl["scans"])
+    raw = bool(wl.get("raw", False))
+    if raw:
+        max_pts = max(max_pts, max((len(r) + 7) // 8 for r in wl["raw_scans"]))
     kd = bool(wl.get("kdtree", False))
     icp = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not kd), AdaptiveMEstimatorConfig(),
                                          MapGeometry(voxel_size=wl["voxel"]), device=local, max_points=max_pts)
@@ -197,6 +212,7 @@ def main():
     rc = L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle)
     assert rc == 0, rc
     d_scans = [torch.from_numpy(s).to(dev) for s in wl["scans"]]
+    d_raw = [torch.from_numpy(r).to(dev) for r in wl["raw_scans"]] if raw else None
     inits = [pose12(T) for T in wl["inits"]]
     fptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))   # noqa: E731
     from lidar_odometry_amd.parallel import RECORD_FLOATS, PoseAllGather
@@ -205,7 +221,11 @@ def main():
 
     def step(k):
         i = k % len(d_scans)
-        rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]))
+        if raw:
+            rc = L.lo_icp_optimize_raw_async(icp.ctx, C.c_void_p(d_raw[i].data_ptr()), d_raw[i].shape[0], 8,
+                                             C.c_float(0.5), fptr(inits[i]))
+        else:
+            rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]))
         if rc != 0:
             raise RuntimeError(f"lo_icp_optimize_async rc={rc}: {L.lo_last_error(icp.ctx).decode()}")
         if world > 1:
@@ -301,6 +321,7 @@ def main():
         "dtype": "f32 (pose, J, H) + f64 (residuals, PKO)",
         "data": "synthetic (deterministic raycast scenes; no dataset reachable offline)",
         "config": {"workload": wl["name"], "points_per_scan_avg": float(np.mean([len(s) for s in wl["scans"]])),
+                   **({"raw_points_per_scan_avg": float(np.mean([len(r) for r in wl["raw_scans"]]))} if raw else {}),
                    "distinct_scans": len(wl["scans"]), "map_surfels": wl["vm"].surfel_count(),
                    "map_l0_points": wl["vm"].l0_count(), "correspondence": "kdtree 5-NN" if kd else "L1 surfel",
                    "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),

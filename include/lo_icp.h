@@ -134,6 +134,21 @@ int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12]
                     int kernel_id, int reps, float* avg_ms);
 
 /* ---- single-stage entry points (parity harness; each synchronous) ---- */
+/* ---- device preprocessing + optimize (Estimator::preprocess_frame, Estimator.cpp:561-588) ----
+ * FastVoxelFilter::filter (VoxelMap.h:73-104) on the device -- stride sampling, Morton-cell grouping with the
+ * reference's clamp, fp32 sums in point order, output in first-occurrence order, bit-identical -- followed by
+ * the optimize loop on the filtered points; the filtered count never leaves the device.
+ * ceil(n_raw / stride) must not exceed cfg.max_points. */
+int lo_icp_optimize_raw_async(lo_ctx* ctx, const float* d_raw, size_t n_raw, int stride, float voxel_size,
+                              const float T_init[12]);
+int lo_icp_optimize_raw(lo_ctx* ctx, const float* raw_xyz, size_t n_raw, int stride, float voxel_size,
+                        const float T_init[12], float T_out[12], lo_iter_log* logs, lo_stats* stats);
+/* The last device-filtered scan (the frame's feature cloud, for the keyframe map update); returns the count. */
+long long lo_filtered_points(lo_ctx* ctx, float* out_xyz, size_t cap);
+/* Filter only (parity): host raw in, host filtered out; returns the count or a negative error. */
+long long lo_voxel_filter_gpu(lo_ctx* ctx, const float* raw_xyz, size_t n_raw, float voxel_size, int stride,
+                              float* out_xyz, size_t cap);
+
 /* find_correspondences (IterativeClosestPointOptimizer.cpp:587-645) at pose T:
  * per-point valid flag and fp64 residual |n.(p_w - c)| (0 where invalid). Returns the count. */
 int lo_find_correspondences(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T[12],

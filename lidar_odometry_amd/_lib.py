@@ -23,7 +23,8 @@ LO_MAX_ITERS = 64
 EXPORTED_SYMBOLS = (
     "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
-    "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_async",
+    "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
+    "lo_voxel_filter_gpu", "lo_icp_optimize_async",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
     # include/lo_map.h
@@ -84,6 +85,15 @@ def lib():
     L.lo_map_set_points.argtypes = [vp, C.POINTER(C.c_float), C.c_size_t]
     L.lo_map_point_count.restype = C.c_size_t
     L.lo_map_point_count.argtypes = [vp]
+    L.lo_icp_optimize_raw_async.restype = C.c_int
+    L.lo_icp_optimize_raw_async.argtypes = [vp, vp, C.c_size_t, C.c_int, C.c_float, fp]
+    L.lo_icp_optimize_raw.restype = C.c_int
+    L.lo_icp_optimize_raw.argtypes = [vp, fp, C.c_size_t, C.c_int, C.c_float, fp, fp, C.POINTER(LoIterLog),
+                                      C.POINTER(LoStats)]
+    L.lo_filtered_points.restype = C.c_longlong
+    L.lo_filtered_points.argtypes = [vp, fp, C.c_size_t]
+    L.lo_voxel_filter_gpu.restype = C.c_longlong
+    L.lo_voxel_filter_gpu.argtypes = [vp, fp, C.c_size_t, C.c_float, C.c_int, fp, C.c_size_t]
     L.lo_get_config.restype = C.c_int
     L.lo_get_config.argtypes = [vp, C.POINTER(LoConfig)]
     L.lo_icp_optimize.argtypes = [vp, fp, C.c_size_t, fp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]

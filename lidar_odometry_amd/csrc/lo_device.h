@@ -62,7 +62,8 @@ struct DevState {
 struct KParams {
     // scan
     const float* pts;
-    int n;
+    int n;                            // points (upper bound when n_dev is set)
+    const int* n_dev;                 // device-side point count (device voxel filter output), or null
     int nb;
     int nb_acc;                       // k_accumulate blocks = min(nb, kAccBlocks)
     int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
@@ -270,6 +271,10 @@ __device__ __forceinline__ T wave_sum(T v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+
+// Points of this scan: the host count, or the device voxel filter's count (lo_vfilter.hip) when the scan was
+// filtered on the device -- grids are then sized for the upper bound and lanes past the count idle.
+__device__ __forceinline__ int scan_n(const KParams& P) { return P.n_dev ? *P.n_dev : P.n; }
 
 // ---------------------------------------------------------------------------------------------------
 // Correspondence-kernel helpers shared by the surfel (k_correspond) and KDTree (lo_kdtree.hip) paths.

@@ -16,6 +16,7 @@
 
 #include "lo_device.h"
 #include "lo_pko_tables.h"
+#include "lo_vfilter.h"
 
 namespace lo {
 __global__ void k_correspond(KParams P, int with_stats);
@@ -71,6 +72,11 @@ struct lo_ctx {
     int32_t* d_kd_unres = nullptr;
     double* d_kd_res = nullptr;
     Slot* d_kd_plane = nullptr;
+    // device preprocessing (FastVoxelFilter): raw staging for host input + filter work buffers
+    float* d_raw = nullptr;
+    size_t raw_cap = 0;
+    VfBuffers vf;
+    bool last_dev_count = false;    // last optimize took its point count from the device filter
     // PKO tables
     PkoTables tables;
     double* d_alphas = nullptr;
@@ -302,6 +308,8 @@ void lo_destroy(lo_ctx* c) {
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->d_kd_pts, c->d_kd_start, c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
     for (void* b : bufs) if (b) (void)hipFree(b);
+    if (c->d_raw) (void)hipFree(c->d_raw);
+    vf_free(c->vf);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -444,7 +452,7 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats) {
     hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
 }
 
-static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12]) {
+static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12], const int* n_dev = nullptr) {
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
     c->last_n = n;
@@ -456,6 +464,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
     } else {
         KParams P = make_params(c, d_pts, static_cast<int>(n));
+        P.n_dev = n_dev;                                  // device-filtered scan: count read on the device
         KParams P0 = P;                                   // first k_correspond also resets the GN state
         P0.init = 1;
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
@@ -481,6 +490,7 @@ int lo_icp_optimize_async(lo_ctx* c, const float* d_pts, size_t n, const float T
     if (!c || !T_init || (n > 0 && !d_pts)) return LO_ERR_ARG;
     if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
     LO_HIP(c, hipSetDevice(c->device));
+    c->last_dev_count = false;
     return enqueue_optimize(c, d_pts, n, T_init);
 }
 
@@ -526,9 +536,82 @@ int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12
     if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
     LO_HIP(c, hipSetDevice(c->device));
     if (n > 0) LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    c->last_dev_count = false;
     int rc = enqueue_optimize(c, c->d_pts, n, T_init);
     if (rc != LO_OK) return rc;
     return lo_icp_result(c, T_out, logs, st);
+}
+
+// ---------------------------------------------------------------- device preprocessing + optimize
+static int stage_raw(lo_ctx* c, const float* raw, size_t n_raw) {
+    if (n_raw > c->raw_cap) {
+        if (c->d_raw) LO_HIP(c, hipFree(c->d_raw));
+        c->d_raw = nullptr;
+        LO_HIP(c, hipMalloc(&c->d_raw, n_raw * 3 * sizeof(float)));
+        c->raw_cap = n_raw;
+    }
+    if (n_raw > 0) LO_HIP(c, hipMemcpyAsync(c->d_raw, raw, n_raw * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    return LO_OK;
+}
+
+static int check_raw_args(lo_ctx* c, size_t n_raw, int stride, float voxel) {
+    if (stride < 1 || !(voxel > 0.0f)) { c->err = "stride must be >= 1 and voxel_size > 0"; return LO_ERR_ARG; }
+    const size_t m = (n_raw + stride - 1) / stride;
+    if (m > static_cast<size_t>(c->cfg.max_points)) { c->err = "ceil(n_raw / stride) exceeds max_points"; return LO_ERR_CAPACITY; }
+    return LO_OK;
+}
+
+int lo_icp_optimize_raw_async(lo_ctx* c, const float* d_raw, size_t n_raw, int stride, float voxel_size,
+                              const float T_init[12]) {
+    if (!c || !T_init || (n_raw > 0 && !d_raw)) return LO_ERR_ARG;
+    int rc = check_raw_args(c, n_raw, stride, voxel_size);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipSetDevice(c->device));
+    int m = 0;
+    LO_HIP(c, vf_enqueue(c->vf, d_raw, n_raw, stride, voxel_size, c->d_pts, c->stream, m));
+    c->last_dev_count = true;
+    return enqueue_optimize(c, c->d_pts, static_cast<size_t>(m), T_init, c->vf.n_out);
+}
+
+int lo_icp_optimize_raw(lo_ctx* c, const float* raw, size_t n_raw, int stride, float voxel_size, const float T_init[12],
+                        float T_out[12], lo_iter_log* logs, lo_stats* st) {
+    if (!c || !T_init || !T_out || (n_raw > 0 && !raw)) return LO_ERR_ARG;
+    int rc = check_raw_args(c, n_raw, stride, voxel_size);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipSetDevice(c->device));
+    rc = stage_raw(c, raw, n_raw);
+    if (rc != LO_OK) return rc;
+    rc = lo_icp_optimize_raw_async(c, c->d_raw, n_raw, stride, voxel_size, T_init);
+    if (rc != LO_OK) return rc;
+    return lo_icp_result(c, T_out, logs, st);
+}
+
+long long lo_filtered_points(lo_ctx* c, float* out, size_t cap) {
+    if (!c) return LO_ERR_ARG;
+    if (!c->last_dev_count || !c->vf.n_out) { c->err = "no device-filtered scan"; return LO_ERR_STATE; }
+    LO_HIP(c, hipSetDevice(c->device));
+    int n = 0;
+    LO_HIP(c, hipMemcpyAsync(&n, c->vf.n_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (out && n > 0) {
+        const size_t k = std::min<size_t>(static_cast<size_t>(n), cap);
+        LO_HIP(c, hipMemcpy(out, c->d_pts, k * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return n;
+}
+
+long long lo_voxel_filter_gpu(lo_ctx* c, const float* raw, size_t n_raw, float voxel_size, int stride, float* out,
+                              size_t out_cap) {
+    if (!c || (n_raw > 0 && !raw)) return LO_ERR_ARG;
+    int rc = check_raw_args(c, n_raw, stride, voxel_size);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipSetDevice(c->device));
+    rc = stage_raw(c, raw, n_raw);
+    if (rc != LO_OK) return rc;
+    int m = 0;
+    LO_HIP(c, vf_enqueue(c->vf, c->d_raw, n_raw, stride, voxel_size, c->d_pts, c->stream, m));
+    c->last_dev_count = true;
+    return lo_filtered_points(c, out, out_cap);
 }
 
 // ---------------------------------------------------------------- parity entry points

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     const int i = gi / kKnnGroup, g = gi % kKnnGroup;
     float T[12];
     scan_pose(P, T);
-    if (i >= P.n) return;                                    // whole groups leave together
+    if (i >= scan_n(P)) return;                              // whole groups leave together
     int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
     float qx, qy, qz;
     transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
     }
     bool valid = false;
     double dist = 0.0;
-    if (i < P.n) {
+    if (i < scan_n(P)) {
         const int32_t* nb = P.kd_nbr + 5 * static_cast<size_t>(i);
         if (nb[0] >= 0) {
             double Pm[5][3];

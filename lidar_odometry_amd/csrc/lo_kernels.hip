@@ -32,8 +32,9 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
     // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
     // instead of serialising at the start of every wave.
     const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
-    if (i < P.n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
     const DevState* cst = P.st;
     const int done = cst->done;
     float T[12];
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
     scan_pose(P, T);
     int slot = -1;
     double r = 0.0;
-    if (i < P.n) {
+    if (i < n) {
         float wx, wy, wz;
         transform_pt(T, px, py, pz, wx, wy, wz);
         const int s = lookup_surfel(P.tab, P.log2cap, P.l1scale, wx, wy, wz);
@@ -90,7 +91,8 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
     const float dl = static_cast<float>(s_alpha);
     // grid-stride (at most kAccBlocks blocks): per-thread fp32 sums of <= 4 points at 1M, then the same
     // wave / block trees; the partial count k_solve reduces stays <= kAccBlocks
-    for (int i = blockIdx.x * kBlock + tid; i < P.n; i += P.nb_acc * kBlock) {
+    const int n = scan_n(P);
+    for (int i = blockIdx.x * kBlock + tid; i < n; i += P.nb_acc * kBlock) {
         const int s = P.slot[i];
         if (s < 0) continue;
         const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];

@@ -187,6 +187,39 @@ class IterativeClosestPointOptimizer:
         logs = (LoIterLog * self._cfg.max_iterations)()
         st = LoStats()
         rc = self._check(lib().lo_icp_optimize(self._ctx, _fptr(p), len(p), _fptr(Ti), _fptr(To), logs, C.byref(st)))
+        self._record(st, logs)
+        return rc == _lib.LO_OK, pose34(To)
+
+    def optimize_raw(self, voxel_map, raw_points, initial_transform, stride: int = 8, voxel_size: float = 0.5):
+        """Estimator::preprocess_frame (FastVoxelFilter on the device) + optimize, no host round trip between them."""
+        self._sync_map(voxel_map)
+        p = _as_pts(raw_points)
+        Ti = _as_pose(initial_transform)
+        To = np.zeros(12, np.float32)
+        logs = (LoIterLog * self._cfg.max_iterations)()
+        st = LoStats()
+        rc = self._check(lib().lo_icp_optimize_raw(self._ctx, _fptr(p), len(p), int(stride), float(voxel_size),
+                                                   _fptr(Ti), _fptr(To), logs, C.byref(st)))
+        self._record(st, logs)
+        return rc == _lib.LO_OK, pose34(To)
+
+    def filtered_points(self) -> np.ndarray:
+        """Feature cloud of the last device-filtered scan (for the keyframe map update)."""
+        n = self._check(lib().lo_filtered_points(self._ctx, None, 0))
+        out = np.zeros((max(n, 1), 3), np.float32)
+        self._check(lib().lo_filtered_points(self._ctx, _fptr(out), n))
+        return out[:n]
+
+    def voxel_filter(self, raw_points, voxel_size: float, stride: int = 1) -> np.ndarray:
+        """FastVoxelFilter::filter on the device (parity entry; synchronous)."""
+        p = _as_pts(raw_points)
+        m = (len(p) + stride - 1) // stride
+        out = np.zeros((max(m, 1), 3), np.float32)
+        n = self._check(lib().lo_voxel_filter_gpu(self._ctx, _fptr(p), len(p), float(voxel_size), int(stride),
+                                                  _fptr(out), max(m, 1)))
+        return out[:n]
+
+    def _record(self, st, logs):
         its = []
         for i in range(st.iterations):
             L = logs[i]
@@ -195,7 +228,6 @@ class IterativeClosestPointOptimizer:
                         "g": np.array(L.g[:], np.float32), "delta": np.array(L.delta[:], np.float32)})
         self._last = OptimizationStats(st.n_corr, st.iterations, st.initial_cost, st.final_cost, st.gpu_ms,
                                        bool(st.converged), its)
-        return rc == _lib.LO_OK, pose34(To)
 
     def get_last_stats(self) -> OptimizationStats:
         return self._last
