@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_voxel_filter",
+    # include/lo_io.h
+    "lo_load_kitti_bin", "lo_load_ply", "lo_kitti_pose_line", "lo_save_trajectory_kitti",
 )
 
 
@@ -94,6 +96,14 @@ def lib():
     L.lo_filtered_points.argtypes = [vp, fp, C.c_size_t]
     L.lo_voxel_filter_gpu.restype = C.c_longlong
     L.lo_voxel_filter_gpu.argtypes = [vp, fp, C.c_size_t, C.c_float, C.c_int, fp, C.c_size_t]
+    L.lo_load_kitti_bin.restype = C.c_longlong
+    L.lo_load_kitti_bin.argtypes = [C.c_char_p, fp, C.c_size_t]
+    L.lo_load_ply.restype = C.c_longlong
+    L.lo_load_ply.argtypes = [C.c_char_p, fp, C.c_size_t]
+    L.lo_kitti_pose_line.restype = C.c_int
+    L.lo_kitti_pose_line.argtypes = [fp, C.c_char_p, C.c_size_t]
+    L.lo_save_trajectory_kitti.restype = C.c_int
+    L.lo_save_trajectory_kitti.argtypes = [C.c_char_p, fp, C.c_size_t]
     L.lo_get_config.restype = C.c_int
     L.lo_get_config.argtypes = [vp, C.POINTER(LoConfig)]
     L.lo_icp_optimize.argtypes = [vp, fp, C.c_size_t, fp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]

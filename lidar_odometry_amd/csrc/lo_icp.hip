@@ -102,11 +102,13 @@ struct lo_ctx {
 static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs, g.num_alpha_segments)); }
 
 static void launch_pko(lo_ctx* c, const KParams& P, int it) {
+    // dynamic LDS for the per-block prefix (nb ints; 64 KB only at the 4M-point maximum)
+    const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     // one GMM sample per thread: 2 waves cover the reference's 100 samples, 4 waves up to 256
     if (c->cfg.gmm_sample_size <= 128)
-        hipLaunchKernelGGL(k_pko_t<2>, dim3(pko_grid(c->cfg)), dim3(128), 0, c->stream, P, it);
+        hipLaunchKernelGGL(k_pko_t<2>, dim3(pko_grid(c->cfg)), dim3(128), pre_bytes, c->stream, P, it);
     else
-        hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), 0, c->stream, P, it);
+        hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), pre_bytes, c->stream, P, it);
 }
 
 static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
@@ -262,6 +264,11 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
+    // k_pko_t's dynamic block-prefix LDS reaches 64 KB at the 4M-point maximum
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(kMaxBlocks * sizeof(int))));
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(kMaxBlocks * sizeof(int))));
     c->kd = g.use_surfel_correspondence == 0;
     if (c->kd) {
         LO_HIP(c, hipMalloc(&c->d_kd_nbr, NB * kBlock * 5 * sizeof(int32_t)));

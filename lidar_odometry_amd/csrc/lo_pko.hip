@@ -282,7 +282,7 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     if (blockIdx.x == 0) dbg = st->dbg;
 #endif
     LO_STAMP(dbg, 0);
-    __shared__ int s_pre[kMaxBlocks];                // 64 KB: exclusive prefix of block counts
+    extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
     __shared__ double s_sd[64 * NW];
     __shared__ double s_gmm[3 * kMaxK];
     __shared__ double s_P[100];

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _declared_symbols():
-    txt = open(os.path.join(ROOT, "include", "lo_icp.h")).read() + open(os.path.join(ROOT, "include", "lo_map.h")).read()
+    txt = "".join(open(os.path.join(ROOT, "include", h)).read() for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+                  if h.endswith(".h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(lo_[a-z0-9_]+)\s*\(", txt)))
 
