@@ -1,0 +1,63 @@
+/* lo_odometry.h — the frame loop around the ICP step (the hot path's caller), MI355X device path.
+ *
+ * Replaces Estimator::process_frame (src/processing/Estimator.cpp:115-233) for odometry without loop
+ * closure / PGO (out of scope, off in all parity runs):
+ *   preprocess_frame (:561-589)            -> device FastVoxelFilter (lo_icp_optimize_raw)
+ *   first frame (:235-269)                 -> pose = initial pose, create_keyframe
+ *   guess = prev_pose * velocity (:154)    -> SE3f product with SO3 re-projection (MathUtils.h:144-147)
+ *   estimate_motion_dual_frame (:271-320) -> lo_icp_optimize_raw on the device map; failure keeps the guess
+ *   velocity = prev^-1 * pose (:177)
+ *   should_create_keyframe (:349-368)      -> |dt| > keyframe_distance or |Log(R_kf^-1 R)| > keyframe_rotation
+ *   create_keyframe (:370-530)             -> host VoxelMap::UpdateVoxelMap(world cloud, position, 1.2 * max_range)
+ *                                             (lo_map.h) + device map upload (and RebuildKdTree in KDTree mode)
+ */
+#ifndef LO_ODOMETRY_H
+#define LO_ODOMETRY_H
+
+#include <stddef.h>
+
+#include "lo_icp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    lo_config icp;                 /* ICP + PKO + map geometry (voxel_size = map voxel, hierarchy_factor) */
+    int    point_stride;           /* point_cloud.point_stride: 8 (kitti.yaml:18) */
+    float  filter_voxel_size;      /* point_cloud.voxel_size: 0.5 (kitti.yaml:17) */
+    double max_range;              /* point_cloud.max_range: 100 (kitti.yaml:20); map radius = 1.2 x */
+    double keyframe_distance;      /* estimator.keyframe_distance_threshold: 1.0 m (kitti.yaml:55) */
+    double keyframe_rotation;      /* estimator.keyframe_rotation_threshold: 0.3 rad (kitti.yaml:56) */
+    float  planarity_threshold;    /* surfel planarity: 0.1 (kitti.yaml:22) */
+} lo_odom_config;
+
+typedef struct {
+    int    status;                 /* LO_OK, or LO_INSUFFICIENT when ICP failed and the guess was kept */
+    int    keyframe;               /* 1 if this frame became a keyframe (map updated) */
+    int    icp_iterations;
+    int    n_filtered;             /* feature cloud size */
+    int    n_corr;
+    double device_ms;              /* preprocessing + ICP on the device (HIP events) */
+    double map_ms;                 /* keyframe map update + upload (host wall time), 0 otherwise */
+} lo_odom_frame;
+
+typedef struct lo_odometry lo_odometry;
+
+void          lo_odom_config_default_kitti(lo_odom_config* cfg);
+lo_odometry*  lo_odom_create(const lo_odom_config* cfg, int device, int* err);
+void          lo_odom_destroy(lo_odometry* o);
+const char*   lo_odom_last_error(const lo_odometry* o);
+/* Pose of the first frame (LidarFrame::get_initial_pose); identity by default. */
+int           lo_odom_set_initial_pose(lo_odometry* o, const float T[12]);
+/* One raw scan (AoS float3, host memory) -> its world pose (row-major 3x4).  Returns LO_OK / LO_INSUFFICIENT
+ * (the guess was kept, as :304-307) or a negative error. */
+int           lo_odom_process(lo_odometry* o, const float* raw_xyz, size_t n, float T_out[12], lo_odom_frame* info);
+size_t        lo_odom_keyframe_count(const lo_odometry* o);
+size_t        lo_odom_map_surfels(const lo_odometry* o);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

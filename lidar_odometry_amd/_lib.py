@@ -31,6 +31,9 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_voxel_filter",
+    # include/lo_odometry.h
+    "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
+    "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels",
     # include/lo_io.h
     "lo_load_kitti_bin", "lo_load_ply", "lo_kitti_pose_line", "lo_save_trajectory_kitti",
 )
@@ -56,6 +59,16 @@ class LoIterLog(C.Structure):
 class LoStats(C.Structure):
     _fields_ = [("iterations", C.c_int), ("n_corr", C.c_int), ("status", C.c_int), ("converged", C.c_int),
                 ("initial_cost", C.c_double), ("final_cost", C.c_double), ("gpu_ms", C.c_double)]
+
+
+class LoOdomConfig(C.Structure):
+    _fields_ = [("icp", LoConfig), ("point_stride", C.c_int), ("filter_voxel_size", C.c_float), ("max_range", C.c_double),
+                ("keyframe_distance", C.c_double), ("keyframe_rotation", C.c_double), ("planarity_threshold", C.c_float)]
+
+
+class LoOdomFrame(C.Structure):
+    _fields_ = [("status", C.c_int), ("keyframe", C.c_int), ("icp_iterations", C.c_int), ("n_filtered", C.c_int),
+                ("n_corr", C.c_int), ("device_ms", C.c_double), ("map_ms", C.c_double)]
 
 
 _lib = None
@@ -96,6 +109,19 @@ def lib():
     L.lo_filtered_points.argtypes = [vp, fp, C.c_size_t]
     L.lo_voxel_filter_gpu.restype = C.c_longlong
     L.lo_voxel_filter_gpu.argtypes = [vp, fp, C.c_size_t, C.c_float, C.c_int, fp, C.c_size_t]
+    L.lo_odom_config_default_kitti.argtypes = [C.POINTER(LoOdomConfig)]
+    L.lo_odom_create.restype = vp
+    L.lo_odom_create.argtypes = [C.POINTER(LoOdomConfig), C.c_int, C.POINTER(C.c_int)]
+    L.lo_odom_destroy.argtypes = [vp]
+    L.lo_odom_last_error.restype = C.c_char_p
+    L.lo_odom_last_error.argtypes = [vp]
+    L.lo_odom_set_initial_pose.argtypes = [vp, fp]
+    L.lo_odom_process.restype = C.c_int
+    L.lo_odom_process.argtypes = [vp, fp, C.c_size_t, fp, C.POINTER(LoOdomFrame)]
+    L.lo_odom_keyframe_count.restype = C.c_size_t
+    L.lo_odom_keyframe_count.argtypes = [vp]
+    L.lo_odom_map_surfels.restype = C.c_size_t
+    L.lo_odom_map_surfels.argtypes = [vp]
     L.lo_load_kitti_bin.restype = C.c_longlong
     L.lo_load_kitti_bin.argtypes = [C.c_char_p, fp, C.c_size_t]
     L.lo_load_ply.restype = C.c_longlong

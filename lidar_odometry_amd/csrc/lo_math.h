@@ -1,0 +1,193 @@
+// lo_math.h — host-side fp32 restatements of the reference's Eigen / MathUtils operations (shared by the
+// host VoxelMap and the odometry loop).  Compiled with -ffp-contract=off: no FMA contraction where Eigen
+// (GCC, no -mfma) rounds every product and sum separately.
+#pragma once
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+namespace lo {
+
+// ---------------------------------------------------------------------------------------------
+// Eigen JacobiSVD<Matrix3f>, square case (JacobiSVD.h compute(), real_2x2_jacobi_svd, makeJacobi)
+// ---------------------------------------------------------------------------------------------
+struct Rot { float c, s; };
+inline Rot rot_t(Rot r) { return {r.c, -r.s}; }
+inline Rot rot_mul(Rot a, Rot b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
+inline void rotate(float& x, float& y, Rot r) {
+    const float xi = x, yi = y;
+    x = r.c * xi + r.s * yi;
+    y = -r.s * xi + r.c * yi;
+}
+inline Rot make_jacobi(float x, float y, float z) {
+    const float deno = 2.0f * std::fabs(y);
+    if (deno < FLT_MIN) return {1.0f, 0.0f};
+    const float tau = (x - z) / deno;
+    const float w = std::sqrt(tau * tau + 1.0f);
+    const float t = tau > 0.0f ? 1.0f / (tau + w) : 1.0f / (tau - w);
+    const float sgn = t > 0.0f ? 1.0f : -1.0f;
+    const float n = 1.0f / std::sqrt(t * t + 1.0f);
+    return {n, ((-sgn) * (y / std::fabs(y))) * std::fabs(t) * n};
+}
+
+// A row-major a[r][c]; U columns = left singular vectors, S descending.
+inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vout[3][3] = nullptr) {
+    float scale = 0.0f;                                               // maxCoeff<PropagateNaN>
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
+        const float v = std::fabs(A[r][c]);
+        scale = (std::isnan(v) || std::isnan(scale)) ? NAN : std::max(scale, v);
+    }
+    float W[3][3], V[3][3];
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) { U[r][c] = V[r][c] = (r == c) ? 1.0f : 0.0f; }
+    if (!std::isfinite(scale)) {
+        S[0] = S[1] = S[2] = NAN;
+        if (Vout) for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vout[r][c] = V[r][c];
+        return;
+    }
+    if (scale == 0.0f) scale = 1.0f;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) W[r][c] = A[r][c] / scale;
+    float maxDiag = std::max(std::fabs(W[0][0]), std::max(std::fabs(W[1][1]), std::fabs(W[2][2])));
+    const float prec = 2.0f * FLT_EPSILON;
+    bool done = false;
+    for (int sweep = 0; !done && sweep < 1000; ++sweep) {
+        done = true;
+        for (int p = 1; p < 3; ++p) {
+            for (int q = 0; q < p; ++q) {
+                const float thr = std::max(FLT_MIN, prec * maxDiag);
+                if (!(std::fabs(W[p][q]) > thr || std::fabs(W[q][p]) > thr)) continue;
+                done = false;
+                // real_2x2_jacobi_svd
+                float m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+                Rot r1;
+                const float t = m00 + m11, d = m10 - m01;
+                if (std::fabs(d) < FLT_MIN) r1 = {1.0f, 0.0f};
+                else {
+                    const float u = t / d;
+                    const float tmp = std::sqrt(1.0f + u * u);
+                    r1 = {u / tmp, 1.0f / tmp};
+                }
+                rotate(m00, m10, r1);
+                rotate(m01, m11, r1);
+                const Rot jr = make_jacobi(m00, m01, m11);
+                const Rot jl = rot_mul(r1, rot_t(jr));
+                for (int i = 0; i < 3; ++i) rotate(W[p][i], W[q][i], jl);       // W.applyOnTheLeft(p,q,jl)
+                for (int i = 0; i < 3; ++i) rotate(U[i][p], U[i][q], jl);       // U.applyOnTheRight(p,q,jl^T)
+                const Rot jrt = rot_t(jr);
+                for (int i = 0; i < 3; ++i) rotate(W[i][p], W[i][q], jrt);      // W.applyOnTheRight(p,q,jr)
+                for (int i = 0; i < 3; ++i) rotate(V[i][p], V[i][q], jrt);
+                maxDiag = std::max(maxDiag, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = W[i][i];
+        S[i] = std::fabs(a);
+        if (a < 0.0f) for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
+    }
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    for (int i = 0; i < 3; ++i) {                                         // descending sort (first max)
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k) if (S[k] > S[pos]) pos = k;
+        if (S[pos] == 0.0f) break;
+        if (pos != i) {
+            std::swap(S[i], S[pos]);
+            for (int r = 0; r < 3; ++r) { std::swap(U[r][i], U[r][pos]); std::swap(V[r][i], V[r][pos]); }
+        }
+    }
+    if (Vout) for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vout[r][c] = V[r][c];
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// SO3 / SE3f (MathUtils.h:57-168, MathUtils.cpp:41-99)
+// ---------------------------------------------------------------------------------------------
+inline float dot3e(float a0, float a1, float a2, float b0, float b1, float b2) {   // Vector3f dot: e0 + (e1 + e2)
+    const float e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;
+    return e0 + (e1 + e2);
+}
+inline void mul33e(const float A[3][3], const float B[3][3], float C[3][3]) {     // Matrix3f * Matrix3f
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) C[r][c] = dot3e(A[r][0], A[r][1], A[r][2], B[0][c], B[1][c], B[2][c]);
+}
+inline float det3e(const float m[3][3]) {                                         // Eigen bruteforce_det3_helper order
+    auto h = [&](int a, int b, int c) { return m[0][a] * (m[1][b] * m[2][c] - m[1][c] * m[2][b]); };
+    return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
+}
+// SO3(const Matrix3f&): U V^T of JacobiSVD, U.col(2) negated when det < 0 (MathUtils.cpp:86-99)
+inline void so3_project(const float M[3][3], float R[3][3]) {
+    float U[3][3], S[3], V[3][3], Vt[3][3];
+    jacobi_svd3(M, U, S, V);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vt[r][c] = V[c][r];
+    mul33e(U, Vt, R);
+    if (det3e(R) < 0.0f) {
+        for (int r = 0; r < 3; ++r) U[r][2] *= -1.0f;
+        mul33e(U, Vt, R);
+    }
+}
+struct SE3f {
+    float R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    float t[3] = {0, 0, 0};
+};
+inline SE3f se3_from12(const float T[12]) {
+    SE3f s;
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) s.R[r][c] = T[r * 4 + c]; s.t[r] = T[r * 4 + 3]; }
+    return s;
+}
+inline void se3_to12(const SE3f& s, float T[12]) {
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) T[r * 4 + c] = s.R[r][c]; T[r * 4 + 3] = s.t[r]; }
+}
+// SE3::operator* (MathUtils.h:144-147): SO3(R1 R2), t1 + R1 t2
+inline SE3f se3_mul(const SE3f& A, const SE3f& B) {
+    SE3f o;
+    float M[3][3];
+    mul33e(A.R, B.R, M);
+    so3_project(M, o.R);
+    for (int r = 0; r < 3; ++r) o.t[r] = A.t[r] + dot3e(A.R[r][0], A.R[r][1], A.R[r][2], B.t[0], B.t[1], B.t[2]);
+    return o;
+}
+// SE3::Inverse (MathUtils.h:155-158): R_inv = SO3(R^T), t = R_inv * (-t)
+inline SE3f se3_inv(const SE3f& A) {
+    SE3f o;
+    float Rt[3][3];
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rt[r][c] = A.R[c][r];
+    so3_project(Rt, o.R);
+    for (int r = 0; r < 3; ++r) o.t[r] = dot3e(o.R[r][0], o.R[r][1], o.R[r][2], -A.t[0], -A.t[1], -A.t[2]);
+    return o;
+}
+// |SO3::Log(R)| (MathUtils.cpp:41-84), kEps = 1e-6f
+inline float so3_log_norm(const float m[3][3]) {
+    const float trace = (m[0][0] + m[1][1]) + m[2][2];
+    const float cos_theta = (trace - 1.0f) * 0.5f;
+    const float theta = std::acos(std::max(-1.0f, std::min(1.0f, cos_theta)));
+    float w[3];
+    if (theta < 1e-6f) {
+        w[0] = m[2][1] - 0.0f; w[1] = m[0][2] - 0.0f; w[2] = m[1][0] - 0.0f;          // Vee(R - I)
+    } else {
+        const float st = std::sin(theta);
+        if (std::fabs(st) < 1e-6f) {
+            int mi = 0;
+            if (m[1][1] > m[0][0]) mi = 1;
+            if (m[2][2] > m[mi][mi]) mi = 2;
+            float axis[3];
+            axis[mi] = std::sqrt((m[mi][mi] + 1.0f) * 0.5f);
+            for (int i = 0; i < 3; ++i) if (i != mi) axis[i] = m[mi][i] / (2.0f * axis[mi]);
+            const float sk[3] = {(m[2][1] - m[1][2]) * 0.5f, (m[0][2] - m[2][0]) * 0.5f, (m[1][0] - m[0][1]) * 0.5f};
+            const float d = dot3e(axis[0], axis[1], axis[2], sk[0], sk[1], sk[2]);
+            if (d < 0) for (float& a : axis) a = -a;
+            for (int i = 0; i < 3; ++i) w[i] = axis[i] * theta;
+        } else {
+            const float f = theta / (2.0f * st);
+            w[0] = f * (m[2][1] - m[1][2]); w[1] = f * (m[0][2] - m[2][0]); w[2] = f * (m[1][0] - m[0][1]);
+        }
+    }
+    return std::sqrt(dot3e(w[0], w[1], w[2], w[0], w[1], w[2]));
+}
+// util::transform_point_cloud (PointCloudUtils.cpp:102-125): Matrix4f * Vector4f(x, y, z, 1), packet order
+inline void transform_points(const SE3f& T, const float* in, size_t n, float* out) {
+    for (size_t i = 0; i < n; ++i) {
+        const float x = in[3 * i], y = in[3 * i + 1], z = in[3 * i + 2];
+        for (int r = 0; r < 3; ++r) out[3 * i + r] = ((T.R[r][0] * x + T.R[r][1] * y) + T.R[r][2] * z) + T.t[r] * 1.0f;
+    }
+}
+
+}  // namespace lo

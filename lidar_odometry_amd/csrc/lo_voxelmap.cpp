@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/lo_map.h"
+#include "lo_math.h"
 
 namespace lo {
 namespace {
@@ -125,90 +126,6 @@ class OrderedMap {
     std::vector<int32_t> slots_;
     uint64_t mask_ = 0;
 };
-
-// ---------------------------------------------------------------------------------------------
-// Eigen JacobiSVD<Matrix3f>, square case (JacobiSVD.h compute(), real_2x2_jacobi_svd, makeJacobi)
-// ---------------------------------------------------------------------------------------------
-struct Rot { float c, s; };
-inline Rot rot_t(Rot r) { return {r.c, -r.s}; }
-inline Rot rot_mul(Rot a, Rot b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
-inline void rotate(float& x, float& y, Rot r) {
-    const float xi = x, yi = y;
-    x = r.c * xi + r.s * yi;
-    y = -r.s * xi + r.c * yi;
-}
-inline Rot make_jacobi(float x, float y, float z) {
-    const float deno = 2.0f * std::fabs(y);
-    if (deno < FLT_MIN) return {1.0f, 0.0f};
-    const float tau = (x - z) / deno;
-    const float w = std::sqrt(tau * tau + 1.0f);
-    const float t = tau > 0.0f ? 1.0f / (tau + w) : 1.0f / (tau - w);
-    const float sgn = t > 0.0f ? 1.0f : -1.0f;
-    const float n = 1.0f / std::sqrt(t * t + 1.0f);
-    return {n, ((-sgn) * (y / std::fabs(y))) * std::fabs(t) * n};
-}
-
-// A row-major a[r][c]; U columns = left singular vectors, S descending.
-void jacobi_svd3(const float A[3][3], float U[3][3], float S[3]) {
-    float scale = 0.0f;                                               // maxCoeff<PropagateNaN>
-    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
-        const float v = std::fabs(A[r][c]);
-        scale = (std::isnan(v) || std::isnan(scale)) ? NAN : std::max(scale, v);
-    }
-    float W[3][3], V[3][3];
-    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) { U[r][c] = V[r][c] = (r == c) ? 1.0f : 0.0f; }
-    if (!std::isfinite(scale)) { S[0] = S[1] = S[2] = NAN; return; }
-    if (scale == 0.0f) scale = 1.0f;
-    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) W[r][c] = A[r][c] / scale;
-    float maxDiag = std::max(std::fabs(W[0][0]), std::max(std::fabs(W[1][1]), std::fabs(W[2][2])));
-    const float prec = 2.0f * FLT_EPSILON;
-    bool done = false;
-    for (int sweep = 0; !done && sweep < 1000; ++sweep) {
-        done = true;
-        for (int p = 1; p < 3; ++p) {
-            for (int q = 0; q < p; ++q) {
-                const float thr = std::max(FLT_MIN, prec * maxDiag);
-                if (!(std::fabs(W[p][q]) > thr || std::fabs(W[q][p]) > thr)) continue;
-                done = false;
-                // real_2x2_jacobi_svd
-                float m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
-                Rot r1;
-                const float t = m00 + m11, d = m10 - m01;
-                if (std::fabs(d) < FLT_MIN) r1 = {1.0f, 0.0f};
-                else {
-                    const float u = t / d;
-                    const float tmp = std::sqrt(1.0f + u * u);
-                    r1 = {u / tmp, 1.0f / tmp};
-                }
-                rotate(m00, m10, r1);
-                rotate(m01, m11, r1);
-                const Rot jr = make_jacobi(m00, m01, m11);
-                const Rot jl = rot_mul(r1, rot_t(jr));
-                for (int i = 0; i < 3; ++i) rotate(W[p][i], W[q][i], jl);       // W.applyOnTheLeft(p,q,jl)
-                for (int i = 0; i < 3; ++i) rotate(U[i][p], U[i][q], jl);       // U.applyOnTheRight(p,q,jl^T)
-                const Rot jrt = rot_t(jr);
-                for (int i = 0; i < 3; ++i) rotate(W[i][p], W[i][q], jrt);      // W.applyOnTheRight(p,q,jr)
-                for (int i = 0; i < 3; ++i) rotate(V[i][p], V[i][q], jrt);
-                maxDiag = std::max(maxDiag, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
-            }
-        }
-    }
-    for (int i = 0; i < 3; ++i) {
-        const float a = W[i][i];
-        S[i] = std::fabs(a);
-        if (a < 0.0f) for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
-    }
-    for (int i = 0; i < 3; ++i) S[i] *= scale;
-    for (int i = 0; i < 3; ++i) {                                         // descending sort (first max)
-        int pos = i;
-        for (int k = i + 1; k < 3; ++k) if (S[k] > S[pos]) pos = k;
-        if (S[pos] == 0.0f) break;
-        if (pos != i) {
-            std::swap(S[i], S[pos]);
-            for (int r = 0; r < 3; ++r) { std::swap(U[r][i], U[r][pos]); std::swap(V[r][i], V[r][pos]); }
-        }
-    }
-}
 
 struct L0 {
     float c[3] = {0.0f, 0.0f, 0.0f};

@@ -126,7 +126,8 @@ class KittiLikeSequence:
     HZ = 10.0
     SENSOR_H = 1.73
 
-    def __init__(self, seed: int = 7, n_frames: int | None = None):
+    def __init__(self, seed: int = 7, n_frames: int | None = None, ramp_s: float = 0.0):
+        """ramp_s > 0: the vehicle starts from rest and reaches cruise speed after ramp_s seconds."""
         self.seed = seed
         self.n_frames = n_frames or self.N_FRAMES
         rng = np.random.default_rng(seed)
@@ -135,6 +136,8 @@ class KittiLikeSequence:
         t = np.arange(self.n_frames) * dt
         heading = 0.6 * np.sin(2 * np.pi * t / 60.0) + 0.3 * np.sin(2 * np.pi * t / 23.0 + 0.7)
         speed = 6.0 + 1.0 * np.sin(2 * np.pi * t / 37.0)
+        if ramp_s > 0.0:
+            speed = speed * np.minimum(1.0, t / ramp_s)
         x = np.cumsum(speed * np.cos(heading) * dt)
         y = np.cumsum(speed * np.sin(heading) * dt)
         self.poses = []

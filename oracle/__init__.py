@@ -65,6 +65,8 @@ def lib():
         L.or_kmeans_seed_draws.argtypes = [C.c_int, C.c_int, ip]
         L.or_pko_tables.argtypes = [C.POINTER(PkoCfg), dp, dp]
         L.or_se3_compose.argtypes = [fp, fp, fp]
+        L.or_se3_inverse.argtypes = [fp, fp]
+        L.or_keyframe_metrics.argtypes = [fp, fp, dp]
         L.or_so3_exp.argtypes = [fp, fp]
         L.or_so3_normalize.argtypes = [fp, fp]
         L.or_jacobi_svd3.argtypes = [fp, fp, fp, fp]
@@ -145,6 +147,60 @@ def pko_tables(cfg: PkoCfg | None = None):
 
 
 # ---------------------------------------------------------------- math
+def se3_inverse(A):
+    a, ap = _f32(A)
+    o = np.zeros(12, np.float32)
+    lib().or_se3_inverse(ap, o.ctypes.data_as(C.POINTER(C.c_float)))
+    return o
+
+
+def keyframe_metrics(kf, pose):
+    """(|t - t_kf|, |Log(R_kf^-1 R)|) as Estimator::should_create_keyframe computes them."""
+    a, ap = _f32(kf)
+    b, bp = _f32(pose)
+    o = np.zeros(2, np.float64)
+    lib().or_keyframe_metrics(ap, bp, o.ctypes.data_as(C.POINTER(C.c_double)))
+    return float(o[0]), float(o[1])
+
+
+def odometry(raw_scans, stride=8, voxel=0.5, map_voxel=0.5, max_range=100.0, kf_dist=1.0, kf_rot=0.3, initial=None):
+    """Estimator::process_frame without loop closure / PGO (Estimator.cpp:115-233), on the oracle primitives.
+    Returns (poses (n, 12) float32, keyframe flags)."""
+    I = np.eye(3, 4, dtype=np.float32).reshape(12)
+    P0 = I if initial is None else np.ascontiguousarray(np.asarray(initial, np.float32)[:3, :4].reshape(12))
+    m = VoxelMap(map_voxel, 3, 0.1, True)
+    poses, kfs = [], []
+    prev = vel = last_kf = I
+    for k, raw in enumerate(raw_scans):
+        pts = voxel_filter(raw, voxel, stride)
+        kf = False
+        if k == 0:
+            pose = P0
+            kf = len(pts) > 0
+        else:
+            guess = se3_compose(prev, vel)
+            g_in = guess.copy().reshape(3, 4)
+            g_in[:, :3] = so3_normalize(g_in[:, :3].reshape(9)).reshape(3, 3)
+            ok, T, _, _ = icp_optimize(m, pts, g_in.reshape(12))
+            if ok:
+                pose = np.asarray(T, np.float32).reshape(3, 4).copy()
+                pose[:, :3] = so3_normalize(pose[:, :3].reshape(9)).reshape(3, 3)
+                pose = pose.reshape(12)
+            else:
+                pose = guess
+            vel = se3_compose(se3_inverse(prev), pose)
+            d, a = keyframe_metrics(last_kf, pose)
+            kf = d > kf_dist or a > kf_rot
+        prev = pose
+        if kf:
+            w = transform_points(pts, pose)
+            m.update(w, np.asarray(pose, np.float32).reshape(3, 4)[:, 3].astype(np.float64), 1.2 * max_range, True)
+            last_kf = pose
+        poses.append(np.asarray(pose, np.float32).reshape(12))
+        kfs.append(kf)
+    return np.stack(poses), kfs
+
+
 def se3_compose(A, B):
     a, ap = _f32(A)
     b, bp = _f32(B)

