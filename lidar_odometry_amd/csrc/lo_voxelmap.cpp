@@ -30,28 +30,24 @@ struct Key3 {
 };
 inline bool operator==(const Key3& a, const Key3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 
-inline uint64_t spread21(int32_t v) {
-    uint64_t q = static_cast<uint64_t>(v + (1 << 20)) & 0x1fffffull;
-    q = (q | (q << 32)) & 0x1f00000000ffffull;
-    q = (q | (q << 16)) & 0x1f0000ff0000ffull;
-    q = (q | (q << 8)) & 0x100f00f00f00f00full;
-    q = (q | (q << 4)) & 0x10c30c30c30c30c3ull;
-    q = (q | (q << 2)) & 0x1249249249249249ull;
-    return q;
-}
 inline uint64_t mix64(uint64_t h) {
     __uint128_t r = static_cast<__uint128_t>(h) * 0x9E3779B97F4A7C15ull;
     return static_cast<uint64_t>(r) ^ static_cast<uint64_t>(r >> 64);
 }
 struct HashKey3 {
-    uint64_t operator()(const Key3& k) const { return mix64(spread21(k.x) | (spread21(k.y) << 1) | (spread21(k.z) << 2)); }
+    uint64_t operator()(const Key3& k) const {
+        const uint64_t xy = static_cast<uint64_t>(static_cast<uint32_t>(k.x)) << 32 | static_cast<uint32_t>(k.y);
+        return mix64(xy ^ static_cast<uint64_t>(static_cast<uint32_t>(k.z)) * 0xD6E8FEB86659FD93ull);
+    }
 };
 struct HashU64 {
     uint64_t operator()(uint64_t k) const { return mix64(k); }
 };
 struct NoValue {};
 
-// Insertion-ordered open-addressing map; erase moves the last entry into the hole.
+// Insertion-ordered open-addressing map; erase moves the last entry into the hole (the value order of
+// ankerl::unordered_dense, which the reference iterates).  The index is linear probing at load <= 1/2 with the
+// 32-bit hash cached in each slot, so a probe touches a key only on a hash match.
 template <class K, class V, class H>
 class OrderedMap {
   public:
@@ -63,67 +59,83 @@ class OrderedMap {
     const V& val_at(size_t i) const { return vals_[i]; }
 
     int64_t find(const K& k) const {
-        uint64_t b = H()(k) & mask_;
-        for (;;) {
-            const int32_t e = slots_[b];
-            if (e < 0) return -1;
-            if (keys_[e] == k) return e;
-            b = (b + 1) & mask_;
+        const uint32_t h = hash32(k);
+        for (uint64_t b = h & mask_;; b = (b + 1) & mask_) {
+            const Slot& e = slots_[b];
+            if (e.idx < 0) return -1;
+            if (e.h == h && keys_[e.idx] == k) return e.idx;
         }
     }
     // returns index; *inserted set when new (value default-constructed)
     size_t upsert(const K& k, bool* inserted) {
-        const int64_t f = find(k);
-        if (f >= 0) { if (inserted) *inserted = false; return static_cast<size_t>(f); }
-        if ((keys_.size() + 1) * 5 > slots_.size() * 4) reindex(slots_.size() * 2);
+        const uint32_t h = hash32(k);
+        uint64_t b = h & mask_;
+        for (;; b = (b + 1) & mask_) {
+            const Slot& e = slots_[b];
+            if (e.idx < 0) break;
+            if (e.h == h && keys_[e.idx] == k) { if (inserted) *inserted = false; return static_cast<size_t>(e.idx); }
+        }
         keys_.push_back(k);
         vals_.emplace_back();
-        place(static_cast<int32_t>(keys_.size() - 1));
+        const int32_t i = static_cast<int32_t>(keys_.size() - 1);
+        if (keys_.size() * 2 > slots_.size()) reindex(slots_.size() * 2);
+        else slots_[b] = {i, h};
         if (inserted) *inserted = true;
         return keys_.size() - 1;
     }
     bool erase(const K& k) {
-        uint64_t b = H()(k) & mask_;
-        for (;;) {
-            const int32_t e = slots_[b];
-            if (e < 0) return false;
-            if (keys_[e] == k) break;
-            b = (b + 1) & mask_;
+        const uint32_t hk = hash32(k);
+        uint64_t b = hk & mask_;
+        for (;; b = (b + 1) & mask_) {
+            const Slot& e = slots_[b];
+            if (e.idx < 0) return false;
+            if (e.h == hk && keys_[e.idx] == k) break;
         }
-        const int32_t victim = slots_[b];
-        slots_[b] = -1;
-        for (uint64_t j = (b + 1) & mask_; slots_[j] >= 0; j = (j + 1) & mask_) {   // backward shift
-            const uint64_t home = H()(keys_[slots_[j]]) & mask_;
-            if (((j - home) & mask_) >= ((j - b) & mask_)) { slots_[b] = slots_[j]; slots_[j] = -1; b = j; }
+        const int32_t victim = slots_[b].idx;
+        slots_[b].idx = -1;
+        for (uint64_t j = (b + 1) & mask_; slots_[j].idx >= 0; j = (j + 1) & mask_) {   // backward shift
+            const uint64_t home = slots_[j].h & mask_;
+            if (((j - home) & mask_) >= ((j - b) & mask_)) { slots_[b] = slots_[j]; slots_[j].idx = -1; b = j; }
         }
         const int32_t last = static_cast<int32_t>(keys_.size() - 1);
         if (victim != last) {
-            uint64_t s = H()(keys_[last]) & mask_;
-            while (slots_[s] != last) s = (s + 1) & mask_;
+            const uint32_t hl = hash32(keys_[last]);
+            uint64_t s = hl & mask_;
+            while (slots_[s].idx != last) s = (s + 1) & mask_;
             keys_[victim] = keys_[last];
             vals_[victim] = std::move(vals_[last]);
-            slots_[s] = victim;
+            slots_[s].idx = victim;
         }
         keys_.pop_back();
         vals_.pop_back();
         return true;
     }
-    void clear() { keys_.clear(); vals_.clear(); reindex(16); }
+    // empties the map but keeps the slot array (a per-update scratch map never re-grows from 16 slots)
+    void clear() {
+        keys_.clear();
+        vals_.clear();
+        std::fill(slots_.begin(), slots_.end(), Slot{-1, 0});
+    }
 
   private:
-    void place(int32_t i) {
-        uint64_t b = H()(keys_[i]) & mask_;
-        while (slots_[b] >= 0) b = (b + 1) & mask_;
-        slots_[b] = i;
-    }
+    struct Slot {
+        int32_t idx;
+        uint32_t h;
+    };
+    static uint32_t hash32(const K& k) { return static_cast<uint32_t>(H()(k)); }
     void reindex(size_t cap) {
-        slots_.assign(cap, -1);
+        slots_.assign(cap, Slot{-1, 0});
         mask_ = cap - 1;
-        for (size_t i = 0; i < keys_.size(); ++i) place(static_cast<int32_t>(i));
+        for (size_t i = 0; i < keys_.size(); ++i) {
+            const uint32_t h = hash32(keys_[i]);
+            uint64_t b = h & mask_;
+            while (slots_[b].idx >= 0) b = (b + 1) & mask_;
+            slots_[b] = {static_cast<int32_t>(i), h};
+        }
     }
     std::vector<K> keys_;
     std::vector<V> vals_;
-    std::vector<int32_t> slots_;
+    std::vector<Slot> slots_;
     uint64_t mask_ = 0;
 };
 
@@ -132,7 +144,43 @@ struct L0 {
     int hit_count = 1;
     int point_count = 0;
 };
-using ChildSet = OrderedMap<Key3, NoValue, HashKey3>;
+
+// occupied_children (ankerl::unordered_dense::set, VoxelMap.h:312-318): insertion order, erase moves the last
+// element into the hole.  An L1 voxel has at most factor^3 children (27 at kitti.yaml's factor 3), so a linear
+// list with the same order semantics replaces the hashed set (no per-voxel allocation, no rehash).
+class ChildSet {
+  public:
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    const Key3& key_at(size_t i) const { return data()[i]; }
+    void upsert(const Key3& k, bool* fresh) {
+        Key3* d = data();
+        for (size_t i = 0; i < n_; ++i) if (d[i] == k) { if (fresh) *fresh = false; return; }
+        if (n_ == kInline) { spill_.assign(inline_, inline_ + kInline); }
+        if (n_ >= kInline) spill_.push_back(k); else inline_[n_] = k;
+        ++n_;
+        if (fresh) *fresh = true;
+    }
+    void erase(const Key3& k) {
+        Key3* d = data();
+        for (size_t i = 0; i < n_; ++i) {
+            if (!(d[i] == k)) continue;
+            d[i] = d[n_ - 1];
+            --n_;
+            if (n_ >= kInline) spill_.pop_back();
+            else if (n_ == kInline - 1 && !spill_.empty()) { std::copy(spill_.begin(), spill_.begin() + n_, inline_); spill_.clear(); }
+            return;
+        }
+    }
+
+  private:
+    static constexpr size_t kInline = 27;
+    Key3* data() { return n_ > kInline || (n_ == kInline && !spill_.empty()) ? spill_.data() : inline_; }
+    const Key3* data() const { return n_ > kInline || (n_ == kInline && !spill_.empty()) ? spill_.data() : inline_; }
+    Key3 inline_[kInline];
+    std::vector<Key3> spill_;
+    size_t n_ = 0;
+};
 struct L1 {
     ChildSet children;
     bool has_surfel = false;
@@ -152,11 +200,15 @@ struct HostVoxelMap {
     OrderedMap<Key3, L0, HashKey3> l0;
     OrderedMap<Key3, L1, HashKey3> l1;
 
-    Key3 key(const float* p, int level) const {
-        float s = voxel;
-        if (level == 1) s *= static_cast<float>(factor);
-        return {static_cast<int32_t>(std::floor(p[0] / s)), static_cast<int32_t>(std::floor(p[1] / s)),
-                static_cast<int32_t>(std::floor(p[2] / s))};
+    OrderedMap<Key3, NoValue, HashKey3> touched;   // scratch, kept across updates
+    std::vector<int32_t> k0, k1;
+
+    // PointToVoxelKey for a whole cloud: floor(p / scale) per coordinate, one flat loop over the 3n floats
+    // (vectorised: divps + roundps; the same IEEE division and floor as the per-point form)
+    static void keys_of(const float* xyz, size_t n, float s, std::vector<int32_t>& out) {
+        out.resize(3 * n);
+        int32_t* o = out.data();
+        for (size_t j = 0; j < 3 * n; ++j) o[j] = static_cast<int32_t>(std::floor(xyz[j] / s));
     }
     Key3 parent(const Key3& k) const {
         const int f = factor;
@@ -172,8 +224,7 @@ struct HostVoxelMap {
         if (n.children.size() < 5) n.has_surfel = false;
         if (n.children.empty()) l1.erase(p);
     }
-    void add_point(const float* p) {
-        const Key3 k = key(p, 0);
+    void add_point(const float* p, const Key3& k) {
         bool fresh = false;
         const size_t i = l0.upsert(k, &fresh);
         L0& v = l0.val_at(i);
@@ -209,10 +260,12 @@ struct HostVoxelMap {
         for (size_t i = 0; i < l1.size(); ++i) if (l1.val_at(i).children.empty()) empty1.push_back(l1.key_at(i));
         for (const Key3& k : empty1) l1.erase(k);
 
-        OrderedMap<Key3, NoValue, HashKey3> touched;
+        keys_of(xyz, n, voxel, k0);
+        keys_of(xyz, n, voxel * static_cast<float>(factor), k1);
+        touched.clear();
         for (size_t i = 0; i < n; ++i) {
-            add_point(xyz + 3 * i);
-            touched.upsert(key(xyz + 3 * i, 1), nullptr);
+            add_point(xyz + 3 * i, Key3{k0[3 * i], k0[3 * i + 1], k0[3 * i + 2]});
+            touched.upsert(Key3{k1[3 * i], k1[3 * i + 1], k1[3 * i + 2]}, nullptr);
         }
         if (!compute_surfels) return;
         std::vector<float> cs;
