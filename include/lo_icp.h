@@ -149,6 +149,21 @@ long long lo_filtered_points(lo_ctx* ctx, float* out_xyz, size_t cap);
 long long lo_voxel_filter_gpu(lo_ctx* ctx, const float* raw_xyz, size_t n_raw, float voxel_size, int stride,
                               float* out_xyz, size_t cap);
 
+/* ---- loop-closure ICP (IterativeClosestPointOptimizer::optimize_loop, IterativeClosestPointOptimizer.cpp:40-251;
+ * find_correspondences_loop :465-585; called from Estimator.cpp:686, :1001) ----
+ * curr / matched: the two keyframes' feature clouds (local frames, AoS float3, host memory) with their world poses.
+ * The matched cloud is put in the world (transform_point_cloud) and gridded on the device (a separate grid: the
+ * context's own map is untouched, whatever its correspondence mode); then up to 100 GN iterations of exact 5-NN +
+ * collinearity gate + plane fit (no distance gate), PKO, normal equations and solve, as optimize_loop.
+ * Returns LO_OK when the iteration converged AND the inlier ratio (nearest matched point < 1 m) is >= 0.5 (the
+ * reference's true); LO_INSUFFICIENT otherwise (too few correspondences, no convergence in 100 iterations, or
+ * too few inliers).  As the reference, T_rel_out = T_curr^-1 * optimized pose and inlier_ratio are written only
+ * when the iteration converged (stats->converged = 1).  logs (nullable) receives the first LO_MAX_ITERS
+ * iterations. */
+int lo_icp_optimize_loop(lo_ctx* ctx, const float* curr_xyz, size_t n_curr, const float T_curr[12],
+                         const float* matched_xyz, size_t n_matched, const float T_matched[12],
+                         float T_rel_out[12], float* inlier_ratio, lo_iter_log* logs, lo_stats* stats);
+
 /* find_correspondences (IterativeClosestPointOptimizer.cpp:587-645) at pose T:
  * per-point valid flag and fp64 residual |n.(p_w - c)| (0 where invalid). Returns the count. */
 int lo_find_correspondences(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T[12],

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
-    "lo_voxel_filter_gpu", "lo_icp_optimize_async",
+    "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
     # include/lo_map.h
@@ -105,6 +105,9 @@ def lib():
     L.lo_icp_optimize_raw.restype = C.c_int
     L.lo_icp_optimize_raw.argtypes = [vp, fp, C.c_size_t, C.c_int, C.c_float, fp, fp, C.POINTER(LoIterLog),
                                       C.POINTER(LoStats)]
+    L.lo_icp_optimize_loop.restype = C.c_int
+    L.lo_icp_optimize_loop.argtypes = [vp, fp, C.c_size_t, fp, fp, C.c_size_t, fp, fp, fp, C.POINTER(LoIterLog),
+                                       C.POINTER(LoStats)]
     L.lo_filtered_points.restype = C.c_longlong
     L.lo_filtered_points.argtypes = [vp, fp, C.c_size_t]
     L.lo_voxel_filter_gpu.restype = C.c_longlong

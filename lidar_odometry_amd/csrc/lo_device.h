@@ -51,6 +51,7 @@ struct DevState {
     int status;
     unsigned int acc_arrive;        // k_accumulate last-block-done counter (reset by the last block)
     unsigned int kd_unres_n;        // KDTree path: queries the grid search could not certify (k_knn_brute)
+    unsigned int inliers;           // loop closure: points whose nearest matched-map point is < 1 m (k_inlier)
     double H_out[36];
     double g_out[6];
     double cost_out;
@@ -78,6 +79,11 @@ struct KParams {
     int32_t* kd_unres;                // queries left to the brute-force pass
     double* kd_res;                   // per point fp64 point-to-plane distance (the reference's residual)
     Slot* kd_plane;                   // per point plane: normal / centroid rounded to fp32 (.cast<float>())
+    // loop-closure ICP (optimize_loop, IterativeClosestPointOptimizer.cpp:40-251): no distance gate, and the
+    // target is neighbour 0 taken to the matched keyframe's local frame (Tlw) and back to the world (Tm)
+    int loop;
+    float Tm[12];                     // matched keyframe pose, row-major 3x4
+    float Tlw[12];                    // its inverse (T_lw_last, :509)
     // map
     const Slot* tab;
     uint32_t log2cap;
@@ -295,6 +301,7 @@ __device__ __forceinline__ void scan_pose(const KParams& P, float (&T)[12]) {
             st->done = 0;
             st->status = LO_OK;
             st->acc_arrive = 0;
+            st->inliers = 0;
             // kd_unres_n is NOT reset here: other blocks of the same k_knn launch may already be appending
             // (k_plane zeroes it after every use; k_init / lo_create start it at 0)
         }

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "lo_device.h"
+#include "lo_math.h"
 #include "lo_pko_tables.h"
 #include "lo_vfilter.h"
 
@@ -30,9 +31,22 @@ __global__ void k_export_pose(const DevState* st, float* out);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
 __global__ void k_plane(KParams P, int with_stats);
+__global__ void k_inlier(KParams P);
 }  // namespace lo
 
 using namespace lo;
+
+// Dense uniform grid over a point set (the kd-tree's role): points sorted by cell, x fastest, index order
+// inside a cell; start[cell] = first point, start[ncell] = m.
+struct PointGrid {
+    float4* d_pts = nullptr;
+    size_t pts_cap = 0;
+    uint32_t* d_start = nullptr;
+    size_t start_cap = 0;
+    int m = 0;
+    int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
+    float h = 1.0f;
+};
 
 struct lo_ctx {
     lo_config cfg{};
@@ -61,13 +75,8 @@ struct lo_ctx {
     size_t n_surfels = 0;
     // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
     bool kd = false;
-    float4* d_kd_pts = nullptr;
-    size_t kd_pts_cap = 0;
-    uint32_t* d_kd_start = nullptr;
-    size_t kd_start_cap = 0;
-    int kd_m = 0;
-    int kd_org[3] = {0, 0, 0}, kd_dim[3] = {1, 1, 1};
-    float kd_h = 1.0f;
+    PointGrid grid;                 // the map's L0 centroids (lo_map_set_points)
+    PointGrid lgrid;                // loop closure: the matched keyframe's local map (lo_icp_optimize_loop)
     int32_t* d_kd_nbr = nullptr;
     int32_t* d_kd_unres = nullptr;
     double* d_kd_res = nullptr;
@@ -109,6 +118,19 @@ static void launch_pko(lo_ctx* c, const KParams& P, int it) {
         hipLaunchKernelGGL(k_pko_t<2>, dim3(pko_grid(c->cfg)), dim3(128), pre_bytes, c->stream, P, it);
     else
         hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), pre_bytes, c->stream, P, it);
+}
+
+static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
+    P.tab = c->d_kd_plane;
+    P.kd_pts = G.d_pts;
+    P.kd_start = G.d_start;
+    P.kd_m = G.m;
+    for (int a = 0; a < 3; ++a) { P.kd_org[a] = G.org[a]; P.kd_dim[a] = G.dim[a]; }
+    P.kd_h = G.h;
+    P.kd_nbr = c->d_kd_nbr;
+    P.kd_unres = c->d_kd_unres;
+    P.kd_res = c->d_kd_res;
+    P.kd_plane = c->d_kd_plane;
 }
 
 static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
@@ -154,18 +176,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.res_dbg = nullptr;
     P.direct_res = nullptr;
     P.st = c->d_st;
-    if (c->kd) {                                         // KDTree path: downstream kernels read per-point planes
-        P.tab = c->d_kd_plane;
-        P.kd_pts = c->d_kd_pts;
-        P.kd_start = c->d_kd_start;
-        P.kd_m = c->kd_m;
-        for (int a = 0; a < 3; ++a) { P.kd_org[a] = c->kd_org[a]; P.kd_dim[a] = c->kd_dim[a]; }
-        P.kd_h = c->kd_h;
-        P.kd_nbr = c->d_kd_nbr;
-        P.kd_unres = c->d_kd_unres;
-        P.kd_res = c->d_kd_res;
-        P.kd_plane = c->d_kd_plane;
-    }
+    if (c->kd) set_kd_params(c, P, c->grid);             // KDTree path: downstream kernels read per-point planes
     return P;
 }
 
@@ -221,6 +232,23 @@ int lo_get_config(const lo_ctx* ctx, lo_config* out) {
 int lo_device(const lo_ctx* ctx) { return ctx ? ctx->device : -1; }
 void* lo_stream(lo_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
+// per-point buffers of the KDTree correspondence stage (KDTree map mode, and the loop-closure ICP of any context)
+static int kd_alloc(lo_ctx* c) {
+    if (c->d_kd_nbr) return LO_OK;
+    const size_t NB = (static_cast<size_t>(c->cfg.max_points) + kBlock - 1) / kBlock;
+    LO_HIP(c, hipMalloc(&c->d_kd_nbr, NB * kBlock * 5 * sizeof(int32_t)));
+    LO_HIP(c, hipMalloc(&c->d_kd_unres, NB * kBlock * sizeof(int32_t)));
+    LO_HIP(c, hipMalloc(&c->d_kd_res, NB * kBlock * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_kd_plane, NB * kBlock * sizeof(Slot)));
+    for (PointGrid* G : {&c->grid, &c->lgrid}) {          // empty grid until a point set is uploaded
+        LO_HIP(c, hipMalloc(&G->d_start, 2 * sizeof(uint32_t)));
+        LO_HIP(c, hipMemset(G->d_start, 0, 2 * sizeof(uint32_t)));
+        G->start_cap = 2;
+        G->h = 2.0f * c->cfg.voxel_size;
+    }
+    return LO_OK;
+}
+
 static int ctx_alloc(lo_ctx* c) {
     const lo_config& g = c->cfg;
     LO_HIP(c, hipSetDevice(c->device));
@@ -271,14 +299,8 @@ static int ctx_alloc(lo_ctx* c) {
                                   static_cast<int>(kMaxBlocks * sizeof(int))));
     c->kd = g.use_surfel_correspondence == 0;
     if (c->kd) {
-        LO_HIP(c, hipMalloc(&c->d_kd_nbr, NB * kBlock * 5 * sizeof(int32_t)));
-        LO_HIP(c, hipMalloc(&c->d_kd_unres, NB * kBlock * sizeof(int32_t)));
-        LO_HIP(c, hipMalloc(&c->d_kd_res, NB * kBlock * sizeof(double)));
-        LO_HIP(c, hipMalloc(&c->d_kd_plane, NB * kBlock * sizeof(Slot)));
-        LO_HIP(c, hipMalloc(&c->d_kd_start, 2 * sizeof(uint32_t)));     // empty grid until lo_map_set_points
-        LO_HIP(c, hipMemset(c->d_kd_start, 0, 2 * sizeof(uint32_t)));
-        c->kd_start_cap = 2;
-        c->kd_h = 2.0f * g.voxel_size;
+        int rc = kd_alloc(c);
+        if (rc != LO_OK) return rc;
     }
     return LO_OK;
 }
@@ -313,7 +335,8 @@ void lo_destroy(lo_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part,
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
-                    c->d_kd_pts, c->d_kd_start, c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
+                    c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
+                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->d_raw) (void)hipFree(c->d_raw);
     vf_free(c->vf);
@@ -373,9 +396,7 @@ size_t lo_map_surfel_count(const lo_ctx* c) { return c ? c->n_surfels : 0; }
 // index order inside a cell; kd_start[cell] = first point, kd_start[ncell] = m.
 static constexpr size_t kKdMaxCells = size_t(1) << 26;
 
-int lo_map_set_points(lo_ctx* c, const float* xyz, size_t m) {
-    if (!c) return LO_ERR_ARG;
-    if (!c->kd) { c->err = "lo_map_set_points needs use_surfel_correspondence = 0"; return LO_ERR_STATE; }
+static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
     if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
     if (m > static_cast<size_t>(INT32_MAX / 2)) { c->err = "too many map points"; return LO_ERR_CAPACITY; }
     for (size_t i = 0; i < 3 * m; ++i)
@@ -419,36 +440,42 @@ int lo_map_set_points(lo_ctx* c, const float* xyz, size_t m) {
     }
     LO_HIP(c, hipSetDevice(c->device));
     LO_HIP(c, hipStreamSynchronize(c->stream));
-    if (pts.size() > c->kd_pts_cap) {
-        if (c->d_kd_pts) LO_HIP(c, hipFree(c->d_kd_pts));
-        c->d_kd_pts = nullptr;
-        LO_HIP(c, hipMalloc(&c->d_kd_pts, pts.size() * sizeof(float4)));
-        c->kd_pts_cap = pts.size();
+    if (pts.size() > G.pts_cap) {
+        if (G.d_pts) LO_HIP(c, hipFree(G.d_pts));
+        G.d_pts = nullptr;
+        LO_HIP(c, hipMalloc(&G.d_pts, pts.size() * sizeof(float4)));
+        G.pts_cap = pts.size();
     }
-    if (start.size() > c->kd_start_cap) {
-        if (c->d_kd_start) LO_HIP(c, hipFree(c->d_kd_start));
-        c->d_kd_start = nullptr;
-        LO_HIP(c, hipMalloc(&c->d_kd_start, start.size() * sizeof(uint32_t)));
-        c->kd_start_cap = start.size();
+    if (start.size() > G.start_cap) {
+        if (G.d_start) LO_HIP(c, hipFree(G.d_start));
+        G.d_start = nullptr;
+        LO_HIP(c, hipMalloc(&G.d_start, start.size() * sizeof(uint32_t)));
+        G.start_cap = start.size();
     }
-    LO_HIP(c, hipMemcpy(c->d_kd_pts, pts.data(), pts.size() * sizeof(float4), hipMemcpyHostToDevice));
-    LO_HIP(c, hipMemcpy(c->d_kd_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    c->kd_m = static_cast<int>(m);
-    c->kd_h = h;
-    for (int a = 0; a < 3; ++a) { c->kd_org[a] = org[a]; c->kd_dim[a] = dim[a]; }
+    LO_HIP(c, hipMemcpy(G.d_pts, pts.data(), pts.size() * sizeof(float4), hipMemcpyHostToDevice));
+    LO_HIP(c, hipMemcpy(G.d_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    G.m = static_cast<int>(m);
+    G.h = h;
+    for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
     return LO_OK;
 }
 
-size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->kd_m) : 0; }
+int lo_map_set_points(lo_ctx* c, const float* xyz, size_t m) {
+    if (!c) return LO_ERR_ARG;
+    if (!c->kd) { c->err = "lo_map_set_points needs use_surfel_correspondence = 0"; return LO_ERR_STATE; }
+    return grid_build(c, c->grid, xyz, m);
+}
+
+size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->grid.m) : 0; }
 
 // ---------------------------------------------------------------- optimize
 // Correspondence stage of one GN iteration: surfel lookup, or (KDTree variant) grid kNN + brute-force
 // fallback + plane fit.  P0 carries init = 1 on a scan's first iteration.
 static constexpr int kBruteBlocks = 256;
 
-static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats) {
+static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool kd) {
     const dim3 grid(P.nb), blk(kBlock);
-    if (!c->kd) {
+    if (!kd) {
         hipLaunchKernelGGL(k_correspond, grid, blk, 0, c->stream, P, with_stats);
         return;
     }
@@ -477,7 +504,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
         const dim3 blk(kBlock);
         for (int it = 0; it < g.max_iterations; ++it) {
-            launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0);
+            launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
             launch_pko(c, P, it);
             if (P.nb_acc <= kFuseMaxBlocks) {          // small scans: the last accumulate block solves
                 hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
@@ -547,6 +574,102 @@ int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12
     int rc = enqueue_optimize(c, c->d_pts, n, T_init);
     if (rc != LO_OK) return rc;
     return lo_icp_result(c, T_out, logs, st);
+}
+
+// ---------------------------------------------------------------- loop-closure ICP
+// IterativeClosestPointOptimizer::optimize_loop (:40-251) + find_correspondences_loop (:465-585): the KDTree
+// correspondence kernels against the matched keyframe's local map (its own grid, so the context's odometry map
+// is left alone), no distance gate, up to 100 GN iterations enqueued kLoopChunk at a time between convergence
+// checks, then the 1-NN inlier ratio (k_inlier) once converged.
+static constexpr int kLoopMaxIters = 100;                // :74
+static constexpr int kLoopChunk = 4;
+
+int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const float T_curr[12], const float* matched,
+                         size_t n_matched, const float T_matched[12], float T_rel_out[12], float* inlier_ratio,
+                         lo_iter_log* logs, lo_stats* st) {
+    if (!c || !T_curr || !T_matched || !T_rel_out || !inlier_ratio || (n_curr > 0 && !curr) || (n_matched > 0 && !matched))
+        return LO_ERR_ARG;
+    if (n_curr > static_cast<size_t>(c->cfg.max_points)) { c->err = "n_curr exceeds max_points"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    int rc = kd_alloc(c);
+    if (rc != LO_OK) return rc;
+    // local map of the matched keyframe: its feature cloud in the world (transform_point_cloud, :60-64)
+    const lo::SE3f Tm = lo::se3_from12(T_matched);
+    std::vector<float> lmap(3 * std::max<size_t>(n_matched, 1));
+    if (n_matched > 0) lo::transform_points(Tm, matched, n_matched, lmap.data());
+    rc = grid_build(c, c->lgrid, lmap.data(), n_matched);
+    if (rc != LO_OK) return rc;
+    if (st) { std::memset(st, 0, sizeof(*st)); st->status = LO_INSUFFICIENT; }
+    if (n_curr == 0 || n_matched == 0) return LO_INSUFFICIENT;       // empty clouds: 0 correspondences (:477-483)
+    LO_HIP(c, hipMemcpyAsync(c->d_pts, curr, n_curr * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    KParams P = make_params(c, c->d_pts, static_cast<int>(n_curr));
+    set_kd_params(c, P, c->lgrid);
+    P.loop = 1;
+    std::memcpy(P.Tm, T_matched, sizeof(float) * 12);
+    // T_lw_last = T_wl_last.inverse() (:509): the rigid inverse [R^T | -R^T t], evaluated in fp64 and rounded
+    for (int r = 0; r < 3; ++r) {
+        double tr = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            P.Tlw[4 * r + k] = T_matched[4 * k + r];
+            tr -= static_cast<double>(T_matched[4 * k + r]) * static_cast<double>(T_matched[4 * k + 3]);
+        }
+        P.Tlw[4 * r + 3] = static_cast<float>(tr);
+    }
+    KParams P0 = P;
+    P0.init = 1;
+    std::memcpy(P0.T0, T_curr, sizeof(float) * 12);
+    const dim3 blk(kBlock);
+    LO_HIP(c, hipEventRecord(c->ev0, c->stream));
+    const size_t head = offsetof(DevState, logs);
+    for (int it = 0; it < kLoopMaxIters;) {
+        for (int k = 0; k < kLoopChunk && it < kLoopMaxIters; ++k, ++it) {
+            launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, true);
+            launch_pko(c, P, it);
+            if (P.nb_acc <= kFuseMaxBlocks) {
+                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
+            } else {
+                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
+                hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
+            }
+        }
+        LO_HIP(c, hipGetLastError());
+        LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, head, hipMemcpyDeviceToHost, c->stream));
+        LO_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->h_st->done) break;                                 // converged, or too few correspondences
+    }
+    const bool converged = c->h_st->done && c->h_st->status == LO_OK;
+    if (converged) hipLaunchKernelGGL(k_inlier, dim3(P.nb), blk, 0, c->stream, P);
+    LO_HIP(c, hipGetLastError());
+    LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+    const size_t bytes = head + sizeof(lo_iter_log) * static_cast<size_t>(LO_MAX_ITERS);
+    LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    const DevState* hs = c->h_st;
+    bool success = false;
+    if (converged) {
+        // optimized_relative_transform = curr.pose^-1 * optimized_curr_pose (:240), set on convergence
+        const lo::SE3f rel = lo::se3_mul(lo::se3_inv(lo::se3_from12(T_curr)), lo::se3_from12(hs->pose));
+        lo::se3_to12(rel, T_rel_out);
+        *inlier_ratio = static_cast<float>(static_cast<int>(hs->inliers)) / static_cast<float>(static_cast<int>(n_curr));
+        success = !(*inlier_ratio < 0.5f);                            // :244-246
+    }
+    const int iters = hs->iter;
+    if (logs) for (int i = 0; i < iters && i < LO_MAX_ITERS; ++i) logs[i] = hs->logs[i];
+    const int status = success ? LO_OK : LO_INSUFFICIENT;
+    if (st) {
+        st->iterations = iters;
+        st->n_corr = hs->n_corr;
+        st->status = status;
+        st->converged = converged ? 1 : 0;
+        const int last = std::min(iters, LO_MAX_ITERS) - 1;
+        st->initial_cost = iters > 0 ? hs->logs[0].cost : 0.0;
+        st->final_cost = last >= 0 ? hs->logs[last].cost : 0.0;
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.0f;
+        st->gpu_ms = ms;
+    }
+    c->pending = false;
+    return status;
 }
 
 // ---------------------------------------------------------------- device preprocessing + optimize
@@ -653,7 +776,7 @@ int lo_find_correspondences(lo_ctx* c, const float* pts, size_t n, const float T
     LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.res_dbg = c->d_res;
-    launch_correspond(c, P, 1);
+    launch_correspond(c, P, 1, c->kd);
     LO_HIP(c, hipGetLastError());
     std::vector<int32_t> slots(n);
     LO_HIP(c, hipMemcpyAsync(slots.data(), c->d_slot, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -696,7 +819,7 @@ int lo_build_normal_equations(lo_ctx* c, const float* pts, size_t n, const float
     LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n));
     P.alpha_given = 1;
-    launch_correspond(c, P, 0);
+    launch_correspond(c, P, 0, c->kd);
     if (P.nb_acc <= kFuseMaxBlocks) {
         hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), dim3(kBlock), 0, c->stream, P, 0, 2);
     } else {
@@ -752,13 +875,13 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     P.alpha_given = 1;
     const dim3 grid(P.nb), blk(kBlock);
     // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials
-    launch_correspond(c, P, 1);
+    launch_correspond(c, P, 1, c->kd);
     hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0, 0);
     LO_HIP(c, hipGetLastError());
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int r = 0; r < reps; ++r) {
         switch (kernel_id) {
-            case 0: launch_correspond(c, P, 0); break;                 // KDTree: kNN + fallback + plane fit
+            case 0: launch_correspond(c, P, 0, c->kd); break;                 // KDTree: kNN + fallback + plane fit
             case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0,
                                        P.nb_acc <= kFuseMaxBlocks ? 2 : 0); break;
             case 2: launch_pko(c, P, 1); break;

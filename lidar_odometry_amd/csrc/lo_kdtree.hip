@@ -350,12 +350,27 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
                 transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
                 const double pd = -dot3d(nrm[0], nrm[1], nrm[2], cen[0], cen[1], cen[2]);
                 dist = fabs(dot3d(nrm[0], nrm[1], nrm[2], qx, qy, qz) + pd);
-                valid = !(dist > P.maxd);                       // :746-748 (NaN kept)
+                valid = P.loop || !(dist > P.maxd);             // :746-748 (NaN kept); the loop ICP has no gate (:573)
                 if (valid) {
                     Slot sl;
                     sl.key = 0;
 #pragma unroll
                     for (int d = 0; d < 3; ++d) { sl.n[d] = static_cast<float>(nrm[d]); sl.c[d] = static_cast<float>(cen[d]); }
+                    if (P.loop) {
+                        // find_correspondences_loop keeps neighbour 0 in the matched keyframe's frame (T_lw in fp64,
+                        // :517-520); optimize_loop casts it to fp32 and puts it back in the world, R_m p + t_m (:148-150)
+                        float lf[3];
+#pragma unroll
+                        for (int r = 0; r < 3; ++r) {
+                            const double l = ((static_cast<double>(P.Tlw[4 * r]) * Pm[0][0] +
+                                               static_cast<double>(P.Tlw[4 * r + 1]) * Pm[0][1]) +
+                                              static_cast<double>(P.Tlw[4 * r + 2]) * Pm[0][2]) + static_cast<double>(P.Tlw[4 * r + 3]);
+                            lf[r] = static_cast<float>(l);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 3; ++r)
+                            sl.c[r] = dot3f(P.Tm[4 * r], P.Tm[4 * r + 1], P.Tm[4 * r + 2], lf[0], lf[1], lf[2]) + P.Tm[4 * r + 3];
+                    }
                     P.kd_plane[i] = sl;
                     P.kd_res[i] = dist;
                 }
@@ -365,6 +380,50 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
         if (P.res_dbg) P.res_dbg[i] = valid ? dist : 0.0;
     }
     corr_epilogue(P, valid, dist, with_stats, blockIdx.x);
+}
+
+// optimize_loop's inlier ratio (:206-238): the curr cloud at the converged pose (t + R p, :220-221), each point an
+// inlier when its nearest matched-map point is closer than 1 m: sqrt of nanoflann's fp32 (dx^2 + dy^2) + dz^2 < 1.
+// Every map point within 1 m lies in the cells spanned by q +- 1 m (one extra cell each side against rounding of
+// the cell index), so the grid answers the 1-NN threshold test exactly.  One lane per point, early exit on a hit.
+__global__ __launch_bounds__(kBlock) void k_inlier(KParams P) {
+    DevState* st = P.st;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    bool in = false;
+    if (i < scan_n(P)) {
+        float T[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+        const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+        const float q[3] = {T[3] + dot3f(T[0], T[1], T[2], px, py, pz), T[7] + dot3f(T[4], T[5], T[6], px, py, pz),
+                            T[11] + dot3f(T[8], T[9], T[10], px, py, pz)};
+        if (isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && P.kd_m > 0) {
+            int lo[3], hi[3];
+            bool any = true;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float fl = floorf((q[a] - 1.0f) / P.kd_h) - 1.0f, fh = floorf((q[a] + 1.0f) / P.kd_h) + 1.0f;
+                const float o = static_cast<float>(P.kd_org[a]), d = static_cast<float>(P.kd_dim[a]);
+                const float l = fmaxf(fl - o, 0.0f), h = fminf(fh - o, d - 1.0f);
+                if (!(l <= h)) any = false;
+                lo[a] = any ? static_cast<int>(l) : 0;
+                hi[a] = any ? static_cast<int>(h) : -1;
+            }
+            for (int z = lo[2]; any && !in && z <= hi[2]; ++z)
+                for (int y = lo[1]; !in && y <= hi[1]; ++y) {
+                    const size_t row = (static_cast<size_t>(z) * P.kd_dim[1] + y) * P.kd_dim[0];
+                    const uint32_t b = P.kd_start[row + lo[0]], e = P.kd_start[row + hi[0] + 1];
+                    for (uint32_t p = b; p < e; ++p) {
+                        const float4 v = P.kd_pts[p];
+                        const float d0 = q[0] - v.x, d1 = q[1] - v.y, d2 = q[2] - v.z;
+                        const float d = (d0 * d0 + d1 * d1) + d2 * d2;
+                        if (sqrtf(d) < 1.0f) { in = true; break; }
+                    }
+                }
+        }
+    }
+    const uint64_t m = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&st->inliers, static_cast<unsigned>(__popcll(m)));
 }
 
 }  // namespace lo

@@ -378,15 +378,17 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only) {
 
     const float tdel = sqrtf(dot3f(dt[0], dt[1], dt[2], dt[0], dt[1], dt[2]));
     const float rdel = sqrtf(dot3f(dw[0], dw[1], dw[2], dw[0], dw[1], dw[2]));
-    lo_iter_log& L = st->logs[it];
-    for (int q = 0; q < 12; ++q) L.pose[q] = st->pose[q];
-    L.n_corr = st->n_corr;
-    L.scale = st->scale;
-    L.alpha = st->alpha;
-    L.cost = static_cast<float>(cost);
-    k = 0;
-    for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L.H[k++] = static_cast<float>(H[r * 6 + c]);
-    for (int j = 0; j < 6; ++j) { L.g[j] = static_cast<float>(g[j]); L.delta[j] = delta[j]; }
+    if (it < LO_MAX_ITERS) {                                          // the loop-closure ICP runs up to 100
+        lo_iter_log& L = st->logs[it];
+        for (int q = 0; q < 12; ++q) L.pose[q] = st->pose[q];
+        L.n_corr = st->n_corr;
+        L.scale = st->scale;
+        L.alpha = st->alpha;
+        L.cost = static_cast<float>(cost);
+        k = 0;
+        for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L.H[k++] = static_cast<float>(H[r * 6 + c]);
+        for (int j = 0; j < 6; ++j) { L.g[j] = static_cast<float>(g[j]); L.delta[j] = delta[j]; }
+    }
     st->iter = it + 1;
     if (tdel < P.tol_t && rdel < P.tol_r) st->done = 1;               // :443-448
 }
@@ -414,6 +416,7 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
         st->status = LO_OK;
         st->acc_arrive = 0;
         st->kd_unres_n = 0;
+        st->inliers = 0;
     }
 }
 

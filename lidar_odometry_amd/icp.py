@@ -203,6 +203,24 @@ class IterativeClosestPointOptimizer:
         self._record(st, logs)
         return rc == _lib.LO_OK, pose34(To)
 
+    def optimize_loop(self, curr_points, curr_pose, matched_points, matched_pose):
+        """IterativeClosestPointOptimizer::optimize_loop (IterativeClosestPointOptimizer.cpp:40-251) on the device:
+        the two keyframes' feature clouds (local frames) and world poses.  Returns (success, T_rel, inlier_ratio);
+        as the reference, T_rel (= curr_pose^-1 * optimized pose, 3x4) and inlier_ratio are None unless the
+        iteration converged.  The context's own map is not touched."""
+        c = _as_pts(curr_points)
+        m = _as_pts(matched_points)
+        Tc, Tm = _as_pose(curr_pose), _as_pose(matched_pose)
+        Tr = np.zeros(12, np.float32)
+        inl = C.c_float(0.0)
+        logs = (LoIterLog * _lib.LO_MAX_ITERS)()
+        st = LoStats()
+        rc = self._check(lib().lo_icp_optimize_loop(self._ctx, _fptr(c), len(c), _fptr(Tc), _fptr(m), len(m), _fptr(Tm),
+                                                    _fptr(Tr), C.byref(inl), logs, C.byref(st)))
+        self._record(st, logs)
+        conv = bool(st.converged)
+        return rc == _lib.LO_OK, (pose34(Tr) if conv else None), (inl.value if conv else None)
+
     def filtered_points(self) -> np.ndarray:
         """Feature cloud of the last device-filtered scan (for the keyframe map update)."""
         n = self._check(lib().lo_filtered_points(self._ctx, None, 0))
@@ -221,7 +239,7 @@ class IterativeClosestPointOptimizer:
 
     def _record(self, st, logs):
         its = []
-        for i in range(st.iterations):
+        for i in range(min(st.iterations, len(logs))):
             L = logs[i]
             its.append({"pose": np.array(L.pose[:], np.float32), "n_corr": L.n_corr, "scale": L.scale,
                         "alpha": L.alpha, "cost": L.cost, "H": np.array(L.H[:], np.float32),

@@ -98,6 +98,9 @@ def lib():
         L.or_icp_optimize.argtypes = [vp, fp, C.c_int, fp, fp, C.POINTER(IcpCfg), C.c_int,
                                       C.POINTER(IterLog), ip]
         L.or_icp_optimize.restype = C.c_int
+        L.or_icp_optimize_loop.argtypes = [fp, C.c_int, fp, fp, C.c_int, fp, C.POINTER(IcpCfg), fp, fp,
+                                           C.POINTER(IterLog), C.c_int, ip, ip]
+        L.or_icp_optimize_loop.restype = C.c_int
         L.or_build_normal_equations.argtypes = [vp, fp, C.c_int, fp, C.POINTER(IcpCfg), C.c_double,
                                                 C.c_double, fp, fp, fp]
         L.or_build_normal_equations.restype = C.c_int
@@ -346,6 +349,37 @@ def icp_optimize(vmap: VoxelMap, pts, T_init, cfg: IcpCfg | None = None, kdtree=
                     "cost": L.cost, "H": np.array(L.H[:], np.float32), "g": np.array(L.g[:], np.float32),
                     "delta": np.array(L.delta[:], np.float32)})
     return bool(ok), To, iters.value, out
+
+
+def _logs_list(logs, n):
+    out = []
+    for i in range(n):
+        L = logs[i]
+        out.append({"pose": np.array(L.pose[:], np.float32), "n_corr": L.n_corr, "scale": L.scale, "alpha": L.alpha,
+                    "cost": L.cost, "H": np.array(L.H[:], np.float32), "g": np.array(L.g[:], np.float32),
+                    "delta": np.array(L.delta[:], np.float32)})
+    return out
+
+
+def icp_optimize_loop(curr, T_curr, matched, T_matched, cfg: IcpCfg | None = None, max_logs=100):
+    """optimize_loop (IterativeClosestPointOptimizer.cpp:40-251).  Returns (ok, converged, T_rel[12] or None,
+    inlier_ratio or None, iterations, logs); T_rel / inlier_ratio exist only when the iteration converged."""
+    cfg = cfg or kitti_icp_cfg()
+    c, cp = _f32(np.asarray(curr).reshape(-1, 3))
+    m, mp = _f32(np.asarray(matched).reshape(-1, 3))
+    def p12(T):
+        a = np.asarray(T, np.float32)
+        return a.reshape(12) if a.size == 12 else a[:3, :4].reshape(12)
+    tc, tcp = _f32(p12(T_curr))
+    tm, tmp = _f32(p12(T_matched))
+    Tr = np.zeros(12, np.float32)
+    inl = C.c_float(0.0)
+    logs = (IterLog * max_logs)()
+    iters, conv = C.c_int(0), C.c_int(0)
+    ok = lib().or_icp_optimize_loop(cp, len(c), tcp, mp, len(m), tmp, C.byref(cfg), Tr.ctypes.data_as(C.POINTER(C.c_float)),
+                                    C.byref(inl), logs, max_logs, C.byref(iters), C.byref(conv))
+    cv = bool(conv.value)
+    return bool(ok), cv, (Tr if cv else None), (inl.value if cv else None), iters.value, _logs_list(logs, min(iters.value, max_logs))
 
 
 def build_normal_equations(vmap: VoxelMap, pts, T, scale, delta, cfg: IcpCfg | None = None):

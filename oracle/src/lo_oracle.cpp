@@ -1039,6 +1039,43 @@ static double iter0_scale(const std::vector<double>& res_in) {   // :304-316
     return std::sqrt(var) / 6.0;
 }
 
+// One GN step on a correspondence set (:304-449): iteration-0 scale, PKO delta, normal equations, LDLT, right
+// update, log; returns true when |dt| and |dw| are both below tolerance.
+static bool gn_step(const Corr& c, SE3& cur, const or_icp_cfg& cfg, PKO& pko, double& scale, int it, or_iter_log* L) {
+    if (it == 0 && !c.residuals.empty()) scale = iter0_scale(c.residuals);
+    double delta_a = cfg.robust_loss_delta;
+    if (cfg.use_pko) {
+        std::vector<double> nr;
+        nr.reserve(c.residuals.size());
+        for (double r : c.residuals) nr.push_back(r / std::max(scale, 1e-6));
+        if (!nr.empty()) delta_a = pko.scale_factor(nr);
+    }
+    float H[6][6], g[6], cost;
+    build_ne(c, cur, cfg, scale, delta_a, H, g, cost);
+    float Hf[36], mg[6], delta[6];
+    for (int r = 0; r < 6; ++r) for (int q = 0; q < 6; ++q) Hf[r * 6 + q] = H[r][q];
+    for (int j = 0; j < 6; ++j) mg[j] = -g[j];
+    ldlt6_solve(Hf, mg, delta);
+    float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
+    SE3 dT;
+    if (norm3f(dw) < 1e-10f) dT.R = so3_normalize(eye3());
+    else dT.R = so3_exp(dw);
+    for (int d = 0; d < 3; ++d) dT.t[d] = dt[d];
+    cur = se3_mul(cur, dT);
+    float tdel = norm3f(dt), rdel = norm3f(dw);
+    if (L) {
+        se3_to12(cur, L->pose);
+        L->n_corr = static_cast<int>(c.size());
+        L->scale = scale;
+        L->alpha = delta_a;
+        L->cost = cost;
+        int k = 0;
+        for (int r = 0; r < 6; ++r) for (int q = r; q < 6; ++q) L->H[k++] = H[r][q];
+        for (int j = 0; j < 6; ++j) { L->g[j] = g[j]; L->delta[j] = delta[j]; }
+    }
+    return (tdel < cfg.translation_tolerance) && (rdel < cfg.rotation_tolerance);
+}
+
 static int icp_optimize(const VoxelMap& map, const float* pts, int n, const float Ti[12], float To[12],
                         const or_icp_cfg& cfg, bool kdtree, or_iter_log* logs, int* iters_out) {
     SE3 cur = se3_from12(Ti);
@@ -1054,45 +1091,126 @@ static int icp_optimize(const VoxelMap& map, const float* pts, int n, const floa
             if (iters_out) *iters_out = iters;
             return 0;
         }
-        if (it == 0 && !c.residuals.empty()) scale = iter0_scale(c.residuals);
-        double delta_a = cfg.robust_loss_delta;
-        if (cfg.use_pko) {
-            std::vector<double> nr;
-            nr.reserve(c.residuals.size());
-            for (double r : c.residuals) nr.push_back(r / std::max(scale, 1e-6));
-            if (!nr.empty()) delta_a = pko.scale_factor(nr);
-        }
-        float H[6][6], g[6], cost;
-        build_ne(c, cur, cfg, scale, delta_a, H, g, cost);
-        float Hf[36], mg[6], delta[6];
-        for (int r = 0; r < 6; ++r) for (int q = 0; q < 6; ++q) Hf[r * 6 + q] = H[r][q];
-        for (int j = 0; j < 6; ++j) mg[j] = -g[j];
-        ldlt6_solve(Hf, mg, delta);
-        float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
-        SE3 dT;
-        if (norm3f(dw) < 1e-10f) dT.R = so3_normalize(eye3());
-        else dT.R = so3_exp(dw);
-        for (int d = 0; d < 3; ++d) dT.t[d] = dt[d];
-        cur = se3_mul(cur, dT);
-        float tdel = norm3f(dt), rdel = norm3f(dw);
+        const bool conv = gn_step(c, cur, cfg, pko, scale, it, logs ? &logs[it] : nullptr);
         ++iters;
-        if (logs) {
-            or_iter_log& L = logs[it];
-            se3_to12(cur, L.pose);
-            L.n_corr = static_cast<int>(nc);
-            L.scale = scale;
-            L.alpha = delta_a;
-            L.cost = cost;
-            int k = 0;
-            for (int r = 0; r < 6; ++r) for (int q = r; q < 6; ++q) L.H[k++] = H[r][q];
-            for (int j = 0; j < 6; ++j) { L.g[j] = g[j]; L.delta[j] = delta[j]; }
-        }
-        bool conv = (tdel < cfg.translation_tolerance) && (rdel < cfg.rotation_tolerance);
         if (conv) break;
     }
     se3_to12(cur, To);
     if (iters_out) *iters_out = iters;
     return 1;
+}
+
+/* ---- loop-closure ICP: optimize_loop (:40-251) + find_correspondences_loop (:465-585) ----
+ * Query = curr point through the curr pose (Matrix4f * Vector4f, :500-503); exact 5-NN in the matched keyframe's
+ * local map (its feature cloud through its pose, :60-64); the collinearity gate and plane fit of the KDTree path;
+ * NO distance gate (:573); target = neighbour 0 in the matched frame, T_lw * p in fp64 (:517-520), cast to fp32
+ * and put back in the world, R_m q + t_m (:148-150).  T_lw is the rigid inverse [R^T | -R^T t] in fp64 rounded to
+ * fp32; the reference's Matrix4f::inverse() agrees with it to fp32 rounding (parity unpinned at that level; the
+ * target only enters H and g).  Up to 100 iterations; success = converged AND inlier ratio >= 0.5. */
+static size_t find_corr_loop(const KdTree3& kd, const std::vector<float>& lmap, const float* pts, int n, const SE3& T,
+                             const float Tlw[12], const SE3& Tm, Corr& c) {
+    c.clear();
+    if (n <= 0 || lmap.empty()) return 0;
+    for (int i = 0; i < n; ++i) {
+        float q[3]; transform_pt(T, pts + 3 * i, q);
+        int idx[5]; float dist[5]; int found;
+        if (g_kd_use_tree) kd.knn5(q, idx, dist, found);
+        else knn5(lmap, q, idx, dist, found);
+        if (found < 5) continue;
+        double P[5][3];
+        for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) P[k][d] = lmap[3 * idx[k] + d];
+        double v1[3], v2[3];
+        for (int d = 0; d < 3; ++d) { v1[d] = P[1][d] - P[0][d]; v2[d] = P[2][d] - P[0][d]; }
+        double n1 = std::sqrt(dot3d(v1[0], v1[1], v1[2], v1[0], v1[1], v1[2]));
+        double n2 = std::sqrt(dot3d(v2[0], v2[1], v2[2], v2[0], v2[1], v2[2]));
+        if (n1 > 0) for (int d = 0; d < 3; ++d) v1[d] /= n1;
+        if (n2 > 0) for (int d = 0; d < 3; ++d) v2[d] /= n2;
+        double cr[3] = {v1[1] * v2[2] - v1[2] * v2[1], v1[2] * v2[0] - v1[0] * v2[2], v1[0] * v2[1] - v1[1] * v2[0]};
+        if (std::sqrt(dot3d(cr[0], cr[1], cr[2], cr[0], cr[1], cr[2])) < 0.5) continue;   // is_collinear (:785-792)
+        double cen[3] = {0, 0, 0};
+        for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) cen[d] += P[k][d];
+        for (int d = 0; d < 3; ++d) cen[d] /= 5.0;
+        double S[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        for (int k = 0; k < 5; ++k) {
+            double a[3] = {P[k][0] - cen[0], P[k][1] - cen[1], P[k][2] - cen[2]};
+            for (int r = 0; r < 3; ++r) for (int s2 = 0; s2 < 3; ++s2) S[r][s2] += a[r] * a[s2];
+        }
+        double nrm[3];
+        smallest_eigvec3d(S, nrm);
+        double pd = -dot3d(nrm[0], nrm[1], nrm[2], cen[0], cen[1], cen[2]);
+        double dist_pl = std::fabs(dot3d(nrm[0], nrm[1], nrm[2], q[0], q[1], q[2]) + pd);
+        float lf[3], qw[3];
+        for (int r = 0; r < 3; ++r)
+            lf[r] = static_cast<float>(((static_cast<double>(Tlw[4 * r]) * P[0][0] + static_cast<double>(Tlw[4 * r + 1]) * P[0][1]) +
+                                        static_cast<double>(Tlw[4 * r + 2]) * P[0][2]) + static_cast<double>(Tlw[4 * r + 3]));
+        for (int r = 0; r < 3; ++r) qw[r] = dot3f(Tm.R.a[r][0], Tm.R.a[r][1], Tm.R.a[r][2], lf[0], lf[1], lf[2]) + Tm.t[r];
+        // the world target goes where find_corr_kdtree keeps the centroid: build_ne reads it as q
+        c.last.push_back({static_cast<double>(qw[0]), static_cast<double>(qw[1]), static_cast<double>(qw[2])});
+        c.curr.push_back({static_cast<double>(pts[3 * i]), static_cast<double>(pts[3 * i + 1]), static_cast<double>(pts[3 * i + 2])});
+        c.normals.push_back({nrm[0], nrm[1], nrm[2]});
+        c.residuals.push_back(dist_pl);
+    }
+    return c.size();
+}
+
+static int icp_optimize_loop(const float* curr, int ncur, const float Tc[12], const float* matched, int nm,
+                             const float Tmat[12], const or_icp_cfg& cfg, float Trel[12], float* inlier,
+                             or_iter_log* logs, int max_logs, int* iters_out, int* conv_out) {
+    SE3 cur = se3_from12(Tc);
+    const SE3 Tm = se3_from12(Tmat);
+    PKO pko; pko.cfg = cfg.pko;                 // m_adaptive_estimator->reset() (:53-55): no state survives anyway
+    std::vector<float> lmap(3 * static_cast<size_t>(std::max(nm, 0)));
+    for (int i = 0; i < nm; ++i) transform_pt(Tm, matched + 3 * i, &lmap[3 * i]);
+    KdTree3 kd;
+    kd.build(lmap);
+    float Tlw[12];
+    for (int r = 0; r < 3; ++r) {
+        double tr = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            Tlw[4 * r + k] = Tmat[4 * k + r];
+            tr -= static_cast<double>(Tmat[4 * k + r]) * static_cast<double>(Tmat[4 * k + 3]);
+        }
+        Tlw[4 * r + 3] = static_cast<float>(tr);
+    }
+    double scale = 1.0;
+    int iters = 0;
+    bool converged = false;
+    Corr c;
+    for (int it = 0; it < 100; ++it) {
+        const size_t nc = find_corr_loop(kd, lmap, curr, ncur, cur, Tlw, Tm, c);
+        if (nc < static_cast<size_t>(cfg.min_correspondence_points)) break;
+        const bool conv = gn_step(c, cur, cfg, pko, scale, it, (logs && it < max_logs) ? &logs[it] : nullptr);
+        ++iters;
+        if (conv) { converged = true; break; }
+    }
+    if (iters_out) *iters_out = iters;
+    if (conv_out) *conv_out = converged ? 1 : 0;
+    if (!converged) return 0;
+    // optimized_relative_transform = curr.pose.Inverse() * optimized_curr_pose (:240)
+    SE3 ci = se3_from12(Tc), inv;
+    M3 Rt;
+    for (int r = 0; r < 3; ++r) for (int k = 0; k < 3; ++k) Rt.a[r][k] = ci.R.a[k][r];
+    inv.R = so3_normalize(Rt);
+    const float mt[3] = {-ci.t[0], -ci.t[1], -ci.t[2]};
+    mul3v(inv.R, mt, inv.t);
+    se3_to12(se3_mul(inv, cur), Trel);
+    // inlier ratio (:206-238): t + R p, nearest matched point by nanoflann's fp32 squared L2, sqrt < 1
+    int inl = 0;
+    for (int i = 0; i < ncur; ++i) {
+        const float* p = curr + 3 * i;
+        float w[3];
+        for (int r = 0; r < 3; ++r) w[r] = cur.t[r] + dot3f(cur.R.a[r][0], cur.R.a[r][1], cur.R.a[r][2], p[0], p[1], p[2]);
+        float best = FLT_MAX;
+        bool any = false;
+        for (int k = 0; k < nm; ++k) {
+            const float d0 = w[0] - lmap[3 * k], d1 = w[1] - lmap[3 * k + 1], d2 = w[2] - lmap[3 * k + 2];
+            const float d = (d0 * d0 + d1 * d1) + d2 * d2;
+            if (d < best) { best = d; any = true; }
+        }
+        if (any && std::sqrt(best) < 1.0f) ++inl;
+    }
+    *inlier = static_cast<float>(inl) / static_cast<float>(ncur);
+    return *inlier < 0.5f ? 0 : 1;
 }
 
 }  // namespace orc
@@ -1313,6 +1431,13 @@ int or_find_correspondences_kdtree(void* map, const float* pts, int n, const flo
 int or_icp_optimize(void* map, const float* pts, int n, const float T_init[12], float T_out[12], const or_icp_cfg* cfg,
                     int use_kdtree, or_iter_log* logs, int* iterations) {
     return icp_optimize(*static_cast<VoxelMap*>(map), pts, n, T_init, T_out, *cfg, use_kdtree != 0, logs, iterations);
+}
+
+int or_icp_optimize_loop(const float* curr, int n_curr, const float T_curr[12], const float* matched, int n_matched,
+                         const float T_matched[12], const or_icp_cfg* cfg, float T_rel[12], float* inlier_ratio,
+                         or_iter_log* logs, int max_logs, int* iterations, int* converged) {
+    return icp_optimize_loop(curr, n_curr, T_curr, matched, n_matched, T_matched, *cfg, T_rel, inlier_ratio, logs,
+                             max_logs, iterations, converged);
 }
 
 int or_build_normal_equations(void* map, const float* pts, int n, const float T[12], const or_icp_cfg* cfg, double scale,

@@ -112,6 +112,11 @@ int    or_find_correspondences_kdtree(void* map, const float* pts, int n, const 
    find_correspondences_kdtree.  logs: max_iterations entries (nullable). */
 int    or_icp_optimize(void* map, const float* pts, int n, const float T_init[12], float T_out[12],
                        const or_icp_cfg* cfg, int use_kdtree, or_iter_log* logs, int* iterations);
+/* optimize_loop (IterativeClosestPointOptimizer.cpp:40-251): returns 1 = success (converged and inlier ratio >= 0.5).
+ * T_rel / inlier_ratio are written only when converged (*converged = 1); logs receives up to max_logs iterations. */
+int    or_icp_optimize_loop(const float* curr, int n_curr, const float T_curr[12], const float* matched, int n_matched,
+                            const float T_matched[12], const or_icp_cfg* cfg, float T_rel[12], float* inlier_ratio,
+                            or_iter_log* logs, int max_logs, int* iterations, int* converged);
 /* Build the weighted normal equations of one iteration for given pose / scale / delta. */
 int    or_build_normal_equations(void* map, const float* pts, int n, const float T[12],
                                  const or_icp_cfg* cfg, double scale, double delta,

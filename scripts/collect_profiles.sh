@@ -17,7 +17,7 @@ for w in kitti 1m kd e2e; do
             --write gpurun_out/pmc_write_$w --out profiles/pmc_traffic.json --note "$tag" > /dev/null
     fi
 done
-for b in kitti patch1m patch1m_random kitti_kdtree mid360 kitti_raw kitti_e2e; do
+for b in kitti patch1m patch1m_random kitti_kdtree mid360 kitti_raw kitti_e2e kitti_loop; do
     [ -s gpurun_out/bench_$b.json ] && tail -n 1 gpurun_out/bench_$b.json > "profiles/${tag}_bench_$b.json"
 done
 [ -f gpurun_out/tests.log ] && tail -n 5 gpurun_out/tests.log > "profiles/${tag}_gpu_tests.txt"

@@ -12,6 +12,7 @@ all=(
   "bench_1m_rand:600:python bench.py --config patch1m --order random --steps 40 --warmup 4 --no-cpu-baseline > gpurun_out/bench_patch1m_random.json"
   "bench_raw:600:python bench.py --config kitti_raw --cpu-budget 10 > gpurun_out/bench_kitti_raw.json"
   "bench_e2e:900:python bench.py --config kitti_e2e --steps 600 --cpu-budget 15 > gpurun_out/bench_kitti_e2e.json"
+  "bench_loop:600:python bench.py --config kitti_loop --steps 200 --warmup 12 --cpu-budget 10 > gpurun_out/bench_kitti_loop.json"
   "bench_kd:600:python bench.py --config kitti_kdtree --cpu-budget 10 > gpurun_out/bench_kitti_kdtree.json"
   "bench_mid360:600:python bench.py --config mid360 --cpu-budget 10 > gpurun_out/bench_mid360.json"
   "stats_kd:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kd -o run --output-format csv -- python bench.py --config kitti_kdtree --steps 200 --warmup 10 --no-cpu-baseline"

@@ -87,3 +87,14 @@ def rot_angle(Ra, Rb) -> float:
     form it does not turn a 1e-7 fp32 orthonormality error into a 4e-4 rad reading."""
     d = np.asarray(Ra, np.float64) - np.asarray(Rb, np.float64)
     return float(np.linalg.norm(d) / np.sqrt(2.0))
+
+
+def loop_case(fa: int, fb: int, seed: int = 0, sigma_t: float = 0.3, sigma_r: float = 0.03, n_frames: int = 40):
+    """Loop-closure pair: (curr feature cloud, curr pose 12 (drifted), matched feature cloud, matched pose 12,
+    ground-truth curr pose 12).  Keyframe fb re-observes fa's surroundings; its pose carries drift."""
+    seq = kitti_seq(n_frames)
+    cur = oracle.voxel_filter(kitti_scan(fb, n_frames), 0.5, 8)
+    mat = oracle.voxel_filter(kitti_scan(fa, n_frames), 0.5, 8)
+    rng = np.random.default_rng(seed)
+    Tb0 = synth.perturb(seq.poses[fb], rng, sigma_t, sigma_r)
+    return cur, pose12(Tb0), mat, pose12(seq.poses[fa]), pose12(seq.poses[fb])
