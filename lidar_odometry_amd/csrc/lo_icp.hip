@@ -113,11 +113,8 @@ static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs
 static void launch_pko(lo_ctx* c, const KParams& P, int it) {
     // dynamic LDS for the per-block prefix (nb ints; 64 KB only at the 4M-point maximum)
     const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
-    // one GMM sample per thread: 2 waves cover the reference's 100 samples, 4 waves up to 256
-    if (c->cfg.gmm_sample_size <= 128)
-        hipLaunchKernelGGL(k_pko_t<2>, dim3(pko_grid(c->cfg)), dim3(128), pre_bytes, c->stream, P, it);
-    else
-        hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), pre_bytes, c->stream, P, it);
+    // 4 waves: the EM runs one GMM component per wave (gmm_fit_split), up to 256 samples (4 per lane)
+    hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), pre_bytes, c->stream, P, it);
 }
 
 static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
@@ -293,8 +290,6 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
     // k_pko_t's dynamic block-prefix LDS reaches 64 KB at the 4M-point maximum
-    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(kMaxBlocks * sizeof(int))));
     LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(kMaxBlocks * sizeof(int))));
     c->kd = g.use_surfel_correspondence == 0;

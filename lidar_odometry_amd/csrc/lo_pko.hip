@@ -11,9 +11,10 @@
 //
 // Layout on the chip: the EM is a strictly sequential chain of (usually all) 100 iterations, so its latency
 // sets the kernel time.  Every workgroup of the launch fits the same GMM redundantly (identical, deterministic
-// results, no inter-workgroup traffic) on ONE wave holding ceil(S/64) samples per lane: each EM / k-means
-// iteration is pure VALU (permlane/DPP butterfly sums, no LDS round trip, no barrier) -- measured faster than
-// splitting the samples over two waves with one LDS exchange + barrier per iteration (scripts/pko_stamps.py).
+// results, no inter-workgroup traffic).  Inside a workgroup the EM is split by component: wave j evaluates
+// only component j's pdf for all samples (ceil(S/64) per lane), the pdfs meet in LDS once per iteration and each
+// wave reduces its own component's sums with a permlane/DPP butterfly (gmm_fit_split).  Splitting the SAMPLES
+// over waves was measured slower (it adds an LDS exchange without shortening the per-lane exp chains).
 // Afterwards workgroup g evaluates the JS divergence for alphas g+1, g+1+G, ... and writes them to global
 // memory.  The argmin over the grid (first strict minimum,
 // as the reference loop) is taken by the consumers (k_accumulate / k_pko_finish) after the kernel boundary,
@@ -61,24 +62,24 @@ __device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {
 #define LO_COUNT(dbg, i, v) do { } while (0)
 #endif
 
-// exp(y) for y <= 0 or NaN (the E-step exponent -(d^2) * 0.5 / var): Cody-Waite reduction by ln2 and a
-// degree-12 Taylor polynomial on |r| <= ln2/2; <= 2 ulp from glibc exp over [-745, 0] (checked on 2e7 points).
+// exp(y) for y <= 0 or NaN (the E-step exponent -(d^2) * 0.5 / var): Cody-Waite reduction by ln2 and the
+// degree-12 Taylor polynomial on |r| <= ln2/2, its tail c3..c12 evaluated by Estrin (r^2, r^4, r^8) and the last
+// three steps by Horner, so the dependent chain is 7 FMAs instead of 13 with Horner's accuracy: <= 2 ulp from
+// glibc exp over [-745, 0] (checked on 2e7 points; differs from the all-Horner form in 0.08% of them).
 // No overflow branch is needed for y <= 0, and the underflow to 0 falls out of v_ldexp_f64.
 __device__ __forceinline__ double exp_nonpos(double y) {
     const double n = rint(y * 0x1.71547652b82fep+0);
     double r = fma(-n, 0x1.62e42fefa39efp-1, y);
     r = fma(-n, 0x1.abc9e3b39803fp-56, r);
-    double p = 0x1.1eed8eff8d898p-29;
-    p = fma(p, r, 0x1.ae64567f544e4p-26);
-    p = fma(p, r, 0x1.27e4fb7789f5cp-22);
-    p = fma(p, r, 0x1.71de3a556c734p-19);
-    p = fma(p, r, 0x1.a01a01a01a01ap-16);
-    p = fma(p, r, 0x1.a01a01a01a01ap-13);
-    p = fma(p, r, 0x1.6c16c16c16c17p-10);
-    p = fma(p, r, 0x1.1111111111111p-7);
-    p = fma(p, r, 0x1.5555555555555p-5);
-    p = fma(p, r, 0x1.5555555555555p-3);
-    p = fma(p, r, 0.5);
+    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+    const double q0 = fma(0x1.5555555555555p-5, r, 0x1.5555555555555p-3);     // c3 + c4 r
+    const double q1 = fma(0x1.6c16c16c16c17p-10, r, 0x1.1111111111111p-7);    // c5 + c6 r
+    const double q2 = fma(0x1.a01a01a01a01ap-16, r, 0x1.a01a01a01a01ap-13);   // c7 + c8 r
+    const double q3 = fma(0x1.27e4fb7789f5cp-22, r, 0x1.71de3a556c734p-19);   // c9 + c10 r
+    const double q4 = fma(0x1.1eed8eff8d898p-29, r, 0x1.ae64567f544e4p-26);   // c11 + c12 r
+    const double s0 = fma(q1, r2, q0), s1 = fma(q3, r2, q2);
+    const double tail = fma(q4, r8, fma(s1, r4, s0));
+    double p = fma(tail, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     return ldexp(p, static_cast<int>(n));
@@ -130,17 +131,20 @@ __device__ __forceinline__ void wave_totals8(double (&v)[NV]) {
     for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 8 * q);
 }
 
-// fit_gmm (AdaptiveMEstimator.cpp:294-485) by ONE wave holding SPL samples per lane (sample s*64 + lane).
-// The EM is a strictly sequential chain, so it runs where the chain is shortest: a single wave with no
-// LDS round trip and no barrier per iteration (wave_totals8), SPL independent exp chains per component for
-// ILP.  The E-step constants w_j / sqrt(2 pi var_j) and 0.5 / var_j come from one Newton-refined rsq per
-// component; reciprocals are Newton-refined hardware estimates and sums are trees, so results move by a
-// few ulp against the reference's sequential evaluation.  The device PKO is checked for identical alpha
-// against the reference's golden vectors (tests/test_gpu_parity.py::test_pko_alpha_matches_reference_golden).
+// fit_gmm (AdaptiveMEstimator.cpp:294-485) with the EM split over the workgroup's waves: wave j < K owns
+// component j (every lane computes ONE pdf per sample instead of K), the per-sample pdfs meet in LDS (s_p) and
+// the summed |d mean| of components >= 1 in s_dm, one barrier per iteration.  Per-lane sample mapping (sample s*64 + lane), the order of the
+// per-sample sum (((0 + p_0) + p_1) + p_2), the per-lane accumulation order and the butterfly tree do not
+// depend on the split (the fitted GMM is bit-identical to a single wave doing all components), with a third of
+// the VALU issue on the critical path.  k-means and the initial variance run redundantly in every wave (identical inputs and code,
+// so identical results, no exchange).  All NW waves execute the loop (waves >= K only join the barriers), and
+// the convergence test reads the same LDS values everywhere, so every wave leaves at the same iteration.
 template <int K, int SPL>
-__device__ __forceinline__ void gmm_fit_w(const double* s_sd, int S, const int32_t* draws, double* gmm, unsigned long long* dbg) {
+__device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const int32_t* draws, double* gmm,
+                                              double* s_p, double* s_dm, unsigned long long* dbg) {
     static_assert(3 * K - 1 <= 8, "partials");
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int j = wid < K ? wid : -1;                      // this wave's component (-1: barriers only)
     double x[SPL];
     bool have[SPL];
 #pragma unroll
@@ -151,13 +155,12 @@ __device__ __forceinline__ void gmm_fit_w(const double* s_sd, int S, const int32
     double mu[K], cnt[K];
     mu[0] = 0.0;
 #pragma unroll
-    for (int j = 1; j < K; ++j) mu[j] = s_sd[draws[j - 1]];
+    for (int q = 1; q < K; ++q) mu[q] = s_sd[draws[q - 1]];
 #pragma unroll
-    for (int j = 0; j < K; ++j) cnt[j] = 0.0;
-
+    for (int q = 0; q < K; ++q) cnt[q] = 0.0;
     // ---- k-means until the means repeat exactly (:351-389) ----
     for (int guard = 0; guard < 100000; ++guard) {
-        double v[2 * K - 1];                               // counts 0..K-1, sums 1..K-1
+        double v[2 * K - 1];
 #pragma unroll
         for (int q = 0; q < 2 * K - 1; ++q) v[q] = 0.0;
 #pragma unroll
@@ -165,30 +168,29 @@ __device__ __forceinline__ void gmm_fit_w(const double* s_sd, int S, const int32
             double md = DBL_MAX;
             int ci = 0;
 #pragma unroll
-            for (int j = 0; j < K; ++j) { const double d = fabs(x[s] - mu[j]); if (d < md) { md = d; ci = j; } }
+            for (int q = 0; q < K; ++q) { const double d = fabs(x[s] - mu[q]); if (d < md) { md = d; ci = q; } }
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const bool mine = have[s] && ci == j;
-                v[j] += mine ? 1.0 : 0.0;
-                if (j > 0) v[K + j - 1] += mine ? x[s] : 0.0;
+            for (int q = 0; q < K; ++q) {
+                const bool mine = have[s] && ci == q;
+                v[q] += mine ? 1.0 : 0.0;
+                if (q > 0) v[K + q - 1] += mine ? x[s] : 0.0;
             }
         }
         wave_totals8<2 * K - 1>(v);
         bool eq = true;
         double nm[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            nm[j] = (j == 0) ? 0.0 : (v[j] > 0.0 ? v[K + j - 1] / v[j] : 0.0);
-            eq = eq && (nm[j] == mu[j]);
-            cnt[j] = v[j];
+        for (int q = 0; q < K; ++q) {
+            nm[q] = (q == 0) ? 0.0 : (v[q] > 0.0 ? v[K + q - 1] / v[q] : 0.0);
+            eq = eq && (nm[q] == mu[q]);
+            cnt[q] = v[q];
         }
         LO_COUNT(dbg, 9, guard + 1);
         if (eq) break;
 #pragma unroll
-        for (int j = 0; j < K; ++j) mu[j] = nm[j];
+        for (int q = 0; q < K; ++q) mu[q] = nm[q];
     }
     LO_STAMP(dbg, 3);
-    // ---- initial variance of the sample (:392-399), weights from cluster sizes (:402-410) ----
     double m1 = 0.0;
 #pragma unroll
     for (int s = 0; s < SPL; ++s) m1 += have[s] ? x[s] : 0.0;
@@ -198,78 +200,86 @@ __device__ __forceinline__ void gmm_fit_w(const double* s_sd, int S, const int32
     for (int s = 0; s < SPL; ++s) m2 += have[s] ? (x[s] - mean) * (x[s] - mean) : 0.0;
     const double iv = wave_total(m2) / S;
     const double invS = 1.0 / static_cast<double>(S);
-    constexpr double kInvSqrt2Pi = 0.3989422804014327;     // 1 / sqrt(2 pi)
-    double w[K], var[K], ca[K], cb[K];
+    constexpr double kInvSqrt2Pi = 0.3989422804014327;
+    // this wave's component state (component 0 for the barrier-only waves: computed, never published)
+    const int jj = j < 0 ? 0 : j;
+    double muj = mu[0], cntj = cnt[0];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        var[j] = iv;
-        w[j] = cnt[j] / static_cast<double>(S);
-        const double rs = rsq64(iv);
-        // gaussian_pdf returns 0 for var <= 0 (:677): ca = 0, cb = 0 gives exactly 0 for every sample
-        ca[j] = (iv <= 0.0) ? 0.0 : w[j] * (rs * kInvSqrt2Pi);
-        cb[j] = (iv <= 0.0) ? 0.0 : 0.5 * (rs * rs);
-    }
+    for (int q = 1; q < K; ++q) if (jj == q) { muj = mu[q]; cntj = cnt[q]; }
+    double wj = cntj / static_cast<double>(S), varj = iv;
+    const double rs0 = rsq64(iv);
+    double ca = (iv <= 0.0) ? 0.0 : wj * (rs0 * kInvSqrt2Pi);
+    double cb = (iv <= 0.0) ? 0.0 : 0.5 * (rs0 * rs0);
     LO_STAMP(dbg, 4);
 
-    // ---- EM, <= 100 iterations, tolerance 1e-6 on the summed |d mean| of components >= 1 (:413-484) ----
-    // One reduction per iteration: N_j, sum r x (j >= 1) and sum r (x - c_j)^2 about the previous mean c_j;
-    // var_j = sum r (x - c_j)^2 / N_j - (mu_j - c_j)^2 (the two-pass sum up to rounding).  var_j >= 1e-6 (or
-    // NaN) after the first M-step, so the var <= 0 branch of gaussian_pdf only matters before it.
-    for (int em = 0; em < 100; ++em) {
-        double v[3 * K - 1];                               // N_j | sum r x (j>=1) | sum r d^2
+    // One barrier per iteration: after its M-step each wave evaluates the NEXT iteration's pdfs with the updated
+    // parameters (speculatively) into the other half of the double-buffered s_p / s_dm, then the barrier; if
+    // the change test then ends the EM, the speculative pdfs are simply dropped (the parameters are those of
+    // the converged M-step, as the reference's loop leaves them).
+    constexpr int kStride = 64 * SPL;                      // s_p[buffer][component][sample]
+    constexpr int kBuf = K * kStride;
+    double p[SPL], d[SPL];
 #pragma unroll
-        for (int q = 0; q < 3 * K - 1; ++q) v[q] = 0.0;
+    for (int s = 0; s < SPL; ++s) {
+        d[s] = x[s] - muj;
+        p[s] = ca * exp_nonpos(-((d[s] * d[s]) * cb));
+        if (j >= 0) s_p[j * kStride + 64 * s + lane] = p[s];
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int em = 0; em < 100; ++em) {
+        const double* sp = s_p + buf * kBuf;
+        double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-            double p[K], d[K], sr = 0.0;
+            double sr = 0.0;
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
-                d[j] = x[s] - mu[j];
-                p[j] = ca[j] * exp_nonpos(-((d[j] * d[j]) * cb[j]));
-                sr += p[j];
-            }
-            const double isr = have[s] ? rcp64(sr) : 0.0;  // empty slots contribute exactly 0
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const double r = p[j] * isr;
-                v[j] += r;
-                if (j > 0) v[K + j - 1] += r * x[s];
-                v[2 * K - 1 + j] += (r * d[j]) * d[j];
-            }
+            for (int q = 0; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
+            const double isr = have[s] ? rcp64(sr) : 0.0;
+            const double r = p[s] * isr;
+            v[0] += r;
+            v[1] += r * x[s];
+            v[2] += (r * d[s]) * d[s];
         }
-        wave_totals8<3 * K - 1>(v);
+        wave_totals8<3>(v);
+        const double Nk = v[0];
+        const double iN = rcp64(Nk);
+        const double nmu = (jj == 0) ? 0.0 : v[1] * iN;
+        const double dm = nmu - muj;
+        double nv = v[2] * iN - dm * dm;
+        nv = (nv < 1e-6) ? 1e-6 : nv;                      // std::max(nv, 1e-6), NaN preserved
+        wj = Nk * invS;
+        muj = nmu;
+        varj = nv;
+        const double rs = rsq64(nv);
+        ca = wj * (rs * kInvSqrt2Pi);
+        cb = 0.5 * (rs * rs);
+        if (j >= 1 && lane == 0) s_dm[buf * kMaxK + j] = fabs(dm);
+        double* spn = s_p + (buf ^ 1) * kBuf;              // speculative E-step of iteration em + 1
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            d[s] = x[s] - muj;
+            p[s] = ca * exp_nonpos(-((d[s] * d[s]) * cb));
+            if (j >= 0) spn[j * kStride + 64 * s + lane] = p[s];
+        }
+        __syncthreads();
         double change = 0.0;
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const double Nk = v[j];
-            const double iN = rcp64(Nk);
-            const double nmu = (j == 0) ? 0.0 : v[K + j - 1] * iN;
-            const double dm = nmu - mu[j];
-            double nv = v[2 * K - 1 + j] * iN - dm * dm;
-            nv = (nv < 1e-6) ? 1e-6 : nv;                  // std::max(nv, 1e-6), NaN preserved
-            if (j >= 1) change += fabs(dm);
-            w[j] = Nk * invS;
-            mu[j] = nmu;
-            var[j] = nv;
-            const double rs = rsq64(nv);
-            ca[j] = w[j] * (rs * kInvSqrt2Pi);
-            cb[j] = 0.5 * (rs * rs);
-        }
+        for (int q = 1; q < K; ++q) change += s_dm[buf * kMaxK + q];
         LO_COUNT(dbg, 8, em + 1);
         if (change < 1e-6) break;
+        buf ^= 1;
     }
     LO_STAMP(dbg, 5);
-    if (lane == 0) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) { gmm[j] = w[j]; gmm[K + j] = mu[j]; gmm[2 * K + j] = var[j]; }
-    }
+    if (j >= 0 && lane == 0) { gmm[j] = wj; gmm[K + j] = muj; gmm[2 * K + j] = varj; }
 }
 
 template <int K>
-__device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm, unsigned long long* dbg) {
-    if (S <= 64) gmm_fit_w<K, 1>(s_sd, S, draws, gmm, dbg);
-    else if (S <= 128) gmm_fit_w<K, 2>(s_sd, S, draws, gmm, dbg);
-    else gmm_fit_w<K, 4>(s_sd, S, draws, gmm, dbg);
+__device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm,
+                                                 double* s_p, double* s_dm, unsigned long long* dbg) {
+    if (S <= 64) gmm_fit_split<K, 1>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+    else if (S <= 128) gmm_fit_split<K, 2>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+    else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
 }
 
 template <int NW>
@@ -286,6 +296,8 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     __shared__ double s_sd[64 * NW];
     __shared__ double s_gmm[3 * kMaxK];
     __shared__ double s_P[100];
+    __shared__ double s_p[2 * kMaxK * 64 * NW];          // EM: per-sample pdf of each component, double-buffered
+    __shared__ double s_dm[2 * kMaxK];
     __shared__ double s_jsd[kPkoAlphaPerWG][100];
     __shared__ int s_iscan[NW];
     __shared__ double s_dscan[NW];
@@ -416,12 +428,10 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     // ---- 3. GMM ----
     const int D = P.K > 1 ? P.K - 1 : 1;
     const int32_t* draws = P.km_draws + S * D;
-    if (wid == 0) {                                             // one wave: see gmm_fit_w
-        switch (P.K) {
-            case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, dbg); break;
-            case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, dbg); break;
-            default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, dbg); break;
-        }
+    switch (P.K) {                                              // every wave: see gmm_fit_split
+        case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+        case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+        default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
     }
     __syncthreads();
     if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
@@ -474,7 +484,6 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     LO_STAMP(dbg, 6);
 }
 
-template __global__ void k_pko_t<2>(KParams, int);
 template __global__ void k_pko_t<4>(KParams, int);
 
 // PKO-only entry point: argmin of the JS grid -> DevState::alpha (lo_pko_scale_factor).
