@@ -7,18 +7,31 @@
 
 namespace lo {
 
+// Voxel slot of the filter's hash table: first / last sample index, member count, bucket fill cursor.
+struct VfSlot {
+    uint32_t first, last, cnt, fill;
+};
+
+// Device counters of one filter pass (reset by the pass itself).
+struct VfCounters {
+    int n_out;                   // voxels = output points (read by the ICP kernels as KParams::n_dev)
+    unsigned arrive;             // k_vf_heads last-block-done counter
+    int n_mid, n_big;            // voxels with 17..64 / more than 64 samples (k_vf_wide)
+};
+
 struct VfBuffers {
-    size_t cap = 0;
-    uint64_t* keys = nullptr;
-    uint64_t* keys_s = nullptr;
-    int32_t* idx = nullptr;
-    int32_t* idx_s = nullptr;
-    int32_t* first = nullptr;
-    int32_t* pos = nullptr;
-    float4* pts_s = nullptr;     // sample coordinates in sorted order, .w = voxel head mark
-    void* temp = nullptr;
-    size_t temp_bytes = 0;
-    int* n_out = nullptr;
+    size_t cap = 0;              // samples
+    size_t tcap = 0;             // table slots (power of two >= 2 * cap)
+    uint64_t* tkey = nullptr;    // table keys (kVfEmpty = free)
+    VfSlot* tslot = nullptr;
+    int32_t* sslot = nullptr;    // per sample: table slot, -1 = non-finite point
+    int2* loc = nullptr;         // per head sample: (output slot, bucket start) inside its k_vf_heads block
+    int2* blk = nullptr;         // per k_vf_heads block: (heads, members), then their exclusive prefix
+    int32_t* bucket = nullptr;   // members of each voxel (bucket order = arrival order; sorted when summed)
+    int32_t* mid = nullptr;      // head samples of voxels with 17..64 members
+    int32_t* big = nullptr;      // head samples of voxels with more than 64 members
+    VfCounters* ctr = nullptr;
+    int* n_out = nullptr;        // &ctr->n_out
 };
 
 hipError_t vf_reserve(VfBuffers& b, size_t m);

@@ -2,22 +2,36 @@
 // Estimator.cpp:561-588) on the device, bit-identical to the reference's sequential pass:
 //   * points i = 0, stride, 2*stride, ...; non-finite points skipped (:83-84);
 //   * voxel = per-axis clamp((int64)floor(x * (1/voxel)) + 2^20, 0, 2^21 - 1) (computeMortonKey :123-135);
-//   * fp32 running sums per voxel in point order, count (:86-90);
+//   * fp32 running sums per voxel from 0 in point order, count (:86-90);
 //   * output = sum * (1 / count) per voxel, in first-occurrence order (unordered_dense iterates in
 //     insertion order, :93-102).
-// Device plan (HBM-bound integer work, no MFMA): key per sampled point -> stable radix sort of (key, sample
-// index) [hipCUB] -> segment heads mark each voxel's first sample -> exclusive scan of those marks over the
-// sample index = output slot in first-occurrence order -> one lane per voxel sums its samples in index order.
-// The output count stays on the device (n_dev) so the ICP kernels can consume it without a host round trip.
+// Device plan (integer / gather work, launch-latency bound at a KITTI scan's 15k samples; five launches):
+//   k_vf_insert  one lane per sample: key, open-addressing insert (CAS), per voxel atomicMin / atomicMax of the
+//                sample index and a member count;
+//   k_vf_heads   a sample is its voxel's head iff it is the voxel's first index; a block scan of (head, members)
+//                gives each head its output slot (first-occurrence order) and bucket start inside the block, and
+//                the last block to finish turns the block totals into offsets (agent-scope fences: the XCDs'
+//                L2s are separate);
+//   k_vf_place   every sample appends its index to its voxel's bucket (arrival order);
+//   k_vf_small   one lane per head with <= 16 members: register bitonic sort of the member indices, fp32 sums in
+//                index order, output, slot reset; larger voxels are listed for
+//   k_vf_wide    one wave per voxel with <= 64 members (wave bitonic sort, in-order sum over the lanes), one
+//                workgroup per larger voxel (ordered compaction of its index range), slot reset.
+// The table slots are reset by the kernel that consumes them last, so the next pass starts from an empty table
+// without a memset.  The output count stays on the device (n_dev): the ICP kernels read it, no host round trip.
 #include "lo_device.h"
 #include "lo_vfilter.h"
 
 #include <algorithm>
-#include <hipcub/hipcub.hpp>
+#include <climits>
 
 namespace lo {
 
-constexpr uint64_t kVfInvalid = ~0ull;
+constexpr uint64_t kVfEmpty = ~0ull;     // no 3 x 21-bit key has bit 63 set
+constexpr int kVfHeadsBlock = 1024;
+constexpr int kVfSmall = 16;
+constexpr int kVfMid = 64;
+constexpr int kVfWideGrid = 64;
 
 // computeMortonKey's per-axis cell.  The reference converts floor(x * inv) to int64 with static_cast; on
 // x86-64 (cvttss2si) every out-of-range value (|f| >= 2^63, inf) becomes INT64_MIN, which the clamp maps to 0.
@@ -30,100 +44,309 @@ __device__ __forceinline__ uint32_t vf_cell(float v, float inv) {
     return static_cast<uint32_t>(k);
 }
 
-__global__ __launch_bounds__(256) void k_vf_keys(const float* __restrict__ raw, int stride, float inv, int m,
-                                                 uint64_t* __restrict__ keys, int32_t* __restrict__ idx) {
+__device__ __forceinline__ void vf_reset(uint64_t* tkey, VfSlot* tslot, int b) {
+    tkey[b] = kVfEmpty;
+    tslot[b] = VfSlot{0xFFFFFFFFu, 0u, 0u, 0u};
+}
+
+__device__ __forceinline__ const float* vf_point(const float* raw, int stride, int j) {
+    return raw + 3 * (static_cast<size_t>(j) * stride);
+}
+
+__global__ __launch_bounds__(256) void k_vf_init(uint64_t* tkey, VfSlot* tslot, int n, VfCounters* ctr) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) vf_reset(tkey, tslot, i);
+    if (i == 0) *ctr = VfCounters{0, 0u, 0, 0};
+}
+
+__global__ __launch_bounds__(256) void k_vf_insert(const float* __restrict__ raw, int stride, float inv, int m,
+                                                   uint64_t* tkey, VfSlot* tslot, uint64_t mask, int l2,
+                                                   int32_t* __restrict__ sslot) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= m) return;
-    const size_t i = static_cast<size_t>(j) * stride;
-    const float x = raw[3 * i], y = raw[3 * i + 1], z = raw[3 * i + 2];
-    uint64_t key = kVfInvalid;
-    if (isfinite(x) && isfinite(y) && isfinite(z))
-        key = static_cast<uint64_t>(vf_cell(x, inv)) | (static_cast<uint64_t>(vf_cell(y, inv)) << 21) |
-              (static_cast<uint64_t>(vf_cell(z, inv)) << 42);
-    keys[j] = key;
-    idx[j] = j;
+    const float* p = vf_point(raw, stride, j);
+    const float x = p[0], y = p[1], z = p[2];
+    if (!(isfinite(x) && isfinite(y) && isfinite(z))) { sslot[j] = -1; return; }
+    const uint64_t key = static_cast<uint64_t>(vf_cell(x, inv)) | (static_cast<uint64_t>(vf_cell(y, inv)) << 21) |
+                         (static_cast<uint64_t>(vf_cell(z, inv)) << 42);
+    uint64_t b = (key * 0x9E3779B97F4A7C15ull) >> (64 - l2);
+    for (;;) {
+        const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(tkey + b),
+                                                 static_cast<unsigned long long>(kVfEmpty),
+                                                 static_cast<unsigned long long>(key));
+        if (old == kVfEmpty || old == key) break;
+        b = (b + 1) & mask;
+    }
+    atomicMin(&tslot[b].first, static_cast<uint32_t>(j));
+    atomicMax(&tslot[b].last, static_cast<uint32_t>(j));
+    atomicAdd(&tslot[b].cnt, 1u);
+    sslot[j] = static_cast<int32_t>(b);
 }
 
-// first[j] = 1 iff sample j is the first (lowest index) sample of its voxel (every j is written once), and the
-// samples' coordinates gathered into sorted order (one parallel pass, so the per-voxel sums read contiguously)
-__global__ __launch_bounds__(256) void k_vf_heads(const uint64_t* __restrict__ ks, const int32_t* __restrict__ is, int m,
-                                                  const float* __restrict__ raw, int stride, int32_t* __restrict__ first,
-                                                  float4* __restrict__ ps) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= m) return;
-    const uint64_t key = ks[k];
-    const int j = is[k];
-    const bool head = key != kVfInvalid && (k == 0 || ks[k - 1] != key);
-    first[j] = head ? 1 : 0;
-    const size_t i = static_cast<size_t>(j) * stride;
-    // .w = 1 starts a run: a voxel head, or an invalid sample (they sort last and must end the last voxel's run)
-    ps[k] = make_float4(raw[3 * i], raw[3 * i + 1], raw[3 * i + 2], (head || key == kVfInvalid) ? 1.0f : 0.0f);
+// inclusive scan of an int2 over the 64 lanes of a wave
+__device__ __forceinline__ int2 wave_incl_scan2(int2 v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int ax = __shfl_up(v.x, o, 64), ay = __shfl_up(v.y, o, 64);
+        if (lane >= o) { v.x += ax; v.y += ay; }
+    }
+    return v;
 }
 
-// one lane per voxel: fp32 running sums over its samples in index order (contiguous after the sort; 4 loads
-// in flight per step, the .w head mark ends the run)
-__global__ __launch_bounds__(256) void k_vf_reduce(const float4* __restrict__ ps, const int32_t* __restrict__ is, int m,
-                                                   const int32_t* __restrict__ first, const int32_t* __restrict__ pos,
-                                                   float* __restrict__ out, int* __restrict__ n_out, const uint64_t* __restrict__ ks) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k == 0) *n_out = m > 0 ? pos[m - 1] + first[m - 1] : 0;
-    if (k >= m) return;
-    const float4 p0 = ps[k];
-    if (p0.w == 0.0f || ks[k] == kVfInvalid) return;                // not a voxel head (invalid samples sort last)
-    float sx = p0.x, sy = p0.y, sz = p0.z;
-    uint32_t count = 1;
-    bool run = true;
-    for (int q = k + 1; run && q < m; q += 4) {
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = (q + u < m) ? ps[q + u] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (!run) break;
-            if (v[u].w != 0.0f) { run = false; break; }             // next voxel (or the end) starts here
-            sx += v[u].x;
-            sy += v[u].y;
-            sz += v[u].z;
-            ++count;
+// exclusive scan of an int2 over a block of NT threads; tot = block total (every thread)
+template <int NT>
+__device__ __forceinline__ int2 block_excl_scan2(int2 v, int2& tot, int2* s_w /* NT/64 + 1 entries */) {
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int2 inc = wave_incl_scan2(v);
+    if (lane == 63) s_w[wid] = inc;
+    __syncthreads();
+    if (wid == 0) {
+        const int2 w = lane < NW ? s_w[lane] : make_int2(0, 0);
+        const int2 wi = wave_incl_scan2(w);
+        if (lane < NW) s_w[lane] = make_int2(wi.x - w.x, wi.y - w.y);
+        if (lane == NW - 1) s_w[NW] = wi;
+    }
+    __syncthreads();
+    tot = s_w[NW];
+    const int2 off = s_w[wid];
+    const int2 ex = make_int2(off.x + inc.x - v.x, off.y + inc.y - v.y);
+    __syncthreads();                                    // s_w may be reused right after
+    return ex;
+}
+
+__global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads(int m, const int32_t* __restrict__ sslot,
+                                                            const VfSlot* __restrict__ tslot, int2* __restrict__ loc,
+                                                            int2* blk, VfCounters* ctr) {
+    __shared__ int2 s_w[kVfHeadsBlock / 64 + 1];
+    __shared__ int s_last;
+    const int tid = threadIdx.x;
+    const int j = blockIdx.x * kVfHeadsBlock + tid;
+    int2 v = make_int2(0, 0);
+    if (j < m) {
+        const int b = sslot[j];
+        if (b >= 0) {
+            const VfSlot s = tslot[b];
+            if (s.first == static_cast<uint32_t>(j)) v = make_int2(1, static_cast<int>(s.cnt));
         }
     }
-    const float inv = 1.0f / static_cast<float>(count);
-    const int o = pos[is[k]];
-    out[3 * o] = sx * inv;
-    out[3 * o + 1] = sy * inv;
-    out[3 * o + 2] = sz * inv;
+    int2 tot;
+    const int2 ex = block_excl_scan2<kVfHeadsBlock>(v, tot, s_w);
+    if (v.x) loc[j] = ex;
+    if (tid == 0) blk[blockIdx.x] = tot;
+    // last-block-done: block totals -> exclusive offsets (release at agent scope, count arrivals)
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = (atomicAdd(&ctr->arrive, 1u) == gridDim.x - 1) ? 1 : 0;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const int nb = gridDim.x;
+    const int per = (nb + kVfHeadsBlock - 1) / kVfHeadsBlock;
+    const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+    int2 loc_sum = make_int2(0, 0);
+    for (int q = b0; q < b1; ++q) { const int2 t = blk[q]; loc_sum.x += t.x; loc_sum.y += t.y; }
+    int2 all;
+    int2 run = block_excl_scan2<kVfHeadsBlock>(loc_sum, all, s_w);
+    for (int q = b0; q < b1; ++q) { const int2 t = blk[q]; blk[q] = run; run.x += t.x; run.y += t.y; }
+    if (tid == 0) {
+        ctr->n_out = all.x;
+        ctr->arrive = 0u;
+        ctr->n_mid = 0;
+        ctr->n_big = 0;
+    }
+}
+
+__device__ __forceinline__ int2 vf_head_offsets(const int2* loc, const int2* blk, int h) {
+    const int2 o = blk[h / kVfHeadsBlock], l = loc[h];
+    return make_int2(o.x + l.x, o.y + l.y);            // (output slot, bucket start)
+}
+
+__global__ __launch_bounds__(256) void k_vf_place(int m, const int32_t* __restrict__ sslot, VfSlot* tslot,
+                                                  const int2* __restrict__ loc, const int2* __restrict__ blk,
+                                                  int32_t* __restrict__ bucket) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= m) return;
+    const int b = sslot[j];
+    if (b < 0) return;
+    const int h = static_cast<int>(tslot[b].first);
+    const int start = vf_head_offsets(loc, blk, h).y;
+    const unsigned r = atomicAdd(&tslot[b].fill, 1u);
+    bucket[start + static_cast<int>(r)] = j;
+}
+
+// ascending bitonic sort of N register values (compile-time indices: stays in VGPRs)
+template <int N>
+__device__ __forceinline__ void bitonic_regs(int (&a)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int jj = k >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const int lo = min(a[i], a[l]), hi = max(a[i], a[l]);
+                    a[i] = up ? lo : hi;
+                    a[l] = up ? hi : lo;
+                }
+            }
+}
+
+__global__ __launch_bounds__(256) void k_vf_small(const float* __restrict__ raw, int stride, int m,
+                                                  const int32_t* __restrict__ sslot, uint64_t* tkey, VfSlot* tslot,
+                                                  const int2* __restrict__ loc, const int2* __restrict__ blk,
+                                                  const int32_t* __restrict__ bucket, int32_t* mid, int32_t* big,
+                                                  VfCounters* ctr, float* __restrict__ out) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= m) return;
+    const int b = sslot[j];
+    if (b < 0) return;
+    const VfSlot s = tslot[b];
+    if (s.first != static_cast<uint32_t>(j)) return;   // one lane per voxel: its head
+    const int c = static_cast<int>(s.cnt);
+    if (c > kVfSmall) {
+        if (c <= kVfMid) mid[atomicAdd(&ctr->n_mid, 1)] = j;
+        else big[atomicAdd(&ctr->n_big, 1)] = j;
+        return;
+    }
+    const int2 o = vf_head_offsets(loc, blk, j);
+    int a[kVfSmall];
+#pragma unroll
+    for (int t = 0; t < kVfSmall; ++t) a[t] = t < c ? bucket[o.y + t] : INT_MAX;
+    bitonic_regs<kVfSmall>(a);
+    float px[kVfSmall] = {}, py[kVfSmall] = {}, pz[kVfSmall] = {};
+#pragma unroll
+    for (int t = 0; t < kVfSmall; ++t) {
+        if (t < c) {
+            const float* p = vf_point(raw, stride, a[t]);
+            px[t] = p[0]; py[t] = p[1]; pz[t] = p[2];
+        }
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;             // FilterAcc starts at 0 (VoxelMap.h:86-90)
+#pragma unroll
+    for (int t = 0; t < kVfSmall; ++t)
+        if (t < c) { sx += px[t]; sy += py[t]; sz += pz[t]; }
+    const float inv = 1.0f / static_cast<float>(c);
+    out[3 * o.x] = sx * inv;
+    out[3 * o.x + 1] = sy * inv;
+    out[3 * o.x + 2] = sz * inv;
+    vf_reset(tkey, tslot, b);
+}
+
+__global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ raw, int stride,
+                                                 const int32_t* __restrict__ sslot, uint64_t* tkey, VfSlot* tslot,
+                                                 const int2* __restrict__ loc, const int2* __restrict__ blk,
+                                                 const int32_t* __restrict__ bucket, const int32_t* __restrict__ mid,
+                                                 const int32_t* __restrict__ big, const VfCounters* ctr,
+                                                 float* __restrict__ out) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // ---- 17..64 members: one wave per voxel ----
+    const int n_mid = ctr->n_mid;
+    for (int q = blockIdx.x * 4 + wid; q < n_mid; q += gridDim.x * 4) {
+        const int j = mid[q];
+        const int b = sslot[j];
+        const int c = static_cast<int>(tslot[b].cnt);
+        const int2 o = vf_head_offsets(loc, blk, j);
+        int v = lane < c ? bucket[o.y + lane] : INT_MAX;
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                const int w = __shfl_xor(v, jj, 64);
+                const bool up = (lane & k) == 0, lower = (lane & jj) == 0;
+                v = (lower == up) ? min(v, w) : max(v, w);
+            }
+        float px = 0.0f, py = 0.0f, pz = 0.0f;
+        if (lane < c) { const float* p = vf_point(raw, stride, v); px = p[0]; py = p[1]; pz = p[2]; }
+        float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // in index order = lane order
+        for (int t = 0; t < c; ++t) {
+            sx += __shfl(px, t, 64);
+            sy += __shfl(py, t, 64);
+            sz += __shfl(pz, t, 64);
+        }
+        if (lane == 0) {
+            const float inv = 1.0f / static_cast<float>(c);
+            out[3 * o.x] = sx * inv;
+            out[3 * o.x + 1] = sy * inv;
+            out[3 * o.x + 2] = sz * inv;
+            vf_reset(tkey, tslot, b);
+        }
+    }
+    // ---- more than 64 members: one workgroup per voxel, ordered compaction of [first, last] ----
+    __shared__ float s_p[256][3];
+    __shared__ int s_wc[4];
+    const int n_big = ctr->n_big;
+    for (int q = blockIdx.x; q < n_big; q += gridDim.x) {
+        const int j = big[q];
+        const int b = sslot[j];
+        const VfSlot s = tslot[b];
+        const int2 o = vf_head_offsets(loc, blk, j);
+        float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // thread 0's running sums
+        for (int base = static_cast<int>(s.first); base <= static_cast<int>(s.last); base += 256) {
+            const int jj = base + tid;
+            const bool f = jj <= static_cast<int>(s.last) && sslot[jj] == b;
+            const uint64_t bal = __ballot(f);
+            if (lane == 0) s_wc[wid] = __popcll(bal);
+            __syncthreads();
+            int off = 0, cnt = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) { off += (w < wid) ? s_wc[w] : 0; cnt += s_wc[w]; }
+            if (f) {
+                const int r = off + __popcll(bal & ((1ull << lane) - 1ull));
+                const float* p = vf_point(raw, stride, jj);
+                s_p[r][0] = p[0]; s_p[r][1] = p[1]; s_p[r][2] = p[2];
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int t = 0; t < cnt; ++t) { sx += s_p[t][0]; sy += s_p[t][1]; sz += s_p[t][2]; }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const float inv = 1.0f / static_cast<float>(s.cnt);
+            out[3 * o.x] = sx * inv;
+            out[3 * o.x + 1] = sy * inv;
+            out[3 * o.x + 2] = sz * inv;
+            vf_reset(tkey, tslot, b);
+        }
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------- host side (called from lo_icp.hip)
 hipError_t vf_reserve(VfBuffers& b, size_t m) {
-    if (b.n_out == nullptr) {
-        hipError_t e = hipMalloc(&b.n_out, sizeof(int));
-        if (e != hipSuccess) return e;
-    }
-    if (m <= b.cap) return hipSuccess;
-    void* old[] = {b.keys, b.keys_s, b.idx, b.idx_s, b.first, b.pos, b.temp, b.pts_s};
+    if (b.ctr != nullptr && m <= b.cap) return hipSuccess;
+    void* old[] = {b.tkey, b.tslot, b.sslot, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : old) if (p) (void)hipFree(p);
+    b = VfBuffers{};
     const size_t cap = std::max<size_t>(m, 4096);
+    size_t tcap = 2;
+    while (tcap < 2 * cap) tcap <<= 1;                  // load factor <= 0.5
+    const size_t nb = (cap + kVfHeadsBlock - 1) / kVfHeadsBlock;
     hipError_t e;
-    if ((e = hipMalloc(&b.keys, cap * 8)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.keys_s, cap * 8)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.idx, cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.idx_s, cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.first, cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.pos, cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc(&b.pts_s, cap * sizeof(float4))) != hipSuccess) return e;
-    size_t sort_bytes = 0, scan_bytes = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, b.keys, b.keys_s, b.idx, b.idx_s,
-                                                static_cast<int>(cap), 0, 64)) != hipSuccess) return e;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, b.first, b.pos, static_cast<int>(cap))) != hipSuccess) return e;
-    b.temp_bytes = std::max(sort_bytes, scan_bytes);
-    if ((e = hipMalloc(&b.temp, b.temp_bytes)) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.tkey, tcap * sizeof(uint64_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.tslot, tcap * sizeof(VfSlot))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.sslot, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.loc, cap * sizeof(int2))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.blk, nb * sizeof(int2))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.bucket, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.mid, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.big, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.ctr, sizeof(VfCounters))) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_vf_init, dim3(static_cast<unsigned>((tcap + 255) / 256)), dim3(256), 0, nullptr, b.tkey, b.tslot,
+                       static_cast<int>(tcap), b.ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
     b.cap = cap;
+    b.tcap = tcap;
+    b.n_out = &b.ctr->n_out;
     return hipSuccess;
 }
 
 void vf_free(VfBuffers& b) {
-    void* all[] = {b.keys, b.keys_s, b.idx, b.idx_s, b.first, b.pos, b.temp, b.n_out, b.pts_s};
+    void* all[] = {b.tkey, b.tslot, b.sslot, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : all) if (p) (void)hipFree(p);
     b = VfBuffers{};
 }
@@ -137,17 +360,20 @@ hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride
     hipError_t e = vf_reserve(b, m);
     if (e != hipSuccess) return e;
     if (m == 0) return hipMemsetAsync(b.n_out, 0, sizeof(int), s);
-    const float inv = 1.0f / voxel_size;                         // m_inv_voxel_size (VoxelMap.h:57)
-    const dim3 g(static_cast<unsigned>((m + 255) / 256)), t(256);
-    hipLaunchKernelGGL(k_vf_keys, g, t, 0, s, d_raw, stride, inv, static_cast<int>(m), b.keys, b.idx);
-    size_t bytes = b.temp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(b.temp, bytes, b.keys, b.keys_s, b.idx, b.idx_s, static_cast<int>(m),
-                                                0, 64, s)) != hipSuccess) return e;   // all 64 bits: ~0 marks invalid
-    hipLaunchKernelGGL(k_vf_heads, g, t, 0, s, b.keys_s, b.idx_s, static_cast<int>(m), d_raw, stride, b.first, b.pts_s);
-    bytes = b.temp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, bytes, b.first, b.pos, static_cast<int>(m), s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_vf_reduce, g, t, 0, s, b.pts_s, b.idx_s, static_cast<int>(m), b.first, b.pos, d_out, b.n_out,
-                       b.keys_s);
+    const float inv = 1.0f / voxel_size;                 // m_inv_voxel_size (VoxelMap.h:57)
+    int l2 = 0;
+    while ((size_t(1) << l2) < b.tcap) ++l2;
+    const int mi = static_cast<int>(m);
+    const dim3 g256(static_cast<unsigned>((m + 255) / 256)), t256(256);
+    const dim3 gh(static_cast<unsigned>((m + kVfHeadsBlock - 1) / kVfHeadsBlock)), th(kVfHeadsBlock);
+    hipLaunchKernelGGL(k_vf_insert, g256, t256, 0, s, d_raw, stride, inv, mi, b.tkey, b.tslot,
+                       static_cast<uint64_t>(b.tcap - 1), l2, b.sslot);
+    hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.ctr);
+    hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.bucket);
+    hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, d_raw, stride, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk,
+                       b.bucket, b.mid, b.big, b.ctr, d_out);
+    hipLaunchKernelGGL(k_vf_wide, dim3(kVfWideGrid), t256, 0, s, d_raw, stride, b.sslot, b.tkey, b.tslot, b.loc,
+                       b.blk, b.bucket, b.mid, b.big, b.ctr, d_out);
     return hipGetLastError();
 }
 

@@ -51,6 +51,22 @@ def test_voxel_filter_edge_cases(icp):
                                   oracle.voxel_filter(one, 0.5, 1).view(np.uint32))
 
 
+def test_voxel_filter_density_mix_and_signed_zero(icp):
+    """Voxels of 1..16, 17..64 and >64 samples interleaved in the input (the device's three summation paths), and a
+    lone -0.0 point: the reference's sums start at +0.0f, so it comes out +0.0."""
+    rng = np.random.default_rng(11)
+    centers = rng.integers(-40, 40, size=(600, 3)).astype(np.float32) * 0.5 + 0.25
+    counts = np.concatenate([rng.integers(1, 17, 300), rng.integers(17, 65, 200), rng.integers(65, 300, 100)])
+    pts = np.concatenate([c + rng.uniform(-0.2, 0.2, size=(k, 3)).astype(np.float32) for c, k in zip(centers, counts)])
+    pts = pts[rng.permutation(len(pts))]
+    pts = np.concatenate([pts, np.array([[-0.0, 100.0, -0.0]], np.float32)])
+    for stride in (1, 2):
+        ref = oracle.voxel_filter(pts, 0.5, stride)
+        got = icp.voxel_filter(pts, 0.5, stride)
+        np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert oracle.voxel_filter(pts, 0.5, 1)[-1].view(np.uint32)[0] == 0      # +0.0, not -0.0
+
+
 @pytest.mark.parametrize("frame", [11, 25])
 def test_optimize_raw_per_iteration(icp, frame):
     m, pts, Ti, _ = _data.kitti_case(frame)
