@@ -143,6 +143,11 @@ int lo_icp_optimize_raw_async(lo_ctx* ctx, const float* d_raw, size_t n_raw, int
                               const float T_init[12]);
 int lo_icp_optimize_raw(lo_ctx* ctx, const float* raw_xyz, size_t n_raw, int stride, float voxel_size,
                         const float T_init[12], float T_out[12], lo_iter_log* logs, lo_stats* stats);
+/* Page-locked, device-accessible host memory for raw scans (a sensor driver's ring buffer).  A scan handed to
+ * lo_icp_optimize_raw / lo_odom_process in such memory is read by the device filter directly (only the sampled
+ * points cross the bus); any other host pointer is staged with one copy of the whole scan. */
+void* lo_host_alloc(size_t bytes);
+void  lo_host_free(void* p);
 /* The last device-filtered scan (the frame's feature cloud, for the keyframe map update); returns the count. */
 long long lo_filtered_points(lo_ctx* ctx, float* out_xyz, size_t cap);
 /* Filter only (parity): host raw in, host filtered out; returns the count or a negative error. */

@@ -4,7 +4,7 @@ Drop-in for the Gauss-Newton scan-to-map step of SiarheiHerasiuta/lidar_odometry
 (IterativeClosestPointOptimizer::optimize + VoxelMap::GetSurfelAtPoint + PKO), implemented as HIP kernels
 for gfx950 behind the C ABI in ``include/lo_icp.h`` (``liblo_icp.so``).
 """
-from ._lib import LIB_PATH, lib  # noqa: F401
+from ._lib import LIB_PATH, lib, pinned_empty  # noqa: F401
 from .icp import (AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer,  # noqa: F401
                   MapGeometry, OptimizationStats)
 

@@ -7,6 +7,9 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
+
+import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LO_ICP_LIB") or os.path.join(_HERE, "liblo_icp.so")
@@ -24,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
-    "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop",
+    "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
     # include/lo_map.h
@@ -105,6 +108,10 @@ def lib():
     L.lo_icp_optimize_raw.restype = C.c_int
     L.lo_icp_optimize_raw.argtypes = [vp, fp, C.c_size_t, C.c_int, C.c_float, fp, fp, C.POINTER(LoIterLog),
                                       C.POINTER(LoStats)]
+    L.lo_host_alloc.restype = vp
+    L.lo_host_alloc.argtypes = [C.c_size_t]
+    L.lo_host_free.restype = None
+    L.lo_host_free.argtypes = [vp]
     L.lo_icp_optimize_loop.restype = C.c_int
     L.lo_icp_optimize_loop.argtypes = [vp, fp, C.c_size_t, fp, fp, C.c_size_t, fp, fp, fp, C.POINTER(LoIterLog),
                                        C.POINTER(LoStats)]
@@ -167,3 +174,16 @@ def lib():
     L.lo_voxel_filter.argtypes = [fp, C.c_size_t, C.c_float, C.c_int, fp]
     _lib = L
     return L
+
+
+def pinned_empty(shape, dtype=np.float32):
+    """A numpy array in page-locked, device-accessible host memory (lo_host_alloc): raw scans placed in it are read
+    by the device filter directly, without a staging copy.  The memory is released with the array."""
+    dt = np.dtype(dtype)
+    n = max(int(np.prod(shape)) * dt.itemsize, 1)
+    ptr = lib().lo_host_alloc(n)
+    if not ptr:
+        raise MemoryError(f"lo_host_alloc({n}) failed")
+    buf = (C.c_char * n).from_address(ptr)
+    buf._release = weakref.finalize(buf, lib().lo_host_free, C.c_void_p(ptr))
+    return np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)

@@ -698,15 +698,39 @@ int lo_icp_optimize_raw_async(lo_ctx* c, const float* d_raw, size_t n_raw, int s
     return enqueue_optimize(c, c->d_pts, static_cast<size_t>(m), T_init, c->vf.n_out);
 }
 
+// A host scan in pinned memory (lo_host_alloc, hipHostMalloc, hipHostRegister): the device address that aliases it,
+// so the filter reads the sampled points over the bus directly instead of a staging copy of the whole scan.
+static const float* pinned_alias(const float* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return nullptr; }   // pageable
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return reinterpret_cast<const float*>(static_cast<const char*>(a.devicePointer) +
+                                          (reinterpret_cast<const char*>(p) - static_cast<const char*>(a.hostPointer)));
+}
+
+void* lo_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void lo_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int lo_icp_optimize_raw(lo_ctx* c, const float* raw, size_t n_raw, int stride, float voxel_size, const float T_init[12],
                         float T_out[12], lo_iter_log* logs, lo_stats* st) {
     if (!c || !T_init || !T_out || (n_raw > 0 && !raw)) return LO_ERR_ARG;
     int rc = check_raw_args(c, n_raw, stride, voxel_size);
     if (rc != LO_OK) return rc;
     LO_HIP(c, hipSetDevice(c->device));
-    rc = stage_raw(c, raw, n_raw);
-    if (rc != LO_OK) return rc;
-    rc = lo_icp_optimize_raw_async(c, c->d_raw, n_raw, stride, voxel_size, T_init);
+    const float* src = n_raw > 0 ? pinned_alias(raw) : nullptr;
+    if (!src) {                                          // pageable: stage the scan in device memory
+        rc = stage_raw(c, raw, n_raw);
+        if (rc != LO_OK) return rc;
+        src = c->d_raw;
+    }
+    rc = lo_icp_optimize_raw_async(c, src, n_raw, stride, voxel_size, T_init);
     if (rc != LO_OK) return rc;
     return lo_icp_result(c, T_out, logs, st);
 }

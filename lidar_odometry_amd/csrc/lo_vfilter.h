@@ -25,6 +25,7 @@ struct VfBuffers {
     uint64_t* tkey = nullptr;    // table keys (kVfEmpty = free)
     VfSlot* tslot = nullptr;
     int32_t* sslot = nullptr;    // per sample: table slot, -1 = non-finite point
+    float* samp = nullptr;       // per sample: its point (compact AoS float3; the raw scan is read once)
     int2* loc = nullptr;         // per head sample: (output slot, bucket start) inside its k_vf_heads block
     int2* blk = nullptr;         // per k_vf_heads block: (heads, members), then their exclusive prefix
     int32_t* bucket = nullptr;   // members of each voxel (bucket order = arrival order; sorted when summed)

@@ -59,13 +59,18 @@ __global__ __launch_bounds__(256) void k_vf_init(uint64_t* tkey, VfSlot* tslot, 
     if (i == 0) *ctr = VfCounters{0, 0u, 0, 0};
 }
 
+// raw may be device memory or pinned host memory (read over the bus exactly once, here: later kernels read the
+// compact per-sample copy)
 __global__ __launch_bounds__(256) void k_vf_insert(const float* __restrict__ raw, int stride, float inv, int m,
                                                    uint64_t* tkey, VfSlot* tslot, uint64_t mask, int l2,
-                                                   int32_t* __restrict__ sslot) {
+                                                   int32_t* __restrict__ sslot, float* __restrict__ samp) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= m) return;
     const float* p = vf_point(raw, stride, j);
     const float x = p[0], y = p[1], z = p[2];
+    samp[3 * j] = x;
+    samp[3 * j + 1] = y;
+    samp[3 * j + 2] = z;
     if (!(isfinite(x) && isfinite(y) && isfinite(z))) { sslot[j] = -1; return; }
     const uint64_t key = static_cast<uint64_t>(vf_cell(x, inv)) | (static_cast<uint64_t>(vf_cell(y, inv)) << 21) |
                          (static_cast<uint64_t>(vf_cell(z, inv)) << 42);
@@ -195,7 +200,7 @@ __device__ __forceinline__ void bitonic_regs(int (&a)[N]) {
             }
 }
 
-__global__ __launch_bounds__(256) void k_vf_small(const float* __restrict__ raw, int stride, int m,
+__global__ __launch_bounds__(256) void k_vf_small(const float* __restrict__ samp, int m,
                                                   const int32_t* __restrict__ sslot, uint64_t* tkey, VfSlot* tslot,
                                                   const int2* __restrict__ loc, const int2* __restrict__ blk,
                                                   const int32_t* __restrict__ bucket, int32_t* mid, int32_t* big,
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(256) void k_vf_small(const float* __restrict__ raw,
 #pragma unroll
     for (int t = 0; t < kVfSmall; ++t) {
         if (t < c) {
-            const float* p = vf_point(raw, stride, a[t]);
+            const float* p = samp + 3 * a[t];
             px[t] = p[0]; py[t] = p[1]; pz[t] = p[2];
         }
     }
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(256) void k_vf_small(const float* __restrict__ raw,
     vf_reset(tkey, tslot, b);
 }
 
-__global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ raw, int stride,
+__global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ samp,
                                                  const int32_t* __restrict__ sslot, uint64_t* tkey, VfSlot* tslot,
                                                  const int2* __restrict__ loc, const int2* __restrict__ blk,
                                                  const int32_t* __restrict__ bucket, const int32_t* __restrict__ mid,
@@ -260,7 +265,7 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ raw, 
                 v = (lower == up) ? min(v, w) : max(v, w);
             }
         float px = 0.0f, py = 0.0f, pz = 0.0f;
-        if (lane < c) { const float* p = vf_point(raw, stride, v); px = p[0]; py = p[1]; pz = p[2]; }
+        if (lane < c) { const float* p = samp + 3 * v; px = p[0]; py = p[1]; pz = p[2]; }
         float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // in index order = lane order
         for (int t = 0; t < c; ++t) {
             sx += __shfl(px, t, 64);
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ raw, 
             for (int w = 0; w < 4; ++w) { off += (w < wid) ? s_wc[w] : 0; cnt += s_wc[w]; }
             if (f) {
                 const int r = off + __popcll(bal & ((1ull << lane) - 1ull));
-                const float* p = vf_point(raw, stride, jj);
+                const float* p = samp + 3 * jj;
                 s_p[r][0] = p[0]; s_p[r][1] = p[1]; s_p[r][2] = p[2];
             }
             __syncthreads();
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ raw, 
 // ---------------------------------------------------------------- host side (called from lo_icp.hip)
 hipError_t vf_reserve(VfBuffers& b, size_t m) {
     if (b.ctr != nullptr && m <= b.cap) return hipSuccess;
-    void* old[] = {b.tkey, b.tslot, b.sslot, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
+    void* old[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : old) if (p) (void)hipFree(p);
     b = VfBuffers{};
     const size_t cap = std::max<size_t>(m, 4096);
@@ -329,6 +334,7 @@ hipError_t vf_reserve(VfBuffers& b, size_t m) {
     if ((e = hipMalloc(&b.tkey, tcap * sizeof(uint64_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.tslot, tcap * sizeof(VfSlot))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.sslot, cap * sizeof(int32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.samp, cap * 3 * sizeof(float))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.loc, cap * sizeof(int2))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.blk, nb * sizeof(int2))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.bucket, cap * sizeof(int32_t))) != hipSuccess) return e;
@@ -346,12 +352,13 @@ hipError_t vf_reserve(VfBuffers& b, size_t m) {
 }
 
 void vf_free(VfBuffers& b) {
-    void* all[] = {b.tkey, b.tslot, b.sslot, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
+    void* all[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : all) if (p) (void)hipFree(p);
     b = VfBuffers{};
 }
 
-// Enqueue the filter of d_raw (n_raw AoS float3) into d_out; the count lands in b.n_out (device).
+// Enqueue the filter of d_raw (n_raw AoS float3, device or pinned host memory) into d_out; the count lands in
+// b.n_out (device).
 // Returns the number of samples m = ceil(n_raw / stride), an upper bound of the output count.
 hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride, float voxel_size, float* d_out,
                       hipStream_t s, int& m_out) {
@@ -367,12 +374,12 @@ hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride
     const dim3 g256(static_cast<unsigned>((m + 255) / 256)), t256(256);
     const dim3 gh(static_cast<unsigned>((m + kVfHeadsBlock - 1) / kVfHeadsBlock)), th(kVfHeadsBlock);
     hipLaunchKernelGGL(k_vf_insert, g256, t256, 0, s, d_raw, stride, inv, mi, b.tkey, b.tslot,
-                       static_cast<uint64_t>(b.tcap - 1), l2, b.sslot);
+                       static_cast<uint64_t>(b.tcap - 1), l2, b.sslot, b.samp);
     hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.ctr);
     hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.bucket);
-    hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, d_raw, stride, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk,
+    hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, b.samp, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk,
                        b.bucket, b.mid, b.big, b.ctr, d_out);
-    hipLaunchKernelGGL(k_vf_wide, dim3(kVfWideGrid), t256, 0, s, d_raw, stride, b.sslot, b.tkey, b.tslot, b.loc,
+    hipLaunchKernelGGL(k_vf_wide, dim3(kVfWideGrid), t256, 0, s, b.samp, b.sslot, b.tkey, b.tslot, b.loc,
                        b.blk, b.bucket, b.mid, b.big, b.ctr, d_out);
     return hipGetLastError();
 }

@@ -97,3 +97,23 @@ def test_optimize_raw_matches_host_filtered(icp):
     ok_b, B = icp.optimize_raw(None, _data.kitti_scan(17), Ti, stride=8, voxel_size=0.5)
     assert ok_a == ok_b
     np.testing.assert_array_equal(A, B)
+
+
+def test_optimize_raw_pinned_input(icp):
+    """A raw scan in pinned host memory (lo_host_alloc) is read by the device filter in place: same filtered cloud
+    and pose as the staged pageable copy, bit for bit."""
+    from lidar_odometry_amd import pinned_empty
+    m, pts, Ti, _ = _data.kitti_case(19)
+    k, n, c = _data.surfels(m)
+    icp.set_surfels(k, n, c)
+    raw = _data.kitti_scan(19)
+    ok_a, A = icp.optimize_raw(None, raw, Ti, stride=8, voxel_size=0.5)
+    fa = icp.filtered_points()
+    pr = pinned_empty(raw.shape)
+    pr[:] = raw
+    ok_b, B = icp.optimize_raw(None, pr, Ti, stride=8, voxel_size=0.5)
+    fb = icp.filtered_points()
+    assert ok_a == ok_b
+    np.testing.assert_array_equal(A, B)
+    np.testing.assert_array_equal(fa.view(np.uint32), fb.view(np.uint32))
+    del pr
