@@ -133,6 +133,40 @@ int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);
 int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
                     int kernel_id, int reps, float* avg_ms);
 
+/* ---- scan-parallel batch on one GPU ----
+ * The north star's scan-parallel model (one independent scan stream per GPU, BASELINE.json configs[4]) applied
+ * inside one GPU: B contexts on the same device -- B independent sequences, each with its own map, scan buffer
+ * and GN state -- advance through optimize() in lockstep, one launch per kernel per GN iteration for all B
+ * (blockIdx.y = job).  Each job computes exactly what lo_icp_optimize computes on its context (bit-identical:
+ * same kernels, same per-job reductions).  The reference has no batch entry point; this is the multi-sequence
+ * form of IterativeClosestPointOptimizer::optimize (IterativeClosestPointOptimizer.cpp:255-463) called once
+ * per sequence.  Requirements: surfel correspondence mode, one device, equal max_iterations.  The batch runs
+ * on its own stream; the contexts must be idle while it runs and each context's lo_icp_result() is not valid
+ * for a batched scan (use lo_batch_result). */
+typedef struct lo_batch lo_batch;
+typedef struct lo_batch_rec {
+    float  pose[12];       /* optimized pose (T_init when status != LO_OK, as lo_icp_optimize) */
+    int    status;         /* LO_OK / LO_INSUFFICIENT */
+    int    iterations;
+    int    n_corr;         /* last iteration */
+    float  initial_cost;
+    float  final_cost;
+    float  pad;
+    double alpha;          /* last PKO Huber delta */
+} lo_batch_rec;
+lo_batch*   lo_batch_create(lo_ctx* const* ctxs, int count, int* err);
+void        lo_batch_destroy(lo_batch* b);
+const char* lo_batch_last_error(const lo_batch* b);
+int         lo_batch_size(const lo_batch* b);
+/* d_pts[j]: device pointer (AoS float3) of job j's scan, or NULL = the points last uploaded to context j by
+ * lo_batch_optimize; n[j] its point count (0 = the job is skipped and reports LO_INSUFFICIENT); T_init: count x 12
+ * row-major poses.  Enqueues every job's whole GN loop and returns. */
+int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t* n, const float* T_init);
+/* Waits for the batch; out[count] receives one record per job.  Returns LO_OK or a negative error. */
+int lo_batch_result(lo_batch* b, lo_batch_rec* out, double* gpu_ms);
+/* Host points in, records out (H2D of every scan on the batch stream, enqueue, wait). */
+int lo_batch_optimize(lo_batch* b, const float* const* pts, const size_t* n, const float* T_init, lo_batch_rec* out);
+
 /* ---- single-stage entry points (parity harness; each synchronous) ---- */
 /* ---- device preprocessing + optimize (Estimator::preprocess_frame, Estimator.cpp:561-588) ----
  * FastVoxelFilter::filter (VoxelMap.h:73-104) on the device -- stride sampling, Morton-cell grouping with the

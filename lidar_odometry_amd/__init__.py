@@ -5,8 +5,8 @@ Drop-in for the Gauss-Newton scan-to-map step of SiarheiHerasiuta/lidar_odometry
 for gfx950 behind the C ABI in ``include/lo_icp.h`` (``liblo_icp.so``).
 """
 from ._lib import LIB_PATH, lib, pinned_empty  # noqa: F401
-from .icp import (AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer,  # noqa: F401
-                  MapGeometry, OptimizationStats)
+from .icp import (AdaptiveMEstimatorConfig, BatchOptimizer, BatchResult, ICPConfig,  # noqa: F401
+                  IterativeClosestPointOptimizer, MapGeometry, OptimizationStats)
 
-__all__ = ["IterativeClosestPointOptimizer", "ICPConfig", "AdaptiveMEstimatorConfig", "MapGeometry",
+__all__ = ["IterativeClosestPointOptimizer", "BatchOptimizer", "BatchResult", "ICPConfig", "AdaptiveMEstimatorConfig", "MapGeometry",
            "OptimizationStats", "lib", "LIB_PATH"]

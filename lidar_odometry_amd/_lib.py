@@ -30,6 +30,8 @@ EXPORTED_SYMBOLS = (
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
+    "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
+    "lo_batch_result", "lo_batch_optimize",
     # include/lo_map.h
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
@@ -62,6 +64,11 @@ class LoIterLog(C.Structure):
 class LoStats(C.Structure):
     _fields_ = [("iterations", C.c_int), ("n_corr", C.c_int), ("status", C.c_int), ("converged", C.c_int),
                 ("initial_cost", C.c_double), ("final_cost", C.c_double), ("gpu_ms", C.c_double)]
+
+
+class LoBatchRec(C.Structure):
+    _fields_ = [("pose", C.c_float * 12), ("status", C.c_int), ("iterations", C.c_int), ("n_corr", C.c_int),
+                ("initial_cost", C.c_float), ("final_cost", C.c_float), ("pad", C.c_float), ("alpha", C.c_double)]
 
 
 class LoOdomConfig(C.Structure):
@@ -158,6 +165,16 @@ def lib():
     L.lo_pko_sample_indices.argtypes = [vp, C.c_size_t, ip]
     L.lo_pko_sample_indices_host.argtypes = [C.c_size_t, C.c_int, ip]
     L.lo_debug_counters.argtypes = [vp, C.POINTER(C.c_ulonglong)]
+    L.lo_batch_create.restype = vp
+    L.lo_batch_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(C.c_int)]
+    L.lo_batch_destroy.restype = None
+    L.lo_batch_destroy.argtypes = [vp]
+    L.lo_batch_last_error.restype = C.c_char_p
+    L.lo_batch_last_error.argtypes = [vp]
+    L.lo_batch_size.argtypes = [vp]
+    L.lo_batch_optimize_async.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), fp]
+    L.lo_batch_result.argtypes = [vp, C.POINTER(LoBatchRec), dp]
+    L.lo_batch_optimize.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), fp, C.POINTER(LoBatchRec)]
     L.lo_voxelmap_create.restype = vp
     L.lo_voxelmap_create.argtypes = [C.c_float, C.c_int, C.c_float, C.c_int]
     L.lo_voxelmap_destroy.argtypes = [vp]

@@ -69,6 +69,7 @@ struct KParams {
     int nb_acc;                       // k_accumulate blocks = min(nb, kAccBlocks)
     int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
     float T0[12];
+    const float* T0p;                 // batched launches: the job's initial pose in device memory (else T0)
     // KDTree correspondence path (use_surfel_correspondence = 0; lo_kdtree.hip)
     const float4* kd_pts;             // L0 centroids sorted by grid cell: x, y, z, original index (int bits)
     const uint32_t* kd_start;         // cell -> first point (dense grid, ncell + 1 entries)
@@ -285,14 +286,20 @@ __device__ __forceinline__ int scan_n(const KParams& P) { return P.n_dev ? *P.n_
 // ---------------------------------------------------------------------------------------------------
 // Correspondence-kernel helpers shared by the surfel (k_correspond) and KDTree (lo_kdtree.hip) paths.
 // ---------------------------------------------------------------------------------------------------
-// Pose of the current GN iteration.  With P.init (first launch of a scan) it is the kernel argument T0 and
-// block 0 writes the fresh GN state that the later kernels of the scan read (k_init folded in).
-__device__ __forceinline__ void scan_pose(const KParams& P, float (&T)[12]) {
+// Pose of the current GN iteration.  With init (first launch of a scan) it is the initial pose (kernel argument
+// T0, or T0p in device memory for batched launches) and block 0 writes the fresh GN state that the later kernels
+// of the scan read (k_init folded in).
+__device__ __forceinline__ void scan_pose(const KParams& P, int init, int blk, float (&T)[12]) {
     DevState* st = P.st;
+    if (init) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = P.init ? P.T0[k] : st->pose[k];
-    if (P.init && blockIdx.x == 0 && threadIdx.x < 12) {
-        st->pose[threadIdx.x] = P.T0[threadIdx.x];
+        for (int k = 0; k < 12; ++k) T[k] = P.T0p ? P.T0p[k] : P.T0[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    }
+    if (init && blk == 0 && threadIdx.x < 12) {
+        st->pose[threadIdx.x] = P.T0p ? P.T0p[threadIdx.x] : P.T0[threadIdx.x];
         if (threadIdx.x == 0) {
             st->scale = 1.0;
             st->alpha = P.robust_delta;

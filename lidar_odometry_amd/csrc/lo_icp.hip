@@ -32,6 +32,12 @@ __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
 __global__ void k_plane(KParams P, int with_stats);
 __global__ void k_inlier(KParams P);
+__global__ void k_correspond_b(const KParams* PB, int with_stats, int init);
+template <int NW> __global__ void k_pko_tb(const KParams* PB, int it);
+__global__ void k_accumulate_b(const KParams* PB, int it);
+__global__ void k_accumulate_b1(const KParams* PB, int it);
+__global__ void k_solve_b(const KParams* PB, int it);
+__global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
 }  // namespace lo
 
 using namespace lo;
@@ -931,6 +937,215 @@ int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {
     const int k = static_cast<int>(std::min<size_t>(n, static_cast<size_t>(sample_size)));
     for (int s = 0; s < k; ++s) out[s] = pko_sample_host(t, static_cast<int>(n), s);
     return k;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- scan-parallel batch (one GPU)
+// B contexts advance through optimize() in lockstep: one launch per kernel per GN iteration for all jobs
+// (blockIdx.y = job).  The per-job KParams live in device memory (the batched kernels read them with scalar
+// loads); they are rebuilt on the host every call but uploaded only when a job's scan pointer, size or map
+// table changed.  The initial poses travel in a separate 12-float-per-job array (KParams::T0p).
+static constexpr int kBatchPkoWGs = 2048;   // PKO workgroups per launch over all jobs (>= 1 per job)
+
+struct lo_batch {
+    std::vector<lo_ctx*> ctx;
+    int device = 0;
+    int max_iters = 0;
+    int pko_max = 1;                 // min over contexts of the single-scan PKO grid
+    int pko_budget = kBatchPkoWGs;   // PKO workgroups per launch over all jobs (LO_BATCH_PKO_WGS overrides)
+    hipStream_t stream = nullptr;
+    std::string err;
+    KParams* d_P = nullptr;
+    KParams* h_P = nullptr;          // pinned staging of the active jobs' params
+    float* d_T0 = nullptr;
+    float* h_T0 = nullptr;           // pinned
+    lo_batch_rec* d_rec = nullptr;
+    lo_batch_rec* h_rec = nullptr;   // pinned
+    std::vector<float> T_in;         // count x 12 (T_out of failed / skipped jobs)
+    std::vector<int> act;            // active job -> job index
+    std::vector<size_t> n;
+    struct Sig { const float* pts; int n; const Slot* tab; uint32_t log2cap; };
+    std::vector<Sig> sig;            // what d_P currently holds, per active slot
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool pending = false;
+};
+
+#define LO_BHIP(b, call)                                                                   \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            (b)->err = std::string(#call) + ": " + hipGetErrorString(e_);                 \
+            return LO_ERR_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+static int batch_alloc(lo_batch* b) {
+    const size_t B = b->ctx.size();
+    LO_BHIP(b, hipSetDevice(b->device));
+    LO_BHIP(b, hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    LO_BHIP(b, hipMalloc(&b->d_P, B * sizeof(KParams)));
+    LO_BHIP(b, hipHostMalloc(&b->h_P, B * sizeof(KParams), hipHostMallocDefault));
+    LO_BHIP(b, hipMalloc(&b->d_T0, B * 12 * sizeof(float)));
+    LO_BHIP(b, hipHostMalloc(&b->h_T0, B * 12 * sizeof(float), hipHostMallocDefault));
+    LO_BHIP(b, hipMalloc(&b->d_rec, B * sizeof(lo_batch_rec)));
+    LO_BHIP(b, hipHostMalloc(&b->h_rec, B * sizeof(lo_batch_rec), hipHostMallocDefault));
+    LO_BHIP(b, hipEventCreate(&b->ev0));
+    LO_BHIP(b, hipEventCreate(&b->ev1));
+    LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   static_cast<int>(kMaxBlocks * sizeof(int))));
+    b->T_in.assign(B * 12, 0.0f);
+    b->n.assign(B, 0);
+    return LO_OK;
+}
+
+extern "C" {
+
+lo_batch* lo_batch_create(lo_ctx* const* ctxs, int count, int* err) {
+    auto fail = [&](int rc, const char* msg) -> lo_batch* {
+        std::fprintf(stderr, "lo_batch_create: %s\n", msg);
+        if (err) *err = rc;
+        return nullptr;
+    };
+    if (!ctxs || count < 1 || count > 65535) return fail(LO_ERR_ARG, "need 1..65535 contexts");
+    for (int j = 0; j < count; ++j) {
+        const lo_ctx* c = ctxs[j];
+        if (!c) return fail(LO_ERR_ARG, "null context");
+        if (c->kd) return fail(LO_ERR_ARG, "batched optimize needs surfel-mode contexts");
+        if (c->device != ctxs[0]->device) return fail(LO_ERR_ARG, "contexts on different devices");
+        if (c->cfg.max_iterations != ctxs[0]->cfg.max_iterations) return fail(LO_ERR_ARG, "max_iterations differ");
+        for (int k = 0; k < j; ++k) if (ctxs[k] == c) return fail(LO_ERR_ARG, "a context appears twice");
+    }
+    lo_batch* b = new lo_batch();
+    b->ctx.assign(ctxs, ctxs + count);
+    b->device = ctxs[0]->device;
+    b->max_iters = ctxs[0]->cfg.max_iterations;
+    b->pko_max = kPkoMaxWGs;
+    for (const lo_ctx* c : b->ctx) b->pko_max = std::min(b->pko_max, pko_grid(c->cfg));
+    if (const char* e = std::getenv("LO_BATCH_PKO_WGS")) b->pko_budget = std::max(1, std::atoi(e));
+    const int rc = batch_alloc(b);
+    if (rc != LO_OK) {
+        std::fprintf(stderr, "lo_batch_create: %s\n", b->err.c_str());
+        lo_batch_destroy(b);
+        if (err) *err = rc;
+        return nullptr;
+    }
+    if (err) *err = LO_OK;
+    return b;
+}
+
+void lo_batch_destroy(lo_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (void* p : {static_cast<void*>(b->d_P), static_cast<void*>(b->d_T0), static_cast<void*>(b->d_rec)})
+        if (p) (void)hipFree(p);
+    for (void* p : {static_cast<void*>(b->h_P), static_cast<void*>(b->h_T0), static_cast<void*>(b->h_rec)})
+        if (p) (void)hipHostFree(p);
+    if (b->ev0) (void)hipEventDestroy(b->ev0);
+    if (b->ev1) (void)hipEventDestroy(b->ev1);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+const char* lo_batch_last_error(const lo_batch* b) { return b ? b->err.c_str() : "null batch"; }
+int lo_batch_size(const lo_batch* b) { return b ? static_cast<int>(b->ctx.size()) : 0; }
+
+int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t* n, const float* T_init) {
+    if (!b || !n || !T_init) return LO_ERR_ARG;
+    if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }
+    const int B = static_cast<int>(b->ctx.size());
+    for (int j = 0; j < B; ++j)
+        if (n[j] > static_cast<size_t>(b->ctx[j]->cfg.max_points)) { b->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    LO_BHIP(b, hipSetDevice(b->device));
+    std::memcpy(b->T_in.data(), T_init, sizeof(float) * 12 * B);
+    b->act.clear();
+    int max_nb = 1, max_acc = 1;
+    bool same = true;
+    for (int j = 0; j < B; ++j) {
+        b->n[j] = n[j];
+        if (n[j] == 0) continue;
+        lo_ctx* c = b->ctx[j];
+        const float* pts = (d_pts && d_pts[j]) ? d_pts[j] : c->d_pts;
+        const int a = static_cast<int>(b->act.size());
+        KParams P = make_params(c, pts, static_cast<int>(n[j]));
+        P.T0p = b->d_T0 + 12 * a;
+        max_nb = std::max(max_nb, P.nb);
+        max_acc = std::max(max_acc, P.nb_acc);
+        const lo_batch::Sig sg{pts, P.n, P.tab, P.log2cap};
+        if (a >= static_cast<int>(b->sig.size()) || std::memcmp(&b->sig[a], &sg, sizeof(sg)) != 0) same = false;
+        if (!same) {
+            if (a < static_cast<int>(b->sig.size())) b->sig[a] = sg; else b->sig.push_back(sg);
+        }
+        b->h_P[a] = P;
+        std::memcpy(b->h_T0 + 12 * a, T_init + 12 * j, sizeof(float) * 12);
+        b->act.push_back(j);
+    }
+    const int nact = static_cast<int>(b->act.size());
+    if (static_cast<int>(b->sig.size()) != nact) { same = false; b->sig.resize(nact); }
+    LO_BHIP(b, hipEventRecord(b->ev0, b->stream));
+    if (nact > 0) {
+        LO_BHIP(b, hipMemcpyAsync(b->d_T0, b->h_T0, sizeof(float) * 12 * nact, hipMemcpyHostToDevice, b->stream));
+        if (!same) LO_BHIP(b, hipMemcpyAsync(b->d_P, b->h_P, sizeof(KParams) * nact, hipMemcpyHostToDevice, b->stream));
+        const int pko_wgs = std::max(1, std::min(b->pko_max, b->pko_budget / nact));
+        const size_t pre_bytes = static_cast<size_t>(max_nb) * sizeof(int);
+        const dim3 blk(kBlock);
+        for (int it = 0; it < b->max_iters; ++it) {
+            hipLaunchKernelGGL(k_correspond_b, dim3(max_nb, nact), blk, 0, b->stream, b->d_P, it == 0 ? 1 : 0, it == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_pko_tb<4>, dim3(pko_wgs, nact), dim3(256), pre_bytes, b->stream, b->d_P, it);
+            if (max_acc <= kFuseMaxBlocks) {           // small jobs: one 8-wave workgroup accumulates + solves
+                hipLaunchKernelGGL(k_accumulate_b1, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
+            } else {
+                hipLaunchKernelGGL(k_accumulate_b, dim3(max_acc, nact), blk, 0, b->stream, b->d_P, it);
+                hipLaunchKernelGGL(k_solve_b, dim3(nact), dim3(kSolveThreads), 0, b->stream, b->d_P, it);
+            }
+        }
+        hipLaunchKernelGGL(k_export_batch, dim3(nact), dim3(64), 0, b->stream, b->d_P, b->d_rec);
+        LO_BHIP(b, hipGetLastError());
+        LO_BHIP(b, hipMemcpyAsync(b->h_rec, b->d_rec, sizeof(lo_batch_rec) * nact, hipMemcpyDeviceToHost, b->stream));
+    }
+    LO_BHIP(b, hipEventRecord(b->ev1, b->stream));
+    b->pending = true;
+    return LO_OK;
+}
+
+int lo_batch_result(lo_batch* b, lo_batch_rec* out, double* gpu_ms) {
+    if (!b || !out) return LO_ERR_ARG;
+    if (!b->pending) { b->err = "no batch in flight"; return LO_ERR_STATE; }
+    LO_BHIP(b, hipSetDevice(b->device));
+    LO_BHIP(b, hipStreamSynchronize(b->stream));
+    b->pending = false;
+    const int B = static_cast<int>(b->ctx.size());
+    for (int j = 0; j < B; ++j) {          // skipped jobs: the reference's false on an empty cloud (:593-603)
+        lo_batch_rec& R = out[j];
+        std::memset(&R, 0, sizeof(R));
+        R.status = LO_INSUFFICIENT;
+    }
+    for (size_t a = 0; a < b->act.size(); ++a) out[b->act[a]] = b->h_rec[a];
+    for (int j = 0; j < B; ++j)            // optimized_transform = initial unless the GN loop succeeded (:266, :301)
+        if (out[j].status != LO_OK) std::memcpy(out[j].pose, b->T_in.data() + 12 * j, sizeof(float) * 12);
+    if (gpu_ms) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, b->ev0, b->ev1) != hipSuccess) ms = -1.0f;
+        *gpu_ms = ms;
+    }
+    return LO_OK;
+}
+
+int lo_batch_optimize(lo_batch* b, const float* const* pts, const size_t* n, const float* T_init, lo_batch_rec* out) {
+    if (!b || !pts || !n || !T_init || !out) return LO_ERR_ARG;
+    if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }
+    const int B = static_cast<int>(b->ctx.size());
+    LO_BHIP(b, hipSetDevice(b->device));
+    for (int j = 0; j < B; ++j) {
+        if (n[j] == 0) continue;
+        if (!pts[j]) return LO_ERR_ARG;
+        if (n[j] > static_cast<size_t>(b->ctx[j]->cfg.max_points)) { b->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+        LO_BHIP(b, hipMemcpyAsync(b->ctx[j]->d_pts, pts[j], n[j] * 3 * sizeof(float), hipMemcpyHostToDevice, b->stream));
+    }
+    const int rc = lo_batch_optimize_async(b, nullptr, n, T_init);
+    if (rc != LO_OK) return rc;
+    return lo_batch_result(b, out, nullptr);
 }
 
 }  // extern "C"

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     const int gi = blockIdx.x * kBlock + threadIdx.x;
     const int i = gi / kKnnGroup, g = gi % kKnnGroup;
     float T[12];
-    scan_pose(P, T);
+    scan_pose(P, P.init, blockIdx.x, T);
     if (i >= scan_n(P)) return;                              // whole groups leave together
     int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
     float qx, qy, qz;

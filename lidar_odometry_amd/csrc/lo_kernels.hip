@@ -26,12 +26,12 @@ namespace lo {
 // ====================================================================================================
 // k_correspond
 // ====================================================================================================
-__global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
-    // P.init: first launch of a scan.  The GN state reset (k_init's job) is folded in here -- the pose comes
-    // from the kernel argument, block 0 writes the fresh DevState that the later kernels of the scan read.
-    // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
-    // instead of serialising at the start of every wave.
-    const int i = blockIdx.x * kBlock + threadIdx.x;
+// init: first launch of a scan.  The GN state reset (k_init's job) is folded in here -- the pose comes from
+// the kernel argument (T0 / T0p), block 0 writes the fresh DevState that the later kernels of the scan read.
+// The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
+// instead of serialising at the start of every wave.
+__device__ __forceinline__ void correspond_body(const KParams& P, int with_stats, int init, int blk) {
+    const int i = blk * kBlock + threadIdx.x;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
     if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
@@ -40,8 +40,8 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
-    if (!P.init && done) return;
-    scan_pose(P, T);
+    if (!init && done) return;
+    scan_pose(P, init, blk, T);
     int slot = -1;
     double r = 0.0;
     if (i < n) {
@@ -55,18 +55,83 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
         P.slot[i] = slot;
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
     }
-    corr_epilogue(P, slot >= 0, r, with_stats, blockIdx.x);
+    corr_epilogue(P, slot >= 0, r, with_stats, blk);
+}
+
+__global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
+    correspond_body(P, with_stats, P.init, blockIdx.x);
+}
+
+// Batched launch (lo_batch_*): blockIdx.y = job (one context each: own scan, map and GN state); the grid is
+// sized for the largest job and a job's surplus blocks leave before touching any of its buffers.
+__global__ __launch_bounds__(kBlock) void k_correspond_b(const KParams* __restrict__ PB, int with_stats, int init) {
+    const KParams& P = PB[blockIdx.y];
+    if (static_cast<int>(blockIdx.x) >= P.nb) return;
+    correspond_body(P, with_stats, init, blockIdx.x);
 }
 
 // ====================================================================================================
 // k_accumulate
 // ====================================================================================================
 template <int NT>
-__device__ void solve_tail(const KParams& P, int it, int ne_only);
+__device__ void solve_tail(const KParams& P, int it, int ne_only, const double* part_src, int nrows);
+
+// One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
+// fp32 products fl(fl(w J_i) J_j) as the reference forms them.
+__device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
+                                          float (&acc)[kNE]) {
+    const int s = P.slot[i];
+    if (s < 0) return;
+    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+    const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
+    double r;
+    if (P.kd_res) {
+        r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
+    } else {
+        float wx, wy, wz;
+        transform_pt(T, px, py, pz, wx, wy, wz);
+        r = residual_f64(sl, wx, wy, wz);
+    }
+    const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
+    // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
+    const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
+    const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
+    const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
+    const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
+    const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
+    // J = [n^T R, -n^T R [p]x] (:376-386)
+    float J[6];
+    J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
+    J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
+    J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
+    const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
+    const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
+    const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
+    J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
+    J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
+    J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
+    float w = 1.0f;
+    if (P.robust) {                                                             // :389-404
+        const float an = fabsf(nres);
+        if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
+        else if (an > dl) w = dl / an;
+    }
+    int k = 0;
+#pragma unroll
+    for (int rr = 0; rr < 6; ++rr) {
+        const float wJ = w * J[rr];
+#pragma unroll
+        for (int c = 0; c <= rr; ++c) acc[k++] += wJ * J[c];
+    }
+    const float wr = w * res;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
+    acc[27] += wr * res;
+}
 
 // fuse: 0 = partials only, 1 = the last block to finish also runs the GN solve / update (k_solve's job),
 // 2 = the last block writes the summed normal equations (lo_build_normal_equations)
-__global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fuse) {
+__device__ __forceinline__ void accumulate_body(const KParams& P, int it, int fuse, int blk, int nblk) {
     DevState* st = P.st;
     if (st->done) return;
     __shared__ float s_acc[kWavesPerBlock][kNE];
@@ -77,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
         const double a = P.alpha_given ? P.st->alpha : (P.use_pko ? pko_select_alpha(P) : P.robust_delta);
         if (lane == 0) {
             s_alpha = a;
-            if (blockIdx.x == 0 && !P.alpha_given) P.st->alpha = a;
+            if (blk == 0 && !P.alpha_given) P.st->alpha = a;
         }
     }
     __syncthreads();
@@ -92,55 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
     // grid-stride (at most kAccBlocks blocks): per-thread fp32 sums of <= 4 points at 1M, then the same
     // wave / block trees; the partial count k_solve reduces stays <= kAccBlocks
     const int n = scan_n(P);
-    for (int i = blockIdx.x * kBlock + tid; i < n; i += P.nb_acc * kBlock) {
-        const int s = P.slot[i];
-        if (s < 0) continue;
-        const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
-        const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
-        double r;
-        if (P.kd_res) {
-            r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
-        } else {
-            float wx, wy, wz;
-            transform_pt(T, px, py, pz, wx, wy, wz);
-            r = residual_f64(sl, wx, wy, wz);
-        }
-        const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
-        // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
-        const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
-        const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
-        const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
-        const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
-        const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
-        // J = [n^T R, -n^T R [p]x] (:376-386)
-        float J[6];
-        J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
-        J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
-        J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
-        const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
-        const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
-        const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
-        J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
-        J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
-        J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
-        float w = 1.0f;
-        if (P.robust) {                                                             // :389-404
-            const float an = fabsf(nres);
-            if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
-            else if (an > dl) w = dl / an;
-        }
-        int k = 0;
-#pragma unroll
-        for (int rr = 0; rr < 6; ++rr) {
-            const float wJ = w * J[rr];
-#pragma unroll
-            for (int c = 0; c <= rr; ++c) acc[k++] += wJ * J[c];
-        }
-        const float wr = w * res;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
-        acc[27] += wr * res;
-    }
+    for (int i = blk * kBlock + tid; i < n; i += P.nb_acc * kBlock) acc_point(P, T, scale, dl, i, acc);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) {
         const float v = wave_total(acc[k]);
@@ -151,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
         double v = 0.0;
 #pragma unroll
         for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
-        P.blk_part[static_cast<size_t>(blockIdx.x) * kNE + tid] = v;
+        P.blk_part[static_cast<size_t>(blk) * kNE + tid] = v;
     }
     if (fuse == 0) return;
     // last-block-done: release the partials at agent scope (the 8 XCDs have separate L2s), count arrivals;
@@ -160,12 +177,24 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fu
     __shared__ int s_last;
     __threadfence();
     __syncthreads();
-    if (tid == 0) s_last = (atomicAdd(&st->acc_arrive, 1u) == gridDim.x - 1) ? 1 : 0;
+    if (tid == 0) s_last = (atomicAdd(&st->acc_arrive, 1u) == static_cast<unsigned>(nblk - 1)) ? 1 : 0;
     __syncthreads();
     if (!s_last) return;
     __threadfence();
     if (tid == 0) st->acc_arrive = 0;
-    solve_tail<kBlock>(P, it, fuse == 2);
+    solve_tail<kBlock>(P, it, fuse == 2, P.blk_part, P.nb_acc);
+}
+
+__global__ __launch_bounds__(kBlock) void k_accumulate(KParams P, int it, int fuse) {
+    accumulate_body(P, it, fuse, blockIdx.x, gridDim.x);
+}
+
+// Batched launch for batches with a large job (> kFuseMaxBlocks blocks): blockIdx.y = job, partials only;
+// k_solve_b reduces and solves every job.
+__global__ __launch_bounds__(kBlock) void k_accumulate_b(const KParams* __restrict__ PB, int it) {
+    const KParams& P = PB[blockIdx.y];
+    if (static_cast<int>(blockIdx.x) >= P.nb_acc) return;
+    accumulate_body(P, it, 0, blockIdx.x, P.nb_acc);
 }
 
 // ====================================================================================================
@@ -311,18 +340,20 @@ __device__ void ldlt6_solve(const double* Hin, const double* b, double* x) {
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
+// NT fixes the summation pattern of the nrows x kNE block partials (part_src: global or LDS); the calling block
+// may be larger than NT (its extra threads only join the barriers).
 template <int NT>
-__device__ void solve_tail(const KParams& P, int it, int ne_only) {
+__device__ void solve_tail(const KParams& P, int it, int ne_only, const double* part_src, int nrows) {
     DevState* st = P.st;
     constexpr int kQ = NT / kNE;                     // partial rows per entry (36 for 1024 threads, 9 for 256)
     __shared__ double part[kQ][kNE];
     __shared__ double tot[kNE];
     const int tid = threadIdx.x;
     if (tid < kQ * kNE) {
-        // thread t sums flat entries t, t + kQ*kNE, ... of blk_part[nb_acc][kNE]: coalesced, entry = t % kNE
+        // thread t sums flat entries t, t + kQ*kNE, ... of part_src[nrows][kNE]: coalesced, entry = t % kNE
         const int k = tid % kNE, q = tid / kNE;
-        const double* src = P.blk_part + tid;
-        const int nrow = (P.nb_acc - q + kQ - 1) / kQ;
+        const double* src = part_src + tid;
+        const int nrow = (nrows - q + kQ - 1) / kQ;
         constexpr size_t kStride = static_cast<size_t>(kQ) * kNE;
         double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // 8 independent loads in flight
         int j = 0;
@@ -396,7 +427,69 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only) {
 // Standalone solve over all block partials (lo_bench_kernel; the GN loop fuses it into k_accumulate)
 __global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int ne_only) {
     if (P.st->done) return;
-    solve_tail<kSolveThreads>(P, it, ne_only);
+    solve_tail<kSolveThreads>(P, it, ne_only, P.blk_part, P.nb_acc);
+}
+
+// Batched solve (jobs with more than kFuseMaxBlocks accumulate blocks present): one block per job, with the
+// partial-sum pattern the single-scan path uses for that job's size, so every job stays bit-identical to it.
+__global__ __launch_bounds__(kSolveThreads) void k_solve_b(const KParams* __restrict__ PB, int it) {
+    const KParams& P = PB[blockIdx.x];
+    if (P.st->done) return;
+    if (P.nb_acc <= kFuseMaxBlocks) solve_tail<kBlock>(P, it, 0, P.blk_part, P.nb_acc);
+    else solve_tail<kSolveThreads>(P, it, 0, P.blk_part, P.nb_acc);
+}
+
+// Batched accumulate + solve for small jobs (nb_acc <= kFuseMaxBlocks): ONE workgroup of 8 waves per job walks
+// the job's 256-point blocks two at a time (wave w takes block 2r + w/4, its quarter w%4), so each point, wave
+// sum and per-block fp64 partial is formed exactly as in the multi-block launch; the partials stay in LDS and the
+// same workgroup solves.  No inter-workgroup hand-off: no atomics and no agent-scope fences (whose L2 write-back
+// and invalidate per workgroup dominated the multi-block form once thousands of workgroups were in flight).
+constexpr int kAcc1Threads = 512;
+__global__ __launch_bounds__(kAcc1Threads) void k_accumulate_b1(const KParams* __restrict__ PB, int it) {
+    const KParams& P = PB[blockIdx.y];
+    DevState* st = P.st;
+    if (st->done) return;
+    constexpr int kW = kAcc1Threads / kWave;           // 8 waves = 2 virtual blocks per pass
+    __shared__ float s_acc[kW][kNE];
+    __shared__ double s_part[kFuseMaxBlocks * kNE];
+    __shared__ double s_alpha;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (wid == 0) {
+        const double a = P.use_pko ? pko_select_alpha(P) : P.robust_delta;
+        if (lane == 0) { s_alpha = a; st->alpha = a; }
+    }
+    __syncthreads();
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    const double scale = st->scale;
+    const float dl = static_cast<float>(s_alpha);
+    const int n = scan_n(P), nb = P.nb_acc;
+    for (int vb0 = 0; vb0 < nb; vb0 += kW / kWavesPerBlock) {
+        const int vb = vb0 + wid / kWavesPerBlock;
+        const int i = vb * kBlock + (wid % kWavesPerBlock) * kWave + lane;
+        float acc[kNE];
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
+        if (vb < nb && i < n) acc_point(P, T, scale, dl, i, acc);
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) {
+            const float v = wave_total(acc[k]);
+            if (lane == 0) s_acc[wid][k] = v;
+        }
+        __syncthreads();
+        if (tid < kW / kWavesPerBlock * kNE) {
+            const int q = tid / kNE, k = tid - q * kNE;
+            if (vb0 + q < nb) {
+                double v = 0.0;
+#pragma unroll
+                for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[q * kWavesPerBlock + w][k]);
+                s_part[(vb0 + q) * kNE + k] = v;
+            }
+        }
+        __syncthreads();
+    }
+    solve_tail<kBlock>(P, it, 0, s_part, nb);
 }
 
 // ====================================================================================================
@@ -428,6 +521,20 @@ __global__ void k_export_pose(const DevState* st, float* out) {
     if (t == 13) out[13] = static_cast<float>(st->iter);
     if (t == 14) out[14] = static_cast<float>(st->n_corr);
     if (t == 15) out[15] = 0.0f;
+}
+
+// Batched result export: one record per job (lo_batch_result reads them with one copy).
+__global__ void k_export_batch(const KParams* __restrict__ PB, lo_batch_rec* out) {
+    const DevState* st = PB[blockIdx.x].st;
+    lo_batch_rec& R = out[blockIdx.x];
+    const int t = threadIdx.x;
+    if (t < 12) R.pose[t] = st->pose[t];
+    if (t == 12) R.status = st->status;
+    if (t == 13) R.iterations = st->iter;
+    if (t == 14) R.n_corr = st->n_corr;
+    if (t == 15) R.alpha = st->alpha;
+    if (t == 16) R.initial_cost = st->iter > 0 ? st->logs[0].cost : 0.0f;
+    if (t == 17) R.final_cost = st->iter > 0 ? st->logs[min(st->iter, LO_MAX_ITERS) - 1].cost : 0.0f;
 }
 
 }  // namespace lo

@@ -282,14 +282,15 @@ __device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, cons
     else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
 }
 
+// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices).
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
+__device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G) {
     constexpr int NT = NW * 64;
     DevState* st = P.st;
     if (st->done) return;
     unsigned long long* dbg = nullptr;
 #ifdef LO_PKO_STAMPS
-    if (blockIdx.x == 0) dbg = st->dbg;
+    if (wg == 0) dbg = st->dbg;
 #endif
     LO_STAMP(dbg, 0);
     extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     __shared__ double s_scale, s_mean;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool lead = blockIdx.x == 0;
+    const bool lead = wg == 0;
 
     // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
     if (P.direct_res) {
@@ -446,8 +447,7 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
         s_P[b] = Pr + 1e-10;
     }
     __syncthreads();
-    const int G = gridDim.x;
-    for (int a0 = 1 + blockIdx.x; a0 <= P.NA; a0 += G * kPkoAlphaPerWG) {
+    for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kPkoAlphaPerWG) {
         for (int idx = tid; idx < kPkoAlphaPerWG * 100; idx += NT) {
             const int a = idx / 100, b = idx - a * 100;
             const int ai = a0 + a * G;
@@ -484,7 +484,19 @@ __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
     LO_STAMP(dbg, 6);
 }
 
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
+    pko_body<NW>(P, it, blockIdx.x, gridDim.x);
+}
+
+// Batched launch: blockIdx.y = job, gridDim.x workgroups per job split its alpha grid.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_pko_tb(const KParams* __restrict__ PB, int it) {
+    pko_body<NW>(PB[blockIdx.y], it, blockIdx.x, gridDim.x);
+}
+
 template __global__ void k_pko_t<4>(KParams, int);
+template __global__ void k_pko_tb<4>(const KParams*, int);
 
 // PKO-only entry point: argmin of the JS grid -> DevState::alpha (lo_pko_scale_factor).
 __global__ void k_pko_finish(KParams P) {

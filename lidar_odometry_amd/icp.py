@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import LoConfig, LoIterLog, LoStats, lib
+from ._lib import LoBatchRec, LoConfig, LoIterLog, LoStats, lib
 
 
 @dataclass
@@ -286,3 +286,86 @@ class IterativeClosestPointOptimizer:
         out = np.zeros(max(self._cfg.gmm_sample_size, 1), np.int32)
         k = self._check(lib().lo_pko_sample_indices(self._ctx, n, out.ctypes.data_as(C.POINTER(C.c_int32))))
         return out[:k]
+
+
+@dataclass
+class BatchResult:
+    """One job of a batched optimize: the fields of lo_batch_rec."""
+    success: bool
+    pose: np.ndarray
+    iterations: int
+    n_corr: int
+    initial_cost: float
+    final_cost: float
+    alpha: float
+
+
+class BatchOptimizer:
+    """Scan-parallel optimize on one GPU (lo_batch_*): B independent contexts -- B sequences, each with its own
+    map and GN state -- run IterativeClosestPointOptimizer::optimize in lockstep, one launch per kernel per GN
+    iteration for all of them.  Each job's result equals ``optimizers[j].optimize`` on the same input."""
+
+    def __init__(self, optimizers):
+        self.optimizers = list(optimizers)
+        arr = (C.c_void_p * len(self.optimizers))(*[o.ctx for o in self.optimizers])
+        err = C.c_int(0)
+        self._b = lib().lo_batch_create(arr, len(self.optimizers), C.byref(err))
+        if not self._b:
+            raise RuntimeError(f"lo_batch_create failed (code {err.value})")
+        self.last_gpu_ms = 0.0
+
+    def close(self):
+        if getattr(self, "_b", None):
+            lib().lo_batch_destroy(self._b)
+            self._b = None
+
+    def __del__(self):
+        self.close()
+
+    def __len__(self):
+        return len(self.optimizers)
+
+    def _check(self, rc):
+        if rc < 0:
+            raise RuntimeError(f"liblo_icp batch error {rc}: {lib().lo_batch_last_error(self._b).decode()}")
+        return rc
+
+    @staticmethod
+    def _results(recs):
+        out = []
+        for r in recs:
+            out.append(BatchResult(r.status == _lib.LO_OK, pose34(np.ctypeslib.as_array(r.pose).copy()),
+                                   r.iterations, r.n_corr, r.initial_cost, r.final_cost, r.alpha))
+        return out
+
+    def optimize(self, voxel_maps, scans, initial_transforms):
+        """Host scans in; returns one BatchResult per job.  voxel_maps (nullable entries) are synced per context."""
+        B = len(self.optimizers)
+        if voxel_maps is not None:
+            for o, vm in zip(self.optimizers, voxel_maps):
+                o._sync_map(vm)
+        pts = [_as_pts(p) for p in scans]
+        if len(pts) != B:
+            raise ValueError(f"need {B} scans")
+        T = np.ascontiguousarray(np.stack([_as_pose(t) for t in initial_transforms]), dtype=np.float32)
+        ptrs = (C.c_void_p * B)(*[p.ctypes.data for p in pts])
+        ns = (C.c_size_t * B)(*[len(p) for p in pts])
+        recs = (LoBatchRec * B)()
+        self._check(lib().lo_batch_optimize(self._b, ptrs, ns, _fptr(T), recs))
+        return self._results(recs)
+
+    def optimize_async(self, device_ptrs, counts, initial_transforms):
+        """Device-resident scans (int device pointers, or 0 for the context's last uploaded scan)."""
+        B = len(self.optimizers)
+        self._T = np.ascontiguousarray(np.asarray(initial_transforms, dtype=np.float32).reshape(B, 12))
+        ptrs = (C.c_void_p * B)(*[int(p) if p else None for p in device_ptrs])
+        ns = (C.c_size_t * B)(*[int(n) for n in counts])
+        self._check(lib().lo_batch_optimize_async(self._b, ptrs, ns, _fptr(self._T)))
+
+    def result(self):
+        B = len(self.optimizers)
+        recs = (LoBatchRec * B)()
+        ms = C.c_double(0.0)
+        self._check(lib().lo_batch_result(self._b, recs, C.byref(ms)))
+        self.last_gpu_ms = ms.value
+        return self._results(recs)

@@ -1,0 +1,149 @@
+"""GPU tests of the scan-parallel batch (lo_batch_*): B independent contexts advanced in lockstep.
+
+Bar: every job's result is bit-identical to the same context running lo_icp_optimize alone on the same input
+(same kernels, same per-job fixed-order reductions), and within the north-star tolerance of the CPU oracle.
+Covers heterogeneous jobs (different maps, voxel sizes, scan sizes), insufficient / empty jobs, the cached
+parameter path (repeat call), a re-pointed scan, and the argument checks.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+
+TOL_T = 1e-4
+TOL_R = 1e-4
+
+
+def _ctx(m, voxel=0.5, max_points=1 << 16):
+    from lidar_odometry_amd import IterativeClosestPointOptimizer, MapGeometry
+    o = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=voxel), max_points=max_points)
+    if m is not None:
+        k, n, c = _data.surfels(m)
+        o.set_surfels(k, n, c)
+    return o
+
+
+def _jobs():
+    """(map, voxel, points, T_init) for a heterogeneous batch."""
+    jobs = []
+    for f in (11, 13, 17, 21, 25, 31):
+        m, pts, Ti, _ = _data.kitti_case(f)
+        jobs.append((m, 0.5, pts, Ti))
+    m, pts, Ti, _ = _data.mid360_case()
+    jobs.append((m, 0.4, pts, Ti))
+    m, pts, Ti, _ = _data.kitti_case(19, seed=5, sigma_t=0.3, sigma_r=0.03)     # large perturbation
+    jobs.append((m, 0.5, pts, Ti))
+    m, pts, Ti, _ = _data.kitti_case(11)
+    jobs.append((m, 0.5, pts + np.float32(5000.0), Ti))                         # insufficient correspondences
+    jobs.append((m, 0.5, pts[:0], Ti))                                          # empty cloud
+    return jobs
+
+
+def _singles(ctxs, jobs):
+    out = []
+    for o, (_, _, pts, Ti) in zip(ctxs, jobs):
+        ok, To = o.optimize(None, pts, Ti)
+        st = o.get_last_stats()
+        out.append((ok, To.reshape(12).copy(), st.num_iterations, st.num_correspondences,
+                    st.iterations[-1]["alpha"] if st.iterations else None))
+    return out
+
+
+def _check_equal(res, singles):
+    for j, (r, s) in enumerate(zip(res, singles)):
+        ok, To, it, nc, alpha = s
+        assert r.success == ok, f"job {j}: success {r.success} vs single {ok}"
+        np.testing.assert_array_equal(r.pose.reshape(12), To, err_msg=f"job {j}")
+        if ok:
+            assert r.iterations == it, f"job {j}: iterations {r.iterations} vs {it}"
+            assert r.n_corr == nc, f"job {j}: n_corr {r.n_corr} vs {nc}"
+            assert r.alpha == alpha, f"job {j}: alpha {r.alpha} vs {alpha}"
+
+
+def test_batch_heterogeneous_bitwise_vs_single():
+    from lidar_odometry_amd import BatchOptimizer
+    jobs = _jobs()
+    ctxs = [_ctx(m, v) for (m, v, _, _) in jobs]
+    try:
+        singles = _singles(ctxs, jobs)
+        b = BatchOptimizer(ctxs)
+        try:
+            res = b.optimize(None, [j[2] for j in jobs], [j[3] for j in jobs])
+            _check_equal(res, singles)
+            assert [r.success for r in res[-2:]] == [False, False]
+            np.testing.assert_array_equal(res[-1].pose.reshape(12), jobs[-1][3])   # T_out = T_init on failure
+            # same inputs again: the cached KParams path gives the same bits
+            res2 = b.optimize(None, [j[2] for j in jobs], [j[3] for j in jobs])
+            for r, r2 in zip(res, res2):
+                np.testing.assert_array_equal(r.pose, r2.pose)
+            # the oracle agrees with every successful job within the north-star tolerance
+            for j, (m, _, pts, Ti) in enumerate(jobs):
+                if not res[j].success:
+                    continue
+                ok_o, To_o, it_o, _ = oracle.icp_optimize(m, pts, Ti)
+                assert ok_o and it_o == res[j].iterations
+                A = res[j].pose.astype(np.float64)
+                B = np.asarray(To_o, np.float64).reshape(3, 4)
+                assert np.linalg.norm(A[:, 3] - B[:, 3]) <= TOL_T
+                assert _data.rot_angle(A[:, :3], B[:, :3]) <= TOL_R
+        finally:
+            b.close()
+    finally:
+        for o in ctxs:
+            o.close()
+
+
+def test_batch_many_jobs_and_repointed_scans():
+    """64 jobs (fewer PKO workgroups per job than a single scan gets), then every job re-pointed at another scan."""
+    from lidar_odometry_amd import BatchOptimizer
+    frames = [11, 13, 15, 17, 19, 21, 23, 25]
+    cases = [_data.kitti_case(f) for f in frames]
+    m = cases[0][0]
+    ctxs = [_ctx(m) for _ in range(64)]
+    try:
+        b = BatchOptimizer(ctxs)
+        try:
+            for shift in (0, 3):
+                sel = [cases[(j + shift) % len(cases)] for j in range(64)]
+                res = b.optimize(None, [c[1] for c in sel], [c[2] for c in sel])
+                ref = {}
+                for j, c in enumerate(sel[:len(cases)]):
+                    ok, To = ctxs[j].optimize(None, c[1], c[2])
+                    ref[j % len(cases)] = (ok, To.reshape(12).copy())
+                for j, r in enumerate(res):
+                    ok, To = ref[j % len(cases)]
+                    assert r.success == ok
+                    np.testing.assert_array_equal(r.pose.reshape(12), To, err_msg=f"job {j} shift {shift}")
+        finally:
+            b.close()
+    finally:
+        for o in ctxs:
+            o.close()
+
+
+def test_batch_argument_checks():
+    from lidar_odometry_amd import BatchOptimizer, ICPConfig, IterativeClosestPointOptimizer
+    a = _ctx(None, max_points=1024)
+    kd = IterativeClosestPointOptimizer(config=ICPConfig(use_surfel_correspondence=False), max_points=1024)
+    try:
+        with pytest.raises(RuntimeError):
+            BatchOptimizer([a, a])             # a context twice
+        with pytest.raises(RuntimeError):
+            BatchOptimizer([a, kd])            # KDTree-mode context
+        b = BatchOptimizer([a])
+        try:
+            with pytest.raises(RuntimeError):
+                b.result()                     # nothing in flight
+            big = np.zeros((2048, 3), np.float32)
+            with pytest.raises(RuntimeError):
+                b.optimize(None, [big], [np.eye(3, 4, dtype=np.float32)])   # exceeds max_points
+            res = b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
+            assert not res[0].success          # empty map: no correspondences
+        finally:
+            b.close()
+    finally:
+        a.close()
+        kd.close()
