@@ -156,6 +156,38 @@ def cpu_baseline(wl, budget_s: float):
                       f"(oracle/liblo_oracle.so, single thread, g++ -O3, same synthetic inputs)"}
 
 
+def cpu_baseline_replicas(wl, budget_s: float, threads: int):
+    """The fair CPU comparator for the batched (multi-sequence) number: `threads` independent
+    replicas of the single-thread oracle ICP, one per core, each with its own map copy and scan stream.  The oracle
+    is a C library called through ctypes (GIL released during the call), so Python threads run it in parallel."""
+    import concurrent.futures as cf
+
+    import oracle
+    scans, inits = wl["scans"], [pose12(T) for T in wl["inits"]]
+
+    def replica(r):
+        m = oracle.VoxelMap(wl["voxel"], 3, 0.1, True)
+        for w, s in wl["keyframes"]:
+            m.update(w, s, wl["max_dist"], True)
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            i = (n + 7 * r) % len(scans)
+            oracle.icp_optimize(m, scans[i], inits[i])
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                return n, el
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(replica, range(threads)))
+    n = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": n / el, "unit": "scans/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} concurrent single-thread oracle replicas (own map each), {n} optimize() calls in "
+                      f"{el:.1f} s on the GPU box's host cores"}
+
+
 def read_pmc_traffic(workload_key: str):
     """HBM bytes per k_correspond launch from a committed rocprofv3 PMC summary (profiles/), if present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -311,7 +343,7 @@ def main():
     ap.add_argument("--sequences", type=int, default=8,
                     help="extra measurement: independent sequences sharing this GPU, one context + HIP stream each "
                          "(0 = skip); reported as multi_sequence, never as value")
-    ap.add_argument("--batch", type=str, default="64,256",
+    ap.add_argument("--batch", type=str, default="64,256,512,1024",
                     help="extra measurement: comma list of B for the scan-parallel batch (lo_batch_*: B independent "
                          "contexts advanced in lockstep, one launch per kernel per GN iteration); '' = skip; "
                          "reported as batched, never as value")
@@ -497,6 +529,7 @@ def main():
     sizes = [int(x) for x in args.batch.split(",") if x.strip()] if (world == 1 and not kd and not raw) else []
     if sizes:
         from lidar_odometry_amd import BatchOptimizer
+        from lidar_odometry_amd._lib import LoBatchRec
         batched = {"unit": "scans/s", "runs": [],
                    "note": "B independent sequences on one GPU (one context each: own map copy, scan, GN state), "
                            "advanced in lockstep by lo_batch_optimize_async; aggregate throughput, not value"}
@@ -509,23 +542,32 @@ def main():
                 pool.append(o)
             bo = BatchOptimizer(pool[:B])
             K3 = max(20, min(args.steps // 4, 100))
-            sel = lambda k: [(k + 7 * j) % len(d_scans) for j in range(B)]     # noqa: E731
-            ptrs = [[d_scans[i].data_ptr() for i in sel(k)] for k in range(len(d_scans))]
-            cnts = [[d_scans[i].shape[0] for i in sel(k)] for k in range(len(d_scans))]
-            Ts = [np.stack([inits[i] for i in sel(k)]) for k in range(len(d_scans))]
+            # the C ABI directly (what a C++ caller does): per distinct step, the device pointers, counts and
+            # initial poses are prepared once; the timed loop is enqueue + wait, records into a fixed array
+            nd = len(d_scans)
+            sel = [[(q + 7 * j) % nd for j in range(B)] for q in range(nd)]
+            c_ptrs = [(C.c_void_p * B)(*[d_scans[i].data_ptr() for i in sel[q]]) for q in range(nd)]
+            c_cnts = [(C.c_size_t * B)(*[d_scans[i].shape[0] for i in sel[q]]) for q in range(nd)]
+            c_T = [np.ascontiguousarray(np.stack([inits[i] for i in sel[q]])) for q in range(nd)]
+            recs = (LoBatchRec * B)()
+            ms = C.c_double(0.0)
+
+            def batch_step(k):
+                q = k % nd
+                rc = L.lo_batch_optimize_async(bo._b, c_ptrs[q], c_cnts[q], fptr(c_T[q]))
+                rc2 = L.lo_batch_result(bo._b, recs, C.byref(ms))
+                if rc != 0 or rc2 != 0:
+                    raise RuntimeError(f"lo_batch rc={rc}/{rc2}: {L.lo_batch_last_error(bo._b).decode()}")
+                return ms.value
             for k in range(5):
-                bo.optimize_async(ptrs[k % len(d_scans)], cnts[k % len(d_scans)], Ts[k % len(d_scans)])
-                res = bo.result()
+                batch_step(k)
             dev_ms = []
             t3 = time.perf_counter()
             for k in range(K3):
-                q = k % len(d_scans)
-                bo.optimize_async(ptrs[q], cnts[q], Ts[q])
-                res = bo.result()
-                dev_ms.append(bo.last_gpu_ms)
+                dev_ms.append(batch_step(k))
             el3 = time.perf_counter() - t3
-            n_it = sum(iters[(k + 7 * j) % len(d_scans)] for k in range(K3) for j in range(B))
-            ok = sum(r.success for r in res)
+            n_it = sum(iters[(k % nd + 7 * j) % nd] for k in range(K3) for j in range(B))
+            ok = sum(r.status == 0 for r in recs)
             batched["runs"].append({"sequences": B, "value": B * K3 / el3, "gn_iters_per_sec": n_it / el3,
                                     "batches": K3, "ms_per_batch": el3 / K3 * 1e3,
                                     "device_ms_per_batch": float(np.mean(dev_ms)), "ok_last_batch": int(ok)})
@@ -533,6 +575,10 @@ def main():
                 f"(device {np.mean(dev_ms):.3f} ms)")
             bo.close()
         batched["value"] = max(r["value"] for r in batched["runs"])
+        if rank == 0 and not args.no_cpu_baseline:
+            thr = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+            batched["cpu_baseline"] = cpu_baseline_replicas(wl, args.cpu_budget / 2, thr)
+            batched["speedup_vs_cpu_replicas"] = batched["value"] / batched["cpu_baseline"]["value"]
         for o in pool:
             o.close()
 

@@ -25,7 +25,6 @@ constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kNE = 28;              // 21 lower-triangular H + 6 g + cost
 constexpr int kPkoBlock = 256;       // PKO workgroup: one GMM sample per thread (S <= 256)
 constexpr int kPkoMaxWGs = 128;      // PKO workgroups per launch (each evaluates a slice of the alpha grid)
-constexpr int kPkoAlphaPerWG = 4;    // alphas per JS pass of one workgroup
 constexpr int kMaxBlocks = 16384;    // => max 4M points per scan
 constexpr int kAccBlocks = 1024;     // k_accumulate grid cap (grid-stride beyond): bounds the k_solve partial sum
 constexpr int kSolveThreads = 1024;  // k_solve: 36 x 28 threads sum the block partials, coalesced

@@ -946,7 +946,7 @@ int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {
 // (blockIdx.y = job).  The per-job KParams live in device memory (the batched kernels read them with scalar
 // loads); they are rebuilt on the host every call but uploaded only when a job's scan pointer, size or map
 // table changed.  The initial poses travel in a separate 12-float-per-job array (KParams::T0p).
-static constexpr int kBatchPkoWGs = 2048;   // PKO workgroups per launch over all jobs (>= 1 per job)
+static constexpr int kBatchPkoWGs = 256;    // PKO workgroups per launch over all jobs (>= 1 per job; measured best)
 
 struct lo_batch {
     std::vector<lo_ctx*> ctx;

@@ -299,7 +299,6 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     __shared__ double s_P[100];
     __shared__ double s_p[2 * kMaxK * 64 * NW];          // EM: per-sample pdf of each component, double-buffered
     __shared__ double s_dm[2 * kMaxK];
-    __shared__ double s_jsd[kPkoAlphaPerWG][100];
     __shared__ int s_iscan[NW];
     __shared__ double s_dscan[NW];
     __shared__ int s_nc;
@@ -447,8 +446,12 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
         s_P[b] = Pr + 1e-10;
     }
     __syncthreads();
-    for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kPkoAlphaPerWG) {
-        for (int idx = tid; idx < kPkoAlphaPerWG * 100; idx += NT) {
+    // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
+    // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25)
+    constexpr int kJsPass = (2 * kMaxK * 64 * NW) / 100;
+    double* s_jsd = s_p;
+    for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kJsPass) {
+        for (int idx = tid; idx < kJsPass * 100; idx += NT) {
             const int a = idx / 100, b = idx - a * 100;
             const int ai = a0 + a * G;
             if (ai > P.NA) continue;
@@ -458,17 +461,18 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
             const double Pr = s_P[b];
             const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
             const double M = 0.5 * (Pr + Q);
-            s_jsd[a][b] = 0.5 * (Pr * log(Pr / M) + Q * log(Q / M));
+            s_jsd[idx] = 0.5 * (Pr * log(Pr / M) + Q * log(Q / M));
         }
         __syncthreads();
-        if (tid < kPkoAlphaPerWG) {
+        if (tid < kJsPass) {
             const int ai = a0 + tid * G;
             if (ai <= P.NA) {
                 double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
+                const double* row = s_jsd + tid * 100;
                 for (int b0 = 0; b0 < 100; b0 += 10) {           // batched LDS reads, then the serial adds
                     double vb[10];
 #pragma unroll
-                    for (int q = 0; q < 10; ++q) vb[q] = s_jsd[tid][b0 + q];
+                    for (int q = 0; q < 10; ++q) vb[q] = row[b0 + q];
 #pragma unroll
                     for (int q = 0; q < 10; ++q) {
                         const bool ok = !isnan(vb[q]);
