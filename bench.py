@@ -534,6 +534,11 @@ def main():
                    "note": "B independent sequences on one GPU (one context each: own map copy, scan, GN state), "
                            "advanced in lockstep by lo_batch_optimize_async; aggregate throughput, not value"}
         pool = []
+        # per distinct scan: algorithmic bytes of one correspondence pass at its initial pose (as alg_bytes above)
+        scan_bytes = []
+        for i in range(len(d_scans)):
+            nv, _, _ = icp.find_correspondences(wl["scans"][i], inits[i])
+            scan_bytes.append(len(wl["scans"][i]) * (12 + 8 + 4 + 0.125) + 24 * nv)
         for B in sizes:
             while len(pool) < B:
                 o = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
@@ -571,6 +576,19 @@ def main():
             batched["runs"].append({"sequences": B, "value": B * K3 / el3, "gn_iters_per_sec": n_it / el3,
                                     "batches": K3, "ms_per_batch": el3 / K3 * 1e3,
                                     "device_ms_per_batch": float(np.mean(dev_ms)), "ok_last_batch": int(ok)})
+            # batched correspondence kernel vs the HBM roofline: algorithmic bytes of all B jobs per launch
+            cms = C.c_float(0.0)
+            q = (K3 - 1) % nd
+            assert L.lo_batch_optimize_async(bo._b, c_ptrs[q], c_cnts[q], fptr(c_T[q])) == 0
+            assert L.lo_batch_result(bo._b, recs, C.byref(ms)) == 0
+            assert L.lo_batch_bench_correspond(bo._b, 50, C.byref(cms)) == 0
+            bbytes = sum(scan_bytes[i] for i in sel[q])
+            ach = bbytes / (cms.value * 1e-3) / 1e9
+            batched["runs"][-1]["roofline"] = {"kernel": "k_correspond_b", "bound": "hbm", "achieved": ach,
+                                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                                               "kernel_us": cms.value * 1e3, "alg_bytes_per_launch": bbytes,
+                                               "points_per_launch": int(sum(d_scans[i].shape[0] for i in sel[q])),
+                                               "traffic": read_pmc_traffic(f"{args.config}_batch{B}")}
             log(f"[batch] B={B}: {B * K3 / el3:.0f} scans/s, {el3 / K3 * 1e3:.3f} ms/batch "
                 f"(device {np.mean(dev_ms):.3f} ms)")
             bo.close()

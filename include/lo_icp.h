@@ -164,6 +164,10 @@ int         lo_batch_size(const lo_batch* b);
 int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t* n, const float* T_init);
 /* Waits for the batch; out[count] receives one record per job.  Returns LO_OK or a negative error. */
 int lo_batch_result(lo_batch* b, lo_batch_rec* out, double* gpu_ms);
+/* Timing harness: reps back-to-back launches of the batched correspondence kernel over the last batch's jobs at
+ * their initial poses (after one resetting launch); writes the average device time per launch (HIP events).
+ * Leaves every job's GN state at its initial pose. */
+int lo_batch_bench_correspond(lo_batch* b, int reps, float* avg_ms);
 /* Host points in, records out (H2D of every scan on the batch stream, enqueue, wait). */
 int lo_batch_optimize(lo_batch* b, const float* const* pts, const size_t* n, const float* T_init, lo_batch_rec* out);
 

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
     "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
-    "lo_batch_result", "lo_batch_optimize",
+    "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
     # include/lo_map.h
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
@@ -174,6 +174,7 @@ def lib():
     L.lo_batch_size.argtypes = [vp]
     L.lo_batch_optimize_async.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), fp]
     L.lo_batch_result.argtypes = [vp, C.POINTER(LoBatchRec), dp]
+    L.lo_batch_bench_correspond.argtypes = [vp, C.c_int, fp]
     L.lo_batch_optimize.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t), fp, C.POINTER(LoBatchRec)]
     L.lo_voxelmap_create.restype = vp
     L.lo_voxelmap_create.argtypes = [C.c_float, C.c_int, C.c_float, C.c_int]

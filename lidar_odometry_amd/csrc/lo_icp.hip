@@ -1132,6 +1132,28 @@ int lo_batch_result(lo_batch* b, lo_batch_rec* out, double* gpu_ms) {
     return LO_OK;
 }
 
+int lo_batch_bench_correspond(lo_batch* b, int reps, float* avg_ms) {
+    if (!b || reps < 1 || !avg_ms) return LO_ERR_ARG;
+    if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }
+    const int nact = static_cast<int>(b->act.size());
+    if (nact == 0) { b->err = "no batch has run yet"; return LO_ERR_STATE; }
+    LO_BHIP(b, hipSetDevice(b->device));
+    int max_nb = 1;
+    for (int a = 0; a < nact; ++a) max_nb = std::max(max_nb, b->h_P[a].nb);
+    const dim3 grid(max_nb, nact), blk(kBlock);
+    // every job back at its initial pose with a fresh GN state (init launch), then reps plain launches
+    hipLaunchKernelGGL(k_correspond_b, grid, blk, 0, b->stream, b->d_P, 1, 1);
+    LO_BHIP(b, hipEventRecord(b->ev0, b->stream));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_correspond_b, grid, blk, 0, b->stream, b->d_P, 0, 0);
+    LO_BHIP(b, hipEventRecord(b->ev1, b->stream));
+    LO_BHIP(b, hipGetLastError());
+    LO_BHIP(b, hipEventSynchronize(b->ev1));
+    float ms = 0.0f;
+    LO_BHIP(b, hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    *avg_ms = ms / reps;
+    return LO_OK;
+}
+
 int lo_batch_optimize(lo_batch* b, const float* const* pts, const size_t* n, const float* T_init, lo_batch_rec* out) {
     if (!b || !pts || !n || !T_init || !out) return LO_ERR_ARG;
     if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }

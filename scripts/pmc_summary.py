@@ -32,7 +32,8 @@ def per_launch(pass_dir: str, counter: str, kernel: str, min_run: int = 20):
                 name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
                 rows.append((int(row["Dispatch_Id"]), name, float(row["Counter_Value"])))
     rows.sort()
-    allv = [v for _, n, v in rows if kernel in n]
+    match = lambda n: (kernel + "(") in n or (kernel + "<") in n   # noqa: E731  (k_correspond vs k_correspond_b)
+    allv = [v for _, n, v in rows if match(n)]
     if not allv:
         raise SystemExit(f"no {counter} rows for {kernel} in {pass_dir}")
     iso, i = [], 0
@@ -40,7 +41,7 @@ def per_launch(pass_dir: str, counter: str, kernel: str, min_run: int = 20):
         j = i
         while j < len(rows) and rows[j][1] == rows[i][1]:
             j += 1
-        if kernel in rows[i][1] and j - i >= min_run:
+        if match(rows[i][1]) and j - i >= min_run:
             iso.extend(v for _, _, v in rows[i:j])
         i = j
     mean = lambda v: sum(v) / len(v) if v else float("nan")   # noqa: E731
@@ -60,7 +61,8 @@ def main():
     w_kib, nw, w_all, nwa = per_launch(a.write, "WRITE_SIZE", a.kernel)
     entry = {
         "kernel": a.kernel,
-        "launches": "isolated back-to-back launches (bench.py lo_bench_kernel phase, the ones kernel_us times)",
+        "launches": "isolated back-to-back launches (bench.py lo_bench_kernel / lo_batch_bench_correspond phase, "
+                    "the ones kernel_us times)",
         "isolated_launches_fetch_pass": nf, "isolated_launches_write_pass": nw,
         "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
         "fetch_bytes_corrected": 2.0 * f_kib * 1024.0,
