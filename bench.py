@@ -392,9 +392,9 @@ def main():
     d_raw = [torch.from_numpy(r).to(dev) for r in wl["raw_scans"]] if raw else None
     inits = [pose12(T) for T in wl["inits"]]
     fptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))   # noqa: E731
-    from lidar_odometry_amd.parallel import RECORD_FLOATS, PoseAllGather
-    pose_rec = torch.zeros(RECORD_FLOATS, dtype=torch.float32, device=dev)
-    gather = PoseAllGather(world, dev)          # scan-parallel replicas: the only collective (RCCL)
+    from lidar_odometry_amd.parallel import PipelinedPoseGather
+    # scan-parallel replicas: the only collective is the per-step pose all-gather (RCCL), on a side stream
+    gather = PipelinedPoseGather(world, dev)
 
     def step(k):
         i = k % len(d_scans)
@@ -406,8 +406,8 @@ def main():
         if rc != 0:
             raise RuntimeError(f"lo_icp_optimize_async rc={rc}: {L.lo_last_error(icp.ctx).decode()}")
         if world > 1:
-            L.lo_icp_export_pose(icp.ctx, C.c_void_p(pose_rec.data_ptr()))
-            gather(pose_rec)
+            L.lo_icp_export_pose(icp.ctx, C.c_void_p(gather.slot().data_ptr()))
+            gather.launch()
 
     # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them)
     iters, errs = [], []
@@ -618,7 +618,7 @@ def main():
                    "distinct_scans": len(wl["scans"]), "map_surfels": wl["vm"].surfel_count(),
                    "map_l0_points": wl["vm"].l0_count(), "correspondence": "kdtree 5-NN" if kd else "L1 surfel",
                    "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),
-                   "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step)" if world > 1
+                   "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step, side stream)" if world > 1
                    else "single GPU, one HIP stream"},
         "gn_iters_per_sec": total_iters / el,
         "translation_error_vs_gt_m_median": float(np.median(errs)),

@@ -53,6 +53,65 @@ class PoseAllGather:
         return self.out
 
 
+class PipelinedPoseGather:
+    """The per-step pose all-gather taken off the critical path: step k's record is exported into ring slot
+    k % depth and gathered on a side stream, so the next scans' ICP kernels on the main stream do not wait for
+    the collective (a ~220 us KITTI scan would otherwise pay the collective's latency every step).  The main
+    stream only waits when it is about to overwrite a slot whose gather has not finished (depth steps later).
+    On CPU tensors (gloo) there are no streams and the gather runs in place.
+
+        rec = pg.slot()          # export this step's record into rec (on the main stream)
+        pg.launch()              # gather it on the side stream
+        ...
+        pg.drain(); pg.records(k)   # [world, 16] of step k (valid for the last `depth` steps)"""
+
+    def __init__(self, world: int, device=None, depth: int = 4):
+        import torch
+        self.world, self.depth, self.k = world, depth, 0
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.recs = torch.zeros(depth, RECORD_FLOATS, dtype=torch.float32, device=dev)
+        self.outs = torch.zeros(depth, RECORD_FLOATS * world, dtype=torch.float32, device=dev)
+        self.cuda = dev.type == "cuda"
+        self.side = torch.cuda.Stream(dev) if (self.cuda and world > 1) else None
+        self.done = [None] * depth
+
+    def slot(self):
+        import torch
+        i = self.k % self.depth
+        if self.done[i] is not None:
+            torch.cuda.current_stream(self.recs.device).wait_event(self.done[i])
+        return self.recs[i]
+
+    def launch(self):
+        i = self.k % self.depth
+        self.k += 1
+        if self.world == 1:
+            self.outs[i].copy_(self.recs[i])
+            return
+        import torch
+        import torch.distributed as dist
+        if self.side is None:
+            dist.all_gather_into_tensor(self.outs[i], self.recs[i])
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.recs.device))
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ev)
+            dist.all_gather_into_tensor(self.outs[i], self.recs[i])
+            d = torch.cuda.Event()
+            d.record(self.side)
+            self.done[i] = d
+
+    def drain(self):
+        if self.side is not None:
+            self.side.synchronize()
+
+    def records(self, step: int) -> np.ndarray:
+        if not (self.k - self.depth <= step < self.k):
+            raise IndexError(f"step {step} is not in the ring (steps {self.k - self.depth}..{self.k - 1})")
+        return self.outs[step % self.depth].detach().cpu().numpy().reshape(self.world, RECORD_FLOATS)
+
+
 def make_record(ok: bool, T34, iterations: int, n_corr: int) -> np.ndarray:
     """Host-side record in lo_icp_export_pose's layout (status: 0 = LO_OK, 1 = LO_INSUFFICIENT)."""
     r = np.zeros(RECORD_FLOATS, np.float32)

@@ -50,7 +50,21 @@ def _worker(rank, world, port, q):
             return parallel.make_record(ok, To, it, logs[0]["n_corr"] if logs else 0)
 
         recs = parallel.run_replicas(one, len(FRAMES), rank, world)
-        q.put((rank, recs))
+        # the pipelined (ring) gather over the same steps: every step's gathered records equal the plain gather's
+        import torch
+        pg = parallel.PipelinedPoseGather(world, depth=2)
+        piped = np.zeros_like(recs)
+        for st in range(parallel.steps_for(len(FRAMES), world)):
+            k = parallel.scan_of(st, rank, world)
+            pg.slot().copy_(torch.as_tensor(one(min(k, len(FRAMES) - 1))))
+            pg.launch()
+            pg.drain()
+            g = pg.records(st)
+            for r in range(world):
+                kk = parallel.scan_of(st, r, world)
+                if kk < len(FRAMES):
+                    piped[kk] = g[r]
+        q.put((rank, recs, piped))
     finally:
         dist.destroy_process_group()
 
@@ -70,6 +84,20 @@ def test_single_rank_no_process_group():
     assert g(t) is t
 
 
+def test_pipelined_gather_single_rank_ring():
+    import torch
+    pg = parallel.PipelinedPoseGather(1, depth=3)
+    for k in range(7):
+        pg.slot().fill_(float(k))
+        pg.launch()
+    pg.drain()
+    for k in range(4, 7):
+        assert (pg.records(k) == k).all()
+    with pytest.raises(IndexError):
+        pg.records(3)
+    assert torch.is_tensor(pg.slot())
+
+
 def test_scan_parallel_gloo_world2():
     ref = _records_single()
     ctx = mp.get_context("spawn")
@@ -80,8 +108,9 @@ def test_scan_parallel_gloo_world2():
         p.start()
     res = {}
     for _ in procs:
-        r, recs = q.get(timeout=300)
+        r, recs, piped = q.get(timeout=300)
         res[r] = recs
+        np.testing.assert_array_equal(piped, recs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
