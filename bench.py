@@ -343,7 +343,7 @@ def main():
     ap.add_argument("--sequences", type=int, default=8,
                     help="extra measurement: independent sequences sharing this GPU, one context + HIP stream each "
                          "(0 = skip); reported as multi_sequence, never as value")
-    ap.add_argument("--batch", type=str, default="64,256,512,1024",
+    ap.add_argument("--batch", type=str, default="64,256,1024,2048,4096",
                     help="extra measurement: comma list of B for the scan-parallel batch (lo_batch_*: B independent "
                          "contexts advanced in lockstep, one launch per kernel per GN iteration); '' = skip; "
                          "reported as batched, never as value")
@@ -356,6 +356,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # one rank per GPU; more ranks than GPUs (a rehearsal on a small box) wrap around
+    local %= max(1, torch.cuda.device_count())
     if world > 1:
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)

@@ -33,7 +33,7 @@ __global__ void k_knn_brute(KParams P);
 __global__ void k_plane(KParams P, int with_stats);
 __global__ void k_inlier(KParams P);
 __global__ void k_correspond_b(const KParams* PB, int with_stats, int init);
-template <int NW> __global__ void k_pko_tb(const KParams* PB, int it);
+template <int NW, bool ONE_WAVE> __global__ void k_pko_tb(const KParams* PB, int it);
 __global__ void k_accumulate_b(const KParams* PB, int it);
 __global__ void k_accumulate_b1(const KParams* PB, int it);
 __global__ void k_solve_b(const KParams* PB, int it);
@@ -947,6 +947,7 @@ int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {
 // loads); they are rebuilt on the host every call but uploaded only when a job's scan pointer, size or map
 // table changed.  The initial poses travel in a separate 12-float-per-job array (KParams::T0p).
 static constexpr int kBatchPkoWGs = 256;    // PKO workgroups per launch over all jobs (>= 1 per job; measured best)
+static constexpr int kBatchOneWaveMin = 2048; // from this many jobs, PKO is one single-wave workgroup per job (measured)
 
 struct lo_batch {
     std::vector<lo_ctx*> ctx;
@@ -954,6 +955,7 @@ struct lo_batch {
     int max_iters = 0;
     int pko_max = 1;                 // min over contexts of the single-scan PKO grid
     int pko_budget = kBatchPkoWGs;   // PKO workgroups per launch over all jobs (LO_BATCH_PKO_WGS overrides)
+    int one_wave_min = kBatchOneWaveMin;   // jobs from which PKO runs one wave per job (LO_BATCH_ONE_WAVE=0/1 forces)
     hipStream_t stream = nullptr;
     std::string err;
     KParams* d_P = nullptr;
@@ -992,8 +994,10 @@ static int batch_alloc(lo_batch* b) {
     LO_BHIP(b, hipHostMalloc(&b->h_rec, B * sizeof(lo_batch_rec), hipHostMallocDefault));
     LO_BHIP(b, hipEventCreate(&b->ev0));
     LO_BHIP(b, hipEventCreate(&b->ev1));
-    LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   static_cast<int>(kMaxBlocks * sizeof(int))));
+    LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<4, false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
+    LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<1, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
     b->T_in.assign(B * 12, 0.0f);
     b->n.assign(B, 0);
     return LO_OK;
@@ -1023,6 +1027,7 @@ lo_batch* lo_batch_create(lo_ctx* const* ctxs, int count, int* err) {
     b->pko_max = kPkoMaxWGs;
     for (const lo_ctx* c : b->ctx) b->pko_max = std::min(b->pko_max, pko_grid(c->cfg));
     if (const char* e = std::getenv("LO_BATCH_PKO_WGS")) b->pko_budget = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LO_BATCH_ONE_WAVE")) b->one_wave_min = std::atoi(e) ? 1 : 0x7fffffff;
     const int rc = batch_alloc(b);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_batch_create: %s\n", b->err.c_str());
@@ -1092,7 +1097,10 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
         const dim3 blk(kBlock);
         for (int it = 0; it < b->max_iters; ++it) {
             hipLaunchKernelGGL(k_correspond_b, dim3(max_nb, nact), blk, 0, b->stream, b->d_P, it == 0 ? 1 : 0, it == 0 ? 1 : 0);
-            hipLaunchKernelGGL(k_pko_tb<4>, dim3(pko_wgs, nact), dim3(256), pre_bytes, b->stream, b->d_P, it);
+            if (nact >= b->one_wave_min)
+                hipLaunchKernelGGL((k_pko_tb<1, true>), dim3(1, nact), dim3(64), pre_bytes, b->stream, b->d_P, it);
+            else
+                hipLaunchKernelGGL((k_pko_tb<4, false>), dim3(pko_wgs, nact), dim3(256), pre_bytes, b->stream, b->d_P, it);
             if (max_acc <= kFuseMaxBlocks) {           // small jobs: one 8-wave workgroup accumulates + solves
                 hipLaunchKernelGGL(k_accumulate_b1, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
             } else {

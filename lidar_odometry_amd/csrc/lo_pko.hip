@@ -274,6 +274,136 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
     if (j >= 0 && lane == 0) { gmm[j] = wj; gmm[K + j] = muj; gmm[2 * K + j] = varj; }
 }
 
+// Batched launches: the whole fit on ONE wave (all K components), bit-identical to gmm_fit_split -- the same
+// per-sample sum (((0 + p_0) + p_1) + p_2), per-lane accumulation order and butterfly tree per value (the tree a
+// value goes through in wave_totals8 does not depend on its slot).  A batch is bound by fp64 issue, not by the
+// EM's latency: one wave drops the two extra butterflies, reciprocals and pdf exchanges the split pays per
+// iteration, and no other wave replicates k-means.
+template <int K, int SPL>
+__device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int32_t* draws, double* gmm) {
+    static_assert(3 * K - 1 <= 8, "partials");
+    const int lane = threadIdx.x & 63;
+    double x[SPL];
+    bool have[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        have[s] = lane + 64 * s < S;
+        x[s] = have[s] ? s_sd[lane + 64 * s] : 0.0;
+    }
+    double mu[K], cnt[K];
+    mu[0] = 0.0;
+#pragma unroll
+    for (int q = 1; q < K; ++q) mu[q] = s_sd[draws[q - 1]];
+#pragma unroll
+    for (int q = 0; q < K; ++q) cnt[q] = 0.0;
+    for (int guard = 0; guard < 100000; ++guard) {            // k-means as gmm_fit_split
+        double v[2 * K - 1];
+#pragma unroll
+        for (int q = 0; q < 2 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double md = DBL_MAX;
+            int ci = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) { const double d = fabs(x[s] - mu[q]); if (d < md) { md = d; ci = q; } }
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const bool mine = have[s] && ci == q;
+                v[q] += mine ? 1.0 : 0.0;
+                if (q > 0) v[K + q - 1] += mine ? x[s] : 0.0;
+            }
+        }
+        wave_totals8<2 * K - 1>(v);
+        bool eq = true;
+        double nm[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            nm[q] = (q == 0) ? 0.0 : (v[q] > 0.0 ? v[K + q - 1] / v[q] : 0.0);
+            eq = eq && (nm[q] == mu[q]);
+            cnt[q] = v[q];
+        }
+        if (eq) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q) mu[q] = nm[q];
+    }
+    double m1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m1 += have[s] ? x[s] : 0.0;
+    const double mean = wave_total(m1) / S;
+    double m2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m2 += have[s] ? (x[s] - mean) * (x[s] - mean) : 0.0;
+    const double iv = wave_total(m2) / S;
+    const double invS = 1.0 / static_cast<double>(S);
+    constexpr double kInvSqrt2Pi = 0.3989422804014327;
+    double w[K], var[K], ca[K], cb[K];
+    const double rs0 = rsq64(iv);
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        w[q] = cnt[q] / static_cast<double>(S);
+        var[q] = iv;
+        ca[q] = (iv <= 0.0) ? 0.0 : w[q] * (rs0 * kInvSqrt2Pi);
+        cb[q] = (iv <= 0.0) ? 0.0 : 0.5 * (rs0 * rs0);
+    }
+    double p[K][SPL], d[K][SPL];
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            d[q][s] = x[s] - mu[q];
+            p[q][s] = ca[q] * exp_nonpos(-((d[q][s] * d[q][s]) * cb[q]));
+        }
+    for (int em = 0; em < 100; ++em) {
+        double v[3 * K - 1];                                  // N_q | sum r x (q >= 1) | sum r d^2
+#pragma unroll
+        for (int q = 0; q < 3 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double sr = 0.0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) sr += p[q][s];
+            const double isr = have[s] ? rcp64(sr) : 0.0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const double r = p[q][s] * isr;
+                v[q] += r;
+                if (q > 0) v[K + q - 1] += r * x[s];
+                v[2 * K - 1 + q] += (r * d[q][s]) * d[q][s];
+            }
+        }
+        wave_totals8<3 * K - 1>(v);
+        double change = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const double Nk = v[q];
+            const double iN = rcp64(Nk);
+            const double nmu = (q == 0) ? 0.0 : v[K + q - 1] * iN;
+            const double dm = nmu - mu[q];
+            double nv = v[2 * K - 1 + q] * iN - dm * dm;
+            nv = (nv < 1e-6) ? 1e-6 : nv;
+            w[q] = Nk * invS;
+            mu[q] = nmu;
+            var[q] = nv;
+            const double rs = rsq64(nv);
+            ca[q] = w[q] * (rs * kInvSqrt2Pi);
+            cb[q] = 0.5 * (rs * rs);
+            if (q >= 1) change += fabs(dm);
+        }
+        if (change < 1e-6) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                d[q][s] = x[s] - mu[q];
+                p[q][s] = ca[q] * exp_nonpos(-((d[q][s] * d[q][s]) * cb[q]));
+            }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) { gmm[q] = w[q]; gmm[K + q] = mu[q]; gmm[2 * K + q] = var[q]; }
+    }
+}
+
 template <int K>
 __device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm,
                                                  double* s_p, double* s_dm, unsigned long long* dbg) {
@@ -282,8 +412,17 @@ __device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, cons
     else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
 }
 
+template <int K>
+__device__ __forceinline__ void gmm_fit_1w_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm) {
+    if ((threadIdx.x >> 6) != 0) return;                  // wave 0 fits; any other wave goes on to the barrier
+    if (S <= 64) gmm_fit_1w<K, 1>(s_sd, S, draws, gmm);
+    else if (S <= 128) gmm_fit_1w<K, 2>(s_sd, S, draws, gmm);
+    else gmm_fit_1w<K, 4>(s_sd, S, draws, gmm);
+}
+
 // wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices).
-template <int NW>
+// ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
+template <int NW, bool ONE_WAVE>
 __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G) {
     constexpr int NT = NW * 64;
     DevState* st = P.st;
@@ -294,10 +433,12 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
 #endif
     LO_STAMP(dbg, 0);
     extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
-    __shared__ double s_sd[64 * NW];
+    // s_p: the split EM's per-sample pdfs of each component (double-buffered), then the JS terms (>= 20 alphas)
+    constexpr int kPbuf = (2 * kMaxK * 64 * NW > 2000) ? 2 * kMaxK * 64 * NW : 2000;
+    __shared__ double s_sd[kMaxS];
     __shared__ double s_gmm[3 * kMaxK];
     __shared__ double s_P[100];
-    __shared__ double s_p[2 * kMaxK * 64 * NW];          // EM: per-sample pdf of each component, double-buffered
+    __shared__ double s_p[kPbuf];
     __shared__ double s_dm[2 * kMaxK];
     __shared__ int s_iscan[NW];
     __shared__ double s_dscan[NW];
@@ -388,8 +529,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
 
     // ---- 2. the reference's GMM sample ----
     const int S = min(P.S, nc);
-    if (tid < S) {
-        const int rank = pko_sample(P, nc, tid);
+    for (int sidx = tid; sidx < S; sidx += NT) {
+        const int rank = pko_sample(P, nc, sidx);
         double v;
         if (P.direct_res) {
             v = P.direct_res[rank];
@@ -398,13 +539,15 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
             while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (s_pre[mid] <= rank) lo = mid; else hi = mid - 1; }
             const int b = lo;
             int k = rank - s_pre[b];
+            uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
+#pragma unroll
+            for (int q = 0; q < kWavesPerBlock; ++q) m4[q] = P.wmask[b * kWavesPerBlock + q];
             int w = 0;
-            uint64_t mk = 0;
-            for (; w < kWavesPerBlock; ++w) {
-                mk = P.wmask[b * kWavesPerBlock + w];
+            uint64_t mk = m4[0];
+#pragma unroll
+            for (int q = 0; q + 1 < kWavesPerBlock; ++q) {
                 const int c = __popcll(mk);
-                if (k < c) break;
-                k -= c;
+                if (w == q && k >= c) { k -= c; w = q + 1; mk = m4[q + 1]; }
             }
             for (int q = 0; q < k; ++q) mk &= mk - 1;
             const int bit = __ffsll(static_cast<unsigned long long>(mk)) - 1;
@@ -420,7 +563,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
                 v = residual_f64(P.tab[P.slot[pidx]], wx, wy, wz) / sden;   // :321-326
             }
         }
-        s_sd[tid] = v;
+        s_sd[sidx] = v;
     }
     __syncthreads();
     LO_STAMP(dbg, 2);
@@ -428,10 +571,18 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     // ---- 3. GMM ----
     const int D = P.K > 1 ? P.K - 1 : 1;
     const int32_t* draws = P.km_draws + S * D;
-    switch (P.K) {                                              // every wave: see gmm_fit_split
-        case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
-        case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
-        default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+    if (ONE_WAVE) {                                             // wave 0 alone: see gmm_fit_1w
+        switch (P.K) {
+            case 1: gmm_fit_1w_dispatch<1>(s_sd, S, draws, s_gmm); break;
+            case 2: gmm_fit_1w_dispatch<2>(s_sd, S, draws, s_gmm); break;
+            default: gmm_fit_1w_dispatch<3>(s_sd, S, draws, s_gmm); break;
+        }
+    } else {
+        switch (P.K) {                                          // every wave: see gmm_fit_split
+            case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+            case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+            default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+        }
     }
     __syncthreads();
     if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
@@ -448,7 +599,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     __syncthreads();
     // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
     // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25)
-    constexpr int kJsPass = (2 * kMaxK * 64 * NW) / 100;
+    constexpr int kJsPass = kPbuf / 100;
     double* s_jsd = s_p;
     for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kJsPass) {
         for (int idx = tid; idx < kJsPass * 100; idx += NT) {
@@ -490,17 +641,20 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
 
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
-    pko_body<NW>(P, it, blockIdx.x, gridDim.x);
+    pko_body<NW, false>(P, it, blockIdx.x, gridDim.x);
 }
 
-// Batched launch: blockIdx.y = job, gridDim.x workgroups per job split its alpha grid.
-template <int NW>
+// Batched launch: blockIdx.y = job, gridDim.x workgroups per job split its alpha grid.  <4, false>: the
+// single-scan workgroup (few jobs); <1, true>: one wave per job that fits the GMM alone (many jobs: the
+// launch is bound by fp64 issue, and single-wave workgroups spread over the SIMDs evenly).
+template <int NW, bool ONE_WAVE>
 __global__ __launch_bounds__(NW * 64) void k_pko_tb(const KParams* __restrict__ PB, int it) {
-    pko_body<NW>(PB[blockIdx.y], it, blockIdx.x, gridDim.x);
+    pko_body<NW, ONE_WAVE>(PB[blockIdx.y], it, blockIdx.x, gridDim.x);
 }
 
 template __global__ void k_pko_t<4>(KParams, int);
-template __global__ void k_pko_tb<4>(const KParams*, int);
+template __global__ void k_pko_tb<4, false>(const KParams*, int);
+template __global__ void k_pko_tb<1, true>(const KParams*, int);
 
 // PKO-only entry point: argmin of the JS grid -> DevState::alpha (lo_pko_scale_factor).
 __global__ void k_pko_finish(KParams P) {

@@ -63,7 +63,14 @@ def _check_equal(res, singles):
             assert r.alpha == alpha, f"job {j}: alpha {r.alpha} vs {alpha}"
 
 
-def test_batch_heterogeneous_bitwise_vs_single():
+@pytest.fixture(params=["split", "one_wave"])
+def pko_mode(request, monkeypatch):
+    """The batch's two PKO launch shapes (k_pko_tb<4, false> below 2048 jobs, <1, true> from 2048): forced."""
+    monkeypatch.setenv("LO_BATCH_ONE_WAVE", "1" if request.param == "one_wave" else "0")
+    return request.param
+
+
+def test_batch_heterogeneous_bitwise_vs_single(pko_mode):
     from lidar_odometry_amd import BatchOptimizer
     jobs = _jobs()
     ctxs = [_ctx(m, v) for (m, v, _, _) in jobs]
@@ -96,7 +103,7 @@ def test_batch_heterogeneous_bitwise_vs_single():
             o.close()
 
 
-def test_batch_many_jobs_and_repointed_scans():
+def test_batch_many_jobs_and_repointed_scans(pko_mode):
     """64 jobs (fewer PKO workgroups per job than a single scan gets), then every job re-pointed at another scan."""
     from lidar_odometry_amd import BatchOptimizer
     frames = [11, 13, 15, 17, 19, 21, 23, 25]
