@@ -232,9 +232,9 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-            double sr = 0.0;
+            double sr = sp[64 * s + lane];                 // pdfs are >= +0 (or NaN): 0 + p_0 == p_0
 #pragma unroll
-            for (int q = 0; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
+            for (int q = 1; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
             const double isr = have[s] ? rcp64(sr) : 0.0;
             const double r = p[s] * isr;
             v[0] += r;
@@ -359,9 +359,9 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
         for (int q = 0; q < 3 * K - 1; ++q) v[q] = 0.0;
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-            double sr = 0.0;
+            double sr = p[0][s];                           // as gmm_fit_split: 0 + p_0 == p_0
 #pragma unroll
-            for (int q = 0; q < K; ++q) sr += p[q][s];
+            for (int q = 1; q < K; ++q) sr += p[q][s];
             const double isr = have[s] ? rcp64(sr) : 0.0;
 #pragma unroll
             for (int q = 0; q < K; ++q) {
@@ -448,6 +448,25 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool lead = wg == 0;
 
+    // ---- 0. prefetch what later phases need but does not depend on n_c, so its latency hides behind the
+    //         prefix phase: this thread's sample slot (s = tid) event-list bounds and base value for the three
+    //         shuffle modes, the k-means draws for S = P.S, and (one alpha per workgroup) this alpha and Z ----
+    __shared__ int32_t s_draws[kMaxK];
+    int pf_lo[3] = {0, 0, 0}, pf_hi[3] = {0, 0, 0}, pf_base[3] = {0, 0, 0};
+    if (tid < P.S) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            pf_lo[m] = P.ev_off[m * (P.S + 1) + tid];
+            pf_hi[m] = P.ev_off[m * (P.S + 1) + tid + 1];
+            pf_base[m] = P.base[m * P.S + tid];
+        }
+    }
+    const int D0 = P.K > 1 ? P.K - 1 : 1;
+    if (tid < D0) s_draws[tid] = P.km_draws[P.S * D0 + tid];
+    const bool one_alpha = G >= P.NA;                       // the single-scan launch: alpha 1 + wg only
+    double pf_alpha = 0.0, pf_Z = 0.0;
+    if (one_alpha && 1 + wg <= P.NA) { pf_alpha = P.alphas[1 + wg]; pf_Z = P.Z[1 + wg]; }
+
     // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
     if (P.direct_res) {
         if (tid == 0) { s_nc = P.n; s_scale = 1.0; }
@@ -530,7 +549,22 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     // ---- 2. the reference's GMM sample ----
     const int S = min(P.S, nc);
     for (int sidx = tid; sidx < S; sidx += NT) {
-        const int rank = pko_sample(P, nc, sidx);
+        int rank;
+        if (sidx == tid && nc >= P.S && sidx < P.S) {          // prefetched bounds: one round of event loads
+            const int mode = (nc <= 65535) ? ((nc & 1) ? 0 : 1) : 2;
+            const int lo0 = mode == 0 ? pf_lo[0] : (mode == 1 ? pf_lo[1] : pf_lo[2]);
+            const int hi0 = mode == 0 ? pf_hi[0] : (mode == 1 ? pf_hi[1] : pf_hi[2]);
+            rank = mode == 0 ? pf_base[0] : (mode == 1 ? pf_base[1] : pf_base[2]);
+            for (int e0 = lo0; e0 < hi0; e0 += 8) {             // ascending steps: the last one <= n - 1 wins
+                int ev[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ev[u] = (e0 + u < hi0) ? P.ev_steps[e0 + u] : 0x7fffffff;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) if (ev[u] <= nc - 1) rank = ev[u];
+            }
+        } else {
+            rank = pko_sample(P, nc, sidx);
+        }
         double v;
         if (P.direct_res) {
             v = P.direct_res[rank];
@@ -570,7 +604,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
 
     // ---- 3. GMM ----
     const int D = P.K > 1 ? P.K - 1 : 1;
-    const int32_t* draws = P.km_draws + S * D;
+    const int32_t* draws = (S == P.S) ? s_draws : P.km_draws + S * D;
     if (ONE_WAVE) {                                             // wave 0 alone: see gmm_fit_1w
         switch (P.K) {
             case 1: gmm_fit_1w_dispatch<1>(s_sd, S, draws, s_gmm); break;
@@ -592,8 +626,12 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     const double dr = P.trunc / 100.0;
     for (int b = tid; b < 100; b += NT) {
         const double r = dr * (1 + static_cast<double>(b));
+        double g[kMaxK];                                         // independent pdf chains, then the ordered sum
+#pragma unroll
+        for (int m = 0; m < kMaxK; ++m) g[m] = m < K ? s_gmm[m] * gpdf(r, s_gmm[K + m], s_gmm[2 * K + m]) : 0.0;
         double Pr = 0.0;
-        for (int m = 0; m < K; ++m) Pr += s_gmm[m] * gpdf(r, s_gmm[K + m], s_gmm[2 * K + m]);
+#pragma unroll
+        for (int m = 0; m < kMaxK; ++m) if (m < K) Pr += g[m];
         s_P[b] = Pr + 1e-10;
     }
     __syncthreads();
@@ -606,8 +644,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
             const int a = idx / 100, b = idx - a * 100;
             const int ai = a0 + a * G;
             if (ai > P.NA) continue;
-            const double alpha = P.alphas[ai];
-            const double pf = P.Z[ai];
+            const double alpha = one_alpha ? pf_alpha : P.alphas[ai];
+            const double pf = one_alpha ? pf_Z : P.Z[ai];
             const double r = dr * (1 + static_cast<double>(b));
             const double Pr = s_P[b];
             const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
@@ -620,16 +658,20 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
             if (ai <= P.NA) {
                 double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
                 const double* row = s_jsd + tid * 100;
-                for (int b0 = 0; b0 < 100; b0 += 10) {           // batched LDS reads, then the serial adds
-                    double vb[10];
+                double vb[10], vn[10];                           // LDS reads of the next 10 bins in flight while
+#pragma unroll                                                   // the serial adds consume the current ones
+                for (int q = 0; q < 10; ++q) vb[q] = row[q];
+                for (int b0 = 0; b0 < 100; b0 += 10) {
 #pragma unroll
-                    for (int q = 0; q < 10; ++q) vb[q] = row[b0 + q];
+                    for (int q = 0; q < 10; ++q) vn[q] = (b0 + 10 < 100) ? row[b0 + 10 + q] : 0.0;
 #pragma unroll
                     for (int q = 0; q < 10; ++q) {
                         const bool ok = !isnan(vb[q]);
                         cost += ok ? vb[q] : 0.0;                // cost starts at +0: adding +0 == skipping
                         cnt += ok ? 1.0 : 0.0;
                     }
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) vb[q] = vn[q];
                 }
                 P.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }
