@@ -32,6 +32,7 @@ constexpr int kFuseMaxBlocks = 64;   // <= this many accumulate blocks: the last
 constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
+constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP row)
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;

@@ -482,8 +482,8 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
     }
     KParams Pn = P;
     Pn.init = 0;
-    hipLaunchKernelGGL(k_knn, dim3((static_cast<size_t>(P.n) * 8 + kBlock - 1) / kBlock), blk, 0, c->stream, P);   // 8 lanes / query
-    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(256), 0, c->stream, Pn);
+    hipLaunchKernelGGL(k_knn, dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock), blk, 0, c->stream, P);
+    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, Pn);
     hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
 }
 

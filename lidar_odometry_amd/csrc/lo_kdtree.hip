@@ -28,6 +28,7 @@
 namespace lo {
 
 constexpr int kKnnRMax = 3;            // grid shells before a query falls back to brute force
+static_assert(kKnnRMax <= 3, "kKnnRowsMax covers (2r+1)^2 rows over kKnnGroup lanes up to r = 3");
 constexpr double kKnnMargin = 1e-2;    // m: covers fp32 binning of centroids near cell faces
 
 struct Top5 {
@@ -87,36 +88,57 @@ __device__ __forceinline__ void scan_range(const KParams& P, uint32_t s, uint32_
     }
 }
 
-// Merge of disjoint top-5 lists across the kKnnGroup lanes of a query (butterfly over __shfl_xor):
-// every lane of the group ends with the group's (dist, index)-smallest five.
-constexpr int kKnnGroup = 8;
+// Merge of disjoint top-5 lists across the kKnnGroup = 16 lanes of a query: a hypercube over the 16-lane DPP row
+// (quad_perm xor 1, quad_perm xor 2, row_half_mirror i <-> 7-i, row_mirror i <-> 15-i) -- VALU moves, no LDS
+// round trips -- after which every lane of the row holds the (dist, index)-smallest five of the group's union.
+template <int CTRL>
+__device__ __forceinline__ void top5_merge_dpp(Top5& t) {
+    Top5 u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        u.d[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t.d[k]), CTRL, 0xf, 0xf, false));
+        u.id[k] = __builtin_amdgcn_mov_dpp(t.id[k], CTRL, 0xf, 0xf, false);
+        u.pos[k] = __builtin_amdgcn_mov_dpp(t.pos[k], CTRL, 0xf, 0xf, false);
+    }
+    u.n = __builtin_amdgcn_mov_dpp(t.n, CTRL, 0xf, 0xf, false);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
+}
 
 __device__ __forceinline__ Top5 group_merge(const Top5& own) {
+    static_assert(kKnnGroup == 16, "the DPP hypercube spans one 16-lane row");
     Top5 t = own;
-#pragma unroll
-    for (int o = 1; o < kKnnGroup; o <<= 1) {
-        Top5 u;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            u.d[k] = __shfl_xor(t.d[k], o, 64);
-            u.id[k] = __shfl_xor(t.id[k], o, 64);
-            u.pos[k] = __shfl_xor(t.pos[k], o, 64);
-        }
-        u.n = __shfl_xor(t.n, o, 64);
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
-    }
+    top5_merge_dpp<0xB1>(t);     // quad_perm [1,0,3,2]
+    top5_merge_dpp<0x4E>(t);     // quad_perm [2,3,0,1]
+    top5_merge_dpp<0x141>(t);    // row_half_mirror
+    top5_merge_dpp<0x140>(t);    // row_mirror
     return t;
 }
 
 // ====================================================================================================
 // k_knn: grid shells.  kd_nbr[5i] = positions of the 5-NN, -1 = fewer than 5 (rejected), -2 = unresolved
 // ====================================================================================================
+// One candidate range of the kd_pts array (a run of cells of one grid row), scanned with 8 loads in flight.
+__device__ __forceinline__ void scan_range8(const KParams& P, uint32_t s, uint32_t e, float qx, float qy, float qz, Top5& t) {
+    for (uint32_t p = s; p < e; p += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (p + u < e) ? P.kd_pts[p + u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (p + u < e) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
+    }
+}
+
+constexpr int kKnnRowsMax = 4;          // rows of one round per lane: r = 3 has 49 rows over 16 lanes
+
 __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     if (!P.init && P.st->done) return;
-    // kKnnGroup consecutive lanes share one query: lane g scans rows g, g + G, ... of each shell, so a query's
-    // candidate loads are spread over G lanes (the scan has only ~N/64 waves: latency, not bandwidth, bounds it)
+    // kKnnGroup consecutive lanes (one DPP row) share one query: lane g takes rows g, g + 16, ... of each round.
+    // The first round scans the whole 3x3x3 cube (the r = 0 cell alone almost never certifies: its faces are
+    // < h / 2 away while the 5th neighbour of a surface sample is ~h); later rounds scan the shell r.  A lane's
+    // cell-range bounds for the round are loaded together, then its ranges are scanned 8 points at a time.
     const int gi = blockIdx.x * kBlock + threadIdx.x;
     const int i = gi / kKnnGroup, g = gi % kKnnGroup;
     float T[12];
@@ -139,22 +161,30 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     Top5 own, grp;
     top5_init(own);
     bool done = false;
-    for (int r = 0; r <= kKnnRMax && !done; ++r) {
+    for (int r = 1; r <= kKnnRMax && !done; ++r) {
         const int side = 2 * r + 1;
-        for (int k = g; k < side * side; k += kKnnGroup) {
+        // this lane's ranges of the round: up to 2 per row (a full row, or the shell's two end cells)
+        uint32_t rs[2 * kKnnRowsMax], re[2 * kKnnRowsMax];
+#pragma unroll
+        for (int j = 0; j < kKnnRowsMax; ++j) {
+            rs[2 * j] = re[2 * j] = rs[2 * j + 1] = re[2 * j + 1] = 0;
+            const int k = g + j * kKnnGroup;
+            if (k >= side * side) continue;
             const int dz = k / side - r, dy = k % side - r;
             const int z = c[2] + dz - oz, y = c[1] + dy - oy;
             if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
             const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
-            if (dz == -r || dz == r || dy == -r || dy == r) {               // whole row of the shell
+            if (r == 1 || dz == -r || dz == r || dy == -r || dy == r) {        // whole row of the cube / shell
                 const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
-                if (x0 <= x1) scan_range(P, P.kd_start[row + x0], P.kd_start[row + x1 + 1], qx, qy, qz, own);
-            } else {                                                        // the two end cells
+                if (x0 <= x1) { rs[2 * j] = P.kd_start[row + x0]; re[2 * j] = P.kd_start[row + x1 + 1]; }
+            } else {                                                            // the two end cells
                 const int xa = c[0] - r - ox, xb = c[0] + r - ox;
-                if (xa >= 0 && xa < dimx) scan_range(P, P.kd_start[row + xa], P.kd_start[row + xa + 1], qx, qy, qz, own);
-                if (xb >= 0 && xb < dimx) scan_range(P, P.kd_start[row + xb], P.kd_start[row + xb + 1], qx, qy, qz, own);
+                if (xa >= 0 && xa < dimx) { rs[2 * j] = P.kd_start[row + xa]; re[2 * j] = P.kd_start[row + xa + 1]; }
+                if (xb >= 0 && xb < dimx) { rs[2 * j + 1] = P.kd_start[row + xb]; re[2 * j + 1] = P.kd_start[row + xb + 1]; }
             }
         }
+#pragma unroll
+        for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, rs[j], re[j], qx, qy, qz, own);
         grp = group_merge(own);
         // every unscanned centroid lies outside the cube of cells [c - r, c + r]
         bool all = true;
@@ -185,20 +215,38 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
 }
 
 // ====================================================================================================
-// k_knn_brute: unresolved queries, one workgroup each (grid-strided over the device-side list)
+// k_knn_brute: unresolved queries, one 1024-thread workgroup each (grid-strided over the device-side list):
+// every lane scans a strided share of the map with 8 loads in flight, the 64 lanes of a wave merge with a
+// hypercube (DPP within 16-lane rows, then __shfl_xor 16 / 32), the 16 wave results meet in LDS and wave 0's
+// first row merges them the same way.
 // ====================================================================================================
-constexpr int kBruteThreads = 256;
+constexpr int kBruteThreads = 1024;
+
+__device__ __forceinline__ void top5_merge_xor(Top5& t, int o) {
+    Top5 u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        u.d[k] = __shfl_xor(t.d[k], o, 64);
+        u.id[k] = __shfl_xor(t.id[k], o, 64);
+        u.pos[k] = __shfl_xor(t.pos[k], o, 64);
+    }
+    u.n = __shfl_xor(t.n, o, 64);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
+}
 
 __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     DevState* st = P.st;
     if (st->done) return;
     const unsigned nu = st->kd_unres_n;
     if (blockIdx.x >= nu) return;
-    __shared__ float s_d[kBruteThreads][5];
-    __shared__ int s_id[kBruteThreads][5];
-    __shared__ int s_pos[kBruteThreads][5];
-    __shared__ int s_n[kBruteThreads];
-    const int tid = threadIdx.x;
+    constexpr int kW = kBruteThreads / 64;
+    __shared__ float s_d[kW][5];
+    __shared__ int s_id[kW][5];
+    __shared__ int s_pos[kW][5];
+    __shared__ int s_n[kW];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
@@ -208,42 +256,39 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
         Top5 t;
         top5_init(t);
-        int p = tid;
-        for (; p + 3 * kBruteThreads < P.kd_m; p += 4 * kBruteThreads) {   // 4 loads in flight per lane
-            float4 v[4];
+        for (int p0 = tid; p0 < P.kd_m; p0 += 8 * kBruteThreads) {           // 8 loads in flight per lane
+            float4 v[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = P.kd_pts[p + u * kBruteThreads];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), p + u * kBruteThreads);
-        }
-        for (; p < P.kd_m; p += kBruteThreads) {
-            const float4 v = P.kd_pts[p];
-            top5_insert(t, l2sq(qx, qy, qz, v), __float_as_int(v.w), p);
-        }
-#pragma unroll
-        for (int k = 0; k < 5; ++k) { s_d[tid][k] = t.d[k]; s_id[tid][k] = t.id[k]; s_pos[tid][k] = t.pos[k]; }
-        s_n[tid] = t.n;
-        __syncthreads();
-        for (int s = kBruteThreads / 2; s > 0; s >>= 1) {
-            if (tid < s) {
-                Top5 a;
-#pragma unroll
-                for (int k = 0; k < 5; ++k) { a.d[k] = s_d[tid][k]; a.id[k] = s_id[tid][k]; a.pos[k] = s_pos[tid][k]; }
-                a.n = s_n[tid];
-                const int nb = s_n[tid + s];
-#pragma unroll
-                for (int k = 0; k < 5; ++k)
-                    if (k < nb) top5_insert(a, s_d[tid + s][k], s_id[tid + s][k], s_pos[tid + s][k]);
-#pragma unroll
-                for (int k = 0; k < 5; ++k) { s_d[tid][k] = a.d[k]; s_id[tid][k] = a.id[k]; s_pos[tid][k] = a.pos[k]; }
-                s_n[tid] = a.n;
+            for (int w = 0; w < 8; ++w) {
+                const int p = p0 + w * kBruteThreads;
+                v[w] = p < P.kd_m ? P.kd_pts[p] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
-            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const int p = p0 + w * kBruteThreads;
+                if (p < P.kd_m) top5_insert(t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
+            }
         }
-        if (tid == 0) {
-            int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
-            if (s_n[0] < 5) out[0] = -1;
-            else for (int k = 0; k < 5; ++k) out[k] = s_pos[0][k];
+        t = group_merge(t);                                // 16-lane rows
+        top5_merge_xor(t, 16);
+        top5_merge_xor(t, 32);                             // the wave's five
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) { s_d[wid][k] = t.d[k]; s_id[wid][k] = t.id[k]; s_pos[wid][k] = t.pos[k]; }
+            s_n[wid] = t.n;
+        }
+        __syncthreads();
+        if (wid == 0 && lane < 16) {
+            Top5 a;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) { a.d[k] = s_d[lane][k]; a.id[k] = s_id[lane][k]; a.pos[k] = s_pos[lane][k]; }
+            a.n = s_n[lane];
+            a = group_merge(a);
+            if (lane == 0) {
+                int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+                if (a.n < 5) out[0] = -1;
+                else for (int k = 0; k < 5; ++k) out[k] = a.pos[k];
+            }
         }
         __syncthreads();
     }
