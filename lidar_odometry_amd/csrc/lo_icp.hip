@@ -472,7 +472,7 @@ size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->g
 // ---------------------------------------------------------------- optimize
 // Correspondence stage of one GN iteration: surfel lookup, or (KDTree variant) grid kNN + brute-force
 // fallback + plane fit.  P0 carries init = 1 on a scan's first iteration.
-static constexpr int kBruteBlocks = 256;
+static constexpr int kBruteBlocks = 64;      // k_knn_brute workgroups (grid-strided over the unresolved list)
 
 static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool kd) {
     const dim3 grid(P.nb), blk(kBlock);

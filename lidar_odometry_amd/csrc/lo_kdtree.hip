@@ -27,8 +27,7 @@
 
 namespace lo {
 
-constexpr int kKnnRMax = 3;            // grid shells before a query falls back to brute force
-static_assert(kKnnRMax <= 3, "kKnnRowsMax covers (2r+1)^2 rows over kKnnGroup lanes up to r = 3");
+constexpr int kKnnRMax = 5;            // grid shells before a query falls back to brute force
 constexpr double kKnnMargin = 1e-2;    // m: covers fp32 binning of centroids near cell faces
 
 struct Top5 {
@@ -163,28 +162,31 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     bool done = false;
     for (int r = 1; r <= kKnnRMax && !done; ++r) {
         const int side = 2 * r + 1;
-        // this lane's ranges of the round: up to 2 per row (a full row, or the shell's two end cells)
-        uint32_t rs[2 * kKnnRowsMax], re[2 * kKnnRowsMax];
+        // this lane's rows of the round in chunks of kKnnRowsMax: the chunk's range bounds (up to 2 per row: a
+        // full row, or the shell's two end cells) are loaded together, then scanned
+        for (int j0 = 0; j0 < side * side; j0 += kKnnRowsMax * kKnnGroup) {
+            uint32_t rs[2 * kKnnRowsMax], re[2 * kKnnRowsMax];
 #pragma unroll
-        for (int j = 0; j < kKnnRowsMax; ++j) {
-            rs[2 * j] = re[2 * j] = rs[2 * j + 1] = re[2 * j + 1] = 0;
-            const int k = g + j * kKnnGroup;
-            if (k >= side * side) continue;
-            const int dz = k / side - r, dy = k % side - r;
-            const int z = c[2] + dz - oz, y = c[1] + dy - oy;
-            if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
-            const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
-            if (r == 1 || dz == -r || dz == r || dy == -r || dy == r) {        // whole row of the cube / shell
-                const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
-                if (x0 <= x1) { rs[2 * j] = P.kd_start[row + x0]; re[2 * j] = P.kd_start[row + x1 + 1]; }
-            } else {                                                            // the two end cells
-                const int xa = c[0] - r - ox, xb = c[0] + r - ox;
-                if (xa >= 0 && xa < dimx) { rs[2 * j] = P.kd_start[row + xa]; re[2 * j] = P.kd_start[row + xa + 1]; }
-                if (xb >= 0 && xb < dimx) { rs[2 * j + 1] = P.kd_start[row + xb]; re[2 * j + 1] = P.kd_start[row + xb + 1]; }
+            for (int j = 0; j < kKnnRowsMax; ++j) {
+                rs[2 * j] = re[2 * j] = rs[2 * j + 1] = re[2 * j + 1] = 0;
+                const int k = j0 + g + j * kKnnGroup;
+                if (k >= side * side) continue;
+                const int dz = k / side - r, dy = k % side - r;
+                const int z = c[2] + dz - oz, y = c[1] + dy - oy;
+                if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
+                const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
+                if (r == 1 || dz == -r || dz == r || dy == -r || dy == r) {        // whole row of the cube / shell
+                    const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
+                    if (x0 <= x1) { rs[2 * j] = P.kd_start[row + x0]; re[2 * j] = P.kd_start[row + x1 + 1]; }
+                } else {                                                            // the two end cells
+                    const int xa = c[0] - r - ox, xb = c[0] + r - ox;
+                    if (xa >= 0 && xa < dimx) { rs[2 * j] = P.kd_start[row + xa]; re[2 * j] = P.kd_start[row + xa + 1]; }
+                    if (xb >= 0 && xb < dimx) { rs[2 * j + 1] = P.kd_start[row + xb]; re[2 * j + 1] = P.kd_start[row + xb + 1]; }
+                }
             }
-        }
 #pragma unroll
-        for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, rs[j], re[j], qx, qy, qz, own);
+            for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, rs[j], re[j], qx, qy, qz, own);
+        }
         grp = group_merge(own);
         // every unscanned centroid lies outside the cube of cells [c - r, c + r]
         bool all = true;
@@ -302,11 +304,13 @@ __device__ __forceinline__ double dot3d(double a0, double a1, double a2, double 
     return (e0 + e1) + e2;
 }
 
-// Smallest-eigenvalue eigenvector of a symmetric 3x3 (cyclic Jacobi, fp64) -- the same sweep as the oracle's
-// smallest_eigvec3d (oracle/src/lo_oracle.cpp), so normals agree bit for bit under -ffp-contract=off.
-// Fully unrolled (p, q) rotations keep A and V in registers.
-__device__ __forceinline__ void jrot(double (&A)[3][3], double (&V)[3][3], int p, int q) {
-    if (A[p][q] == 0.0) return;
+// Smallest-eigenvalue eigenvector of a symmetric 3x3 (cyclic Jacobi, fp64) -- the same sweep and stopping rule as the
+// oracle's smallest_eigvec3d (oracle/src/lo_oracle.cpp; Eigen JacobiSVD's: rotate a pair only while
+// |a_pq| > max(DBL_MIN, 2 eps * running max |diagonal|), stop after a sweep without rotations), so normals agree bit
+// for bit under -ffp-contract=off.  Fully unrolled (p, q) rotations keep A and V in registers.
+__device__ __forceinline__ bool jrot(double (&A)[3][3], double (&V)[3][3], int p, int q, double& maxd) {
+    const double thr = std_max(DBL_MIN, 2.0 * DBL_EPSILON * maxd);     // std::max semantics, as the oracle
+    if (!(fabs(A[p][q]) > thr)) return false;
     const double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
     const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
     const double cc = 1.0 / sqrt(t * t + 1.0), s = t * cc;
@@ -325,16 +329,18 @@ __device__ __forceinline__ void jrot(double (&A)[3][3], double (&V)[3][3], int p
         const double vkp = V[k][p], vkq = V[k][q];
         V[k][p] = cc * vkp - s * vkq; V[k][q] = s * vkp + cc * vkq;
     }
+    maxd = std_max(maxd, std_max(fabs(A[p][p]), fabs(A[q][q])));
+    return true;
 }
 
 __device__ __forceinline__ void smallest_eigvec3d(double (&A)[3][3], double (&v)[3]) {
     double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    double maxd = std_max(fabs(A[0][0]), std_max(fabs(A[1][1]), fabs(A[2][2])));
     for (int sweep = 0; sweep < 50; ++sweep) {
-        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
-        if (off < 1e-300) break;
-        jrot(A, V, 0, 1);
-        jrot(A, V, 0, 2);
-        jrot(A, V, 1, 2);
+        bool rot = jrot(A, V, 0, 1, maxd);
+        rot = jrot(A, V, 0, 2, maxd) || rot;
+        rot = jrot(A, V, 1, 2, maxd) || rot;
+        if (!rot) break;
     }
     int mi = 0;
     if (A[1][1] < A[0][0]) mi = 1;

@@ -908,14 +908,20 @@ static void knn5(const std::vector<float>& cloud, const float q[3], int idx[5], 
 }
 
 // symmetric 3x3 eigen decomposition in double (cyclic Jacobi); returns eigenvector of smallest eigenvalue
+// Cyclic Jacobi on the 3x3 scatter matrix.  Stopping rule as Eigen's JacobiSVD (JacobiSVD.h compute(): a pair is
+// rotated only while |a_pq| > max(DBL_MIN, 2 eps * maxDiagEntry), the running maximum of the |diagonal|; the sweep
+// loop ends after a sweep that rotated nothing): ~4 sweeps on plane-like neighbourhoods instead of the ~11 an
+// absolute off-diagonal test down to 1e-300 needs.
 static void smallest_eigvec3d(const double A_in[3][3], double v_out[3]) {
     double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     std::memcpy(A, A_in, sizeof(A));
+    double maxd = std::max(std::fabs(A[0][0]), std::max(std::fabs(A[1][1]), std::fabs(A[2][2])));
     for (int sweep = 0; sweep < 50; ++sweep) {
-        double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
-        if (off < 1e-300) break;
+        bool rotated = false;
         for (int p = 0; p < 2; ++p) for (int q = p + 1; q < 3; ++q) {
-            if (A[p][q] == 0.0) continue;
+            const double thr = std::max(std::numeric_limits<double>::min(), 2.0 * std::numeric_limits<double>::epsilon() * maxd);
+            if (!(std::fabs(A[p][q]) > thr)) continue;
+            rotated = true;
             double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
             double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
             double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
@@ -931,7 +937,9 @@ static void smallest_eigvec3d(const double A_in[3][3], double v_out[3]) {
                 double vkp = V[k][p], vkq = V[k][q];
                 V[k][p] = c * vkp - s * vkq; V[k][q] = s * vkp + c * vkq;
             }
+            maxd = std::max(maxd, std::max(std::fabs(A[p][p]), std::fabs(A[q][q])));
         }
+        if (!rotated) break;
     }
     int mi = 0;
     for (int i = 1; i < 3; ++i) if (A[i][i] < A[mi][mi]) mi = i;
