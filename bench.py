@@ -474,7 +474,10 @@ def main():
     traffic = read_pmc_traffic(args.config + ("_random" if args.config == "patch1m" and ORDER == "random" else ""))
     # where a step's device time goes: isolated kernel time x launches per scan (working launches only)
     gi = float(np.mean(iters))
-    per_scan = {k: v * gi for k, v in kern_us.items()}
+    # small scans with PKO (<= 64 accumulate blocks): the accumulate runs inside the k_pko launch (one candidate
+    # per alpha, off the critical path; kern_us["k_pko"] includes it) and a one-workgroup k_solve_pick solves
+    spec = bool(icp.adaptive.use_adaptive_m_estimator) and (n0 + 255) // 256 <= 64
+    per_scan = {k: v * gi for k, v in kern_us.items() if not (spec and k == "k_accumulate")}
     dom = max(per_scan, key=per_scan.get)
 
     # PCIe-inclusive rate (never `value`): lo_icp_optimize on HOST buffers = H2D points, the same device

@@ -33,6 +33,7 @@ constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
 constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP row)
+constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;
@@ -116,6 +117,7 @@ struct KParams {
     double* blk_sum;
     double* blk_m2;
     double* blk_part;
+    double* acc_part;         // speculative normal equations: [NA + 1 candidates][kFuseMaxBlocks][kNE] partials
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
@@ -252,10 +254,10 @@ __device__ __forceinline__ double rsq64(double x) {
 // std::max(a, b) for doubles (returns a when the comparison is false, so a NaN first argument survives)
 __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
 
-// calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the FIRST alpha with the
-// strictly smallest JS cost, min_scale_factor if none is below DBL_MAX.  Every wave computes it
+// calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the index of the FIRST alpha with
+// the strictly smallest JS cost, 0 (min_scale_factor) if none is below DBL_MAX.  Every wave computes it
 // redundantly from P.js (lexicographic (cost, index) minimum == first strict minimum).
-__device__ __forceinline__ double pko_select_alpha(const KParams& P) {
+__device__ __forceinline__ int pko_select_index(const KParams& P) {
     const int lane = threadIdx.x & 63;
     double bv = 1.7976931348623157e308;
     int bi = 0x7fffffff;
@@ -269,7 +271,11 @@ __device__ __forceinline__ double pko_select_alpha(const KParams& P) {
         const int oi = __shfl_xor(bi, o, 64);
         if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
     }
-    return (bv < 1.7976931348623157e308) ? P.alphas[bi] : P.min_scale;
+    return (bv < 1.7976931348623157e308) ? bi : 0;
+}
+__device__ __forceinline__ double pko_select_alpha(const KParams& P) {
+    const int bi = pko_select_index(P);
+    return bi > 0 ? P.alphas[bi] : P.min_scale;
 }
 
 template <typename T>
@@ -359,6 +365,60 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
         for (int w = 0; w < kWavesPerBlock; ++w) m2 += s_red[w];
         P.blk_m2[vb] = m2;
     }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
+// fp32 products fl(fl(w J_i) J_j) as the reference forms them.
+__device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
+                                          float (&acc)[kNE]) {
+    const int s = P.slot[i];
+    if (s < 0) return;
+    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+    const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
+    double r;
+    if (P.kd_res) {
+        r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
+    } else {
+        float wx, wy, wz;
+        transform_pt(T, px, py, pz, wx, wy, wz);
+        r = residual_f64(sl, wx, wy, wz);
+    }
+    const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
+    // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
+    const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
+    const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
+    const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
+    const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
+    const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
+    // J = [n^T R, -n^T R [p]x] (:376-386)
+    float J[6];
+    J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
+    J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
+    J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
+    const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
+    const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
+    const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
+    J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
+    J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
+    J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
+    float w = 1.0f;
+    if (P.robust) {                                                             // :389-404
+        const float an = fabsf(nres);
+        if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
+        else if (an > dl) w = dl / an;
+    }
+    int k = 0;
+#pragma unroll
+    for (int rr = 0; rr < 6; ++rr) {
+        const float wJ = w * J[rr];
+#pragma unroll
+        for (int c = 0; c <= rr; ++c) acc[k++] += wJ * J[c];
+    }
+    const float wr = w * res;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
+    acc[27] += wr * res;
 }
 
 }  // namespace lo

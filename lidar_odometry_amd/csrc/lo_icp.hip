@@ -21,10 +21,11 @@
 
 namespace lo {
 __global__ void k_correspond(KParams P, int with_stats);
-template <int NW> __global__ void k_pko_t(KParams P, int it);
+template <int NW> __global__ void k_pko_t(KParams P, int it, int G);
 __global__ void k_pko_finish(KParams P);
 __global__ void k_accumulate(KParams P, int it, int fuse);
 __global__ void k_solve(KParams P, int it, int ne_only);
+__global__ void k_solve_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
@@ -68,6 +69,7 @@ struct lo_ctx {
     double* d_blk_sum = nullptr;
     double* d_blk_m2 = nullptr;
     double* d_blk_part = nullptr;
+    double* d_acc_part = nullptr;   // speculative normal equations (allocated on the first PKO optimize)
     double* d_js = nullptr;
     double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
     size_t res_cap = 0;
@@ -120,7 +122,45 @@ static void launch_pko(lo_ctx* c, const KParams& P, int it) {
     // dynamic LDS for the per-block prefix (nb ints; 64 KB only at the 4M-point maximum)
     const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     // 4 waves: the EM runs one GMM component per wave (gmm_fit_split), up to 256 samples (4 per lane)
-    hipLaunchKernelGGL(k_pko_t<4>, dim3(pko_grid(c->cfg)), dim3(256), pre_bytes, c->stream, P, it);
+    const int G = pko_grid(c->cfg);
+    hipLaunchKernelGGL(k_pko_t<4>, dim3(G), dim3(256), pre_bytes, c->stream, P, it, G);
+}
+
+// Small scans with PKO: the PKO launch also evaluates the normal equations for every alpha candidate
+// (acc_candidate, lo_pko.hip, (NA + 1) x ceil(nb_acc / kSpecBlocksPerWG) extra workgroups); k_solve_pick then
+// solves the selected one.
+static bool spec_ok(const KParams& P) { return P.use_pko && P.acc_part && P.nb_acc <= kFuseMaxBlocks; }
+
+static void launch_pko_spec(lo_ctx* c, const KParams& P, int it) {
+    const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
+    const int G = pko_grid(c->cfg);
+    const int W = (P.nb_acc + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
+    hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, c->stream, P, it, G);
+}
+
+// One GN iteration after the correspondence stage: PKO with the speculative normal equations + k_solve_pick
+// (small scans), else PKO, then k_accumulate whose last block solves (small) or k_solve over 1024 threads (large).
+static void launch_gn_tail(lo_ctx* c, const KParams& P, int it) {
+    const dim3 blk(kBlock);
+    if (spec_ok(P)) {
+        launch_pko_spec(c, P, it);
+        hipLaunchKernelGGL(k_solve_pick, dim3(1), blk, 0, c->stream, P, it);
+        return;
+    }
+    launch_pko(c, P, it);
+    if (P.nb_acc <= kFuseMaxBlocks) {
+        hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
+    } else {
+        hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
+        hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
+    }
+}
+
+static int ensure_acc_part(lo_ctx* c) {
+    if (c->d_acc_part || !c->cfg.use_adaptive_m_estimator) return LO_OK;
+    const size_t cand = static_cast<size_t>(c->cfg.num_alpha_segments) + 1;
+    LO_HIP(c, hipMalloc(&c->d_acc_part, cand * kFuseMaxBlocks * kNE * sizeof(double)));
+    return LO_OK;
 }
 
 static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
@@ -175,6 +215,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.blk_sum = c->d_blk_sum;
     P.blk_m2 = c->d_blk_m2;
     P.blk_part = c->d_blk_part;
+    P.acc_part = c->d_acc_part;
     P.js = c->d_js;
     P.res_dbg = nullptr;
     P.direct_res = nullptr;
@@ -334,7 +375,7 @@ void lo_destroy(lo_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part,
+    void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part, c->d_acc_part,
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
@@ -498,21 +539,16 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
     if (n == 0) {
         hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
     } else {
+        const int rc = ensure_acc_part(c);
+        if (rc != LO_OK) return rc;
         KParams P = make_params(c, d_pts, static_cast<int>(n));
         P.n_dev = n_dev;                                  // device-filtered scan: count read on the device
         KParams P0 = P;                                   // first k_correspond also resets the GN state
         P0.init = 1;
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
-        const dim3 blk(kBlock);
         for (int it = 0; it < g.max_iterations; ++it) {
             launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
-            launch_pko(c, P, it);
-            if (P.nb_acc <= kFuseMaxBlocks) {          // small scans: the last accumulate block solves
-                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
-            } else {                                   // large scans: 1024 threads reduce the partials
-                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
-                hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
-            }
+            launch_gn_tail(c, P, it);
         }
         LO_HIP(c, hipGetLastError());
     }
@@ -602,6 +638,7 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     if (rc != LO_OK) return rc;
     if (st) { std::memset(st, 0, sizeof(*st)); st->status = LO_INSUFFICIENT; }
     if (n_curr == 0 || n_matched == 0) return LO_INSUFFICIENT;       // empty clouds: 0 correspondences (:477-483)
+    if ((rc = ensure_acc_part(c)) != LO_OK) return rc;
     LO_HIP(c, hipMemcpyAsync(c->d_pts, curr, n_curr * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n_curr));
     set_kd_params(c, P, c->lgrid);
@@ -625,13 +662,7 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     for (int it = 0; it < kLoopMaxIters;) {
         for (int k = 0; k < kLoopChunk && it < kLoopMaxIters; ++k, ++it) {
             launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, true);
-            launch_pko(c, P, it);
-            if (P.nb_acc <= kFuseMaxBlocks) {
-                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 1);
-            } else {
-                hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
-                hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
-            }
+            launch_gn_tail(c, P, it);
         }
         LO_HIP(c, hipGetLastError());
         LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, head, hipMemcpyDeviceToHost, c->stream));
@@ -896,6 +927,7 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     LO_HIP(c, hipSetDevice(c->device));
     int rc = reset_state(c, T, scale, alpha);
     if (rc != LO_OK) return rc;
+    if ((rc = ensure_acc_part(c)) != LO_OK) return rc;
     KParams P = make_params(c, d_pts, static_cast<int>(n));
     P.alpha_given = 1;
     const dim3 grid(P.nb), blk(kBlock);
@@ -909,7 +941,7 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
             case 0: launch_correspond(c, P, 0, c->kd); break;                 // KDTree: kNN + fallback + plane fit
             case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0,
                                        P.nb_acc <= kFuseMaxBlocks ? 2 : 0); break;
-            case 2: launch_pko(c, P, 1); break;
+            case 2: if (spec_ok(P)) launch_pko_spec(c, P, 1); else launch_pko(c, P, 1); break;
             default: hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, 0, 1); break;
         }
     }

@@ -76,59 +76,6 @@ __global__ __launch_bounds__(kBlock) void k_correspond_b(const KParams* __restri
 template <int NT>
 __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* part_src, int nrows);
 
-// One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
-// fp32 products fl(fl(w J_i) J_j) as the reference forms them.
-__device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
-                                          float (&acc)[kNE]) {
-    const int s = P.slot[i];
-    if (s < 0) return;
-    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
-    const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
-    double r;
-    if (P.kd_res) {
-        r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
-    } else {
-        float wx, wy, wz;
-        transform_pt(T, px, py, pz, wx, wy, wz);
-        r = residual_f64(sl, wx, wy, wz);
-    }
-    const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
-    // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
-    const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
-    const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
-    const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
-    const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
-    const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
-    // J = [n^T R, -n^T R [p]x] (:376-386)
-    float J[6];
-    J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
-    J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
-    J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
-    const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
-    const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
-    const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
-    J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
-    J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
-    J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
-    float w = 1.0f;
-    if (P.robust) {                                                             // :389-404
-        const float an = fabsf(nres);
-        if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
-        else if (an > dl) w = dl / an;
-    }
-    int k = 0;
-#pragma unroll
-    for (int rr = 0; rr < 6; ++rr) {
-        const float wJ = w * J[rr];
-#pragma unroll
-        for (int c = 0; c <= rr; ++c) acc[k++] += wJ * J[c];
-    }
-    const float wr = w * res;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
-    acc[27] += wr * res;
-}
-
 // fuse: 0 = partials only, 1 = the last block to finish also runs the GN solve / update (k_solve's job),
 // 2 = the last block writes the summed normal equations (lo_build_normal_equations)
 __device__ __forceinline__ void accumulate_body(const KParams& P, int it, int fuse, int blk, int nblk) {
@@ -428,6 +375,24 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* 
 __global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int ne_only) {
     if (P.st->done) return;
     solve_tail<kSolveThreads>(P, it, ne_only, P.blk_part, P.nb_acc);
+}
+
+// Solve from the speculative normal equations (single scans with nb_acc <= kFuseMaxBlocks): the candidate of
+// the selected alpha (acc_candidate, lo_pko.hip) holds the same per-block partials the fused k_accumulate would
+// have formed, reduced here with the same solve_tail<kBlock> pattern -- bit-identical, one launch fewer.
+__global__ __launch_bounds__(kBlock) void k_solve_pick(KParams P, int it) {
+    DevState* st = P.st;
+    if (st->done) return;
+    __shared__ int s_c;
+    if (threadIdx.x < kWave) {
+        const int bi = pko_select_index(P);
+        if (threadIdx.x == 0) {
+            s_c = bi > 0 ? bi - 1 : P.NA;
+            st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
+        }
+    }
+    __syncthreads();
+    solve_tail<kBlock>(P, it, 0, P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc);
 }
 
 // Batched solve (jobs with more than kFuseMaxBlocks accumulate blocks present): one block per job, with the

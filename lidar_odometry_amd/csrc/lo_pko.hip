@@ -131,6 +131,27 @@ __device__ __forceinline__ void wave_totals8(double (&v)[NV]) {
     for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 8 * q);
 }
 
+// Up to 4 values with the same pairing tree as wave_totals8 -- lanes (l, l+32), (l, l+16), (l, l+8), then the
+// quad and half-row steps -- so each total is bit-identical to wave_totals8's, with half the permlane traffic:
+// after the 32- and 16-lane swaps row r holds value r, and one row_ror:8 replaces the half-row selects.
+template <int NV>
+__device__ __forceinline__ void wave_totals4(double (&v)[NV]) {
+    static_assert(NV >= 1 && NV <= 4, "butterfly handles up to 4 values");
+    double u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u[q] = q < NV ? v[q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { pl32_swap(u[q], u[q + 2]); u[q] += u[q + 2]; }   // lo: v_q, hi: v_{q+2}
+    pl16_swap(u[0], u[1]);
+    double t = u[0] + u[1];         // row r: value r
+    t += dpp64<0x128, 0xf>(t);      // row_ror:8
+    t += dpp64<0xB1, 0xf>(t);       // quad_perm [1,0,3,2]
+    t += dpp64<0x4E, 0xf>(t);       // quad_perm [2,3,0,1]
+    t += dpp64<0x141, 0xf>(t);      // row_half_mirror: 8-lane group total
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 16 * q);
+}
+
 // fit_gmm (AdaptiveMEstimator.cpp:294-485) with the EM split over the workgroup's waves: wave j < K owns
 // component j (every lane computes ONE pdf per sample instead of K), the per-sample pdfs meet in LDS (s_p) and
 // the summed |d mean| of components >= 1 in s_dm, one barrier per iteration.  Per-lane sample mapping (sample s*64 + lane), the order of the
@@ -241,7 +262,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
             v[1] += r * x[s];
             v[2] += (r * d[s]) * d[s];
         }
-        wave_totals8<3>(v);
+        wave_totals4<3>(v);
         const double Nk = v[0];
         const double iN = rcp64(Nk);
         const double nmu = (jj == 0) ? 0.0 : v[1] * iN;
@@ -420,7 +441,51 @@ __device__ __forceinline__ void gmm_fit_1w_dispatch(const double* s_sd, int S, c
     else gmm_fit_1w<K, 4>(s_sd, S, draws, gmm);
 }
 
-// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices).
+// Speculative normal equations (single-scan launches of small scans, nb_acc <= kFuseMaxBlocks).  The accumulate
+// pass depends on the PKO only through the Huber delta, one of NA + 1 values (alphas[1..NA], or min_scale when no
+// JS cost is finite).  Workgroups G, G+1, ... of the PKO launch evaluate every candidate while the GMM fit runs,
+// and k_solve_pick reduces the selected one: the accumulate leaves the iteration's critical path.  Workgroup wgi
+// takes candidate wgi / W (W = ceil(nb_acc / kSpecBlocksPerWG)) and its kSpecBlocksPerWG 256-point blocks
+// starting at kSpecBlocksPerWG * (wgi % W); each block's partial is formed exactly as accumulate_body forms it
+// (one point per thread, fp32 wave_total, fp64 sum over the 4 waves), so the solve is bit-identical.
+__device__ void acc_candidate(const KParams& P, double scale, int wgi) {
+    const int nb = P.nb_acc;
+    const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
+    const int c = wgi / W, part = wgi - c * W;
+    if (c > P.NA) return;
+    const float dl = static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
+    __shared__ float s_acc[kWavesPerBlock][kNE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+    const int n = scan_n(P);
+    double* dst = P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE;
+    const int vb1 = min(nb, (part + 1) * kSpecBlocksPerWG);
+    for (int vb = part * kSpecBlocksPerWG; vb < vb1; ++vb) {
+        float acc[kNE];
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
+        const int i = vb * kBlock + tid;
+        if (i < n) acc_point(P, T, scale, dl, i, acc);
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) {
+            const float v = wave_total(acc[k]);
+            if (lane == 0) s_acc[wid][k] = v;
+        }
+        __syncthreads();
+        if (tid < kNE) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
+            dst[static_cast<size_t>(vb) * kNE + tid] = v;
+        }
+        __syncthreads();
+    }
+}
+
+// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
+// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate).
 // ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
 template <int NW, bool ONE_WAVE>
 __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G) {
@@ -539,6 +604,12 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
         if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
         return;
+    }
+    if constexpr (NW == 4 && !ONE_WAVE) {
+        if (wg >= G) {                                          // after the scale: the candidates need it
+            acc_candidate(P, s_scale, wg - G);
+            return;
+        }
     }
     if (lead && tid == 0) st->n_corr = nc;
     if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
@@ -682,8 +753,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, int it, int wg, int G
 }
 
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it) {
-    pko_body<NW, false>(P, it, blockIdx.x, gridDim.x);
+__global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it, int G) {
+    pko_body<NW, false>(P, it, blockIdx.x, G);
 }
 
 // Batched launch: blockIdx.y = job, gridDim.x workgroups per job split its alpha grid.  <4, false>: the
@@ -694,7 +765,7 @@ __global__ __launch_bounds__(NW * 64) void k_pko_tb(const KParams* __restrict__ 
     pko_body<NW, ONE_WAVE>(PB[blockIdx.y], it, blockIdx.x, gridDim.x);
 }
 
-template __global__ void k_pko_t<4>(KParams, int);
+template __global__ void k_pko_t<4>(KParams, int, int);
 template __global__ void k_pko_tb<4, false>(const KParams*, int);
 template __global__ void k_pko_tb<1, true>(const KParams*, int);
 

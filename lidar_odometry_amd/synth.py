@@ -227,19 +227,34 @@ def mid360_scene(seed: int = 107) -> Scene:
         yaw = k * np.pi / 2
         c = rot_z(yaw) @ np.array([18.0, 0.0, 0.0])
         boxes.append([c[0], c[1], 4.0, 0.4, 18.0, 4.0, yaw])
-    for _ in range(40):
-        boxes.append([rng.uniform(-15, 15), rng.uniform(-15, 15), rng.uniform(0.4, 1.5),
-                      rng.uniform(0.3, 1.5), rng.uniform(0.3, 1.5), rng.uniform(0.4, 1.5), rng.uniform(0, np.pi)])
-    cyls = [[rng.uniform(-15, 15), rng.uniform(-15, 15), rng.uniform(0.1, 0.3), 0.0, rng.uniform(2, 5)] for _ in range(12)]
+    # furniture stands on the floor, at most 1.4 m tall, and keeps >= 2.5 m clear of the sensor path
+    # (x, y) = 0.3 k, 0.1 k, k < 42 (bench.py, tests): a sensor boxed in by tall clutter sees only the nearest
+    # faces (a few hundred filtered points instead of the rosette's thousands)
+    def clear(x, y, radius):
+        t = np.clip((x * 12.3 + y * 4.1) / (12.3 ** 2 + 4.1 ** 2), 0.0, 1.0)
+        return math.hypot(x - 12.3 * t, y - 4.1 * t) - radius > 2.5
+    while len(boxes) < 28:
+        hz = rng.uniform(0.3, 0.7)
+        b = [rng.uniform(-15, 15), rng.uniform(-15, 15), hz,
+             rng.uniform(0.3, 1.2), rng.uniform(0.3, 1.2), hz, rng.uniform(0, np.pi)]
+        if clear(b[0], b[1], math.hypot(b[3], b[4])):
+            boxes.append(b)
+    cyls = []
+    while len(cyls) < 12:
+        c = [rng.uniform(-15, 15), rng.uniform(-15, 15), rng.uniform(0.15, 0.35), 0.0, rng.uniform(3, 8)]
+        if clear(c[0], c[1], c[2]):
+            cyls.append(c)
     return Scene(np.array(boxes), np.array(cyls))
 
 
 def mid360_like_scan(scene: Scene, T: np.ndarray, frame: int, n_rays: int = 24000) -> np.ndarray:
-    """Rosette-like non-repetitive pattern: golden-angle azimuth, petal-modulated elevation in [-7, 52] deg."""
+    """Non-repetitive pattern over the MID360 field of view (360 deg x [-7, 52] deg): the R2 low-discrepancy
+    sequence in (azimuth, elevation), continued across frames.  (A golden-angle azimuth with a 7x golden-ratio
+    elevation phase puts every ray on one 7-petal curve -- 11k returns in ~350 voxels of 0.4 m.)"""
     k = np.arange(n_rays) + frame * n_rays
-    az = (k * 2.399963229728653) % (2 * np.pi)
-    phase = (k * 0.618033988749895 * 7.0) % 1.0
-    el = np.deg2rad(-7.0 + 59.0 * (0.5 - 0.5 * np.cos(np.pi * phase)))
+    az = 2.0 * np.pi * ((k * 0.7548776662466927) % 1.0)
+    phase = (k * 0.5698402909980532) % 1.0
+    el = np.deg2rad(-7.0 + 59.0 * phase)
     dirs = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], axis=-1)
     rng = np.random.default_rng(1107 + frame)
     r = scene.raycast(T[:3, 3], dirs @ T[:3, :3].T, max_range=40.0, near=60.0)
