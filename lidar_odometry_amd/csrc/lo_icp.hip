@@ -26,6 +26,7 @@ __global__ void k_pko_finish(KParams P);
 __global__ void k_accumulate(KParams P, int it, int fuse);
 __global__ void k_solve(KParams P, int it, int ne_only);
 __global__ void k_solve_pick(KParams P, int it);
+__global__ void k_solve_correspond(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
@@ -546,9 +547,22 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         KParams P0 = P;                                   // first k_correspond also resets the GN state
         P0.init = 1;
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
+        std::memcpy(P.T0, T_init, sizeof(float) * 12);   // k_solve_correspond's pose before iteration 0
+        // surfel path, small scan, PKO: the solve of iteration it runs fused with the correspondence search of
+        // it + 1 (k_solve_correspond), the last solve alone (k_solve_pick)
+        const bool fused = !c->kd && spec_ok(P) && g.max_iterations <= LO_MAX_ITERS;
         for (int it = 0; it < g.max_iterations; ++it) {
-            launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
-            launch_gn_tail(c, P, it);
+            if (!fused) {
+                launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
+                launch_gn_tail(c, P, it);
+                continue;
+            }
+            if (it == 0) launch_correspond(c, P0, 1, false);
+            launch_pko_spec(c, P, it);
+            if (it + 1 < g.max_iterations)
+                hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
+            else
+                hipLaunchKernelGGL(k_solve_pick, dim3(1), dim3(kBlock), 0, c->stream, P, it);
         }
         LO_HIP(c, hipGetLastError());
     }

@@ -30,18 +30,8 @@ namespace lo {
 // the kernel argument (T0 / T0p), block 0 writes the fresh DevState that the later kernels of the scan read.
 // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
 // instead of serialising at the start of every wave.
-__device__ __forceinline__ void correspond_body(const KParams& P, int with_stats, int init, int blk) {
-    const int i = blk * kBlock + threadIdx.x;
-    const int n = scan_n(P);
-    float px = 0.0f, py = 0.0f, pz = 0.0f;
-    if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
-    const DevState* cst = P.st;
-    const int done = cst->done;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
-    if (!init && done) return;
-    scan_pose(P, init, blk, T);
+__device__ __forceinline__ void correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
+                                                int i, int n, int with_stats, int blk) {
     int slot = -1;
     double r = 0.0;
     if (i < n) {
@@ -56,6 +46,21 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
     }
     corr_epilogue(P, slot >= 0, r, with_stats, blk);
+}
+
+__device__ __forceinline__ void correspond_body(const KParams& P, int with_stats, int init, int blk) {
+    const int i = blk * kBlock + threadIdx.x;
+    const int n = scan_n(P);
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    const DevState* cst = P.st;
+    const int done = cst->done;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
+    if (!init && done) return;
+    scan_pose(P, init, blk, T);
+    correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
 }
 
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
@@ -287,14 +292,12 @@ __device__ void ldlt6_solve(const double* Hin, const double* b, double* x) {
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 
-// NT fixes the summation pattern of the nrows x kNE block partials (part_src: global or LDS); the calling block
-// may be larger than NT (its extra threads only join the barriers).
+// NT fixes the summation pattern of the nrows x kNE block partials (part_src: global or LDS) into tot[kNE] (LDS);
+// the calling block may be larger than NT (its extra threads only join the barriers).
 template <int NT>
-__device__ void solve_tail(const KParams& P, int it, int ne_only, const double* part_src, int nrows) {
-    DevState* st = P.st;
+__device__ __forceinline__ void solve_sums(const double* part_src, int nrows, double* tot) {
     constexpr int kQ = NT / kNE;                     // partial rows per entry (36 for 1024 threads, 9 for 256)
     __shared__ double part[kQ][kNE];
-    __shared__ double tot[kNE];
     const int tid = threadIdx.x;
     if (tid < kQ * kNE) {
         // thread t sums flat entries t, t + kQ*kNE, ... of part_src[nrows][kNE]: coalesced, entry = t % kNE
@@ -318,20 +321,21 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* 
         tot[tid] = s;
     }
     __syncthreads();
-    if (tid != 0) return;
+}
 
+// One lane: H, g, cost from the summed normal equations, pivoted LDLT (:418), SE3 right-update of pose_old into
+// pose_new with SO(3) re-projection (:422-434); with publish also the GN state (pose, per-iteration log, iteration
+// count, convergence flag :437-448).  Returns the convergence test.  pose_old may alias DevState::pose (it is read
+// before anything is written).
+__device__ bool solve_core(const KParams& P, int it, const double* tot, const float* pose_old, float* pose_new,
+                           bool publish) {
+    DevState* st = P.st;
     double H[36], g[6];
     int k = 0;
     for (int r = 0; r < 6; ++r)
         for (int c = 0; c <= r; ++c) { H[r * 6 + c] = tot[k]; H[c * 6 + r] = tot[k]; ++k; }
     for (int j = 0; j < 6; ++j) g[j] = tot[21 + j];
     const double cost = tot[27];
-    if (ne_only) {
-        for (int q = 0; q < 36; ++q) st->H_out[q] = H[q];
-        for (int j = 0; j < 6; ++j) st->g_out[j] = g[j];
-        st->cost_out = cost;
-        return;
-    }
     double mg[6], dd[6];
     for (int j = 0; j < 6; ++j) mg[j] = -g[j];
     ldlt6_solve(H, mg, dd);                                           // :418
@@ -340,7 +344,7 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* 
     const float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
 
     float R[9], t[3];
-    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) R[r * 3 + c] = st->pose[r * 4 + c]; t[r] = st->pose[r * 4 + 3]; }
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) R[r * 3 + c] = pose_old[r * 4 + c]; t[r] = pose_old[r * 4 + 3]; }
     float Rd[9];
     if (sqrtf(dot3f(dw[0], dw[1], dw[2], dw[0], dw[1], dw[2])) < 1e-10f) {   // :427-431
         for (int q = 0; q < 9; ++q) Rd[q] = (q % 4 == 0) ? 1.0f : 0.0f;
@@ -352,13 +356,16 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* 
     so3_project(M, Rn);
     float tn[3];
     for (int r = 0; r < 3; ++r) tn[r] = t[r] + dot3f(R[r * 3], R[r * 3 + 1], R[r * 3 + 2], dt[0], dt[1], dt[2]);
-    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) st->pose[r * 4 + c] = Rn[r * 3 + c]; st->pose[r * 4 + 3] = tn[r]; }
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) pose_new[r * 4 + c] = Rn[r * 3 + c]; pose_new[r * 4 + 3] = tn[r]; }
 
     const float tdel = sqrtf(dot3f(dt[0], dt[1], dt[2], dt[0], dt[1], dt[2]));
     const float rdel = sqrtf(dot3f(dw[0], dw[1], dw[2], dw[0], dw[1], dw[2]));
+    const bool conv = tdel < P.tol_t && rdel < P.tol_r;               // :443-448
+    if (!publish) return conv;
+    for (int q = 0; q < 12; ++q) st->pose[q] = pose_new[q];
     if (it < LO_MAX_ITERS) {                                          // the loop-closure ICP runs up to 100
         lo_iter_log& L = st->logs[it];
-        for (int q = 0; q < 12; ++q) L.pose[q] = st->pose[q];
+        for (int q = 0; q < 12; ++q) L.pose[q] = pose_new[q];
         L.n_corr = st->n_corr;
         L.scale = st->scale;
         L.alpha = st->alpha;
@@ -368,7 +375,26 @@ __device__ void solve_tail(const KParams& P, int it, int ne_only, const double* 
         for (int j = 0; j < 6; ++j) { L.g[j] = static_cast<float>(g[j]); L.delta[j] = delta[j]; }
     }
     st->iter = it + 1;
-    if (tdel < P.tol_t && rdel < P.tol_r) st->done = 1;               // :443-448
+    if (conv) st->done = 1;
+    return conv;
+}
+
+template <int NT>
+__device__ void solve_tail(const KParams& P, int it, int ne_only, const double* part_src, int nrows) {
+    DevState* st = P.st;
+    __shared__ double tot[kNE];
+    solve_sums<NT>(part_src, nrows, tot);
+    if (threadIdx.x != 0) return;
+    if (ne_only) {
+        int k = 0;
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c <= r; ++c) { st->H_out[r * 6 + c] = tot[k]; st->H_out[c * 6 + r] = tot[k]; ++k; }
+        for (int j = 0; j < 6; ++j) st->g_out[j] = tot[21 + j];
+        st->cost_out = tot[27];
+        return;
+    }
+    float pn[12];
+    solve_core(P, it, tot, st->pose, pn, true);
 }
 
 // Standalone solve over all block partials (lo_bench_kernel; the GN loop fuses it into k_accumulate)
@@ -393,6 +419,43 @@ __global__ __launch_bounds__(kBlock) void k_solve_pick(KParams P, int it) {
     }
     __syncthreads();
     solve_tail<kBlock>(P, it, 0, P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc);
+}
+
+// The solve of GN iteration it fused with the correspondence search of iteration it + 1 (single small scans with
+// PKO, surfel path): every block reduces the selected candidate's partials and solves redundantly -- same data,
+// same code, so the same pose in every block -- then searches its 256 points with the new pose; block 0
+// publishes the GN state.  The old pose is read from the previous iteration's log (the initial pose for it = 0),
+// which no block of this launch writes.  One launch per GN iteration fewer than k_solve_pick + k_correspond.
+__global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) {
+    DevState* st = P.st;
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    const int i = blk * kBlock + tid;
+    const int n = scan_n(P);
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    if (st->done) return;
+    __shared__ int s_c, s_done;
+    __shared__ double tot[kNE];
+    __shared__ float s_T[12];
+    if (tid < kWave) {
+        const int bi = pko_select_index(P);
+        if (tid == 0) {
+            s_c = bi > 0 ? bi - 1 : P.NA;
+            if (blk == 0) st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
+        }
+    }
+    __syncthreads();
+    solve_sums<kBlock>(P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc, tot);
+    if (tid == 0) {
+        const float* pose_old = it == 0 ? P.T0 : st->logs[it - 1].pose;
+        s_done = solve_core(P, it, tot, pose_old, s_T, blk == 0) ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_done) return;                          // converged: the later launches of the scan see DevState::done
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = s_T[k];
+    correspond_tail(P, T, px, py, pz, i, n, 0, blk);
 }
 
 // Batched solve (jobs with more than kFuseMaxBlocks accumulate blocks present): one block per job, with the
