@@ -167,6 +167,39 @@ def test_optimize_kitti_like_per_iteration(icp, frame):
     _compare_optimize(icp, m, pts, Ti)
 
 
+@pytest.mark.parametrize("max_iters,tol,pko", [(1, 0.005, True), (2, 1e-9, True), (6, 1e-9, True), (6, 1e-9, False)])
+def test_optimize_launch_shapes(max_iters, tol, pko):
+    """Every GN-loop launch shape of a small scan against the oracle with the same config.  With PKO: the first
+    k_correspond, then per iteration k_pko_t (+ every alpha candidate's normal equations) and k_solve_correspond
+    (the solve fused with the next iteration's correspondences), the last solve alone (k_solve_pick).  Without
+    PKO: k_correspond, k_accumulate with the last-block solve.  Tolerance 1e-9 runs all max_iterations."""
+    from lidar_odometry_amd import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer
+    m, pts, Ti, _ = _data.kitti_case(13)
+    cfg = ICPConfig(max_iterations=max_iters, translation_tolerance=tol, rotation_tolerance=tol)
+    o = IterativeClosestPointOptimizer(cfg, AdaptiveMEstimatorConfig(use_adaptive_m_estimator=pko), max_points=1 << 16)
+    try:
+        _load_map(o, m)
+        ocfg = oracle.kitti_icp_cfg(max_iters)
+        ocfg.translation_tolerance = tol
+        ocfg.rotation_tolerance = tol
+        ocfg.use_pko = int(pko)
+        ok_o, To_o, it_o, logs_o = oracle.icp_optimize(m, pts, Ti, ocfg)
+        ok_g, To_g = o.optimize(None, pts, Ti)
+        st = o.get_last_stats()
+        assert ok_g == ok_o and st.num_iterations == it_o
+        if tol < 1e-6:
+            assert it_o == max_iters
+        for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+            et, er = _pose_err(lg["pose"], lo["pose"])
+            assert et <= TOL_T and er <= TOL_R, f"iter {k}: dt {et:.2e} m, dr {er:.2e} rad"
+            if k == 0:
+                assert lg["n_corr"] == lo["n_corr"] and lg["alpha"] == lo["alpha"]
+        et, er = _pose_err(To_g, To_o)
+        assert et <= TOL_T and er <= TOL_R
+    finally:
+        o.close()
+
+
 def test_optimize_large_perturbation(icp):
     m, pts, Ti, Tgt = _data.kitti_case(15, seed=5, sigma_t=0.3, sigma_r=0.03)
     _load_map(icp, m)
