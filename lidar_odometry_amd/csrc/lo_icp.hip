@@ -27,6 +27,7 @@ __global__ void k_accumulate(KParams P, int it, int fuse);
 __global__ void k_solve(KParams P, int it, int ne_only);
 __global__ void k_solve_pick(KParams P, int it);
 __global__ void k_solve_correspond(KParams P, int it);
+__global__ void k_solve_knn(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
@@ -548,20 +549,25 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         P0.init = 1;
         std::memcpy(P0.T0, T_init, sizeof(float) * 12);
         std::memcpy(P.T0, T_init, sizeof(float) * 12);   // k_solve_correspond's pose before iteration 0
-        // surfel path, small scan, PKO: the solve of iteration it runs fused with the correspondence search of
-        // it + 1 (k_solve_correspond), the last solve alone (k_solve_pick)
-        const bool fused = !c->kd && spec_ok(P) && g.max_iterations <= LO_MAX_ITERS;
+        // small scan with PKO: the solve of iteration it runs fused with the correspondence search of it + 1
+        // (k_solve_correspond; KDTree: k_solve_knn, then k_knn_brute + k_plane), the last solve alone (k_solve_pick)
+        const bool fused = spec_ok(P) && g.max_iterations <= LO_MAX_ITERS;
         for (int it = 0; it < g.max_iterations; ++it) {
             if (!fused) {
                 launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
                 launch_gn_tail(c, P, it);
                 continue;
             }
-            if (it == 0) launch_correspond(c, P0, 1, false);
+            if (it == 0) launch_correspond(c, P0, 1, c->kd);
             launch_pko_spec(c, P, it);
-            if (it + 1 < g.max_iterations)
+            if (it + 1 < g.max_iterations && !c->kd) {
                 hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
-            else
+            } else if (it + 1 < g.max_iterations) {
+                hipLaunchKernelGGL(k_solve_knn, dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock),
+                                   dim3(kBlock), 0, c->stream, P, it);
+                hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, P);
+                hipLaunchKernelGGL(k_plane, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
+            } else
                 hipLaunchKernelGGL(k_solve_pick, dim3(1), dim3(kBlock), 0, c->stream, P, it);
         }
         LO_HIP(c, hipGetLastError());

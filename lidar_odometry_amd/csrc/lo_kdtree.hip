@@ -22,6 +22,7 @@
 // breaks them by tree-visit order (NANOFLANN_FIRST_MATCH is not defined), so exact ties are parity-unpinned.
 // Non-finite queries find nothing (nanoflann only adds points with dist < worstDist = FLT_MAX).
 #include "lo_device.h"
+#include "lo_solve.h"
 
 #include <cfloat>
 
@@ -132,16 +133,13 @@ __device__ __forceinline__ void scan_range8(const KParams& P, uint32_t s, uint32
 
 constexpr int kKnnRowsMax = 4;          // rows of one round per lane: r = 3 has 49 rows over 16 lanes
 
-__global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
-    if (!P.init && P.st->done) return;
+__device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12]) {
     // kKnnGroup consecutive lanes (one DPP row) share one query: lane g takes rows g, g + 16, ... of each round.
     // The first round scans the whole 3x3x3 cube (the r = 0 cell alone almost never certifies: its faces are
     // < h / 2 away while the 5th neighbour of a surface sample is ~h); later rounds scan the shell r.  A lane's
     // cell-range bounds for the round are loaded together, then its ranges are scanned 8 points at a time.
     const int gi = blockIdx.x * kBlock + threadIdx.x;
     const int i = gi / kKnnGroup, g = gi % kKnnGroup;
-    float T[12];
-    scan_pose(P, P.init, blockIdx.x, T);
     if (i >= scan_n(P)) return;                              // whole groups leave together
     int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
     float qx, qy, qz;
@@ -214,6 +212,45 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     if (grp.n < 5) { out[0] = -1; return; }
 #pragma unroll
     for (int k = 0; k < 5; ++k) out[k] = grp.pos[k];
+}
+
+__global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
+    if (!P.init && P.st->done) return;
+    float T[12];
+    scan_pose(P, P.init, blockIdx.x, T);
+    knn_body(P, T);
+}
+
+// The solve of GN iteration it fused with the kNN search of iteration it + 1 (small scans with PKO; the
+// counterpart of k_solve_correspond in lo_kernels.hip): every block reduces the selected candidate's partials and
+// solves redundantly (the same pose everywhere), block 0 publishes the GN state -- k_knn_brute and k_plane read
+// the pose from it -- and the old pose comes from the previous iteration's log (the initial pose for it = 0).
+__global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
+    DevState* st = P.st;
+    if (st->done) return;
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    __shared__ int s_c, s_done;
+    __shared__ double tot[kNE];
+    __shared__ float s_T[12];
+    if (tid < kWave) {
+        const int bi = pko_select_index(P);
+        if (tid == 0) {
+            s_c = bi > 0 ? bi - 1 : P.NA;
+            if (blk == 0) st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
+        }
+    }
+    __syncthreads();
+    solve_sums<kBlock>(P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc, tot);
+    if (tid == 0) {
+        const float* pose_old = it == 0 ? P.T0 : st->logs[it - 1].pose;
+        s_done = solve_core(P, it, tot, pose_old, s_T, blk == 0) ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_done) return;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = s_T[k];
+    knn_body(P, T);
 }
 
 // ====================================================================================================
