@@ -1,7 +1,10 @@
 // lo_kernels.hip — HIP kernels of the point-to-plane ICP hot path for gfx950 (MI355X / CDNA4).
 //
 // One Gauss-Newton iteration of IterativeClosestPointOptimizer::optimize
-// (reference src/optimization/IterativeClosestPointOptimizer.cpp:281-449) is four launches on one stream:
+// (reference src/optimization/IterativeClosestPointOptimizer.cpp:281-449) is built from these launches on one
+// stream (small scans with PKO: k_pko also accumulates every alpha candidate's normal equations and the solve runs
+// fused with the next iteration's correspondences, k_solve_correspond -- two launches per iteration; see
+// launch_gn_tail / enqueue_optimize in lo_icp.hip):
 //   k_correspond  per point: transform, L1 surfel probe, fp64 residual, accept r <= max_corr
 //                 (find_correspondences :587-645); per-wave validity ballots; iteration 0 also the
 //                 per-block residual sum / M2 for the normalisation scale (:304-316)
