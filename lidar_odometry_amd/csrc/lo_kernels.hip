@@ -206,11 +206,11 @@ __global__ __launch_bounds__(kBlock) void k_solve_pick(KParams P, int it) {
 __global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) {
     DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
+    if (st->done) return;                        // before any other load: an early exit costs one round trip
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);
-    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    float px = 0.0f, py = 0.0f, pz = 0.0f;       // in flight during the solve
     if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
-    if (st->done) return;
     __shared__ int s_c, s_done;
     __shared__ double tot[kNE];
     __shared__ float s_T[12];
