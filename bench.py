@@ -35,6 +35,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_JSON_OUT = None
+
+
+def emit(result: dict):
+    """Print the ONE JSON line on the original stdout.  Native libraries (gloo, RCCL, HIP) print to fd 1 too, so
+    once the ranks are up fd 1 points at stderr and only this line reaches stdout."""
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(result) + "\n")
+    out.flush()
+
+
+def _claim_stdout():
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
 # --------------------------------------------------------------------------------------------------
 # workloads (product-side data path only: synth + lo_voxelmap + lo_voxel_filter)
 # --------------------------------------------------------------------------------------------------
@@ -331,9 +350,119 @@ def run_loop(args, world, rank, local):
     return result
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script, one per GPU (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1), and return the worst exit code.  This parent never imports torch
+    or touches the GPU, so no process that initialised HIP is ever replaced; the children inherit stdout, and only
+    rank 0 prints the JSON line.  If one rank fails the others are terminated (they would wait in a barrier)."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                log(f"[launcher] rank {procs.index(p)} exited with {c}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def check_gathered(gather, step: int, own: np.ndarray, rank: int, world: int, dist) -> dict:
+    """The RCCL (or gloo) all-gathered records of `step` must hold every rank's own exported record in rank order:
+    each rank contributes its own record through a separate object all-gather (host side, independent of the
+    pipelined tensor collective) and every rank compares the two."""
+    got = gather.records(step)
+    mine = [None] * world
+    dist.all_gather_object(mine, own.tolist())
+    want = np.asarray(mine, np.float32).reshape(world, -1)
+    ok = bool(np.array_equal(got, want))
+    if not ok:
+        raise RuntimeError(f"[rank {rank}] gathered pose records differ from the ranks' own records at step {step}:\n"
+                           f"{got}\nvs\n{want}")
+    return {"step": step, "ranks": world, "records_equal": ok,
+            "statuses": [int(x) for x in got[:, 12]], "iterations": [int(x) for x in got[:, 13]]}
+
+
+def run_dry(args, world, rank):
+    """`--dry-run`: the launcher / rendezvous / gather / timing plumbing on CPU (gloo) with NO ICP: each step's
+    record is the step's initial pose with the rank and step in the status fields.  For rehearsing `--gpus N` where
+    no GPU exists; the line says so and carries no throughput claim about the ICP."""
+    import torch
+    import torch.distributed as dist
+    from lidar_odometry_amd.parallel import PipelinedPoseGather
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    gather = PipelinedPoseGather(world, None)
+    rng = np.random.default_rng(rank)
+    own = None
+
+    def step(k):
+        nonlocal own
+        r = gather.slot()
+        rec = np.zeros(16, np.float32)
+        rec[:12] = rng.standard_normal(12)
+        rec[12], rec[13], rec[14] = 0.0, float(k % 4 + 1), float(rank)
+        r.copy_(torch.from_numpy(rec))
+        own = rec
+        gather.launch()
+
+    for k in range(args.warmup):
+        step(k)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    els = [el]
+    chk = None
+    if world > 1:
+        gather.drain()
+        chk = check_gathered(gather, args.warmup + args.steps - 1, own, rank, world, dist)
+        els = [None] * world
+        dist.all_gather_object(els, el)
+        el = max(els)
+    res = {"metric": "bench.py --dry-run (launcher / gather plumbing only, no ICP)", "value": args.steps * world / el,
+           "unit": "records/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic records",
+           "config": {"workload": "dry run: pose-record all-gather over gloo", "parallelism": f"x{world} ranks"},
+           "per_rank_s": els, "gather_check": chk}
+    if world > 1:
+        dist.destroy_process_group()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment this process spawns them")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for the pose gather (nccl = RCCL; gloo moves the records through host "
+                         "memory, e.g. to rehearse N ranks sharing one GPU)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU plumbing rehearsal without ICP (see run_dry)")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS) + ["kitti_e2e", "kitti_loop"])
@@ -351,22 +480,38 @@ def main():
     global ORDER
     ORDER = args.order
 
+    if args.gpus < 1:
+        sys.exit(f"--gpus must be >= 1 (got {args.gpus})")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    _claim_stdout()
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report a {args.gpus}-GPU line "
+                 f"from {world} rank(s)")
+    if args.dry_run:
+        res = run_dry(args, world, rank)
+        if rank == 0:
+            emit(res)
+        return
     import torch
     import torch.distributed as dist
     # one rank per GPU; more ranks than GPUs (a rehearsal on a small box) wrap around
     local %= max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend="gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     if args.config in ("kitti_e2e", "kitti_loop"):
         result = (run_e2e if args.config == "kitti_e2e" else run_loop)(args, world, rank, local)
         if rank == 0:
-            print(json.dumps(result), flush=True)
+            emit(result)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -396,7 +541,9 @@ def main():
     fptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))   # noqa: E731
     from lidar_odometry_amd.parallel import PipelinedPoseGather
     # scan-parallel replicas: the only collective is the per-step pose all-gather (RCCL), on a side stream
-    gather = PipelinedPoseGather(world, dev)
+    gloo = world > 1 and args.dist_backend == "gloo"
+    gather = PipelinedPoseGather(world, None if gloo else dev)
+    dev_rec = torch.zeros(16, dtype=torch.float32, device=dev)
 
     def step(k):
         i = k % len(d_scans)
@@ -408,7 +555,11 @@ def main():
         if rc != 0:
             raise RuntimeError(f"lo_icp_optimize_async rc={rc}: {L.lo_last_error(icp.ctx).decode()}")
         if world > 1:
-            L.lo_icp_export_pose(icp.ctx, C.c_void_p(gather.slot().data_ptr()))
+            if gloo:                                  # host-memory collective: D2H of the record, then gloo
+                L.lo_icp_export_pose(icp.ctx, C.c_void_p(dev_rec.data_ptr()))
+                gather.slot().copy_(dev_rec)
+            else:                                     # RCCL on the side stream, off the critical path
+                L.lo_icp_export_pose(icp.ctx, C.c_void_p(gather.slot().data_ptr()))
             gather.launch()
 
     # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them)
@@ -433,10 +584,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    per_rank = [el]
+    gather_check = None
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        gather.drain()
+        last = args.warmup + args.steps - 1
+        own = gather.recs[last % gather.depth].detach().cpu().numpy()
+        # this rank's own record of the last step, exported by the ICP context, against the collective's result
+        want_it = iters[(args.steps - 1) % len(iters)]           # the last timed step ran scan (steps-1) % n
+        assert int(own[13]) == want_it, (own, want_it)
+        gather_check = check_gathered(gather, last, own, rank, world, dist)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, el)
+        el = max(per_rank)
     total_scans = args.steps * world
     total_iters = sum(iters[k % len(iters)] for k in range(args.steps)) * world
 
@@ -626,6 +786,8 @@ def main():
                    "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step, side stream)" if world > 1
                    else "single GPU, one HIP stream"},
         "gn_iters_per_sec": total_iters / el,
+        "per_rank": None if world == 1 else {"scans_per_s": [args.steps / e for e in per_rank], "timed_s": per_rank,
+                                             "backend": args.dist_backend, "gather_check": gather_check},
         "translation_error_vs_gt_m_median": float(np.median(errs)),
         "kernel_us": kern_us,
         "step_device_us_est": {"per_kernel": per_scan, "dominant_kernel": dom,
@@ -646,7 +808,7 @@ def main():
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
     icp.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if world > 1:
         dist.destroy_process_group()
 

@@ -229,6 +229,9 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
 static int validate_config(const lo_config* g, std::string& err) {
     if (!g) { err = "null config"; return LO_ERR_ARG; }
     if (g->max_iterations < 1 || g->max_iterations > LO_MAX_ITERS) { err = "max_iterations out of [1, 64]"; return LO_ERR_ARG; }
+    // >= 1: an iteration with no correspondence always fails (the reference would fall back to robust_loss_delta
+    // with an empty system, IterativeClosestPointOptimizer.cpp:298-331; never reached with its default of 10)
+    if (g->min_correspondence_points < 1) { err = "min_correspondence_points must be >= 1"; return LO_ERR_ARG; }
     if (g->gmm_sample_size < 1 || g->gmm_sample_size > kMaxS) { err = "gmm_sample_size out of [1, 256]"; return LO_ERR_ARG; }
     if (g->gmm_components < 1 || g->gmm_components > 3) { err = "gmm_components out of [1, 3]"; return LO_ERR_ARG; }
     if (g->num_alpha_segments < 1 || g->num_alpha_segments > kMaxAlpha) { err = "num_alpha_segments out of [1, 1000]"; return LO_ERR_ARG; }

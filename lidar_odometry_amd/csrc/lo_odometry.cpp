@@ -114,6 +114,13 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
         fi->status = LO_OK;
         return LO_OK;
     }
+    if (o->keyframes == 0) {
+        // the first frame filtered to nothing: the reference made no keyframe and every later frame returns at
+        // "No keyframe available" (Estimator.cpp:140-144) without ICP, pose update or keyframe test
+        lo::se3_to12(o->prev, T_out);
+        fi->status = LO_OK;
+        return LO_OK;
+    }
     const SE3f guess = lo::se3_mul(o->prev, o->velocity);                    // :154
     // estimate_motion_dual_frame hands optimize SE3f(guess.R, guess.t), i.e. SO3(R) re-projected (:284), and
     // wraps the result the same way (:308); on failure it returns the guess itself (:304-307)

@@ -35,7 +35,7 @@ struct VfBuffers {
     int* n_out = nullptr;        // &ctr->n_out
 };
 
-hipError_t vf_reserve(VfBuffers& b, size_t m);
+hipError_t vf_reserve(VfBuffers& b, size_t m, hipStream_t s);
 void vf_free(VfBuffers& b);
 // Filter d_raw (n_raw AoS float3) into d_out on stream s; the output count lands in b.n_out (device).
 // m_out = ceil(n_raw / stride), an upper bound of the output count.

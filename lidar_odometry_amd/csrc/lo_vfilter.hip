@@ -321,8 +321,15 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ samp,
 }
 
 // ---------------------------------------------------------------- host side (called from lo_icp.hip)
-hipError_t vf_reserve(VfBuffers& b, size_t m) {
+// Grows the filter's buffers on the context stream s: the old buffers may still be read by filter launches
+// queued on s, so s (only) is drained before they are freed, and the table init runs on s, ordered before the
+// next k_vf_insert without a device-wide synchronisation that would stall other contexts sharing the GPU.
+hipError_t vf_reserve(VfBuffers& b, size_t m, hipStream_t s) {
     if (b.ctr != nullptr && m <= b.cap) return hipSuccess;
+    if (b.ctr != nullptr) {
+        hipError_t e0 = hipStreamSynchronize(s);
+        if (e0 != hipSuccess) return e0;
+    }
     void* old[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : old) if (p) (void)hipFree(p);
     b = VfBuffers{};
@@ -341,10 +348,9 @@ hipError_t vf_reserve(VfBuffers& b, size_t m) {
     if ((e = hipMalloc(&b.mid, cap * sizeof(int32_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.big, cap * sizeof(int32_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.ctr, sizeof(VfCounters))) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_vf_init, dim3(static_cast<unsigned>((tcap + 255) / 256)), dim3(256), 0, nullptr, b.tkey, b.tslot,
+    hipLaunchKernelGGL(k_vf_init, dim3(static_cast<unsigned>((tcap + 255) / 256)), dim3(256), 0, s, b.tkey, b.tslot,
                        static_cast<int>(tcap), b.ctr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
     b.cap = cap;
     b.tcap = tcap;
     b.n_out = &b.ctr->n_out;
@@ -364,7 +370,7 @@ hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride
                       hipStream_t s, int& m_out) {
     const size_t m = (n_raw + stride - 1) / stride;
     m_out = static_cast<int>(m);
-    hipError_t e = vf_reserve(b, m);
+    hipError_t e = vf_reserve(b, m, s);
     if (e != hipSuccess) return e;
     if (m == 0) return hipMemsetAsync(b.n_out, 0, sizeof(int), s);
     const float inv = 1.0f / voxel_size;                 // m_inv_voxel_size (VoxelMap.h:57)

@@ -125,7 +125,8 @@ class IterativeClosestPointOptimizer:
         self.geometry = geometry or MapGeometry()
         self._cfg = make_config(self.config, self.adaptive, self.geometry, max_points)
         err = C.c_int(0)
-        self._ctx = lib().lo_create(C.byref(self._cfg), device, C.byref(err))
+        self._L = lib()
+        self._ctx = self._L.lo_create(C.byref(self._cfg), device, C.byref(err))
         if not self._ctx:
             raise RuntimeError(f"lo_create failed (code {err.value}); is a HIP device present?")
         self._map_token = None
@@ -133,12 +134,18 @@ class IterativeClosestPointOptimizer:
 
     # ------------------------------------------------------------------ lifetime
     def close(self):
-        if getattr(self, "_ctx", None):
-            lib().lo_destroy(self._ctx)
+        h = getattr(self, "_ctx", None)
+        if h:
             self._ctx = None
+            self._L.lo_destroy(h)
 
     def __del__(self):
-        self.close()
+        # at interpreter teardown module globals (lib, os) may already be None: the handle keeps its own
+        # reference to the loaded library, and a destructor never raises
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _check(self, rc):
         if rc < 0:
@@ -309,18 +316,25 @@ class BatchOptimizer:
         self.optimizers = list(optimizers)
         arr = (C.c_void_p * len(self.optimizers))(*[o.ctx for o in self.optimizers])
         err = C.c_int(0)
-        self._b = lib().lo_batch_create(arr, len(self.optimizers), C.byref(err))
+        self._L = lib()
+        self._b = self._L.lo_batch_create(arr, len(self.optimizers), C.byref(err))
         if not self._b:
             raise RuntimeError(f"lo_batch_create failed (code {err.value})")
         self.last_gpu_ms = 0.0
 
     def close(self):
-        if getattr(self, "_b", None):
-            lib().lo_batch_destroy(self._b)
+        h = getattr(self, "_b", None)
+        if h:
             self._b = None
+            self._L.lo_batch_destroy(h)
 
     def __del__(self):
-        self.close()
+        # at interpreter teardown module globals (lib, os) may already be None: the handle keeps its own
+        # reference to the loaded library, and a destructor never raises
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def __len__(self):
         return len(self.optimizers)

@@ -40,7 +40,8 @@ class LidarOdometry:
         cfg.keyframe_distance = float(keyframe_distance)
         cfg.keyframe_rotation = float(keyframe_rotation)
         err = C.c_int(0)
-        self._o = lib().lo_odom_create(C.byref(cfg), int(device), C.byref(err))
+        self._L = lib()
+        self._o = self._L.lo_odom_create(C.byref(cfg), int(device), C.byref(err))
         if not self._o:
             raise RuntimeError(f"lo_odom_create failed (code {err.value}); is a HIP device present?")
         if initial_pose is not None:
@@ -48,12 +49,18 @@ class LidarOdometry:
             lib().lo_odom_set_initial_pose(self._o, T.ctypes.data_as(C.POINTER(C.c_float)))
 
     def close(self):
-        if getattr(self, "_o", None):
-            lib().lo_odom_destroy(self._o)
+        h = getattr(self, "_o", None)
+        if h:
             self._o = None
+            self._L.lo_odom_destroy(h)
 
     def __del__(self):
-        self.close()
+        # at interpreter teardown module globals (lib, os) may already be None: the handle keeps its own
+        # reference to the loaded library, and a destructor never raises
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def process(self, raw_points):
         p = np.ascontiguousarray(raw_points, dtype=np.float32).reshape(-1, 3)

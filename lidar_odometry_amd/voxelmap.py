@@ -20,7 +20,8 @@ def _f(a):
 class VoxelMap:
     def __init__(self, voxel_size: float = 0.5, hierarchy_factor: int = 3, planarity_threshold: float = 0.1,
                  compute_surfels: bool = True):
-        self._h = lib().lo_voxelmap_create(voxel_size, hierarchy_factor, planarity_threshold, int(compute_surfels))
+        self._L = lib()
+        self._h = self._L.lo_voxelmap_create(voxel_size, hierarchy_factor, planarity_threshold, int(compute_surfels))
         if not self._h:
             raise ValueError("invalid VoxelMap parameters (voxel_size > 0, odd hierarchy_factor)")
         self.voxel_size = voxel_size
@@ -28,12 +29,18 @@ class VoxelMap:
         self.revision = 0
 
     def close(self):
-        if getattr(self, "_h", None):
-            lib().lo_voxelmap_destroy(self._h)
+        h = getattr(self, "_h", None)
+        if h:
             self._h = None
+            self._L.lo_voxelmap_destroy(h)
 
     def __del__(self):
-        self.close()
+        # at interpreter teardown module globals (lib, os) may already be None: the handle keeps its own
+        # reference to the loaded library, and a destructor never raises
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @property
     def handle(self):

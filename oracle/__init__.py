@@ -174,12 +174,18 @@ def odometry(raw_scans, stride=8, voxel=0.5, map_voxel=0.5, max_range=100.0, kf_
     m = VoxelMap(map_voxel, 3, 0.1, True)
     poses, kfs = [], []
     prev = vel = last_kf = I
+    n_kf = 0
     for k, raw in enumerate(raw_scans):
         pts = voxel_filter(raw, voxel, stride)
         kf = False
         if k == 0:
             pose = P0
             kf = len(pts) > 0
+        elif n_kf == 0:
+            # empty first frame: no keyframe was made, so every later frame returns early (Estimator.cpp:140-144)
+            poses.append(np.asarray(prev, np.float32).reshape(12))
+            kfs.append(False)
+            continue
         else:
             guess = se3_compose(prev, vel)
             g_in = guess.copy().reshape(3, 4)
@@ -196,6 +202,7 @@ def odometry(raw_scans, stride=8, voxel=0.5, map_voxel=0.5, max_range=100.0, kf_
             kf = d > kf_dist or a > kf_rot
         prev = pose
         if kf:
+            n_kf += 1
             w = transform_points(pts, pose)
             m.update(w, np.asarray(pose, np.float32).reshape(3, 4)[:, 3].astype(np.float64), 1.2 * max_range, True)
             last_kf = pose

@@ -69,3 +69,25 @@ def test_trajectory_file_roundtrip(runs, tmp_path):
     io.save_trajectory_kitti(f, [g.reshape(3, 4) for g in got])
     back = io.load_trajectory_kitti(f)
     np.testing.assert_allclose(back[:, :3, :4].reshape(-1, 12), got, atol=2e-9 + 1e-9 * np.abs(got).max())
+
+
+def test_empty_first_frame_never_starts_a_map():
+    """The reference's first frame with an empty feature cloud creates no keyframe (Estimator.cpp:247-251) and
+    every later frame returns at "No keyframe available" (:140-144): the pose stays at the initial pose."""
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.odometry import LidarOdometry
+    seq = synth.KittiLikeSequence(seed=7, n_frames=4, ramp_s=2.0)
+    raws = [np.zeros((0, 3), np.float32)] + [seq.scan(k) for k in range(1, 4)]
+    T0 = seq.poses[0]
+    od = LidarOdometry(initial_pose=T0)
+    try:
+        out = [od.process(r) for r in raws]
+        assert od.keyframes == 0
+    finally:
+        od.close()
+    ref, kfs = oracle.odometry(raws, initial=T0)
+    assert not any(kfs)
+    for k, (T, info) in enumerate(out):
+        assert info.status == 0 and not info.keyframe
+        np.testing.assert_array_equal(T.reshape(12), ref[k])
+        np.testing.assert_array_equal(T.reshape(12), np.asarray(T0, np.float32)[:3, :4].reshape(12))
