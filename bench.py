@@ -463,6 +463,9 @@ def main():
                     help="collective backend for the pose gather (nccl = RCCL; gloo moves the records through host "
                          "memory, e.g. to rehearse N ranks sharing one GPU)")
     ap.add_argument("--dry-run", action="store_true", help="CPU plumbing rehearsal without ICP (see run_dry)")
+    ap.add_argument("--check-records", action="store_true",
+                    help="diagnostic: keep every step's pose record and compare its iteration count with the pre-pass")
+    ap.add_argument("--data-rank", type=int, default=None, help="diagnostic: build the workload of this rank")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS) + ["kitti_e2e", "kitti_loop"])
@@ -520,7 +523,7 @@ def main():
     from lidar_odometry_amd.icp import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
 
     t_data = time.perf_counter()
-    wl = WORKLOADS[args.config](rank)
+    wl = WORKLOADS[args.config](rank if args.data_rank is None else args.data_rank)
     log(f"[rank {rank}] data built in {time.perf_counter() - t_data:.1f} s: {len(wl['scans'])} scans, "
         f"avg {np.mean([len(s) for s in wl['scans']]):.0f} pts, {wl['vm'].surfel_count()} surfels")
     max_pts = max(len(s) for s in wl["scans"])
@@ -531,7 +534,11 @@ def main():
     icp = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not kd), AdaptiveMEstimatorConfig(),
                                          MapGeometry(voxel_size=wl["voxel"]), device=local, max_points=max_pts)
     L = lib()
-    stream = torch.cuda.current_stream(dev)
+    # one stream shared by the ICP context and torch (pose-record copies, the gather's events): a dedicated stream,
+    # because handle 0 (torch's legacy default stream) means "the context's own non-blocking stream" to
+    # lo_set_stream, which the default stream does not order against
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
     rc = L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle)
     assert rc == 0, rc
@@ -544,6 +551,9 @@ def main():
     gloo = world > 1 and args.dist_backend == "gloo"
     gather = PipelinedPoseGather(world, None if gloo else dev)
     dev_rec = torch.zeros(16, dtype=torch.float32, device=dev)
+    # --check-records: every step's exported record kept on the device (diagnostic; adds one tiny launch per step)
+    rec_log = torch.zeros(args.warmup + args.steps, 16, dtype=torch.float32, device=dev) if args.check_records else None
+    n_step = [0]
 
     def step(k):
         i = k % len(d_scans)
@@ -561,6 +571,9 @@ def main():
             else:                                     # RCCL on the side stream, off the critical path
                 L.lo_icp_export_pose(icp.ctx, C.c_void_p(gather.slot().data_ptr()))
             gather.launch()
+        if rec_log is not None:
+            L.lo_icp_export_pose(icp.ctx, C.c_void_p(rec_log[n_step[0]].data_ptr()))
+        n_step[0] += 1
 
     # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them)
     iters, errs = [], []
@@ -584,6 +597,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    if rec_log is not None:
+        recs = rec_log.cpu().numpy()
+        ks = list(range(args.warmup)) + list(range(args.steps))
+        bad = [(j, ks[j] % len(iters), int(recs[j, 13]), iters[ks[j] % len(iters)]) for j in range(len(ks))
+               if int(recs[j, 13]) != iters[ks[j] % len(iters)]]
+        log(f"[rank {rank}] record check: {len(bad)} of {len(ks)} steps differ from the pre-pass iteration counts; "
+            f"first: {bad[:8]}")
     per_rank = [el]
     gather_check = None
     if world > 1:

@@ -123,7 +123,8 @@ int lo_icp_optimize_async(lo_ctx* ctx, const float* d_pts, size_t n, const float
 int lo_icp_result(lo_ctx* ctx, float T_out[12], lo_iter_log* logs, lo_stats* stats);
 int lo_sync(lo_ctx* ctx);
 void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
-/* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again. */
+/* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again (a fresh
+ * hipStreamNonBlocking stream -- so the legacy default stream, handle 0, cannot be selected: pass a created stream). */
 int lo_set_stream(lo_ctx* ctx, void* hip_stream);
 /* Enqueue a copy of the current GN state into device memory: 16 floats = pose[12], status, iterations,
  * n_corr, 0.  For the scan-parallel pose gather (RCCL all-gather of these 16 floats per rank). */
@@ -211,6 +212,12 @@ int lo_icp_optimize_loop(lo_ctx* ctx, const float* curr_xyz, size_t n_curr, cons
  * per-point valid flag and fp64 residual |n.(p_w - c)| (0 where invalid). Returns the count. */
 int lo_find_correspondences(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T[12],
                             uint8_t* valid, double* residual);
+/* KDTree variant's neighbour search (util::KdTree::nearestKSearch(q, 5), PointCloudUtils.h:398-423, over the map
+ * cloud set by lo_map_set_points; use_surfel_correspondence = 0): for each world-frame query, the 5 nearest map
+ * points by fp32 squared distance, ascending, equal distances in nanoflann's visit order.  idx (n x 5): original
+ * map-point indices; dist (n x 5): fp32 squared distances.  A query with fewer than 5 neighbours (the ICP skips it,
+ * IterativeClosestPointOptimizer.cpp:699-701) gets idx -1 / dist +inf.  Returns the number of queries with 5. */
+int lo_knn_search(lo_ctx* ctx, const float* query_xyz, size_t n, int32_t* idx, float* dist);
 /* AdaptiveMEstimator::calculate_scale_factor on given normalised residuals (device PKO).
  * gmm_out (nullable): weights, means, variances (3*gmm_components doubles). Returns alpha, NaN on error. */
 double lo_pko_scale_factor(lo_ctx* ctx, const double* residuals, size_t n, double* gmm_out);

@@ -15,6 +15,7 @@
 #include <cstdint>
 
 #include "../../include/lo_icp.h"
+#include "lo_kdorder.h"
 
 namespace lo {
 
@@ -74,6 +75,8 @@ struct KParams {
     // KDTree correspondence path (use_surfel_correspondence = 0; lo_kdtree.hip)
     const float4* kd_pts;             // L0 centroids sorted by grid cell: x, y, z, original index (int bits)
     const uint32_t* kd_start;         // cell -> first point (dense grid, ncell + 1 entries)
+    const uint32_t* kd_vpos;          // reference kd-tree visit order (lo_kdorder.h): vAcc_ position per index
+    const KdNode* kd_nodes;    //   and its nodes, for equal-distance tie-breaks
     int kd_m;                         // map points
     int kd_org[3], kd_dim[3];         // grid origin (cell coords) and extent
     float kd_h;                       // grid cell edge

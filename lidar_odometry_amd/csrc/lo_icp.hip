@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "lo_device.h"
+#include "lo_kdorder.h"
 #include "lo_math.h"
 #include "lo_pko_tables.h"
 #include "lo_vfilter.h"
@@ -33,6 +34,7 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
+__global__ void k_knn_reset(KParams P);
 __global__ void k_plane(KParams P, int with_stats);
 __global__ void k_inlier(KParams P);
 __global__ void k_correspond_b(const KParams* PB, int with_stats, int init);
@@ -52,6 +54,10 @@ struct PointGrid {
     size_t pts_cap = 0;
     uint32_t* d_start = nullptr;
     size_t start_cap = 0;
+    uint32_t* d_vpos = nullptr;     // nanoflann visit order (lo_kdorder.h): vAcc_ position per original index
+    size_t vpos_cap = 0;
+    KdNode* d_nodes = nullptr;      //   and the tree's nodes (root = 0)
+    size_t nodes_cap = 0;
     int m = 0;
     int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
     float h = 1.0f;
@@ -169,6 +175,8 @@ static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
     P.tab = c->d_kd_plane;
     P.kd_pts = G.d_pts;
     P.kd_start = G.d_start;
+    P.kd_vpos = G.d_vpos;
+    P.kd_nodes = G.d_nodes;
     P.kd_m = G.m;
     for (int a = 0; a < 3; ++a) { P.kd_org[a] = G.org[a]; P.kd_dim[a] = G.dim[a]; }
     P.kd_h = G.h;
@@ -383,6 +391,7 @@ void lo_destroy(lo_ctx* c) {
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part, c->d_acc_part,
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
+                    c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->d_raw) (void)hipFree(c->d_raw);
@@ -501,6 +510,26 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
     }
     LO_HIP(c, hipMemcpy(G.d_pts, pts.data(), pts.size() * sizeof(float4), hipMemcpyHostToDevice));
     LO_HIP(c, hipMemcpy(G.d_start, start.data(), start.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // the reference kd-tree's visit order over the same cloud: equal-distance neighbours are ranked by it
+    std::vector<KdNode> nodes;
+    std::vector<uint32_t> vpos;
+    KdOrderBuilder(xyz, m).build(nodes, vpos);
+    if (nodes.empty()) nodes.push_back(KdNode{-1, -1, 0, 0, 0.0f, 0.0f});
+    if (vpos.empty()) vpos.push_back(0);
+    if (vpos.size() > G.vpos_cap) {
+        if (G.d_vpos) LO_HIP(c, hipFree(G.d_vpos));
+        G.d_vpos = nullptr;
+        LO_HIP(c, hipMalloc(&G.d_vpos, vpos.size() * sizeof(uint32_t)));
+        G.vpos_cap = vpos.size();
+    }
+    if (nodes.size() > G.nodes_cap) {
+        if (G.d_nodes) LO_HIP(c, hipFree(G.d_nodes));
+        G.d_nodes = nullptr;
+        LO_HIP(c, hipMalloc(&G.d_nodes, nodes.size() * sizeof(KdNode)));
+        G.nodes_cap = nodes.size();
+    }
+    LO_HIP(c, hipMemcpy(G.d_vpos, vpos.data(), vpos.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    LO_HIP(c, hipMemcpy(G.d_nodes, nodes.data(), nodes.size() * sizeof(KdNode), hipMemcpyHostToDevice));
     G.m = static_cast<int>(m);
     G.h = h;
     for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
@@ -863,6 +892,46 @@ int lo_find_correspondences(lo_ctx* c, const float* pts, size_t n, const float T
     LO_HIP(c, hipStreamSynchronize(c->stream));
     int cnt = 0;
     for (size_t i = 0; i < n; ++i) { valid[i] = slots[i] >= 0 ? 1 : 0; cnt += valid[i]; }
+    return cnt;
+}
+
+int lo_knn_search(lo_ctx* c, const float* q, size_t n, int32_t* idx, float* dist) {
+    if (!c || (n > 0 && (!q || !idx || !dist))) return LO_ERR_ARG;
+    if (!c->kd) { c->err = "lo_knn_search needs use_surfel_correspondence = 0"; return LO_ERR_STATE; }
+    if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    if (n == 0) return 0;
+    LO_HIP(c, hipSetDevice(c->device));
+    const float I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};       // Matrix4f * (x, y, z, 1) is exact at I
+    int rc = reset_state(c, I, 1.0, 0.1);
+    if (rc != LO_OK) return rc;
+    LO_HIP(c, hipMemcpyAsync(c->d_pts, q, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    KParams P = make_params(c, c->d_pts, static_cast<int>(n));
+    KParams Pn = P;
+    Pn.init = 0;
+    hipLaunchKernelGGL(k_knn, dim3((n * kKnnGroup + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, P);
+    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, Pn);
+    hipLaunchKernelGGL(k_knn_reset, dim3(1), dim3(64), 0, c->stream, Pn);
+    LO_HIP(c, hipGetLastError());
+    std::vector<int32_t> nb(5 * n);
+    std::vector<float4> mp(static_cast<size_t>(std::max(c->grid.m, 1)));
+    LO_HIP(c, hipMemcpyAsync(nb.data(), c->d_kd_nbr, nb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (c->grid.m > 0)
+        LO_HIP(c, hipMemcpyAsync(mp.data(), c->grid.d_pts, c->grid.m * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    int cnt = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const bool ok = nb[5 * i] >= 0;
+        cnt += ok ? 1 : 0;
+        for (int k = 0; k < 5; ++k) {
+            if (!ok) { idx[5 * i + k] = -1; dist[5 * i + k] = INFINITY; continue; }
+            const float4 v = mp[nb[5 * i + k]];
+            int32_t id;
+            std::memcpy(&id, &v.w, sizeof(id));
+            const float dx = q[3 * i] - v.x, dy = q[3 * i + 1] - v.y, dz = q[3 * i + 2] - v.z;
+            idx[5 * i + k] = id;
+            dist[5 * i + k] = (dx * dx + dy * dy) + dz * dz;
+        }
+    }
     return cnt;
 }
 

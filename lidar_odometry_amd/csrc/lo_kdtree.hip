@@ -18,8 +18,10 @@
 //                distance <= max_correspondence_distance; writes the per-point plane (fp32-rounded normal and
 //                centroid, as .cast<float>() at :361-365), the fp64 distance (residuals[i]) and the same ballots /
 //                block statistics as the surfel path, so k_pko_t / k_accumulate run unchanged.
-// Ties in distance are broken by the centroid's original index (an index-ordered brute force); nanoflann
-// breaks them by tree-visit order (NANOFLANN_FIRST_MATCH is not defined), so exact ties are parity-unpinned.
+// Equal distances are ranked as nanoflann ranks them: by the order its searchLevel visits the points (an earlier
+// visit wins, NANOFLANN_FIRST_MATCH is not defined), evaluated on the reference's own tree (lo_kdorder.h, built with
+// the grid) only when two distances are equal -- so the 5-NN lists, their order and their tie-breaks equal
+// nanoflann's (tests/test_gpu_kdtree.py against tests/golden/knn_golden.npz, written by nanoflann itself).
 // Non-finite queries find nothing (nanoflann only adds points with dist < worstDist = FLT_MAX).
 #include "lo_device.h"
 #include "lo_solve.h"
@@ -38,8 +40,35 @@ struct Top5 {
     int n;
 };
 
-__device__ __forceinline__ bool lex_less(float da, int ia, float db, int ib) {
-    return da < db || (da == db && ia < ib);
+// The query and the reference tree's order, for ties.
+struct KnnQ {
+    float q[3];
+    const uint32_t* vpos;
+    const KdNode* nodes;
+};
+
+// nanoflann visits original index a before b (both in the tree): descend while both vAcc_ positions fall on the
+// same side of a node's split; the node that separates them is entered on the query's side first
+// (searchLevel: (q - divlow) + (q - divhigh) < 0 -> child1, fp32 as nanoflann); one leaf: vAcc_ order.
+__device__ __noinline__ bool kd_visit_before(const KnnQ& Q, int a, int b) {
+    const uint32_t pa = Q.vpos[a], pb = Q.vpos[b];
+    int ni = 0;
+    for (int depth = 0; depth < 64; ++depth) {
+        const KdNode nd = Q.nodes[ni];
+        if (nd.child1 < 0) break;
+        const bool sa = pa >= nd.mid, sb = pb >= nd.mid;
+        if (sa != sb) {
+            const float val = Q.q[nd.divfeat];
+            const bool near2 = !(((val - nd.divlow) + (val - nd.divhigh)) < 0.0f);
+            return sa == near2;
+        }
+        ni = sa ? nd.child2 : nd.child1;
+    }
+    return pa < pb;
+}
+
+__device__ __forceinline__ bool lex_less(const KnnQ& Q, float da, int ia, float db, int ib) {
+    return da < db || (da == db && ia != ib && kd_visit_before(Q, ia, ib));
 }
 
 __device__ __forceinline__ void top5_init(Top5& t) {
@@ -49,18 +78,18 @@ __device__ __forceinline__ void top5_init(Top5& t) {
 }
 
 // KNNResultSet::addPoint behind searchLevel's `dist < worstDist` (worstDist = FLT_MAX until 5 are held),
-// with (dist, index) order; unrolled compare-swaps keep the list in VGPRs.
-__device__ __forceinline__ void top5_insert(Top5& t, float d, int id, int pos) {
+// with (dist, visit order) order; unrolled compare-swaps keep the list in VGPRs.
+__device__ __forceinline__ void top5_insert(const KnnQ& Q, Top5& t, float d, int id, int pos) {
     if (t.n < 5) {
         if (!(d < FLT_MAX)) return;
         ++t.n;
-    } else if (!lex_less(d, id, t.d[4], t.id[4])) {
+    } else if (!lex_less(Q, d, id, t.d[4], t.id[4])) {
         return;
     }
     t.d[4] = d; t.id[4] = id; t.pos[4] = pos;
 #pragma unroll
     for (int k = 4; k > 0; --k) {
-        if (lex_less(t.d[k], t.id[k], t.d[k - 1], t.id[k - 1])) {
+        if (lex_less(Q, t.d[k], t.id[k], t.d[k - 1], t.id[k - 1])) {
             const float fd = t.d[k]; t.d[k] = t.d[k - 1]; t.d[k - 1] = fd;
             const int fi = t.id[k]; t.id[k] = t.id[k - 1]; t.id[k - 1] = fi;
             const int fp = t.pos[k]; t.pos[k] = t.pos[k - 1]; t.pos[k - 1] = fp;
@@ -73,26 +102,11 @@ __device__ __forceinline__ float l2sq(float qx, float qy, float qz, const float4
     return (dx * dx + dy * dy) + dz * dz;
 }
 
-__device__ __forceinline__ void scan_range(const KParams& P, uint32_t s, uint32_t e, float qx, float qy, float qz, Top5& t) {
-    uint32_t p = s;
-    for (; p + 4 <= e; p += 4) {                 // 4 independent loads in flight per lane
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = P.kd_pts[p + u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
-    }
-    for (; p < e; ++p) {
-        const float4 v = P.kd_pts[p];
-        top5_insert(t, l2sq(qx, qy, qz, v), __float_as_int(v.w), static_cast<int>(p));
-    }
-}
-
 // Merge of disjoint top-5 lists across the kKnnGroup = 16 lanes of a query: a hypercube over the 16-lane DPP row
 // (quad_perm xor 1, quad_perm xor 2, row_half_mirror i <-> 7-i, row_mirror i <-> 15-i) -- VALU moves, no LDS
 // round trips -- after which every lane of the row holds the (dist, index)-smallest five of the group's union.
 template <int CTRL>
-__device__ __forceinline__ void top5_merge_dpp(Top5& t) {
+__device__ __forceinline__ void top5_merge_dpp(const KnnQ& Q, Top5& t) {
     Top5 u;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -103,16 +117,16 @@ __device__ __forceinline__ void top5_merge_dpp(Top5& t) {
     u.n = __builtin_amdgcn_mov_dpp(t.n, CTRL, 0xf, 0xf, false);
 #pragma unroll
     for (int k = 0; k < 5; ++k)
-        if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
+        if (k < u.n) top5_insert(Q, t, u.d[k], u.id[k], u.pos[k]);
 }
 
-__device__ __forceinline__ Top5 group_merge(const Top5& own) {
+__device__ __forceinline__ Top5 group_merge(const KnnQ& Q, const Top5& own) {
     static_assert(kKnnGroup == 16, "the DPP hypercube spans one 16-lane row");
     Top5 t = own;
-    top5_merge_dpp<0xB1>(t);     // quad_perm [1,0,3,2]
-    top5_merge_dpp<0x4E>(t);     // quad_perm [2,3,0,1]
-    top5_merge_dpp<0x141>(t);    // row_half_mirror
-    top5_merge_dpp<0x140>(t);    // row_mirror
+    top5_merge_dpp<0xB1>(Q, t);     // quad_perm [1,0,3,2]
+    top5_merge_dpp<0x4E>(Q, t);     // quad_perm [2,3,0,1]
+    top5_merge_dpp<0x141>(Q, t);    // row_half_mirror
+    top5_merge_dpp<0x140>(Q, t);    // row_mirror
     return t;
 }
 
@@ -120,14 +134,15 @@ __device__ __forceinline__ Top5 group_merge(const Top5& own) {
 // k_knn: grid shells.  kd_nbr[5i] = positions of the 5-NN, -1 = fewer than 5 (rejected), -2 = unresolved
 // ====================================================================================================
 // One candidate range of the kd_pts array (a run of cells of one grid row), scanned with 8 loads in flight.
-__device__ __forceinline__ void scan_range8(const KParams& P, uint32_t s, uint32_t e, float qx, float qy, float qz, Top5& t) {
+__device__ __forceinline__ void scan_range8(const KParams& P, const KnnQ& Q, uint32_t s, uint32_t e, float qx, float qy,
+                                            float qz, Top5& t) {
     for (uint32_t p = s; p < e; p += 8) {
         float4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = (p + u < e) ? P.kd_pts[p + u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (p + u < e) top5_insert(t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
+            if (p + u < e) top5_insert(Q, t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
     }
 }
 
@@ -155,6 +170,7 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
     const int dimx = P.kd_dim[0], dimy = P.kd_dim[1], dimz = P.kd_dim[2];
     const int ox = P.kd_org[0], oy = P.kd_org[1], oz = P.kd_org[2];
     const double q[3] = {qx, qy, qz};
+    const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
     Top5 own, grp;
     top5_init(own);
     bool done = false;
@@ -183,9 +199,9 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, rs[j], re[j], qx, qy, qz, own);
+            for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, Q, rs[j], re[j], qx, qy, qz, own);
         }
-        grp = group_merge(own);
+        grp = group_merge(Q, own);
         // every unscanned centroid lies outside the cube of cells [c - r, c + r]
         bool all = true;
         double b = DBL_MAX;
@@ -261,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
 // ====================================================================================================
 constexpr int kBruteThreads = 1024;
 
-__device__ __forceinline__ void top5_merge_xor(Top5& t, int o) {
+__device__ __forceinline__ void top5_merge_xor(const KnnQ& Q, Top5& t, int o) {
     Top5 u;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -272,7 +288,7 @@ __device__ __forceinline__ void top5_merge_xor(Top5& t, int o) {
     u.n = __shfl_xor(t.n, o, 64);
 #pragma unroll
     for (int k = 0; k < 5; ++k)
-        if (k < u.n) top5_insert(t, u.d[k], u.id[k], u.pos[k]);
+        if (k < u.n) top5_insert(Q, t, u.d[k], u.id[k], u.pos[k]);
 }
 
 __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
@@ -293,6 +309,7 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         const int i = P.kd_unres[u];
         float qx, qy, qz;
         transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+        const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
         Top5 t;
         top5_init(t);
         for (int p0 = tid; p0 < P.kd_m; p0 += 8 * kBruteThreads) {           // 8 loads in flight per lane
@@ -305,12 +322,12 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
 #pragma unroll
             for (int w = 0; w < 8; ++w) {
                 const int p = p0 + w * kBruteThreads;
-                if (p < P.kd_m) top5_insert(t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
+                if (p < P.kd_m) top5_insert(Q, t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
             }
         }
-        t = group_merge(t);                                // 16-lane rows
-        top5_merge_xor(t, 16);
-        top5_merge_xor(t, 32);                             // the wave's five
+        t = group_merge(Q, t);                             // 16-lane rows
+        top5_merge_xor(Q, t, 16);
+        top5_merge_xor(Q, t, 32);                          // the wave's five
         if (lane == 0) {
 #pragma unroll
             for (int k = 0; k < 5; ++k) { s_d[wid][k] = t.d[k]; s_id[wid][k] = t.id[k]; s_pos[wid][k] = t.pos[k]; }
@@ -322,7 +339,7 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
 #pragma unroll
             for (int k = 0; k < 5; ++k) { a.d[k] = s_d[lane][k]; a.id[k] = s_id[lane][k]; a.pos[k] = s_pos[lane][k]; }
             a.n = s_n[lane];
-            a = group_merge(a);
+            a = group_merge(Q, a);
             if (lane == 0) {
                 int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
                 if (a.n < 5) out[0] = -1;
@@ -331,6 +348,11 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         }
         __syncthreads();
     }
+}
+
+// lo_knn_search (kNN without the plane stage): the unresolved-query counter k_plane would zero
+__global__ void k_knn_reset(KParams P) {
+    if (threadIdx.x == 0) P.st->kd_unres_n = 0;
 }
 
 // ====================================================================================================

@@ -268,6 +268,16 @@ class IterativeClosestPointOptimizer:
                                                       res.ctypes.data_as(C.POINTER(C.c_double))))
         return n, valid.astype(bool), res
 
+    def nearest_k_search(self, queries):
+        """util::KdTree::nearestKSearch(q, 5) for world-frame queries over the map cloud (KDTree configuration):
+        (idx (n, 5) int32, dist (n, 5) float32, found (n,) int32 = 5 or 0)."""
+        q = _as_pts(queries)
+        idx = np.full((len(q), 5), -1, np.int32)
+        dist = np.full((len(q), 5), np.inf, np.float32)
+        self._check(lib().lo_knn_search(self._ctx, _fptr(q), len(q), idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        dist.ctypes.data_as(C.POINTER(C.c_float))))
+        return idx, dist, np.where(idx[:, 0] >= 0, 5, 0).astype(np.int32)
+
     def pko_scale_factor(self, residuals):
         r = np.ascontiguousarray(residuals, dtype=np.float64)
         K = self._cfg.gmm_components

@@ -93,6 +93,8 @@ def lib():
         L.or_find_correspondences.restype = C.c_int
         L.or_find_correspondences_kdtree.argtypes = [vp, fp, C.c_int, fp, C.c_double, u8p, dp, fp, fp]
         L.or_find_correspondences_kdtree.restype = C.c_int
+        L.or_kdtree_knn5.argtypes = [fp, C.c_int, fp, C.c_int, C.c_int, ip, fp, ip]
+        L.or_kdtree_knn5.restype = None
         L.or_set_kdtree_search.argtypes = [C.c_int]
         L.or_set_kdtree_search.restype = None
         L.or_icp_optimize.argtypes = [vp, fp, C.c_int, fp, fp, C.POINTER(IcpCfg), C.c_int,
@@ -320,6 +322,22 @@ class VoxelMap:
 
 
 # ---------------------------------------------------------------- ICP
+def kdtree_knn5(cloud, queries, use_tree=True):
+    """util::KdTree::nearestKSearch(q, 5) (PointCloudUtils.h:398-423) on the restated nanoflann tree.
+    Returns (idx (nq, 5) int32, dist (nq, 5) float32, found (nq,) int32); idx -1 / dist inf past `found`."""
+    c, cp = _f32(np.asarray(cloud, np.float32).reshape(-1, 3))
+    q, qp = _f32(np.asarray(queries, np.float32).reshape(-1, 3))
+    nq = len(q)
+    idx = np.full((nq, 5), -1, np.int32)
+    dist = np.full((nq, 5), np.inf, np.float32)
+    found = np.zeros(nq, np.int32)
+    ip = C.POINTER(C.c_int)
+    fp = C.POINTER(C.c_float)
+    lib().or_kdtree_knn5(cp, len(c), qp, nq, int(bool(use_tree)),
+                         idx.ctypes.data_as(ip), dist.ctypes.data_as(fp), found.ctypes.data_as(ip))
+    return idx, dist, found
+
+
 def set_kdtree_search(use_tree: bool):
     """KDTree-variant neighbour search: kd-tree (default) or the index-ordered brute force (same results)."""
     lib().or_set_kdtree_search(int(bool(use_tree)))

@@ -398,82 +398,268 @@ struct L1Node {
 };
 
 
-/* ---- static kd-tree over the map cloud (VoxelMap::RebuildKdTree :420-438 role, nanoflann leaf size 10) ----
- * Exact 5-NN by the fp32 squared L2 of nanoflann's L2_Simple_Adaptor; the result set keeps the (dist, index)
- * lexicographic smallest, i.e. exactly what an index-ordered brute force returns (tests check this).  A node is
- * skipped only when its box lower bound, shrunk by 1e-6 relative against fp32 rounding of point distances, is
- * strictly above the current 5th distance, so equal-distance lower-index points are never pruned. */
+/* ---- nanoflann 1.7.1 KDTreeSingleIndexAdaptor, restated (util::KdTree, PointCloudUtils.h:370-423, built by
+ * VoxelMap::RebuildKdTree :420-438; thirdparty/nanoflann/nanoflann.hpp) ----
+ * Leaf size 10, DIM 3, L2_Simple_Adaptor<float>: every quantity is fp32 as nanoflann computes it.
+ *  build   computeBoundingBox (:1845-1880) over vAcc_ = iota; divideTree (:1149-1210): a range of <= 10 points is
+ *          a leaf whose box is its points' min / max; otherwise middleSplit_ (:1320-1370) picks, among the axes whose
+ *          inherited box span is >= (1 - 1e-5) * the largest span, the one with the largest point spread, cuts at
+ *          the box midpoint clamped to the points' [min, max], and planeSplit (:1382-1427) partitions vAcc_ in place
+ *          (two Hoare-style passes); the split index is lim1 / lim2 / count / 2 as nanoflann balances it; divlow /
+ *          divhigh are the children's actual extents in the cut axis, the node box the union of its children's.
+ *  search  findNeighbors (:1708-1730): per-axis squared distances to the root box, then searchLevel (:1885-1960):
+ *          a leaf adds each point with dist < the worstDist read at leaf entry; an inner node descends first into
+ *          child1 if (q - divlow) + (q - divhigh) < 0, else child2, and visits the other child when the
+ *          incrementally updated fp32 box distance is <= worstDist.  KNNResultSet (:199-282) insertion-sorts and
+ *          keeps the earlier-visited point among equal distances (NANOFLANN_FIRST_MATCH is not defined).
+ * So the result is the 5 smallest by (fp32 distance, visit order) -- visit_before() states that order directly:
+ * leaves in the near-child-first DFS order of the query, points of one leaf in vAcc_ order.  knn_brute() (an
+ * exhaustive scan ranked by that order) equals the tree search except where the tree's fp32 box-distance bound
+ * rounds above a point's own fp32 distance (never seen on the fixtures; tests/test_oracle.py checks both against
+ * nanoflann itself, tests/golden/knn_*.npz). */
 struct KdTree3 {
-    struct Node { float lo[3], hi[3]; int left = -1, right = -1, begin = 0, end = 0; };
-    std::vector<float> pts;     // xyz by original index
-    std::vector<int> perm;
+    struct Node {
+        int child1 = -1, child2 = -1;         // -1: leaf
+        size_t left = 0, right = 0;           // vAcc_ range; inner nodes: [left, mid) -> child1, [mid, right) -> child2
+        size_t mid = 0;
+        int divfeat = 0;
+        float divlow = 0.0f, divhigh = 0.0f;
+    };
+    struct Box { float low[3], high[3]; };
+    std::vector<float> pts;                  // xyz by original index (GetPointCloud order)
+    std::vector<uint32_t> vacc;              // vAcc_
+    std::vector<uint32_t> vpos;              // original index -> position in vAcc_
     std::vector<Node> nodes;
+    Box root_bbox{};
+    int root = -1;
+
+    float get(uint32_t i, int d) const { return pts[3 * static_cast<size_t>(i) + d]; }
+
     void build(const std::vector<float>& cloud) {
         pts = cloud;
-        const int m = static_cast<int>(cloud.size() / 3);
-        perm.resize(m);
-        for (int i = 0; i < m; ++i) perm[i] = i;
+        const size_t m = cloud.size() / 3;
+        vacc.resize(m);
+        for (size_t i = 0; i < m; ++i) vacc[i] = static_cast<uint32_t>(i);
         nodes.clear();
-        if (m > 0) build_rec(0, m);
-    }
-    int build_rec(int b, int e) {
-        Node nd;
-        for (int a = 0; a < 3; ++a) { nd.lo[a] = FLT_MAX; nd.hi[a] = -FLT_MAX; }
-        for (int i = b; i < e; ++i)
-            for (int a = 0; a < 3; ++a) {
-                nd.lo[a] = std::min(nd.lo[a], pts[3 * perm[i] + a]);
-                nd.hi[a] = std::max(nd.hi[a], pts[3 * perm[i] + a]);
+        root = -1;
+        if (m == 0) { vpos.clear(); return; }
+        for (int d = 0; d < 3; ++d) root_bbox.low[d] = root_bbox.high[d] = get(vacc[0], d);
+        for (size_t k = 1; k < m; ++k)
+            for (int d = 0; d < 3; ++d) {
+                const float v = get(vacc[k], d);
+                if (v < root_bbox.low[d]) root_bbox.low[d] = v;
+                if (v > root_bbox.high[d]) root_bbox.high[d] = v;
             }
-        nd.begin = b; nd.end = e;
+        Box bb = root_bbox;
+        root = divide(0, m, bb);
+        vpos.assign(m, 0);
+        for (size_t i = 0; i < m; ++i) vpos[vacc[i]] = static_cast<uint32_t>(i);
+    }
+
+    int divide(size_t left, size_t right, Box& bbox) {
         const int id = static_cast<int>(nodes.size());
-        nodes.push_back(nd);
-        if (e - b > 10) {
-            int ax = 0;
-            for (int a = 1; a < 3; ++a) if (nd.hi[a] - nd.lo[a] > nd.hi[ax] - nd.lo[ax]) ax = a;
-            const int mid = (b + e) / 2;
-            std::nth_element(perm.begin() + b, perm.begin() + mid, perm.begin() + e,
-                             [&](int x, int y) { return pts[3 * x + ax] < pts[3 * y + ax]; });
-            const int l = build_rec(b, mid), r = build_rec(mid, e);
-            nodes[id].left = l; nodes[id].right = r;
+        nodes.emplace_back();
+        if (right - left <= 10) {
+            nodes[id].left = left;
+            nodes[id].right = right;
+            for (int d = 0; d < 3; ++d) bbox.low[d] = bbox.high[d] = get(vacc[left], d);
+            for (size_t k = left + 1; k < right; ++k)
+                for (int d = 0; d < 3; ++d) {
+                    const float v = get(vacc[k], d);
+                    if (bbox.low[d] > v) bbox.low[d] = v;
+                    if (bbox.high[d] < v) bbox.high[d] = v;
+                }
+            return id;
+        }
+        size_t idx;
+        int cutfeat;
+        float cutval;
+        middle_split(left, right - left, idx, cutfeat, cutval, bbox);
+        Box lb = bbox;
+        lb.high[cutfeat] = cutval;
+        const int c1 = divide(left, left + idx, lb);
+        Box rb = bbox;
+        rb.low[cutfeat] = cutval;
+        const int c2 = divide(left + idx, right, rb);
+        Node& nd = nodes[id];
+        nd.child1 = c1;
+        nd.child2 = c2;
+        nd.left = left;
+        nd.right = right;
+        nd.mid = left + idx;
+        nd.divfeat = cutfeat;
+        nd.divlow = lb.high[cutfeat];
+        nd.divhigh = rb.low[cutfeat];
+        for (int d = 0; d < 3; ++d) {
+            bbox.low[d] = std::min(lb.low[d], rb.low[d]);
+            bbox.high[d] = std::max(lb.high[d], rb.high[d]);
         }
         return id;
     }
-    static bool lex_less(float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); }
-    void insert(const float q[3], int i, int idx[5], float dist[5], int& found) const {
-        const float d0 = q[0] - pts[3 * i], d1 = q[1] - pts[3 * i + 1], d2 = q[2] - pts[3 * i + 2];
-        const float d = d0 * d0 + d1 * d1 + d2 * d2;
-        if (found < 5) { if (!(d < FLT_MAX)) return; }
-        else if (!lex_less(d, i, dist[4], idx[4])) return;
-        int j = found < 5 ? found : 4;
-        if (found < 5) ++found;
-        while (j > 0 && lex_less(d, i, dist[j - 1], idx[j - 1])) { dist[j] = dist[j - 1]; idx[j] = idx[j - 1]; --j; }
-        dist[j] = d; idx[j] = i;
-    }
-    double box_d2(const Node& nd, const float q[3]) const {
-        double s = 0.0;
-        for (int a = 0; a < 3; ++a) {
-            double g = 0.0;
-            if (q[a] < nd.lo[a]) g = static_cast<double>(nd.lo[a]) - q[a];
-            else if (q[a] > nd.hi[a]) g = static_cast<double>(q[a]) - nd.hi[a];
-            s += g * g;
+
+    void middle_split(size_t ind, size_t count, size_t& index, int& cutfeat, float& cutval, const Box& bbox) {
+        const float EPS = static_cast<float>(0.00001);
+        float max_span = bbox.high[0] - bbox.low[0];
+        for (int i = 1; i < 3; ++i) {
+            const float span = bbox.high[i] - bbox.low[i];
+            if (span > max_span) max_span = span;
         }
-        return s;
+        float max_spread = -1.0f;
+        cutfeat = 0;
+        float min_elem = 0.0f, max_elem = 0.0f;
+        for (int i = 0; i < 3; ++i) {
+            const float span = bbox.high[i] - bbox.low[i];
+            if (span >= (1 - EPS) * max_span) {
+                float mn = get(vacc[ind], i), mx = mn;
+                for (size_t k = 1; k < count; ++k) {
+                    const float v = get(vacc[ind + k], i);
+                    if (v < mn) mn = v;
+                    if (v > mx) mx = v;
+                }
+                const float spread = mx - mn;
+                if (spread > max_spread) { cutfeat = i; max_spread = spread; min_elem = mn; max_elem = mx; }
+            }
+        }
+        const float split_val = (bbox.low[cutfeat] + bbox.high[cutfeat]) / 2;
+        if (split_val < min_elem) cutval = min_elem;
+        else if (split_val > max_elem) cutval = max_elem;
+        else cutval = split_val;
+        size_t lim1, lim2;
+        plane_split(ind, count, cutfeat, cutval, lim1, lim2);
+        if (lim1 > count / 2) index = lim1;
+        else if (lim2 < count / 2) index = lim2;
+        else index = count / 2;
     }
-    void search(int ni, const float q[3], int idx[5], float dist[5], int& found) const {
+
+    void plane_split(size_t ind, size_t count, int cutfeat, float cutval, size_t& lim1, size_t& lim2) {
+        size_t left = 0, right = count - 1;
+        for (;;) {
+            while (left <= right && get(vacc[ind + left], cutfeat) < cutval) ++left;
+            while (right && left <= right && get(vacc[ind + right], cutfeat) >= cutval) --right;
+            if (left > right || !right) break;
+            std::swap(vacc[ind + left], vacc[ind + right]);
+            ++left;
+            --right;
+        }
+        lim1 = left;
+        right = count - 1;
+        for (;;) {
+            while (left <= right && get(vacc[ind + left], cutfeat) <= cutval) ++left;
+            while (right && left <= right && get(vacc[ind + right], cutfeat) > cutval) --right;
+            if (left > right || !right) break;
+            std::swap(vacc[ind + left], vacc[ind + right]);
+            ++left;
+            --right;
+        }
+        lim2 = left;
+    }
+
+    // L2_Simple_Adaptor::evalMetric (:638-649): ((0 + d0^2) + d1^2) + d2^2 in fp32
+    float metric(const float q[3], uint32_t i) const {
+        float r = 0.0f;
+        for (int d = 0; d < 3; ++d) { const float df = q[d] - get(i, d); r += df * df; }
+        return r;
+    }
+
+    struct Result {                          // KNNResultSet<float, uint32_t>, capacity 5
+        uint32_t idx[5];
+        float dist[5];
+        size_t count = 0;
+        float worst() const { return (count < 5 || !count) ? std::numeric_limits<float>::max() : dist[count - 1]; }
+        void add(float d, uint32_t index) {
+            size_t i;
+            for (i = count; i > 0; --i) {
+                if (dist[i - 1] > d) {
+                    if (i < 5) { dist[i] = dist[i - 1]; idx[i] = idx[i - 1]; }
+                } else {
+                    break;
+                }
+            }
+            if (i < 5) { dist[i] = d; idx[i] = index; }
+            if (count < 5) ++count;
+        }
+    };
+
+    void search_level(Result& rs, const float q[3], int ni, float mindist, float (&dists)[3]) const {
         const Node& nd = nodes[ni];
-        if (found == 5 && box_d2(nd, q) * (1.0 - 1e-6) > static_cast<double>(dist[4])) return;
-        if (nd.left < 0) {
-            for (int k = nd.begin; k < nd.end; ++k) insert(q, perm[k], idx, dist, found);
+        if (nd.child1 < 0 && nd.child2 < 0) {
+            const float worst = rs.worst();
+            for (size_t i = nd.left; i < nd.right; ++i) {
+                const float d = metric(q, vacc[i]);
+                if (d < worst) rs.add(d, vacc[i]);
+            }
             return;
         }
-        const double dl = box_d2(nodes[nd.left], q), dr = box_d2(nodes[nd.right], q);
-        if (dl <= dr) { search(nd.left, q, idx, dist, found); search(nd.right, q, idx, dist, found); }
-        else { search(nd.right, q, idx, dist, found); search(nd.left, q, idx, dist, found); }
+        const int f = nd.divfeat;
+        const float val = q[f];
+        const float diff1 = val - nd.divlow, diff2 = val - nd.divhigh;
+        int best, other;
+        float cut;
+        if ((diff1 + diff2) < 0) { best = nd.child1; other = nd.child2; cut = (val - nd.divhigh) * (val - nd.divhigh); }
+        else { best = nd.child2; other = nd.child1; cut = (val - nd.divlow) * (val - nd.divlow); }
+        search_level(rs, q, best, mindist, dists);
+        const float dst = dists[f];
+        mindist = mindist + cut - dst;
+        dists[f] = cut;
+        if (mindist * 1.0f <= rs.worst()) search_level(rs, q, other, mindist, dists);
+        dists[f] = dst;
     }
+
     void knn5(const float q[3], int idx[5], float dist[5], int& found) const {
         found = 0;
-        if (nodes.empty() || !(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) return;
-        search(0, q, idx, dist, found);
+        if (root < 0) return;
+        float dists[3] = {0.0f, 0.0f, 0.0f};
+        float d0 = 0.0f;
+        for (int d = 0; d < 3; ++d) {            // computeInitialDistances (:1429-1453)
+            if (q[d] < root_bbox.low[d]) { dists[d] = (q[d] - root_bbox.low[d]) * (q[d] - root_bbox.low[d]); d0 += dists[d]; }
+            if (q[d] > root_bbox.high[d]) { dists[d] = (q[d] - root_bbox.high[d]) * (q[d] - root_bbox.high[d]); d0 += dists[d]; }
+        }
+        Result rs;
+        search_level(rs, q, root, d0, dists);
+        found = static_cast<int>(rs.count);
+        for (int k = 0; k < found; ++k) { idx[k] = static_cast<int>(rs.idx[k]); dist[k] = rs.dist[k]; }
+    }
+
+    // true when searchLevel reaches original index a before b for query q: descend while both vAcc_ positions
+    // fall on the same side of a node's split; at the first node that separates them the near child
+    // ((q - divlow) + (q - divhigh) < 0 -> child1) is visited first; inside one leaf, vAcc_ order
+    bool visit_before(const float q[3], uint32_t a, uint32_t b) const {
+        const size_t pa = vpos[a], pb = vpos[b];
+        int ni = root;
+        while (nodes[ni].child1 >= 0) {
+            const Node& nd = nodes[ni];
+            const bool sa = pa >= nd.mid, sb = pb >= nd.mid;
+            if (sa != sb) {
+                const float val = q[nd.divfeat];
+                const bool near2 = !(((val - nd.divlow) + (val - nd.divhigh)) < 0);
+                return sa == near2;
+            }
+            ni = sa ? nd.child2 : nd.child1;
+        }
+        return pa < pb;
+    }
+
+    // exhaustive 5-NN ranked by (fp32 distance, visit order); non-finite distances are never added (dist < FLT_MAX)
+    void knn_brute(const float q[3], int idx[5], float dist[5], int& found) const {
+        found = 0;
+        const size_t m = pts.size() / 3;
+        for (size_t i = 0; i < m; ++i) {
+            const float d = metric(q, static_cast<uint32_t>(i));
+            if (!(d < std::numeric_limits<float>::max())) continue;
+            auto before = [&](float da, uint32_t ia, float db, uint32_t ib) {
+                return da < db || (da == db && visit_before(q, ia, ib));
+            };
+            if (found == 5 && !before(d, static_cast<uint32_t>(i), dist[4], static_cast<uint32_t>(idx[4]))) continue;
+            int j = found < 5 ? found : 4;
+            if (found < 5) ++found;
+            while (j > 0 && before(d, static_cast<uint32_t>(i), dist[j - 1], static_cast<uint32_t>(idx[j - 1]))) {
+                dist[j] = dist[j - 1];
+                idx[j] = idx[j - 1];
+                --j;
+            }
+            dist[j] = d;
+            idx[j] = static_cast<int>(i);
+        }
     }
 };
 
@@ -883,30 +1069,10 @@ static size_t find_corr(const VoxelMap& map, const float* pts, int n, const SE3&
     return c.size();
 }
 
-static bool g_kd_use_tree = true;      // or_set_kdtree_search(0) -> index-ordered brute force
+static bool g_kd_use_tree = true;      // or_set_kdtree_search(0) -> exhaustive scan, nanoflann order
 
-/* ---- KDTree variant (find_correspondences_kdtree :647-767), exact 5-NN (kd-tree or brute force) ----
- * nanoflann KNNResultSet keeps the K smallest squared L2 distances (fp32 accumulate
- * d0*d0 + d1*d1 + d2*d2) sorted ascending; equal distances keep the first-inserted
- * (insertion sort shifts only strictly larger entries).  The tree visit order only matters
- * for exact ties, which this brute force resolves by smaller index (parity unpinned there). */
-static void knn5(const std::vector<float>& cloud, const float q[3], int idx[5], float dist[5], int& found) {
-    found = 0;
-    size_t m = cloud.size() / 3;
-    for (size_t i = 0; i < m; ++i) {
-        float d0 = q[0] - cloud[3 * i], d1 = q[1] - cloud[3 * i + 1], d2 = q[2] - cloud[3 * i + 2];
-        float d = d0 * d0 + d1 * d1 + d2 * d2;
-        // searchLevel adds a leaf point only if dist < worstDist, and worstDist is FLT_MAX until K are held
-        // (nanoflann.hpp:1893-1900, KNNResultSet): NaN / inf distances are never added
-        const float worst = found < 5 ? FLT_MAX : dist[4];
-        if (!(d < worst)) continue;
-        int j = found < 5 ? found : 4;
-        if (found < 5) found++;
-        while (j > 0 && dist[j - 1] > d) { dist[j] = dist[j - 1]; idx[j] = idx[j - 1]; --j; }
-        dist[j] = d; idx[j] = static_cast<int>(i);
-    }
-}
-
+/* ---- KDTree variant (find_correspondences_kdtree :647-767): exact 5-NN from the restated nanoflann tree, or
+ * (or_set_kdtree_search(0)) the exhaustive scan ranked by the same (distance, visit order) ---- */
 // symmetric 3x3 eigen decomposition in double (cyclic Jacobi); returns eigenvector of smallest eigenvalue
 // Cyclic Jacobi on the 3x3 scatter matrix.  Stopping rule as Eigen's JacobiSVD (JacobiSVD.h compute(): a pair is
 // rotated only while |a_pq| > max(DBL_MIN, 2 eps * maxDiagEntry), the running maximum of the |diagonal|; the sweep
@@ -954,13 +1120,13 @@ static size_t find_corr_kdtree(const VoxelMap& map, const float* pts, int n, con
     cloud.reserve(map.L0.size() * 3);
     for (auto& kv : map.L0.vals) { cloud.push_back(kv.second.c[0]); cloud.push_back(kv.second.c[1]); cloud.push_back(kv.second.c[2]); }
     const bool use_tree = g_kd_use_tree;
-    if (use_tree && map.kd_rev != map.revision) { map.kd.build(cloud); map.kd_rev = map.revision; }   // RebuildKdTree
+    if (map.kd_rev != map.revision) { map.kd.build(cloud); map.kd_rev = map.revision; }   // RebuildKdTree
     for (int i = 0; i < n; ++i) {
         if (valid_out) { valid_out[i] = 0; res_out[i] = 0.0; }
         float q[3]; transform_pt(T, pts + 3 * i, q);
         int idx[5]; float dist[5]; int found;
         if (use_tree) map.kd.knn5(q, idx, dist, found);
-        else knn5(cloud, q, idx, dist, found);
+        else map.kd.knn_brute(q, idx, dist, found);
         if (found < 5) continue;
         double P[5][3];
         for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) P[k][d] = cloud[3 * idx[k] + d];
@@ -1123,7 +1289,7 @@ static size_t find_corr_loop(const KdTree3& kd, const std::vector<float>& lmap, 
         float q[3]; transform_pt(T, pts + 3 * i, q);
         int idx[5]; float dist[5]; int found;
         if (g_kd_use_tree) kd.knn5(q, idx, dist, found);
-        else knn5(lmap, q, idx, dist, found);
+        else kd.knn_brute(q, idx, dist, found);
         if (found < 5) continue;
         double P[5][3];
         for (int k = 0; k < 5; ++k) for (int d = 0; d < 3; ++d) P[k][d] = lmap[3 * idx[k] + d];
@@ -1428,6 +1594,18 @@ int or_find_correspondences(void* map, const float* pts, int n, const float T[12
 }
 
 void or_set_kdtree_search(int use_tree) { g_kd_use_tree = use_tree != 0; }
+
+void or_kdtree_knn5(const float* cloud, int m, const float* q, int nq, int use_tree, int* idx, float* dist, int* found) {
+    KdTree3 kd;
+    kd.build(std::vector<float>(cloud, cloud + 3 * static_cast<size_t>(std::max(m, 0))));
+    for (int i = 0; i < nq; ++i) {
+        int* ix = idx + 5 * static_cast<size_t>(i);
+        float* ds = dist + 5 * static_cast<size_t>(i);
+        for (int k = 0; k < 5; ++k) { ix[k] = -1; ds[k] = std::numeric_limits<float>::infinity(); }
+        if (use_tree) kd.knn5(q + 3 * static_cast<size_t>(i), ix, ds, found[i]);
+        else kd.knn_brute(q + 3 * static_cast<size_t>(i), ix, ds, found[i]);
+    }
+}
 
 int or_find_correspondences_kdtree(void* map, const float* pts, int n, const float T[12], double maxd, uint8_t* valid,
                                    double* residual, float* normal_out, float* target_out) {

@@ -104,7 +104,9 @@ void   or_transform_points(const float* in, int n, const float T[12], float* out
 int    or_find_correspondences(void* map, const float* pts, int n, const float T[12],
                                double max_corr_dist, uint8_t* valid, double* residual);
 /* find_correspondences_kdtree at pose T (brute-force exact 5-NN over L0 centroids). */
-void   or_set_kdtree_search(int use_tree);   /* 1: kd-tree (default), 0: index-ordered brute force */
+void   or_set_kdtree_search(int use_tree);   /* 1: kd-tree (default), 0: exhaustive scan in nanoflann's order */
+/* util::KdTree::nearestKSearch(q, 5) over `cloud` for every query (nanoflann restated); idx -1 / dist inf past found */
+void   or_kdtree_knn5(const float* cloud, int m, const float* q, int nq, int use_tree, int* idx, float* dist, int* found);
 int    or_find_correspondences_kdtree(void* map, const float* pts, int n, const float T[12],
                                       double max_corr_dist, uint8_t* valid, double* residual,
                                       float* normal_out /* nullable, n*3 */, float* target_out /* nullable */);
