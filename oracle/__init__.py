@@ -93,6 +93,12 @@ def lib():
         L.or_find_correspondences.restype = C.c_int
         L.or_find_correspondences_kdtree.argtypes = [vp, fp, C.c_int, fp, C.c_double, u8p, dp, fp, fp]
         L.or_find_correspondences_kdtree.restype = C.c_int
+        L.or_map_trace.argtypes = [vp, C.c_int]
+        L.or_map_trace.restype = None
+        L.or_map_trace_get.argtypes = [vp, ip, C.c_size_t]
+        L.or_map_trace_get.restype = C.c_size_t
+        L.or_map_orders.argtypes = [vp, ip, ip, ip, ip, C.c_size_t]
+        L.or_map_orders.restype = C.c_size_t
         L.or_kdtree_knn5.argtypes = [fp, C.c_int, fp, C.c_int, C.c_int, ip, fp, ip]
         L.or_kdtree_knn5.restype = None
         L.or_set_kdtree_search.argtypes = [C.c_int]
@@ -286,6 +292,29 @@ class VoxelMap:
     def apply_transform(self, T):
         t, tp = _f32(np.asarray(T).reshape(12))
         lib().or_map_apply_transform(self.h, tp)
+
+    def enable_trace(self, on=True):
+        """Record the container-operation trace (insert / erase / clear on L0, L1, children; see lo_oracle.cpp)."""
+        lib().or_map_trace(self.h, int(bool(on)))
+
+    def trace(self):
+        n = lib().or_map_trace_get(self.h, None, 0)
+        out = np.zeros(n, np.int32)
+        if n:
+            lib().or_map_trace_get(self.h, out.ctypes.data_as(C.POINTER(C.c_int)), n)
+        return out.reshape(-1, 7)
+
+    def orders(self):
+        """Iteration orders: (L0 keys (n0, 3), L1 keys (n1, 3), children per L1 (n1,), children keys (nc, 3))."""
+        ip = C.POINTER(C.c_int)
+        nc = lib().or_map_orders(self.h, None, None, None, None, 0)
+        l0 = np.zeros((self.l0_count(), 3), np.int32)
+        l1 = np.zeros((self.l1_count(), 3), np.int32)
+        cnt = np.zeros(self.l1_count(), np.int32)
+        ch = np.zeros((max(nc, 1), 3), np.int32)
+        lib().or_map_orders(self.h, l0.ctypes.data_as(ip), l1.ctypes.data_as(ip), cnt.ctypes.data_as(ip),
+                            ch.ctypes.data_as(ip), nc)
+        return l0, l1, cnt, ch[:nc]
 
     def l0_count(self):
         return lib().or_map_l0_count(self.h)

@@ -674,6 +674,19 @@ struct VoxelMap {
     int init_hit_count = 1;
     DenseMap<L0Node> L0;
     DenseMap<L1Node> L1;
+    // container-operation trace (or_map_trace): the insert / erase / clear sequence the reference's UpdateVoxelMap /
+    // ApplyTransformAndRehash issue on m_voxels_L0, m_voxels_L1 and the occupied_children sets, replayed on the real
+    // ankerl::unordered_dense containers by oracle/ref/map_order_golden.cpp to pin the iteration orders.
+    // Records of 7 int32: op, key xyz, child xyz.  op: 1 L0 insert, 2 L0 erase, 3 L1 insert, 4 L1 erase,
+    // 5 child insert (key = L1, child), 6 child erase, 7 L0 clear, 8 L1 clear, 9 end of an update call.
+    std::vector<int32_t>* trace = nullptr;
+    void emit(int op, const VKey& k, const VKey& c = VKey{0, 0, 0}) {
+        if (!trace) return;
+        const int32_t r[7] = {op, k.x, k.y, k.z, c.x, c.y, c.z};
+        trace->insert(trace->end(), r, r + 7);
+    }
+    void l0_erase(const VKey& k) { if (L0.erase(k)) emit(2, k); }
+    void l1_erase(const VKey& k) { if (L1.erase(k)) emit(4, k); }
 
     // PointToVoxelKey — VoxelMap.cpp:50-58
     VKey key_of(const float p[3], int level) const {
@@ -694,18 +707,23 @@ struct VoxelMap {
         p.z = k.z >= 0 ? k.z / f : (k.z - (f - 1)) / f;
         return p;
     }
-    void register_to_parent(const VKey& k) { L1[parent_of(k)].children.insert_key(k); }   // :77-80
+    void register_to_parent(const VKey& k) {                                             // :77-80
+        const VKey p = parent_of(k);
+        if (trace && !L1.find(p)) emit(3, p);
+        if (L1[p].children.insert_key(k)) emit(5, p, k);
+    }
     void unregister_from_parent(const VKey& k) {                                        // :82-97
         VKey p = parent_of(k);
         L1Node* n = L1.find(p);
         if (!n) return;
-        n->children.erase(k);
+        if (n->children.erase(k)) emit(6, p, k);
         if (n->children.size() < 5) n->has_surfel = false;
-        if (n->children.empty()) L1.erase(p);
+        if (n->children.empty()) l1_erase(p);
     }
     void add_point(const float p[3]) {                                                    // :99-120
         VKey key = key_of(p, 0);
         bool was_empty = L0.find(key) == nullptr;
+        if (was_empty) emit(1, key);
         L0Node& v = L0[key];
         int n = v.point_count;
         if (n == 0) {
@@ -739,6 +757,10 @@ struct VoxelMap {
     }
 
     void update(const float* xyz, int n, const double sensor[3], double max_distance, bool is_keyframe) {
+        update_body(xyz, n, sensor, max_distance, is_keyframe);
+        emit(9, VKey{0, 0, 0});
+    }
+    void update_body(const float* xyz, int n, const double sensor[3], double max_distance, bool is_keyframe) {
         ++revision;
         if (!xyz || n <= 0) return;
         if (!is_keyframe) return;
@@ -750,10 +772,10 @@ struct VoxelMap {
             float dsq = dot3f(d0, d1, d2, d0, d1, d2);
             if (dsq > radius_sq) rm.push_back(kv.first);
         }
-        for (auto& k : rm) { unregister_from_parent(k); L0.erase(k); }
+        for (auto& k : rm) { unregister_from_parent(k); l0_erase(k); }
         std::vector<VKey> rm1;
         for (auto& kv : L1.vals) if (kv.second.children.empty()) rm1.push_back(kv.first);
-        for (auto& k : rm1) L1.erase(k);
+        for (auto& k : rm1) l1_erase(k);
 
         KeySet affected;
         for (int i = 0; i < n; ++i) {
@@ -783,8 +805,8 @@ struct VoxelMap {
                 node->has_surfel = false;
                 std::vector<VKey> kids;
                 for (auto& ck : node->children.vals) kids.push_back(ck.first);
-                for (auto& k : kids) L0.erase(k);
-                L1.erase(key1);
+                for (auto& k : kids) l0_erase(k);
+                l1_erase(key1);
                 continue;
             }
             node->has_surfel = true;
@@ -828,7 +850,10 @@ struct VoxelMap {
             tr.emplace_back(key_of(nn.c, 0), nn);
         }
         L0.clear(); L1.clear();
+        emit(7, VKey{0, 0, 0});
+        emit(8, VKey{0, 0, 0});
         for (auto& kn : tr) {
+            if (trace && !L0.find(kn.first)) emit(1, kn.first);
             L0Node& ex = L0[kn.first];
             if (ex.point_count == 0) ex = kn.second;
             else {
@@ -839,6 +864,7 @@ struct VoxelMap {
             register_to_parent(kn.first);
         }
         recompute_all_surfels();
+        emit(9, VKey{0, 0, 0});
     }
 
     // GetSurfelAtPoint — :368-386
@@ -1503,11 +1529,47 @@ void* or_map_create(float voxel_size, int hierarchy_factor, float planarity_thre
     m->compute_surfels = compute_surfels != 0;
     return m;
 }
-void or_map_destroy(void* m) { delete static_cast<VoxelMap*>(m); }
+void or_map_destroy(void* m) { VoxelMap* v = static_cast<VoxelMap*>(m); delete v->trace; delete v; }
 void or_map_update(void* m, const float* xyz, int n, const double sensor[3], double max_distance, int is_keyframe) {
     static_cast<VoxelMap*>(m)->update(xyz, n, sensor, max_distance, is_keyframe != 0);
 }
 void or_map_apply_transform(void* m, const float T[12]) { static_cast<VoxelMap*>(m)->apply_transform(T); }
+
+void or_map_trace(void* m, int enable) {
+    VoxelMap* vm = static_cast<VoxelMap*>(m);
+    delete vm->trace;
+    vm->trace = enable ? new std::vector<int32_t>() : nullptr;
+}
+
+size_t or_map_trace_get(const void* m, int32_t* out, size_t cap) {
+    const VoxelMap* vm = static_cast<const VoxelMap*>(m);
+    if (!vm->trace) return 0;
+    const size_t n = vm->trace->size();
+    if (out) std::memcpy(out, vm->trace->data(), std::min(n, cap) * sizeof(int32_t));
+    return n;
+}
+
+// Iteration orders: L0 keys, L1 keys, and each L1's children (concatenated, L1 order) -- int32 xyz triples.
+size_t or_map_orders(const void* m, int32_t* l0, int32_t* l1, int32_t* child_cnt, int32_t* children, size_t cap) {
+    const VoxelMap* vm = static_cast<const VoxelMap*>(m);
+    size_t nc = 0;
+    for (auto& kv : vm->L1.vals) nc += kv.second.children.size();
+    if (!l0) return nc;
+    size_t i = 0;
+    for (auto& kv : vm->L0.vals) { l0[3 * i] = kv.first.x; l0[3 * i + 1] = kv.first.y; l0[3 * i + 2] = kv.first.z; ++i; }
+    i = 0;
+    size_t c = 0;
+    for (auto& kv : vm->L1.vals) {
+        l1[3 * i] = kv.first.x; l1[3 * i + 1] = kv.first.y; l1[3 * i + 2] = kv.first.z;
+        child_cnt[i] = static_cast<int32_t>(kv.second.children.size());
+        for (auto& ck : kv.second.children.vals) {
+            if (c < cap) { children[3 * c] = ck.first.x; children[3 * c + 1] = ck.first.y; children[3 * c + 2] = ck.first.z; }
+            ++c;
+        }
+        ++i;
+    }
+    return nc;
+}
 int or_map_l0_count(void* m) { return static_cast<int>(static_cast<VoxelMap*>(m)->L0.size()); }
 int or_map_l1_count(void* m) { return static_cast<int>(static_cast<VoxelMap*>(m)->L1.size()); }
 int or_map_surfel_count(void* m) {

@@ -17,6 +17,7 @@
 #ifndef LO_ORACLE_H
 #define LO_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -84,6 +85,10 @@ void*  or_map_create(float voxel_size, int hierarchy_factor, float planarity_thr
 void   or_map_destroy(void* m);
 void   or_map_update(void* m, const float* xyz, int n, const double sensor[3], double max_distance, int is_keyframe);
 void   or_map_apply_transform(void* m, const float T[12]);
+/* container-operation trace of the map (7 int32 per record, see VoxelMap::trace) and the iteration orders */
+void   or_map_trace(void* m, int enable);
+size_t or_map_trace_get(const void* m, int32_t* out, size_t cap);
+size_t or_map_orders(const void* m, int32_t* l0, int32_t* l1, int32_t* child_cnt, int32_t* children, size_t cap);
 int    or_map_l0_count(void* m);
 int    or_map_l1_count(void* m);
 int    or_map_surfel_count(void* m);
