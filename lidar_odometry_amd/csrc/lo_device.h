@@ -202,11 +202,18 @@ template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ int dpp32(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
 }
+// full row mask: v_mov_b32_dpp without an "old" operand (no zeroing move in front of every DPP step)
+template <int CTRL>
+__device__ __forceinline__ int dpp32m(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp64(double v) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const int lo = dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u)));
-    const int hi = dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u >> 32)));
+    const int lo = ROW_MASK == 0xf ? dpp32m<CTRL>(static_cast<int>(static_cast<uint32_t>(u)))
+                                   : dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u)));
+    const int hi = ROW_MASK == 0xf ? dpp32m<CTRL>(static_cast<int>(static_cast<uint32_t>(u >> 32)))
+                                   : dpp32<CTRL, ROW_MASK>(static_cast<int>(static_cast<uint32_t>(u >> 32)));
     return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
 }
 
@@ -224,7 +231,7 @@ __device__ __forceinline__ double wave_total(double v) {
 }
 
 __device__ __forceinline__ float wave_total(float v) {
-#define LO_DPPF(CTRL, RM) __builtin_bit_cast(float, dpp32<CTRL, RM>(__builtin_bit_cast(int, v)))
+#define LO_DPPF(CTRL, RM) __builtin_bit_cast(float, (RM) == 0xf ? dpp32m<CTRL>(__builtin_bit_cast(int, v)) : dpp32<CTRL, RM>(__builtin_bit_cast(int, v)))
     v += LO_DPPF(0xB1, 0xf);
     v += LO_DPPF(0x4E, 0xf);
     v += LO_DPPF(0x141, 0xf);
