@@ -126,6 +126,11 @@ void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
 /* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again (a fresh
  * hipStreamNonBlocking stream -- so the legacy default stream, handle 0, cannot be selected: pass a created stream). */
 int lo_set_stream(lo_ctx* ctx, void* hip_stream);
+/* Lookahead launches for small scans with PKO (default off): every alpha candidate's next GN iteration -- its whole
+ * PKO included -- runs while the current iteration's PKO runs, two iterations per launch, results bit-identical to
+ * the one-iteration-at-a-time path.  Off by default: at KITTI size a candidate chain's sequential normal equations,
+ * solve and correspondence sweeps inside one workgroup outweigh the EM overlap. */
+int lo_set_lookahead(lo_ctx* ctx, int enable);
 /* Enqueue a copy of the current GN state into device memory: 16 floats = pose[12], status, iterations,
  * n_corr, 0.  For the scan-parallel pose gather (RCCL all-gather of these 16 floats per rank). */
 int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);

@@ -62,6 +62,7 @@ struct DevState {
     lo_iter_log logs[LO_MAX_ITERS];
 };
 
+struct KParams;
 struct KParams {
     // scan
     const float* pts;
@@ -72,6 +73,8 @@ struct KParams {
     int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
     float T0[12];
     const float* T0p;                 // batched launches: the job's initial pose in device memory (else T0)
+    KParams* stash;                   // nullable: the first k_correspond of a scan copies these parameters here (init
+                                      // cleared) for kernels that read them from memory (k_la: no kernarg SGPR pressure)
     // KDTree correspondence path (use_surfel_correspondence = 0; lo_kdtree.hip)
     const float4* kd_pts;             // L0 centroids sorted by grid cell: x, y, z, original index (int bits)
     const uint32_t* kd_start;         // cell -> first point (dense grid, ncell + 1 entries)
@@ -126,6 +129,46 @@ struct KParams {
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     DevState* st;
 };
+
+// Lookahead launches (lo_lookahead.hip): one candidate chain's results for GN iterations k, k + 1 of a launch.
+struct LaRec {
+    lo_iter_log log[2];
+    int n_exec;                       // iterations the chain executed: 1 (converged / max_iterations) or 2
+    int conv0, conv1;                 // convergence after iteration k / k + 1
+    int status1;                      // LO_INSUFFICIENT: iteration k + 1 found too few correspondences
+};
+constexpr int kLaThreads = 512;       // lookahead workgroup (8 waves: 2 blocks per pass in the chains' sweeps)
+
+// Per-context lookahead buffers (host-allocated once; candidates c = 0..NA).
+struct LaParams {
+    int n_cap;                        // points per candidate buffer (kFuseMaxBlocks x kBlock)
+    int32_t* slotX;                   // [NA+1][n_cap]      chain-private correspondences of iteration k + 1
+    uint64_t* wmaskX;                 // [NA+1][n_cap/64]
+    int32_t* blkX;                    // [NA+1][kFuseMaxBlocks]
+    int32_t* slotO;                   // [2][NA+1][n_cap]   correspondences of iteration k + 2 (next launch's input)
+    uint64_t* wmaskO;                 // [2][NA+1][n_cap/64]
+    int32_t* blkO;                    // [2][NA+1][kFuseMaxBlocks]
+    double* jsC;                      // [NA+1][NA+1]       each chain's JS grid of iteration k + 1
+    double* jsM;                      // [2][NA+1]          the main JS grid of iteration k
+    DevState* stC;                    // [NA+1]             each chain's GN state for its PKO
+    LaRec* rec;                       // [2][NA+1]
+    unsigned long long* stamp;        // diagnostic build: chain 0's stage timestamps (DevState::dbg + 8)
+};
+
+// The per-iteration buffers a PKO / accumulate / correspondence pass works on: the context's own (own_bufs), or a
+// lookahead chain's (lo_lookahead.hip).  Passed beside the kernel-argument KParams, so a kernel that works on several
+// buffer sets holds a few pointers instead of several KParams copies.
+struct ScanBufs {
+    int32_t* slot;
+    uint64_t* wmask;
+    int32_t* blk_cnt;
+    double* js;
+    DevState* st;
+    const float* pose_in;             // the iteration's pose (nullable: st->pose)
+};
+__device__ __forceinline__ ScanBufs own_bufs(const KParams& P) {
+    return ScanBufs{P.slot, P.wmask, P.blk_cnt, P.js, P.st, nullptr};
+}
 
 // ---------------------------------------------------------------------------------------------------
 // Bit-faithful scalar numerics (compiled with -ffp-contract=off; see DESIGN.md "fp order")
@@ -267,12 +310,12 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 // calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the index of the FIRST alpha with
 // the strictly smallest JS cost, 0 (min_scale_factor) if none is below DBL_MAX.  Every wave computes it
 // redundantly from P.js (lexicographic (cost, index) minimum == first strict minimum).
-__device__ __forceinline__ int pko_select_index(const KParams& P) {
+__device__ __forceinline__ int pko_select_index(const KParams& P, const double* js) {
     const int lane = threadIdx.x & 63;
     double bv = 1.7976931348623157e308;
     int bi = 0x7fffffff;
     for (int i = 1 + lane; i <= P.NA; i += 64) {
-        const double v = P.js[i];
+        const double v = js[i];
         if (v < bv) { bv = v; bi = i; }
     }
 #pragma unroll
@@ -283,6 +326,7 @@ __device__ __forceinline__ int pko_select_index(const KParams& P) {
     }
     return (bv < 1.7976931348623157e308) ? bi : 0;
 }
+__device__ __forceinline__ int pko_select_index(const KParams& P) { return pko_select_index(P, P.js); }
 __device__ __forceinline__ double pko_select_alpha(const KParams& P) {
     const int bi = pko_select_index(P);
     return bi > 0 ? P.alphas[bi] : P.min_scale;
@@ -380,9 +424,9 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
 // ---------------------------------------------------------------------------------------------------
 // One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
 // fp32 products fl(fl(w J_i) J_j) as the reference forms them.
-__device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
-                                          float (&acc)[kNE]) {
-    const int s = P.slot[i];
+__device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot, const float (&T)[12], double scale,
+                                          float dl, int i, float (&acc)[kNE]) {
+    const int s = slot[i];
     if (s < 0) return;
     const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
     const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
@@ -429,6 +473,10 @@ __device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12]
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
     acc[27] += wr * res;
+}
+__device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
+                                          float (&acc)[kNE]) {
+    acc_point(P, P.slot, T, scale, dl, i, acc);
 }
 
 }  // namespace lo

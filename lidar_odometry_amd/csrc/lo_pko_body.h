@@ -1,0 +1,788 @@
+// lo_pko_body.h — PKO adaptive Huber scale (AdaptiveMEstimator::calculate_scale_factor) on the device.
+//
+// Reference: src/optimization/AdaptiveMEstimator.cpp:243-291 (calculate_pko_scale_factor), :294-485 (fit_gmm),
+// :710-787 (calculate_js_divergence).  Per GN iteration:
+//   1. correspondence count n_c and (iteration 0) the normalisation scale std/6 from the per-block stats
+//      that k_correspond wrote (IterativeClosestPointOptimizer.cpp:304-316);
+//   2. the GMM sample r_hat[perm[s]], s < min(100, n_c), where perm = std::shuffle(iota(n_c), mt19937(42))
+//      is answered from host-built tables (lo_pko_tables.h) and rank -> point via block prefix + ballots;
+//   3. k-means (component 0 pinned at 0) + up to 100 EM iterations (fit_gmm);
+//   4. JS divergence of the GMM against the normalised Huber kernel for every alpha of the 100-point grid.
+//
+// Layout on the chip: the EM is a strictly sequential chain of (usually all) 100 iterations, so its latency
+// sets the kernel time.  Every workgroup of the launch fits the same GMM redundantly (identical, deterministic
+// results, no inter-workgroup traffic).  Inside a workgroup the EM is split by component: wave j evaluates
+// only component j's pdf for all samples (ceil(S/64) per lane), the pdfs meet in LDS once per iteration and each
+// wave reduces its own component's sums with a permlane/DPP butterfly (gmm_fit_split).  Splitting the SAMPLES
+// over waves was measured slower (it adds an LDS exchange without shortening the per-lane exp chains).
+// Afterwards workgroup g evaluates the JS divergence for alphas g+1, g+1+G, ... and writes them to global
+// memory.  The argmin over the grid (first strict minimum,
+// as the reference loop) is taken by the consumers (k_accumulate / k_pko_finish) after the kernel boundary,
+// so no in-launch hand-off is needed.
+#pragma once
+#include "lo_device.h"
+
+#include <cfloat>
+
+namespace lo {
+
+__device__ __forceinline__ int pko_sample(const KParams& P, int n, int s) {
+    if (n < P.S) return P.small_perm[P.small_off[n] + s];
+    const int mode = (n <= 65535) ? ((n & 1) ? 0 : 1) : 2;
+    const int lo0 = P.ev_off[mode * (P.S + 1) + s], hi0 = P.ev_off[mode * (P.S + 1) + s + 1];
+    int lo = lo0, hi = hi0;                       // last event step <= n - 1
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (P.ev_steps[mid] <= n - 1) lo = mid + 1; else hi = mid;
+    }
+    return lo == lo0 ? P.base[mode * P.S + s] : P.ev_steps[lo - 1];
+}
+
+// gaussian_pdf (AdaptiveMEstimator.cpp:675-685); NaN variances fall through like the reference
+__device__ __forceinline__ double gpdf(double x, double mean, double variance) {
+    if (variance <= 0.0) return 0.0;
+    const double diff = x - mean;
+    const double expo = -0.5 * (diff * diff) / variance;
+    const double norm = 1.0 / sqrt(2.0 * M_PI * variance);
+    return norm * exp(expo);
+}
+
+__device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {   // :128-156
+    if (!cauchy) { const double a = fabs(r); return a <= d ? 1.0 : d / a; }
+    const double e2 = r * r, d2 = d * d;
+    return d2 / (d2 + e2);
+}
+
+// Diagnostic build only (-DLO_PKO_STAMPS): workgroup 0 / thread 0 stores s_memtime at phase boundaries
+// into DevState::dbg (never read by any other code; the real kernel executes no stamp).
+#ifdef LO_PKO_STAMPS
+#define LO_STAMP(dbg, i) do { if ((dbg) && threadIdx.x == 0) (dbg)[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define LO_COUNT(dbg, i, v) do { if ((dbg) && threadIdx.x == 0) (dbg)[i] = (v); } while (0)
+#else
+#define LO_STAMP(dbg, i) do { } while (0)
+#define LO_COUNT(dbg, i, v) do { } while (0)
+#endif
+
+// exp(y) for y <= 0 or NaN (the E-step exponent -(d^2) * 0.5 / var): Cody-Waite reduction by ln2 and the
+// degree-12 Taylor polynomial on |r| <= ln2/2, its tail c3..c12 evaluated by Estrin (r^2, r^4, r^8) and the last
+// three steps by Horner, so the dependent chain is 7 FMAs instead of 13 with Horner's accuracy: <= 2 ulp from
+// glibc exp over [-745, 0] (checked on 2e7 points; differs from the all-Horner form in 0.08% of them).
+// No overflow branch is needed for y <= 0, and the underflow to 0 falls out of v_ldexp_f64.
+__device__ __forceinline__ double exp_nonpos(double y) {
+    const double n = rint(y * 0x1.71547652b82fep+0);
+    double r = fma(-n, 0x1.62e42fefa39efp-1, y);
+    r = fma(-n, 0x1.abc9e3b39803fp-56, r);
+    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+    const double q0 = fma(0x1.5555555555555p-5, r, 0x1.5555555555555p-3);     // c3 + c4 r
+    const double q1 = fma(0x1.6c16c16c16c17p-10, r, 0x1.1111111111111p-7);    // c5 + c6 r
+    const double q2 = fma(0x1.a01a01a01a01ap-16, r, 0x1.a01a01a01a01ap-13);   // c7 + c8 r
+    const double q3 = fma(0x1.27e4fb7789f5cp-22, r, 0x1.71de3a556c734p-19);   // c9 + c10 r
+    const double q4 = fma(0x1.1eed8eff8d898p-29, r, 0x1.ae64567f544e4p-26);   // c11 + c12 r
+    const double s0 = fma(q1, r2, q0), s1 = fma(q3, r2, q2);
+    const double tail = fma(q4, r8, fma(s1, r4, s0));
+    double p = fma(tail, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, static_cast<int>(n));
+}
+
+// ---- single-wave reductions ------------------------------------------------------------------------
+// Sum of 8 fp64 values over the 64 lanes of a wave without LDS: a butterfly that halves the values per lane
+// while halving the lane group (v_permlane32_swap: lanes 32-63 <-> 0-31, v_permlane16_swap: odd <-> even
+// 16-lane rows, DPP row_ror:8), after which value q sits in lanes 8q..8q+7; three DPP steps finish each
+// 8-lane group and v_readlane broadcasts the totals (wave-uniform results).  ~50 VALU ops, no waits.
+__device__ __forceinline__ void pl32_swap(double& a, double& b) {   // a <- [a_lo | b_lo], b <- [a_hi | b_hi]
+    const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(__double2loint(a)),
+                                                     static_cast<unsigned>(__double2loint(b)), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(__double2hiint(a)),
+                                                     static_cast<unsigned>(__double2hiint(b)), false, false);
+    a = __hiloint2double(static_cast<int>(hi[0]), static_cast<int>(lo[0]));
+    b = __hiloint2double(static_cast<int>(hi[1]), static_cast<int>(lo[1]));
+}
+__device__ __forceinline__ void pl16_swap(double& a, double& b) {   // a <- [a0 b0 a2 b2], b <- [a1 b1 a3 b3] (rows)
+    const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(__double2loint(a)),
+                                                     static_cast<unsigned>(__double2loint(b)), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(__double2hiint(a)),
+                                                     static_cast<unsigned>(__double2hiint(b)), false, false);
+    a = __hiloint2double(static_cast<int>(hi[0]), static_cast<int>(lo[0]));
+    b = __hiloint2double(static_cast<int>(hi[1]), static_cast<int>(lo[1]));
+}
+__device__ __forceinline__ double readlane64(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+template <int NV>
+__device__ __forceinline__ void wave_totals8(double (&v)[NV]) {
+    static_assert(NV >= 1 && NV <= 8, "butterfly handles up to 8 values");
+    double u[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) u[q] = q < NV ? v[q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { pl32_swap(u[q], u[q + 4]); u[q] += u[q + 4]; }   // lo: v_q, hi: v_{q+4}
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { pl16_swap(u[q], u[q + 2]); u[q] += u[q + 2]; }   // rows: v_q v_{q+2} v_{q+4} v_{q+6}
+    const bool up = (threadIdx.x & 8) != 0;
+    double t = up ? u[1] : u[0];
+    const double o = up ? u[0] : u[1];
+    t += dpp64<0x128, 0xf>(o);      // row_ror:8 = lane ^ 8 inside a row -> value q in lanes 8q..8q+7
+    t += dpp64<0xB1, 0xf>(t);       // quad_perm [1,0,3,2]
+    t += dpp64<0x4E, 0xf>(t);       // quad_perm [2,3,0,1]
+    t += dpp64<0x141, 0xf>(t);      // row_half_mirror: 8-lane group total
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 8 * q);
+}
+
+// Up to 4 values with the same pairing tree as wave_totals8 -- lanes (l, l+32), (l, l+16), (l, l+8), then the
+// quad and half-row steps -- so each total is bit-identical to wave_totals8's, with half the permlane traffic:
+// after the 32- and 16-lane swaps row r holds value r, and one row_ror:8 replaces the half-row selects.
+template <int NV>
+__device__ __forceinline__ void wave_totals4(double (&v)[NV]) {
+    static_assert(NV >= 1 && NV <= 4, "butterfly handles up to 4 values");
+    double u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u[q] = q < NV ? v[q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) { pl32_swap(u[q], u[q + 2]); u[q] += u[q + 2]; }   // lo: v_q, hi: v_{q+2}
+    pl16_swap(u[0], u[1]);
+    double t = u[0] + u[1];         // row r: value r
+    t += dpp64<0x128, 0xf>(t);      // row_ror:8
+    t += dpp64<0xB1, 0xf>(t);       // quad_perm [1,0,3,2]
+    t += dpp64<0x4E, 0xf>(t);       // quad_perm [2,3,0,1]
+    t += dpp64<0x141, 0xf>(t);      // row_half_mirror: 8-lane group total
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = readlane64(t, 16 * q);
+}
+
+// fit_gmm (AdaptiveMEstimator.cpp:294-485) with the EM split over the workgroup's waves: wave j < K owns
+// component j (every lane computes ONE pdf per sample instead of K), the per-sample pdfs meet in LDS (s_p) and
+// the summed |d mean| of components >= 1 in s_dm, one barrier per iteration.  Per-lane sample mapping (sample s*64 + lane), the order of the
+// per-sample sum (((0 + p_0) + p_1) + p_2), the per-lane accumulation order and the butterfly tree do not
+// depend on the split (the fitted GMM is bit-identical to a single wave doing all components), with a third of
+// the VALU issue on the critical path.  k-means and the initial variance run redundantly in every wave (identical inputs and code,
+// so identical results, no exchange).  All NW waves execute the loop (waves >= K only join the barriers), and
+// the convergence test reads the same LDS values everywhere, so every wave leaves at the same iteration.
+template <int K, int SPL>
+__device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const int32_t* draws, double* gmm,
+                                              double* s_p, double* s_dm, unsigned long long* dbg) {
+    static_assert(3 * K - 1 <= 8, "partials");
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int j = wid < K ? wid : -1;                      // this wave's component (-1: barriers only)
+    if (j < 0) {
+        // a wave without a component only follows the barriers and the change test (no VALU work that would compete
+        // for issue with a component wave on the same SIMD in workgroups of more than 4 waves)
+        __syncthreads();
+        int buf = 0;
+        for (int em = 0; em < 100; ++em) {
+            __syncthreads();
+            double change = 0.0;
+#pragma unroll
+            for (int q = 1; q < K; ++q) change += s_dm[buf * kMaxK + q];
+            if (change < 1e-6) break;
+            buf ^= 1;
+        }
+        return;
+    }
+    double x[SPL];
+    bool have[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        have[s] = lane + 64 * s < S;
+        x[s] = have[s] ? s_sd[lane + 64 * s] : 0.0;
+    }
+    double mu[K], cnt[K];
+    mu[0] = 0.0;
+#pragma unroll
+    for (int q = 1; q < K; ++q) mu[q] = s_sd[draws[q - 1]];
+#pragma unroll
+    for (int q = 0; q < K; ++q) cnt[q] = 0.0;
+    // ---- k-means until the means repeat exactly (:351-389) ----
+    for (int guard = 0; guard < 100000; ++guard) {
+        double v[2 * K - 1];
+#pragma unroll
+        for (int q = 0; q < 2 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double md = DBL_MAX;
+            int ci = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) { const double d = fabs(x[s] - mu[q]); if (d < md) { md = d; ci = q; } }
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const bool mine = have[s] && ci == q;
+                v[q] += mine ? 1.0 : 0.0;
+                if (q > 0) v[K + q - 1] += mine ? x[s] : 0.0;
+            }
+        }
+        wave_totals8<2 * K - 1>(v);
+        bool eq = true;
+        double nm[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            nm[q] = (q == 0) ? 0.0 : (v[q] > 0.0 ? v[K + q - 1] / v[q] : 0.0);
+            eq = eq && (nm[q] == mu[q]);
+            cnt[q] = v[q];
+        }
+        LO_COUNT(dbg, 9, guard + 1);
+        if (eq) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q) mu[q] = nm[q];
+    }
+    LO_STAMP(dbg, 3);
+    double m1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m1 += have[s] ? x[s] : 0.0;
+    const double mean = wave_total(m1) / S;
+    double m2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m2 += have[s] ? (x[s] - mean) * (x[s] - mean) : 0.0;
+    const double iv = wave_total(m2) / S;
+    const double invS = 1.0 / static_cast<double>(S);
+    constexpr double kInvSqrt2Pi = 0.3989422804014327;
+    // this wave's component state
+    const int jj = j < 0 ? 0 : j;
+    double muj = mu[0], cntj = cnt[0];
+#pragma unroll
+    for (int q = 1; q < K; ++q) if (jj == q) { muj = mu[q]; cntj = cnt[q]; }
+    double wj = cntj / static_cast<double>(S), varj = iv;
+    const double rs0 = rsq64(iv);
+    double ca = (iv <= 0.0) ? 0.0 : wj * (rs0 * kInvSqrt2Pi);
+    double cb = (iv <= 0.0) ? 0.0 : 0.5 * (rs0 * rs0);
+    LO_STAMP(dbg, 4);
+
+    // One barrier per iteration: after its M-step each wave evaluates the NEXT iteration's pdfs with the updated
+    // parameters (speculatively) into the other half of the double-buffered s_p / s_dm, then the barrier; if
+    // the change test then ends the EM, the speculative pdfs are simply dropped (the parameters are those of
+    // the converged M-step, as the reference's loop leaves them).
+    constexpr int kStride = 64 * SPL;                      // s_p[buffer][component][sample]
+    constexpr int kBuf = K * kStride;
+    double p[SPL], d[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        d[s] = x[s] - muj;
+        p[s] = ca * exp_nonpos(-((d[s] * d[s]) * cb));
+        if (j >= 0) s_p[j * kStride + 64 * s + lane] = p[s];
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int em = 0; em < 100; ++em) {
+        const double* sp = s_p + buf * kBuf;
+        double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double sr = sp[64 * s + lane];                 // pdfs are >= +0 (or NaN): 0 + p_0 == p_0
+#pragma unroll
+            for (int q = 1; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
+            const double isr = have[s] ? rcp64(sr) : 0.0;
+            const double r = p[s] * isr;
+            v[0] += r;
+            v[1] += r * x[s];
+            v[2] += (r * d[s]) * d[s];
+        }
+        wave_totals4<3>(v);
+        const double Nk = v[0];
+        const double iN = rcp64(Nk);
+        const double nmu = (jj == 0) ? 0.0 : v[1] * iN;
+        const double dm = nmu - muj;
+        double nv = v[2] * iN - dm * dm;
+        nv = (nv < 1e-6) ? 1e-6 : nv;                      // std::max(nv, 1e-6), NaN preserved
+        wj = Nk * invS;
+        muj = nmu;
+        varj = nv;
+        const double rs = rsq64(nv);
+        ca = wj * (rs * kInvSqrt2Pi);
+        cb = 0.5 * (rs * rs);
+        if (j >= 1 && lane == 0) s_dm[buf * kMaxK + j] = fabs(dm);
+        double* spn = s_p + (buf ^ 1) * kBuf;              // speculative E-step of iteration em + 1
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            d[s] = x[s] - muj;
+            p[s] = ca * exp_nonpos(-((d[s] * d[s]) * cb));
+            if (j >= 0) spn[j * kStride + 64 * s + lane] = p[s];
+        }
+        __syncthreads();
+        double change = 0.0;
+#pragma unroll
+        for (int q = 1; q < K; ++q) change += s_dm[buf * kMaxK + q];
+        LO_COUNT(dbg, 8, em + 1);
+        if (change < 1e-6) break;
+        buf ^= 1;
+    }
+    LO_STAMP(dbg, 5);
+    if (j >= 0 && lane == 0) { gmm[j] = wj; gmm[K + j] = muj; gmm[2 * K + j] = varj; }
+}
+
+// Batched launches: the whole fit on ONE wave (all K components), bit-identical to gmm_fit_split -- the same
+// per-sample sum (((0 + p_0) + p_1) + p_2), per-lane accumulation order and butterfly tree per value (the tree a
+// value goes through in wave_totals8 does not depend on its slot).  A batch is bound by fp64 issue, not by the
+// EM's latency: one wave drops the two extra butterflies, reciprocals and pdf exchanges the split pays per
+// iteration, and no other wave replicates k-means.
+template <int K, int SPL>
+__device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int32_t* draws, double* gmm) {
+    static_assert(3 * K - 1 <= 8, "partials");
+    const int lane = threadIdx.x & 63;
+    double x[SPL];
+    bool have[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        have[s] = lane + 64 * s < S;
+        x[s] = have[s] ? s_sd[lane + 64 * s] : 0.0;
+    }
+    double mu[K], cnt[K];
+    mu[0] = 0.0;
+#pragma unroll
+    for (int q = 1; q < K; ++q) mu[q] = s_sd[draws[q - 1]];
+#pragma unroll
+    for (int q = 0; q < K; ++q) cnt[q] = 0.0;
+    for (int guard = 0; guard < 100000; ++guard) {            // k-means as gmm_fit_split
+        double v[2 * K - 1];
+#pragma unroll
+        for (int q = 0; q < 2 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double md = DBL_MAX;
+            int ci = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) { const double d = fabs(x[s] - mu[q]); if (d < md) { md = d; ci = q; } }
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const bool mine = have[s] && ci == q;
+                v[q] += mine ? 1.0 : 0.0;
+                if (q > 0) v[K + q - 1] += mine ? x[s] : 0.0;
+            }
+        }
+        wave_totals8<2 * K - 1>(v);
+        bool eq = true;
+        double nm[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            nm[q] = (q == 0) ? 0.0 : (v[q] > 0.0 ? v[K + q - 1] / v[q] : 0.0);
+            eq = eq && (nm[q] == mu[q]);
+            cnt[q] = v[q];
+        }
+        if (eq) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q) mu[q] = nm[q];
+    }
+    double m1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m1 += have[s] ? x[s] : 0.0;
+    const double mean = wave_total(m1) / S;
+    double m2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) m2 += have[s] ? (x[s] - mean) * (x[s] - mean) : 0.0;
+    const double iv = wave_total(m2) / S;
+    const double invS = 1.0 / static_cast<double>(S);
+    constexpr double kInvSqrt2Pi = 0.3989422804014327;
+    double w[K], var[K], ca[K], cb[K];
+    const double rs0 = rsq64(iv);
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        w[q] = cnt[q] / static_cast<double>(S);
+        var[q] = iv;
+        ca[q] = (iv <= 0.0) ? 0.0 : w[q] * (rs0 * kInvSqrt2Pi);
+        cb[q] = (iv <= 0.0) ? 0.0 : 0.5 * (rs0 * rs0);
+    }
+    double p[K][SPL], d[K][SPL];
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            d[q][s] = x[s] - mu[q];
+            p[q][s] = ca[q] * exp_nonpos(-((d[q][s] * d[q][s]) * cb[q]));
+        }
+    for (int em = 0; em < 100; ++em) {
+        double v[3 * K - 1];                                  // N_q | sum r x (q >= 1) | sum r d^2
+#pragma unroll
+        for (int q = 0; q < 3 * K - 1; ++q) v[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            double sr = p[0][s];                           // as gmm_fit_split: 0 + p_0 == p_0
+#pragma unroll
+            for (int q = 1; q < K; ++q) sr += p[q][s];
+            const double isr = have[s] ? rcp64(sr) : 0.0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const double r = p[q][s] * isr;
+                v[q] += r;
+                if (q > 0) v[K + q - 1] += r * x[s];
+                v[2 * K - 1 + q] += (r * d[q][s]) * d[q][s];
+            }
+        }
+        wave_totals8<3 * K - 1>(v);
+        double change = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const double Nk = v[q];
+            const double iN = rcp64(Nk);
+            const double nmu = (q == 0) ? 0.0 : v[K + q - 1] * iN;
+            const double dm = nmu - mu[q];
+            double nv = v[2 * K - 1 + q] * iN - dm * dm;
+            nv = (nv < 1e-6) ? 1e-6 : nv;
+            w[q] = Nk * invS;
+            mu[q] = nmu;
+            var[q] = nv;
+            const double rs = rsq64(nv);
+            ca[q] = w[q] * (rs * kInvSqrt2Pi);
+            cb[q] = 0.5 * (rs * rs);
+            if (q >= 1) change += fabs(dm);
+        }
+        if (change < 1e-6) break;
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                d[q][s] = x[s] - mu[q];
+                p[q][s] = ca[q] * exp_nonpos(-((d[q][s] * d[q][s]) * cb[q]));
+            }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) { gmm[q] = w[q]; gmm[K + q] = mu[q]; gmm[2 * K + q] = var[q]; }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm,
+                                                 double* s_p, double* s_dm, unsigned long long* dbg) {
+    if (S <= 64) gmm_fit_split<K, 1>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+    else if (S <= 128) gmm_fit_split<K, 2>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+    else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+}
+
+template <int K>
+__device__ __forceinline__ void gmm_fit_1w_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm) {
+    if ((threadIdx.x >> 6) != 0) return;                  // wave 0 fits; any other wave goes on to the barrier
+    if (S <= 64) gmm_fit_1w<K, 1>(s_sd, S, draws, gmm);
+    else if (S <= 128) gmm_fit_1w<K, 2>(s_sd, S, draws, gmm);
+    else gmm_fit_1w<K, 4>(s_sd, S, draws, gmm);
+}
+
+// Speculative normal equations (single-scan launches of small scans, nb_acc <= kFuseMaxBlocks).  The accumulate
+// pass depends on the PKO only through the Huber delta, one of NA + 1 values (alphas[1..NA], or min_scale when no
+// JS cost is finite).  Workgroups G, G+1, ... of the PKO launch evaluate every candidate while the GMM fit runs,
+// and k_solve_pick reduces the selected one: the accumulate leaves the iteration's critical path.  Workgroup wgi
+// takes candidate wgi / W (W = ceil(nb_acc / kSpecBlocksPerWG)) and its kSpecBlocksPerWG 256-point blocks
+// starting at kSpecBlocksPerWG * (wgi % W); each block's partial is formed exactly as accumulate_body forms it
+// (one point per thread, fp32 wave_total, fp64 sum over the 4 waves), so the solve is bit-identical.
+__device__ void acc_candidate(const KParams& P, double scale, int wgi) {
+    const int nb = P.nb_acc;
+    const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
+    const int c = wgi / W, part = wgi - c * W;
+    if (c > P.NA) return;
+    const float dl = static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
+    __shared__ float s_acc[kWavesPerBlock][kNE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+    const int n = scan_n(P);
+    double* dst = P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE;
+    const int vb1 = min(nb, (part + 1) * kSpecBlocksPerWG);
+    for (int vb = part * kSpecBlocksPerWG; vb < vb1; ++vb) {
+        float acc[kNE];
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
+        const int i = vb * kBlock + tid;
+        if (i < n) acc_point(P, T, scale, dl, i, acc);
+#pragma unroll
+        for (int k = 0; k < kNE; ++k) {
+            const float v = wave_total(acc[k]);
+            if (lane == 0) s_acc[wid][k] = v;
+        }
+        __syncthreads();
+        if (tid < kNE) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
+            dst[static_cast<size_t>(vb) * kNE + tid] = v;
+        }
+        __syncthreads();
+    }
+}
+
+// Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts
+// (s_pre, nb ints of LDS) and the normalisation scale -- iteration 0: std/6 of the accepted residuals from the
+// per-block (count, sum, M2) by a Chan merge about the global mean (IterativeClosestPointOptimizer.cpp:304-316);
+// later iterations: DevState::scale.  With nb <= 64 every block sits in wave 0, so the result does not depend on
+// NW.  lead: this workgroup publishes the iteration-0 scale.
+template <int NW>
+__device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, int it, bool lead, int* s_pre,
+                                           int& nc_out, double& scale_out) {
+    constexpr int NT = NW * 64;
+    DevState* st = B.st;
+    __shared__ int s_iscan[NW];
+    __shared__ double s_dscan[NW];
+    __shared__ int s_nc;
+    __shared__ double s_scale, s_mean;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (P.direct_res) {
+        if (tid == 0) { s_nc = P.n; s_scale = 1.0; }
+        __syncthreads();
+    } else {
+        const int nb = P.nb;
+        // (a) coalesced pass: block counts -> LDS, total count / residual sum
+        int cnt = 0;
+        double lsum = 0.0;
+#pragma unroll 4
+        for (int b = tid; b < nb; b += NT) {
+            const int c = B.blk_cnt[b];
+            s_pre[b] = c;
+            cnt += c;
+            if (it == 0) lsum += P.blk_sum[b];
+        }
+        cnt = wave_sum(cnt);
+        lsum = wave_total(lsum);
+        if (lane == 0) { s_iscan[wid] = cnt; s_dscan[wid] = lsum; }
+        __syncthreads();
+        if (tid == 0) {
+            int run = 0;
+            double tot = 0.0;
+            for (int w = 0; w < NW; ++w) { run += s_iscan[w]; tot += s_dscan[w]; }
+            s_nc = run;
+            s_mean = run > 0 ? tot / run : 0.0;
+        }
+        __syncthreads();
+        // (b) contiguous ranges of the counts (LDS) for the exclusive prefix; iteration 0: Chan merge of the
+        //     per-block (count, sum, M2) about the global mean, coalesced
+        const int per = (nb + NT - 1) / NT;
+        const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+        int loc = 0;
+        for (int b = b0; b < b1; ++b) loc += s_pre[b];
+        int inc = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
+        double m2 = 0.0;
+        if (it == 0) {
+            const double mean = s_mean;
+#pragma unroll 4
+            for (int b = tid; b < nb; b += NT) {
+                const int c = s_pre[b];
+                if (c > 0) { const double dm = P.blk_sum[b] / c - mean; m2 += P.blk_m2[b] + c * (dm * dm); }
+            }
+            m2 = wave_total(m2);
+        }
+        __syncthreads();                                         // s_iscan / s_dscan reuse
+        if (lane == 63) s_iscan[wid] = inc;
+        if (lane == 0) s_dscan[wid] = m2;
+        __syncthreads();
+        if (tid == 0) {
+            int run = 0;
+            double M2 = 0.0;
+            for (int w = 0; w < NW; ++w) { const int c = s_iscan[w]; s_iscan[w] = run; run += c; M2 += s_dscan[w]; }
+            if (it == 0) {
+                const double var = s_nc > 0 ? M2 / s_nc : 0.0;
+                s_scale = sqrt(var) / 6.0;                      // IterativeClosestPointOptimizer.cpp:314-315
+                if (lead) st->scale = s_scale;
+            } else {
+                s_scale = st->scale;
+            }
+        }
+        __syncthreads();
+        int excl = s_iscan[wid] + inc - loc;
+        for (int b = b0; b < b1; ++b) { const int c = s_pre[b]; s_pre[b] = excl; excl += c; }
+        __syncthreads();
+    }
+    nc_out = s_nc;
+    scale_out = s_scale;
+}
+
+// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
+// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate).
+// ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
+template <int NW, bool ONE_WAVE>
+__device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, int it, int wg, int G) {
+    constexpr int NT = NW * 64;
+    DevState* st = B.st;
+    if (st->done) return;
+    unsigned long long* dbg = nullptr;
+#ifdef LO_PKO_STAMPS
+    if (wg == 0) dbg = st->dbg;
+#endif
+    LO_STAMP(dbg, 0);
+    extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
+    // s_p: the split EM's per-sample pdfs of each component (double-buffered), then the JS terms (>= 20 alphas)
+    constexpr int kPbuf = (2 * kMaxK * 64 * NW > 2000) ? 2 * kMaxK * 64 * NW : 2000;
+    __shared__ double s_sd[kMaxS];
+    __shared__ double s_gmm[3 * kMaxK];
+    __shared__ double s_P[100];
+    __shared__ double s_p[kPbuf];
+    __shared__ double s_dm[2 * kMaxK];
+
+    const int tid = threadIdx.x;
+    const bool lead = wg == 0;
+
+    // ---- 0. prefetch what later phases need but does not depend on n_c, so its latency hides behind the
+    //         prefix phase: this thread's sample slot (s = tid) event-list bounds and base value for the three
+    //         shuffle modes, the k-means draws for S = P.S, and (one alpha per workgroup) this alpha and Z ----
+    __shared__ int32_t s_draws[kMaxK];
+    int pf_lo[3] = {0, 0, 0}, pf_hi[3] = {0, 0, 0}, pf_base[3] = {0, 0, 0};
+    if (tid < P.S) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            pf_lo[m] = P.ev_off[m * (P.S + 1) + tid];
+            pf_hi[m] = P.ev_off[m * (P.S + 1) + tid + 1];
+            pf_base[m] = P.base[m * P.S + tid];
+        }
+    }
+    const int D0 = P.K > 1 ? P.K - 1 : 1;
+    if (tid < D0) s_draws[tid] = P.km_draws[P.S * D0 + tid];
+    const bool one_alpha = G >= P.NA;                       // the single-scan launch: alpha 1 + wg only
+    double pf_alpha = 0.0, pf_Z = 0.0;
+    if (one_alpha && 1 + wg <= P.NA) { pf_alpha = P.alphas[1 + wg]; pf_Z = P.Z[1 + wg]; }
+
+    // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
+    int nc;
+    double s_scale;
+    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale);
+    if (!P.direct_res && nc < P.min_corr) {                     // :298-302
+        if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
+        return;
+    }
+    if constexpr (NW == 4 && !ONE_WAVE) {
+        if (wg >= G) {                                          // after the scale: the candidates need it
+            acc_candidate(P, s_scale, wg - G);
+            return;
+        }
+    }
+    if (lead && tid == 0) st->n_corr = nc;
+    if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
+    const double scale = s_scale;
+    const double sden = (scale < 1e-6) ? 1e-6 : scale;         // std::max(scale, 1e-6)
+    LO_STAMP(dbg, 1);
+
+    // ---- 2. the reference's GMM sample ----
+    const int S = min(P.S, nc);
+    for (int sidx = tid; sidx < S; sidx += NT) {
+        int rank;
+        if (sidx == tid && nc >= P.S && sidx < P.S) {          // prefetched bounds: one round of event loads
+            const int mode = (nc <= 65535) ? ((nc & 1) ? 0 : 1) : 2;
+            const int lo0 = mode == 0 ? pf_lo[0] : (mode == 1 ? pf_lo[1] : pf_lo[2]);
+            const int hi0 = mode == 0 ? pf_hi[0] : (mode == 1 ? pf_hi[1] : pf_hi[2]);
+            rank = mode == 0 ? pf_base[0] : (mode == 1 ? pf_base[1] : pf_base[2]);
+            for (int e0 = lo0; e0 < hi0; e0 += 8) {             // ascending steps: the last one <= n - 1 wins
+                int ev[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ev[u] = (e0 + u < hi0) ? P.ev_steps[e0 + u] : 0x7fffffff;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) if (ev[u] <= nc - 1) rank = ev[u];
+            }
+        } else {
+            rank = pko_sample(P, nc, sidx);
+        }
+        double v;
+        if (P.direct_res) {
+            v = P.direct_res[rank];
+        } else {
+            int lo = 0, hi = P.nb - 1;                          // last block with prefix <= rank
+            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (s_pre[mid] <= rank) lo = mid; else hi = mid - 1; }
+            const int b = lo;
+            int k = rank - s_pre[b];
+            uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
+#pragma unroll
+            for (int q = 0; q < kWavesPerBlock; ++q) m4[q] = B.wmask[b * kWavesPerBlock + q];
+            int w = 0;
+            uint64_t mk = m4[0];
+#pragma unroll
+            for (int q = 0; q + 1 < kWavesPerBlock; ++q) {
+                const int c = __popcll(mk);
+                if (w == q && k >= c) { k -= c; w = q + 1; mk = m4[q + 1]; }
+            }
+            for (int q = 0; q < k; ++q) mk &= mk - 1;
+            const int bit = __ffsll(static_cast<unsigned long long>(mk)) - 1;
+            const int pidx = b * kBlock + w * kWave + bit;
+            if (P.kd_res) {
+                v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
+            } else {
+                float T[12];
+#pragma unroll
+                for (int q = 0; q < 12; ++q) T[q] = B.pose_in ? B.pose_in[q] : st->pose[q];
+                float wx, wy, wz;
+                transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
+                v = residual_f64(P.tab[B.slot[pidx]], wx, wy, wz) / sden;   // :321-326
+            }
+        }
+        s_sd[sidx] = v;
+    }
+    __syncthreads();
+    LO_STAMP(dbg, 2);
+
+    // ---- 3. GMM ----
+    const int D = P.K > 1 ? P.K - 1 : 1;
+    const int32_t* draws = (S == P.S) ? s_draws : P.km_draws + S * D;
+    if (ONE_WAVE) {                                             // wave 0 alone: see gmm_fit_1w
+        switch (P.K) {
+            case 1: gmm_fit_1w_dispatch<1>(s_sd, S, draws, s_gmm); break;
+            case 2: gmm_fit_1w_dispatch<2>(s_sd, S, draws, s_gmm); break;
+            default: gmm_fit_1w_dispatch<3>(s_sd, S, draws, s_gmm); break;
+        }
+    } else {
+        switch (P.K) {                                          // every wave: see gmm_fit_split
+            case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+            case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+            default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+        }
+    }
+    __syncthreads();
+    if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
+
+    // ---- 4. JS divergence for this workgroup's alphas (calculate_js_divergence :710-787) ----
+    const int K = P.K;
+    const double dr = P.trunc / 100.0;
+    for (int b = tid; b < 100; b += NT) {
+        const double r = dr * (1 + static_cast<double>(b));
+        double g[kMaxK];                                         // independent pdf chains, then the ordered sum
+#pragma unroll
+        for (int m = 0; m < kMaxK; ++m) g[m] = m < K ? s_gmm[m] * gpdf(r, s_gmm[K + m], s_gmm[2 * K + m]) : 0.0;
+        double Pr = 0.0;
+#pragma unroll
+        for (int m = 0; m < kMaxK; ++m) if (m < K) Pr += g[m];
+        s_P[b] = Pr + 1e-10;
+    }
+    __syncthreads();
+    // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
+    // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25)
+    constexpr int kJsPass = kPbuf / 100;
+    double* s_jsd = s_p;
+    for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kJsPass) {
+        for (int idx = tid; idx < kJsPass * 100; idx += NT) {
+            const int a = idx / 100, b = idx - a * 100;
+            const int ai = a0 + a * G;
+            if (ai > P.NA) continue;
+            const double alpha = one_alpha ? pf_alpha : P.alphas[ai];
+            const double pf = one_alpha ? pf_Z : P.Z[ai];
+            const double r = dr * (1 + static_cast<double>(b));
+            const double Pr = s_P[b];
+            const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
+            const double M = 0.5 * (Pr + Q);
+            s_jsd[idx] = 0.5 * (Pr * log(Pr / M) + Q * log(Q / M));
+        }
+        __syncthreads();
+        if (tid < kJsPass) {
+            const int ai = a0 + tid * G;
+            if (ai <= P.NA) {
+                double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
+                const double* row = s_jsd + tid * 100;
+                double vb[10], vn[10];                           // LDS reads of the next 10 bins in flight while
+#pragma unroll                                                   // the serial adds consume the current ones
+                for (int q = 0; q < 10; ++q) vb[q] = row[q];
+                for (int b0 = 0; b0 < 100; b0 += 10) {
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) vn[q] = (b0 + 10 < 100) ? row[b0 + 10 + q] : 0.0;
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) {
+                        const bool ok = !isnan(vb[q]);
+                        cost += ok ? vb[q] : 0.0;                // cost starts at +0: adding +0 == skipping
+                        cnt += ok ? 1.0 : 0.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) vb[q] = vn[q];
+                }
+                B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
+            }
+        }
+        __syncthreads();
+    }
+    LO_STAMP(dbg, 6);
+}
+
+}  // namespace lo

@@ -180,12 +180,10 @@ __device__ __forceinline__ void solve_sums(const double* part_src, int nrows, do
 }
 
 // One lane: H, g, cost from the summed normal equations, pivoted LDLT (:418), SE3 right-update of pose_old into
-// pose_new with SO(3) re-projection (:422-434); with publish also the GN state (pose, per-iteration log, iteration
-// count, convergence flag :437-448).  Returns the convergence test.  pose_old may alias DevState::pose (it is read
-// before anything is written).
-__device__ inline bool solve_core(const KParams& P, int it, const double* tot, const float* pose_old, float* pose_new,
-                           bool publish) {
-    DevState* st = P.st;
+// pose_new with SO(3) re-projection (:422-434) and the convergence test (:437-448).  L (nullable) receives the
+// iteration's log except n_corr / scale / alpha.  pose_old may alias pose_new's source state (read first).
+__device__ inline bool solve_step(const KParams& P, const double* tot, const float* pose_old, float* pose_new,
+                                  lo_iter_log* L) {
     double H[36], g[6];
     int k = 0;
     for (int r = 0; r < 6; ++r)
@@ -216,19 +214,31 @@ __device__ inline bool solve_core(const KParams& P, int it, const double* tot, c
 
     const float tdel = sqrtf(dot3f(dt[0], dt[1], dt[2], dt[0], dt[1], dt[2]));
     const float rdel = sqrtf(dot3f(dw[0], dw[1], dw[2], dw[0], dw[1], dw[2]));
-    const bool conv = tdel < P.tol_t && rdel < P.tol_r;               // :443-448
-    if (!publish) return conv;
+    if (L) {
+        for (int q = 0; q < 12; ++q) L->pose[q] = pose_new[q];
+        L->cost = static_cast<float>(cost);
+        k = 0;
+        for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L->H[k++] = static_cast<float>(H[r * 6 + c]);
+        for (int j = 0; j < 6; ++j) { L->g[j] = static_cast<float>(g[j]); L->delta[j] = delta[j]; }
+    }
+    return tdel < P.tol_t && rdel < P.tol_r;                          // :443-448
+}
+
+// solve_step, and with publish also the GN state (pose, per-iteration log, iteration count, convergence flag).
+// Returns the convergence test.  pose_old may alias DevState::pose (it is read before anything is written).
+__device__ inline bool solve_core(const KParams& P, int it, const double* tot, const float* pose_old, float* pose_new,
+                                  bool publish) {
+    DevState* st = P.st;
+    if (!publish) return solve_step(P, tot, pose_old, pose_new, nullptr);
+    lo_iter_log Lg;
+    const bool conv = solve_step(P, tot, pose_old, pose_new, &Lg);
     for (int q = 0; q < 12; ++q) st->pose[q] = pose_new[q];
     if (it < LO_MAX_ITERS) {                                          // the loop-closure ICP runs up to 100
         lo_iter_log& L = st->logs[it];
-        for (int q = 0; q < 12; ++q) L.pose[q] = pose_new[q];
+        L = Lg;
         L.n_corr = st->n_corr;
         L.scale = st->scale;
         L.alpha = st->alpha;
-        L.cost = static_cast<float>(cost);
-        k = 0;
-        for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L.H[k++] = static_cast<float>(H[r * 6 + c]);
-        for (int j = 0; j < 6; ++j) { L.g[j] = static_cast<float>(g[j]); L.delta[j] = delta[j]; }
     }
     st->iter = it + 1;
     if (conv) st->done = 1;
