@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MALL_BYTES = 256 << 20     # Infinity Cache (MALL) capacity
 METRIC = "ICP GN-iterations/sec and scans/sec on KITTI-07 @ 1/2/4/8 GPU; % HBM BW"
 ORDER = "azimuth"          # patch1m point order (--order)
 
@@ -57,26 +58,45 @@ def _claim_stdout():
 # --------------------------------------------------------------------------------------------------
 # workloads (product-side data path only: synth + lo_voxelmap + lo_voxel_filter)
 # --------------------------------------------------------------------------------------------------
-def build_kitti(rank: int):
+def _raycast_device(rank: int):
+    """Device for generating the synthetic scans (torch raycast on the rank's GPU; numpy on a CPU-only host)."""
+    import torch
+    if not torch.cuda.is_available():
+        return None
+    return f"cuda:{int(os.environ.get('LOCAL_RANK', rank)) % max(torch.cuda.device_count(), 1)}"
+
+
+def build_kitti(rank: int, n_map: int = 300, name: str = ""):
+    """KITTI-07-like workload: the surfel map after n_map frames of keyframing (a keyframe every
+    2 frames ~ 1.2 m, kitti.yaml keyframe_distance 1.0; UpdateVoxelMap prunes to 1.2 x 100 m), then 20 scans from the
+    last 40 frames between keyframes with perturbed initial poses."""
     from lidar_odometry_amd import synth
     from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
-    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
+    dev = _raycast_device(rank)
+    seq = synth.KittiLikeSequence(seed=7, n_frames=n_map + 2)
     vm = VoxelMap(0.5, 3, 0.1, True)
     kf = []
-    for k in range(0, 41, 2):                       # keyframes ~1.2 m apart (kitti.yaml keyframe_distance 1.0)
-        pts = voxel_filter(seq.scan(k), 0.5, 8)     # FastVoxelFilter, point_stride 8, voxel 0.5
+    for k in range(0, n_map + 1, 2):
+        pts = voxel_filter(seq.scan(k, device=dev), 0.5, 8)     # FastVoxelFilter, point_stride 8, voxel 0.5
         T = seq.poses[k]
         w = synth.transform(T, pts)
         vm.update(w, T[:3, 3], 120.0, True)         # UpdateVoxelMap(.., 1.2 * max_range)
         kf.append((w, T[:3, 3].copy()))
     rng = np.random.default_rng(42 + rank)
-    scans, inits, gts = [], [], []
-    for f in range(1, 40, 2):                       # the frames between keyframes
-        scans.append(voxel_filter(seq.scan(f), 0.5, 8))
+    scans, inits, gts, frames = [], [], [], list(range(n_map - 39, n_map, 2))
+    for f in frames:
+        scans.append(voxel_filter(seq.scan(f, device=dev), 0.5, 8))
         inits.append(synth.perturb(seq.poses[f], rng, 0.05, 0.01))
         gts.append(seq.poses[f])
-    return {"name": "KITTI-07-like HDL-64 scan (stride 8, 0.5 m voxels) surfel ICP, config/kitti.yaml",
-            "voxel": 0.5, "max_dist": 120.0, "vm": vm, "scans": scans, "inits": inits, "gts": gts, "keyframes": kf}
+    return {"name": name or f"KITTI-07-like HDL-64 scan (stride 8, 0.5 m voxels) surfel ICP, config/kitti.yaml, map after "
+                            f"{n_map} frames",
+            "voxel": 0.5, "max_dist": 120.0, "vm": vm, "scans": scans, "inits": inits, "gts": gts, "keyframes": kf,
+            "seq": seq, "frames": frames, "raycast_device": dev}
+
+
+def build_kitti_small(rank: int):
+    """Round-1 workload, kept as a labelled secondary line: the map after 42 frames (1.5k surfels)."""
+    return build_kitti(rank, n_map=40, name="KITTI-07-like HDL-64 scan surfel ICP, small map (42 frames, round-1 line)")
 
 
 def build_mid360(rank: int):
@@ -125,10 +145,8 @@ def build_patch1m(rank: int):
 
 def build_kitti_raw(rank: int):
     """Raw HDL-64 scans: the step is Estimator::preprocess_frame (device FastVoxelFilter, stride 8, 0.5 m) + optimize."""
-    from lidar_odometry_amd import synth
     wl = build_kitti(rank)
-    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
-    wl["raw_scans"] = [seq.scan(f) for f in range(1, 40, 2)]
+    wl["raw_scans"] = [wl["seq"].scan(f, device=wl["raycast_device"]) for f in wl["frames"]]
     wl["name"] = "KITTI-07-like raw HDL-64 scan -> device voxel filter (stride 8, 0.5 m) -> surfel ICP, config/kitti.yaml"
     wl["raw"] = True
     return wl
@@ -141,7 +159,7 @@ def build_kitti_kdtree(rank: int):
     return wl
 
 
-WORKLOADS = {"kitti": build_kitti, "kitti_raw": build_kitti_raw, "kitti_kdtree": build_kitti_kdtree, "mid360": build_mid360,
+WORKLOADS = {"kitti": build_kitti, "kitti_small": build_kitti_small, "kitti_raw": build_kitti_raw, "kitti_kdtree": build_kitti_kdtree, "mid360": build_mid360,
              "patch1m": build_patch1m}
 
 
@@ -215,6 +233,17 @@ def read_pmc_traffic(workload_key: str):
             d = json.load(f)
         e = d.get(workload_key)
         return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def read_pko_latency():
+    """The dominant kernel's latency roofline (k_pko_t: a strictly sequential fp64 EM chain, neither HBM- nor
+    MFMA-bound): measured cycles per EM iteration against the floor from measured instruction costs, from the
+    committed profiles/pko_latency.json (scripts/pko_stamps.py + scripts/lat_bench.hip on the GPU box)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pko_latency.json")) as f:
+            return json.load(f)
     except Exception:
         return None
 
@@ -582,6 +611,12 @@ def main():
         st = icp.get_last_stats()
         iters.append(st.num_iterations)
         errs.append(float(np.linalg.norm(To[:, 3] - wl["gts"][i][:3, 3])))
+    # algorithmic bytes of each scan's first correspondence pass at its initial pose (formula: see alg_bytes below)
+    scan_alg_bytes = []
+    for i in range(len(d_scans)):
+        nv_i, _, _ = icp.find_correspondences(wl["scans"][i], inits[i])
+        ni = len(wl["scans"][i])
+        scan_alg_bytes.append(ni * (12 + 80 + 40 + 4 + 0.125) + 40 * nv_i if kd else ni * (12 + 8 + 4 + 0.125) + 24 * nv_i)
     L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
     for k in range(args.warmup):
         step(k)
@@ -637,6 +672,23 @@ def main():
                                C.c_double(scale0), C.c_double(alpha0), kid, reps, C.byref(ms))
         assert rc == 0, rc
         kern_us[name] = ms.value * 1e3
+    # in-step duration of each scan's first correspondence launch (HIP events on the context stream around that
+    # launch inside the real GN loop), over a separate pass of the same steps (events would perturb the timed pass)
+    n_in = min(args.steps, 200)
+    L.lo_set_stage_timing(icp.ctx, 1)
+    in_bytes = 0.0
+    for k in range(n_in):
+        i = k % len(d_scans)
+        if raw:
+            rc = L.lo_icp_optimize_raw_async(icp.ctx, C.c_void_p(d_raw[i].data_ptr()), d_raw[i].shape[0], 8,
+                                             C.c_float(0.5), fptr(inits[i]))
+        else:
+            rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]))
+        assert rc == 0, rc
+        in_bytes += scan_alg_bytes[i]
+    in_us, in_cnt = C.c_double(0.0), C.c_int(0)
+    assert L.lo_stage_time(icp.ctx, C.byref(in_us), C.byref(in_cnt)) == 0
+    L.lo_set_stage_timing(icp.ctx, 0)
     n0 = d_scans[i0].shape[0]
     n_valid, valid, _ = icp.find_correspondences(wl["scans"][i0], inits[i0])
     v = n_valid / n0
@@ -650,6 +702,7 @@ def main():
         alg_bytes = n0 * (12 + 80 + 40 + 4 + 0.125 + 40 * v)
         corr_kernel = stage0
     t_corr = kern_us[stage0] * 1e-6
+    ws_bytes = float(n0 * (12 + 4 + 32))
     achieved = alg_bytes / t_corr / 1e9
     traffic = read_pmc_traffic(args.config + ("_random" if args.config == "patch1m" and ORDER == "random" else ""))
     # where a step's device time goes: isolated kernel time x launches per scan (working launches only)
@@ -735,16 +788,18 @@ def main():
             # the C ABI directly (what a C++ caller does): per distinct step, the device pointers, counts and
             # initial poses are prepared once; the timed loop is enqueue + wait, records into a fixed array
             nd = len(d_scans)
-            sel = [[(q + 7 * j) % nd for j in range(B)] for q in range(nd)]
-            c_ptrs = [(C.c_void_p * B)(*[d_scans[i].data_ptr() for i in sel[q]]) for q in range(nd)]
-            c_cnts = [(C.c_size_t * B)(*[d_scans[i].shape[0] for i in sel[q]]) for q in range(nd)]
-            c_T = [np.ascontiguousarray(np.stack([inits[i] for i in sel[q]])) for q in range(nd)]
+            # job j's scan: a private device copy of distinct scan j % nd (B separate buffers, as B sensors have;
+            # every job also has its own map copy), optimized from its initial pose each batch
+            sel = [j % nd for j in range(B)]
+            job_scans = [d_scans[i].clone() for i in sel]
+            c_ptrs = (C.c_void_p * B)(*[t.data_ptr() for t in job_scans])
+            c_cnts = (C.c_size_t * B)(*[t.shape[0] for t in job_scans])
+            c_T = np.ascontiguousarray(np.stack([inits[i] for i in sel]))
             recs = (LoBatchRec * B)()
             ms = C.c_double(0.0)
 
             def batch_step(k):
-                q = k % nd
-                rc = L.lo_batch_optimize_async(bo._b, c_ptrs[q], c_cnts[q], fptr(c_T[q]))
+                rc = L.lo_batch_optimize_async(bo._b, c_ptrs, c_cnts, fptr(c_T))
                 rc2 = L.lo_batch_result(bo._b, recs, C.byref(ms))
                 if rc != 0 or rc2 != 0:
                     raise RuntimeError(f"lo_batch rc={rc}/{rc2}: {L.lo_batch_last_error(bo._b).decode()}")
@@ -756,24 +811,27 @@ def main():
             for k in range(K3):
                 dev_ms.append(batch_step(k))
             el3 = time.perf_counter() - t3
-            n_it = sum(iters[(k % nd + 7 * j) % nd] for k in range(K3) for j in range(B))
+            n_it = sum(iters[i] for i in sel) * K3
             ok = sum(r.status == 0 for r in recs)
             batched["runs"].append({"sequences": B, "value": B * K3 / el3, "gn_iters_per_sec": n_it / el3,
                                     "batches": K3, "ms_per_batch": el3 / K3 * 1e3,
                                     "device_ms_per_batch": float(np.mean(dev_ms)), "ok_last_batch": int(ok)})
             # batched correspondence kernel vs the HBM roofline: algorithmic bytes of all B jobs per launch
             cms = C.c_float(0.0)
-            q = (K3 - 1) % nd
-            assert L.lo_batch_optimize_async(bo._b, c_ptrs[q], c_cnts[q], fptr(c_T[q])) == 0
+            assert L.lo_batch_optimize_async(bo._b, c_ptrs, c_cnts, fptr(c_T)) == 0
             assert L.lo_batch_result(bo._b, recs, C.byref(ms)) == 0
             assert L.lo_batch_bench_correspond(bo._b, 50, C.byref(cms)) == 0
-            bbytes = sum(scan_bytes[i] for i in sel[q])
+            bbytes = sum(scan_bytes[i] for i in sel)
+            npts = int(sum(d_scans[i].shape[0] for i in sel))
             ach = bbytes / (cms.value * 1e-3) / 1e9
+            wsb = float(npts * (12 + 4 + 32))
             batched["runs"][-1]["roofline"] = {"kernel": "k_correspond_b", "bound": "hbm", "achieved": ach,
                                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                                                "kernel_us": cms.value * 1e3, "alg_bytes_per_launch": bbytes,
-                                               "points_per_launch": int(sum(d_scans[i].shape[0] for i in sel[q])),
+                                               "points_per_launch": npts, "working_set_bytes": wsb,
+                                               "in_cache": wsb <= MALL_BYTES,
                                                "traffic": read_pmc_traffic(f"{args.config}_batch{B}")}
+            del job_scans
             log(f"[batch] B={B}: {B * K3 / el3:.0f} scans/s, {el3 / K3 * 1e3:.3f} ms/batch "
                 f"(device {np.mean(dev_ms):.3f} ms)")
             bo.close()
@@ -820,8 +878,19 @@ def main():
                            "path": "lo_icp_optimize on host buffers (H2D points, D2H pose+logs, sync per scan)"},
         "roofline": {"kernel": corr_kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes, "points_per_launch": int(n0), "valid_fraction": v},
+                     "traffic": traffic, "traffic_source": "profiles/pmc_traffic.json (separate rocprofv3 --pmc passes)",
+                     "alg_bytes_per_launch": alg_bytes, "points_per_launch": int(n0), "valid_fraction": v,
+                     "timing": "isolated: back-to-back launches of the largest scan (lo_bench_kernel, HIP events)",
+                     "kernel_us": kern_us[stage0],
+                     "in_step": {"kernel_us": in_us.value, "scans": in_cnt.value,
+                                 "achieved": (in_bytes / max(in_cnt.value, 1)) / (in_us.value * 1e-6) / 1e9 if in_us.value else None,
+                                 "frac": (in_bytes / max(in_cnt.value, 1)) / (in_us.value * 1e-6) / 1e9 / HBM_PEAK_GBS
+                                 if in_us.value else None,
+                                 "timing": "each scan's first correspondence launch inside the GN loop (HIP events)"},
+                     "working_set_bytes": ws_bytes, "in_cache": ws_bytes <= MALL_BYTES,
+                     "in_cache_note": "working set (points + slot writes + one 32-B table sector per point) within the "
+                                      "256 MB Infinity Cache: the fraction measures cache, not HBM, bandwidth"},
+        "roofline_dominant": read_pko_latency(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)

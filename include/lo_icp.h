@@ -131,6 +131,11 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * the one-iteration-at-a-time path.  Off by default: at KITTI size a candidate chain's sequential normal equations,
  * solve and correspondence sweeps inside one workgroup outweigh the EM overlap. */
 int lo_set_lookahead(lo_ctx* ctx, int enable);
+/* In-step timing: with enable, each optimize brackets its FIRST correspondence launch (k_correspond, or the KDTree
+ * k_knn + k_knn_brute + k_plane) with HIP events on the context stream (up to 1024 scans; enabling resets them).
+ * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */
+int lo_set_stage_timing(lo_ctx* ctx, int enable);
+int lo_stage_time(lo_ctx* ctx, double* avg_us, int* count);
 /* Enqueue a copy of the current GN state into device memory: 16 floats = pose[12], status, iterations,
  * n_corr, 0.  For the scan-parallel pose gather (RCCL all-gather of these 16 floats per rank). */
 int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);

@@ -116,6 +116,10 @@ struct lo_ctx {
     int32_t* d_tabs_i = nullptr;    // small_off | small_perm | base | ev_off | ev_steps | km_draws
     size_t off_small_off = 0, off_small_perm = 0, off_base = 0, off_ev_off = 0, off_ev_steps = 0, off_km = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // in-step timing of each scan's first correspondence launch (lo_set_stage_timing / lo_stage_time)
+    bool stage_timing = false;
+    std::vector<hipEvent_t> st_ev;  // pairs: [2 i] before, [2 i + 1] after
+    int st_n = 0;
     float T_init[12];
     size_t last_n = 0;
     bool pending = false;
@@ -445,6 +449,7 @@ void lo_destroy(lo_ctx* c) {
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (hipEvent_t e : c->st_ev) (void)hipEventDestroy(e);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -608,6 +613,17 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
     hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
 }
 
+static constexpr int kStageEvents = 1024;          // scans whose first correspondence launch is timed
+
+// A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
+// (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
+static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
+    const bool timed = c->stage_timing && c->st_n < kStageEvents;
+    if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n], c->stream);
+    launch_correspond(c, P0, 1, kd);
+    if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n++ + 1], c->stream);
+}
+
 static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12], const int* n_dev = nullptr) {
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
@@ -635,7 +651,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             const int rc2 = ensure_la(c);
             if (rc2 != LO_OK) return rc2;
             P0.stash = c->d_la_params;                    // k_correspond copies the parameters for k_la
-            launch_correspond(c, P0, 1, false);
+            launch_correspond_first(c, P0, false);
             const int G = pko_grid(g);
             // dynamic LDS: the prefix (nb ints), padded so that one workgroup fills a CU's LDS -- the 201 workgroups
             // then sit on 201 CUs and no two EM chains share a SIMD
@@ -652,11 +668,12 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         }
         for (int it = 0; it < g.max_iterations; ++it) {
             if (!fused) {
-                launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, c->kd);
+                if (it == 0) launch_correspond_first(c, P0, c->kd);
+                else launch_correspond(c, P, 0, c->kd);
                 launch_gn_tail(c, P, it);
                 continue;
             }
-            if (it == 0) launch_correspond(c, P0, 1, c->kd);
+            if (it == 0) launch_correspond_first(c, P0, c->kd);
             launch_pko_spec(c, P, it);
             if (it + 1 < g.max_iterations && !c->kd) {
                 hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
@@ -1059,6 +1076,31 @@ int lo_pko_sample_indices(lo_ctx* c, size_t n, int32_t* out) {
     const int k = static_cast<int>(std::min<size_t>(n, static_cast<size_t>(c->cfg.gmm_sample_size)));
     for (int s = 0; s < k; ++s) out[s] = pko_sample_host(c->tables, static_cast<int>(n), s);
     return k;
+}
+
+int lo_set_stage_timing(lo_ctx* c, int enable) {
+    if (!c) return LO_ERR_ARG;
+    if (enable && c->st_ev.empty()) {
+        c->st_ev.resize(2 * kStageEvents, nullptr);
+        for (hipEvent_t& e : c->st_ev) LO_HIP(c, hipEventCreate(&e));
+    }
+    c->stage_timing = enable != 0;
+    c->st_n = 0;
+    return LO_OK;
+}
+
+int lo_stage_time(lo_ctx* c, double* avg_us, int* count) {
+    if (!c || !avg_us) return LO_ERR_ARG;
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    double tot = 0.0;
+    for (int i = 0; i < c->st_n; ++i) {
+        float ms = 0.0f;
+        LO_HIP(c, hipEventElapsedTime(&ms, c->st_ev[2 * i], c->st_ev[2 * i + 1]));
+        tot += ms;
+    }
+    *avg_us = c->st_n > 0 ? tot * 1e3 / c->st_n : 0.0;
+    if (count) *count = c->st_n;
+    return LO_OK;
 }
 
 int lo_set_lookahead(lo_ctx* c, int enable) {

@@ -117,6 +117,66 @@ class Scene:
         best[best > max_range] = np.inf
         return best
 
+    def raycast_torch(self, origin: np.ndarray, dirs: np.ndarray, max_range: float, device, near: float = 120.0):
+        """raycast() with torch (float64) on `device` -- the same geometry, for generating long sequences quickly
+        (bench maps); results agree with the numpy path to rounding.  Benchmark data only, never the product."""
+        import torch
+        d = torch.as_tensor(dirs, dtype=torch.float64, device=device)
+        o = [float(v) for v in origin]
+        n = d.shape[0]
+        inf = torch.tensor(float("inf"), dtype=torch.float64, device=device)
+        best = torch.full((n,), float("inf"), dtype=torch.float64, device=device)
+        if self.ground:
+            dz = d[:, 2]
+            t = -o[2] / dz
+            t = torch.where((dz >= -1e-9) | (t <= 0), inf, t)
+            best = torch.minimum(best, t)
+        if len(self.boxes):
+            b = self.boxes
+            dist = np.hypot(b[:, 0] - o[0], b[:, 1] - o[1]) - np.hypot(b[:, 3], b[:, 4])
+            b = b[dist < near]
+            for j0 in range(0, len(b), 64):
+                bb = torch.as_tensor(b[j0:j0 + 64], dtype=torch.float64, device=device)
+                c, sn = torch.cos(-bb[:, 6]), torch.sin(-bb[:, 6])
+                ox = o[0] - bb[:, 0]; oy = o[1] - bb[:, 1]; oz = o[2] - bb[:, 2]
+                lox = c * ox - sn * oy; loy = sn * ox + c * oy
+                dx = d[:, 0:1] * c[None] - d[:, 1:2] * sn[None]
+                dy = d[:, 0:1] * sn[None] + d[:, 1:2] * c[None]
+                dzz = d[:, 2:3].expand(n, bb.shape[0])
+                tn = torch.full((n, bb.shape[0]), -float("inf"), dtype=torch.float64, device=device)
+                tf = torch.full((n, bb.shape[0]), float("inf"), dtype=torch.float64, device=device)
+                for lo_, d_, h in ((lox, dx, bb[:, 3]), (loy, dy, bb[:, 4]), (oz, dzz, bb[:, 5])):
+                    t1 = (-h[None] - lo_[None]) / d_
+                    t2 = (h[None] - lo_[None]) / d_
+                    tmin = torch.minimum(t1, t2)
+                    tmax = torch.maximum(t1, t2)
+                    par = d_.abs() < 1e-12
+                    inside = (lo_.abs() <= h)[None].expand(n, -1)
+                    tmin = torch.where(par, torch.where(inside, -inf, inf), tmin)
+                    tmax = torch.where(par, torch.where(inside, inf, -inf), tmax)
+                    tn = torch.maximum(tn, tmin)
+                    tf = torch.minimum(tf, tmax)
+                hit = (tn <= tf) & (tn > 0)
+                best = torch.minimum(best, torch.where(hit, tn, inf).min(dim=1).values)
+        if len(self.cyls):
+            cy = self.cyls
+            dist = np.hypot(cy[:, 0] - o[0], cy[:, 1] - o[1])
+            cy = cy[dist < near]
+            if len(cy):
+                cy = torch.as_tensor(cy, dtype=torch.float64, device=device)
+                ox = o[0] - cy[:, 0]; oy = o[1] - cy[:, 1]
+                a = d[:, 0:1] ** 2 + d[:, 1:2] ** 2
+                bq = 2 * (d[:, 0:1] * ox[None] + d[:, 1:2] * oy[None])
+                cq = (ox ** 2 + oy ** 2 - cy[:, 2] ** 2)[None]
+                disc = bq * bq - 4 * a * cq
+                sq = torch.sqrt(torch.clamp(disc, min=0))
+                t1 = (-bq - sq) / (2 * a)
+                z = o[2] + t1 * d[:, 2:3]
+                ok = (disc > 0) & (t1 > 0) & (z >= cy[:, 3][None]) & (z <= cy[:, 4][None])
+                best = torch.minimum(best, torch.where(ok, t1, inf).min(dim=1).values)
+        best = torch.where(best > max_range, inf, best)
+        return best.cpu().numpy()
+
 
 # ----------------------------------------------------------------------------------------------------
 # KITTI-07-like sequence
@@ -205,11 +265,15 @@ class KittiLikeSequence:
         E, A = np.meshgrid(elev, az, indexing="ij")
         self.dirs = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
 
-    def scan(self, i: int) -> np.ndarray:
+    def scan(self, i: int, device=None) -> np.ndarray:
+        """Raw HDL-64-like scan of frame i (local frame).  device: raycast with torch there (raycast_torch)."""
         T = self.poses[i]
         rng = np.random.default_rng(1007 + i)
         dw = self.dirs @ T[:3, :3].T
-        r = self.scene.raycast(T[:3, 3], dw, max_range=100.0)
+        if device is None:
+            r = self.scene.raycast(T[:3, 3], dw, max_range=100.0)
+        else:
+            r = self.scene.raycast_torch(T[:3, 3], dw, max_range=100.0, device=device)
         ok = np.isfinite(r)
         r = r[ok] + rng.normal(0.0, 0.02, ok.sum())
         pts = self.dirs[ok] * r[:, None]
