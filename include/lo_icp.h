@@ -101,6 +101,13 @@ int         lo_get_config(const lo_ctx* ctx, lo_config* out);   /* the configura
  * keys_xyz: int32 L1 voxel keys (VoxelKey, VoxelMap.h:152-164), |key| < 2^20 per axis.
  * Full upload; call again after every VoxelMap::UpdateVoxelMap (Estimator.cpp:457). */
 int lo_map_set_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids, size_t m);
+/* Incremental form: the L1 voxels an UpdateVoxelMap changed, patched into the device table in place
+ * -- present[i] = 1: voxel i has a surfel (inserted, or its normal / centroid refitted), 0: it lost it or was erased
+ * (VoxelMap.cpp:187-261).  Asynchronous on the context stream, no full-table rebuild or host sync.  Returns
+ * LO_ERR_CAPACITY (nothing changed) when the table's load, tombstones included, would pass 1/2: upload the whole
+ * map with lo_map_set_surfels instead. */
+int lo_map_patch_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids,
+                         const uint8_t* present, size_t m);
 size_t lo_map_surfel_count(const lo_ctx* ctx);
 
 /* KDTree variant (use_surfel_correspondence = 0): the map point cloud the reference's kd-tree indexes,

@@ -38,6 +38,11 @@ size_t       lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys_xyz, fl
 size_t       lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap);
 /* Upload the map's surfels to an ICP context (lo_map_set_surfels). */
 int          lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m);
+/* Bring the context's device surfel table up to date with the map after UpdateVoxelMap (Estimator.cpp:457): when the
+ * table was last synced from this map, only the L1 voxels changed since then are patched in place
+ * (lo_map_patch_surfels); otherwise (first sync, another map, KDTree mode, table full) the whole map is uploaded.
+ * patched (nullable): the number of patched voxels, or -1 after a full upload. */
+int          lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched);
 
 /* FastVoxelFilter::filter(input, output, stride): returns the number of output points (<= n). */
 size_t       lo_voxel_filter(const float* in_xyz, size_t n, float voxel_size, int stride, float* out_xyz);

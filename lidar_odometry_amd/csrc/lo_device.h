@@ -23,6 +23,7 @@ constexpr int kBlock = 256;          // threads per block for the per-point kern
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr uint64_t kEmptyKey = ~0ull;
+constexpr uint64_t kTombKey = ~0ull - 1;   // erased slot (lo_map_patch_surfels): never a packed key, never empty
 constexpr int kNE = 28;              // 21 lower-triangular H + 6 g + cost
 constexpr int kPkoBlock = 256;       // PKO workgroup: one GMM sample per thread (S <= 256)
 constexpr int kPkoMaxWGs = 128;      // PKO workgroups per launch (each evaluates a slice of the alpha grid)

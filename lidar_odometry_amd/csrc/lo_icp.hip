@@ -12,8 +12,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
+#include "lo_ctx_internal.h"
 #include "lo_device.h"
 #include "lo_kdorder.h"
 #include "lo_math.h"
@@ -44,6 +46,8 @@ __global__ void k_accumulate_b1(const KParams* PB, int it);
 __global__ void k_solve_b(const KParams* PB, int it);
 __global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
 __global__ void k_la(const KParams* Pp, LaParams L, int k, int G);
+struct MapPatchRec;
+__global__ void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n);
 __global__ void k_la_finish(const KParams* Pp, LaParams L, int k_next);
 }  // namespace lo
 
@@ -96,6 +100,15 @@ struct lo_ctx {
     size_t tab_cap = 0;             // allocated slots
     uint32_t log2cap = 1;
     size_t n_surfels = 0;
+    // in-place table patches (lo_map_patch_surfels): the keys resident on the device, tombstones left by erases,
+    // a pinned staging buffer + device copy of the patch records, and the synced host map (lo_map_sync_voxelmap)
+    std::unordered_set<uint64_t> resident;
+    size_t n_tomb = 0;
+    void* h_patch = nullptr;
+    void* d_patch = nullptr;
+    size_t patch_cap = 0;
+    hipEvent_t ev_patch = nullptr;
+    uint64_t map_src = 0, map_epoch = 0, map_pos = 0;
     // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
     bool kd = false;
     PointGrid grid;                 // the map's L0 centroids (lo_map_set_points)
@@ -450,6 +463,9 @@ void lo_destroy(lo_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->st_ev) (void)hipEventDestroy(e);
+    if (c->ev_patch) (void)hipEventDestroy(c->ev_patch);
+    if (c->h_patch) (void)hipHostFree(c->h_patch);
+    if (c->d_patch) (void)hipFree(c->d_patch);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -467,16 +483,19 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
     if (m > 0 && (!keys || !normals || !centroids)) { c->err = "null surfel arrays"; return LO_ERR_ARG; }
     size_t cap = 2;
     uint32_t l2 = 1;
-    while (cap < 2 * m) { cap <<= 1; ++l2; }            // load factor <= 0.5
+    while (cap < 4 * m) { cap <<= 1; ++l2; }            // load <= 1/4: room for in-place patches up to 1/2
     std::vector<Slot> h(cap);
     for (auto& s : h) { s.key = kEmptyKey; s.n[0] = s.n[1] = s.n[2] = 0.0f; s.c[0] = s.c[1] = s.c[2] = 0.0f; }
     const uint64_t mask = cap - 1;
+    std::unordered_set<uint64_t> resident;
+    resident.reserve(2 * m);
     for (size_t i = 0; i < m; ++i) {
         for (int a = 0; a < 3; ++a) {
             const int32_t v = keys[3 * i + a];
             if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
         }
         const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        resident.insert(key);
         uint64_t b = (key * 0x9E3779B97F4A7C15ull) >> (64 - l2);
         while (h[b].key != kEmptyKey && h[b].key != key) b = (b + 1) & mask;
         h[b].key = key;                                    // duplicate keys: last one wins (map semantics)
@@ -492,7 +511,90 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
     }
     LO_HIP(c, hipMemcpy(c->d_tab, h.data(), cap * sizeof(Slot), hipMemcpyHostToDevice));
     c->log2cap = l2;
-    c->n_surfels = m;
+    c->n_surfels = resident.size();
+    c->resident.swap(resident);
+    c->n_tomb = 0;
+    c->map_src = 0;                                      // no longer mirrors a synced host map
+    return LO_OK;
+}
+
+}  // extern "C"
+
+namespace lo {
+struct MapPatchRec {                  // one L1 voxel's change: upsert (op 1: key + payload) or erase (op 0)
+    uint64_t key;
+    float n[3];
+    float c[3];
+    uint32_t op;
+    uint32_t pad;
+};
+void ctx_map_source(const lo_ctx* c, uint64_t* src, uint64_t* epoch, uint64_t* pos) {
+    *src = c->map_src; *epoch = c->map_epoch; *pos = c->map_pos;
+}
+void ctx_set_map_source(lo_ctx* c, uint64_t src, uint64_t epoch, uint64_t pos) {
+    c->map_src = src; c->map_epoch = epoch; c->map_pos = pos;
+}
+}  // namespace lo
+
+extern "C" {
+
+// In-place patch of the device table (the §8b lo_map_patch_surfels): upserts claim the first empty slot of their
+// probe sequence (atomic CAS) or overwrite their key's payload, erases leave a tombstone that lookups probe past.
+// Asynchronous on the context stream (pinned staging, no host sync).  LO_ERR_CAPACITY when live keys + tombstones
+// would exceed half the table: the caller uploads the whole map instead (lo_map_set_surfels).
+int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, const float* centroids,
+                         const uint8_t* present, size_t m) {
+    if (!c) return LO_ERR_ARG;
+    if (m == 0) return LO_OK;
+    if (!keys || !normals || !centroids || !present) { c->err = "null patch arrays"; return LO_ERR_ARG; }
+    if (!c->d_tab) { c->err = "no surfel table to patch"; return LO_ERR_STATE; }
+    size_t ins = 0, ers = 0;
+    for (size_t i = 0; i < m; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            const int32_t v = keys[3 * i + a];
+            if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
+        }
+        const bool res = c->resident.count(pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2])) != 0;
+        ins += (present[i] && !res) ? 1 : 0;
+        ers += (!present[i] && res) ? 1 : 0;
+    }
+    const size_t cap = size_t(1) << c->log2cap;
+    if ((c->resident.size() + ins - ers) + (c->n_tomb + ers) > cap / 2) { c->err = "table full"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    const size_t bytes = m * sizeof(MapPatchRec);
+    if (bytes > c->patch_cap) {
+        if (c->ev_patch) LO_HIP(c, hipEventSynchronize(c->ev_patch));
+        if (c->h_patch) LO_HIP(c, hipHostFree(c->h_patch));
+        if (c->d_patch) LO_HIP(c, hipFree(c->d_patch));
+        c->h_patch = c->d_patch = nullptr;
+        const size_t cap_b = std::max<size_t>(bytes * 2, 64 * 1024);
+        LO_HIP(c, hipHostMalloc(&c->h_patch, cap_b, hipHostMallocDefault));
+        LO_HIP(c, hipMalloc(&c->d_patch, cap_b));
+        c->patch_cap = cap_b;
+    }
+    if (!c->ev_patch) LO_HIP(c, hipEventCreateWithFlags(&c->ev_patch, hipEventDisableTiming));
+    else LO_HIP(c, hipEventSynchronize(c->ev_patch));   // the previous patch's copy has left the staging buffer
+    MapPatchRec* r = static_cast<MapPatchRec*>(c->h_patch);
+    int n_rec = 0;
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        const bool res = c->resident.count(key) != 0;
+        if (!present[i] && !res) continue;                 // nothing on the device to remove
+        MapPatchRec& q = r[n_rec++];
+        q.key = key;
+        q.op = present[i] ? 1u : 0u;
+        q.pad = 0;
+        for (int a = 0; a < 3; ++a) { q.n[a] = normals[3 * i + a]; q.c[a] = centroids[3 * i + a]; }
+        if (present[i]) c->resident.insert(key); else c->resident.erase(key);
+    }
+    c->n_tomb += ers;
+    c->n_surfels = c->resident.size();
+    if (n_rec == 0) return LO_OK;
+    LO_HIP(c, hipMemcpyAsync(c->d_patch, c->h_patch, n_rec * sizeof(MapPatchRec), hipMemcpyHostToDevice, c->stream));
+    LO_HIP(c, hipEventRecord(c->ev_patch, c->stream));
+    hipLaunchKernelGGL(k_map_patch, dim3((n_rec + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_tab,
+                       c->log2cap, static_cast<const MapPatchRec*>(c->d_patch), n_rec);
+    LO_HIP(c, hipGetLastError());
     return LO_OK;
 }
 

@@ -307,6 +307,52 @@ __global__ __launch_bounds__(kAcc1Threads) void k_accumulate_b1(const KParams* _
 }
 
 // ====================================================================================================
+// k_map_patch: in-place surfel table patch (lo_map_patch_surfels).  One thread per changed L1 voxel (keys unique
+// within a patch): an upsert finds its key and overwrites the payload, or claims the first EMPTY slot of its probe
+// sequence with a CAS on the key (tombstones are never reused, so the key cannot sit past an empty slot); an erase
+// turns its slot into a tombstone, which lookup_surfel probes past (never equal to a packed key, never empty).
+// The ICP kernels read the table only after this launch (stream order), so payload stores need no ordering.
+// ====================================================================================================
+struct MapPatchRec {
+    uint64_t key;
+    float n[3];
+    float c[3];
+    uint32_t op;
+    uint32_t pad;
+};
+
+__global__ __launch_bounds__(kBlock) void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const MapPatchRec r = rec[i];
+    const uint32_t mask = (1u << log2cap) - 1u;
+    uint32_t h = hash_slot(r.key, log2cap);
+    for (uint32_t p = 0; p <= mask; ++p) {
+        unsigned long long* kp = reinterpret_cast<unsigned long long*>(&tab[h].key);
+        unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == r.key) {
+            if (r.op == 0) {
+                __hip_atomic_store(kp, static_cast<unsigned long long>(kTombKey), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                for (int a = 0; a < 3; ++a) { tab[h].n[a] = r.n[a]; tab[h].c[a] = r.c[a]; }
+            }
+            return;
+        }
+        if (k == kEmptyKey) {
+            if (r.op == 0) return;                           // not present (the host mirror said it was)
+            const unsigned long long prev = atomicCAS(kp, static_cast<unsigned long long>(kEmptyKey),
+                                                      static_cast<unsigned long long>(r.key));
+            if (prev == kEmptyKey) {
+                for (int a = 0; a < 3; ++a) { tab[h].n[a] = r.n[a]; tab[h].c[a] = r.c[a]; }
+                return;
+            }
+            continue;                                        // another insert took the slot: look at it again
+        }
+        h = (h + 1u) & mask;
+    }
+}
+
+// ====================================================================================================
 // k_init: reset the GN state for a new scan.  The initial pose travels as a kernel argument, so any
 // number of scans can be enqueued back to back without a host staging buffer.
 // ====================================================================================================

@@ -37,7 +37,7 @@ static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info
     lo::transform_points(pose, o->feat.data(), static_cast<size_t>(n), o->world.data());   // feature_cloud_global
     const double sensor[3] = {pose.t[0], pose.t[1], pose.t[2]};                          // Vector3f -> Vector3d
     int rc = lo_voxelmap_update(o->map, o->world.data(), static_cast<size_t>(n), sensor, o->cfg.max_range * 1.2, 1);
-    if (rc == LO_OK) rc = lo_map_set_from_voxelmap(o->icp, o->map);                     // (+ RebuildKdTree)
+    if (rc == LO_OK) rc = lo_map_sync_voxelmap(o->icp, o->map, nullptr);                 // patch (+ RebuildKdTree)
     if (rc != LO_OK) { o->err = "keyframe map update failed"; return rc; }
     o->last_kf = pose;
     ++o->keyframes;

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/lo_map.h"
+#include "lo_ctx_internal.h"
 #include "lo_math.h"
 
 namespace lo {
@@ -202,6 +203,12 @@ struct HostVoxelMap {
 
     OrderedMap<Key3, NoValue, HashKey3> touched;   // scratch, kept across updates
     std::vector<int32_t> k0, k1;
+    // L1 keys whose surfel may have changed (created, refitted, lost, erased), in update order: a device table
+    // synced at journal position p catches up by patching the keys of journal[p:] (lo_map_sync_voxelmap).  epoch
+    // changes when the journal restarts, which forces a full upload.
+    std::vector<Key3> journal;
+    uint64_t epoch = 1;
+    void note(const Key3& k) { journal.push_back(k); }
 
     // PointToVoxelKey for a whole cloud: floor(p / scale) per coordinate, one flat loop over the 3n floats
     // (vectorised: divps + roundps; the same IEEE division and floor as the per-point form)
@@ -219,6 +226,7 @@ struct HostVoxelMap {
         const Key3 p = parent(k);
         const int64_t i = l1.find(p);
         if (i < 0) return;
+        note(p);
         L1& n = l1.val_at(i);
         n.children.erase(k);
         if (n.children.size() < 5) n.has_surfel = false;
@@ -258,7 +266,8 @@ struct HostVoxelMap {
         for (const Key3& k : doomed) { unregister(k); l0.erase(k); }
         std::vector<Key3> empty1;
         for (size_t i = 0; i < l1.size(); ++i) if (l1.val_at(i).children.empty()) empty1.push_back(l1.key_at(i));
-        for (const Key3& k : empty1) l1.erase(k);
+        for (const Key3& k : empty1) { note(k); l1.erase(k); }
+        if (journal.size() > (size_t(1) << 22)) { journal.clear(); ++epoch; }
 
         keys_of(xyz, n, voxel, k0);
         keys_of(xyz, n, voxel * static_cast<float>(factor), k1);
@@ -275,8 +284,13 @@ struct HostVoxelMap {
             if (li < 0) continue;
             L1& node = l1.val_at(li);
             const int cnt = static_cast<int>(node.children.size());
-            if (cnt < 5) { node.has_surfel = false; continue; }
+            if (cnt < 5) {
+                if (node.has_surfel) note(k1);                 // loses its surfel
+                node.has_surfel = false;
+                continue;
+            }
             if (node.has_surfel && node.last_child_count == cnt) continue;
+            note(k1);                                          // refitted, erased or losing its surfel below
             cs.clear();
             for (size_t q = 0; q < node.children.size(); ++q) {
                 const int64_t c0 = l0.find(node.children.key_at(q));
@@ -373,6 +387,48 @@ size_t lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap) {
     size_t c = 0;
     for (; c < m->m.l0.size() && c < cap; ++c) std::memcpy(xyz + 3 * c, m->m.l0.val_at(c).c, sizeof(float) * 3);
     return c;
+}
+
+int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
+    if (!ctx || !m) return LO_ERR_ARG;
+    if (patched) *patched = -1;
+    lo_config cfg;
+    if (lo_get_config(ctx, &cfg) != LO_OK) return LO_ERR_ARG;
+    const HostVoxelMap& H = m->m;
+    if (cfg.use_surfel_correspondence) {
+        uint64_t src = 0, epoch = 0, pos = 0;
+        lo::ctx_map_source(ctx, &src, &epoch, &pos);
+        if (src == reinterpret_cast<uint64_t>(m) && epoch == H.epoch && pos <= H.journal.size()) {
+            lo::OrderedMap<lo::Key3, lo::NoValue, lo::HashKey3> keys;      // the changed L1 keys, once each
+            for (size_t i = pos; i < H.journal.size(); ++i) keys.upsert(H.journal[i], nullptr);
+            const size_t cnt = keys.size();
+            std::vector<int32_t> k(3 * std::max<size_t>(cnt, 1));
+            std::vector<float> nn(3 * std::max<size_t>(cnt, 1)), cc(3 * std::max<size_t>(cnt, 1));
+            std::vector<uint8_t> present(std::max<size_t>(cnt, 1));
+            for (size_t i = 0; i < cnt; ++i) {
+                const lo::Key3& kk = keys.key_at(i);
+                k[3 * i] = kk.x; k[3 * i + 1] = kk.y; k[3 * i + 2] = kk.z;
+                const int64_t li = H.l1.find(kk);
+                const bool has = li >= 0 && H.l1.val_at(li).has_surfel;
+                present[i] = has ? 1 : 0;
+                for (int a = 0; a < 3; ++a) {
+                    nn[3 * i + a] = has ? H.l1.val_at(li).normal[a] : 0.0f;
+                    cc[3 * i + a] = has ? H.l1.val_at(li).centroid[a] : 0.0f;
+                }
+            }
+            const int rc = lo_map_patch_surfels(ctx, k.data(), nn.data(), cc.data(), present.data(), cnt);
+            if (rc == LO_OK) {
+                lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());
+                if (patched) *patched = static_cast<int>(cnt);
+                return LO_OK;
+            }
+            if (rc != LO_ERR_CAPACITY) return rc;           // capacity: the table is rebuilt below
+        }
+    }
+    const int rc = lo_map_set_from_voxelmap(ctx, m);
+    if (rc == LO_OK && cfg.use_surfel_correspondence)
+        lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());
+    return rc;
 }
 
 int lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m) {

@@ -133,6 +133,10 @@ class IterativeClosestPointOptimizer:
         self._last = OptimizationStats()
 
     # ------------------------------------------------------------------ lifetime
+    def surfel_count(self) -> int:
+        """Surfels in the device table (lo_map_surfel_count)."""
+        return int(self._L.lo_map_surfel_count(self.ctx))
+
     def set_lookahead(self, enable: bool = True):
         """Two GN iterations per launch for small PKO scans (default off; bit-identical either way)."""
         rc = self._L.lo_set_lookahead(self.ctx, int(bool(enable)))

@@ -1,0 +1,97 @@
+"""Incremental device map (SURVEY.md §8f-1, §8b lo_map_patch_surfels): a context kept in sync with a growing,
+pruned voxel map by in-place table patches (lo_map_sync_voxelmap) answers every surfel lookup exactly as a
+context that re-uploads the whole map after each update (lo_map_set_from_voxelmap): identical correspondence sets
+and bit-identical fp64 residuals, across keyframes that insert, refit, lose and prune surfels.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from lidar_odometry_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx():
+    from lidar_odometry_amd import IterativeClosestPointOptimizer
+    return IterativeClosestPointOptimizer(max_points=1 << 16)
+
+
+def _sync(icp, vm):
+    from lidar_odometry_amd import lib
+    patched = C.c_int(0)
+    rc = lib().lo_map_sync_voxelmap(icp.ctx, vm.handle, C.byref(patched))
+    assert rc == 0, rc
+    return patched.value
+
+
+def _full(icp, vm):
+    from lidar_odometry_amd import lib
+    assert lib().lo_map_set_from_voxelmap(icp.ctx, vm.handle) == 0
+
+
+def _same_lookups(a, b, pts, poses):
+    for T in poses:
+        na, va, ra = a.find_correspondences(pts, T)
+        nb, vb, rb = b.find_correspondences(pts, T)
+        assert na == nb
+        np.testing.assert_array_equal(va, vb)
+        np.testing.assert_array_equal(ra, rb)
+
+
+def test_patched_table_matches_full_upload():
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=62)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A, B = _ctx(), _ctx()
+    try:
+        kinds = []
+        for k in range(0, 61, 2):
+            T = seq.poses[k]
+            pts = voxel_filter(seq.scan(k), 0.5, 8)
+            # 60 m pruning radius: surfels leave the map as the sensor moves on (erase -> tombstones)
+            vm.update(synth.transform(T, pts), T[:3, 3], 60.0, True)
+            p = _sync(A, vm)
+            _full(B, vm)
+            kinds.append(p)
+            assert A.surfel_count() == B.surfel_count() == vm.surfel_count()
+            if k % 10 == 0:
+                f = k + 1
+                scan = voxel_filter(seq.scan(f), 0.5, 8)
+                rng = np.random.default_rng(k)
+                poses = [seq.poses[f][:3].astype(np.float32).reshape(12)] + \
+                        [synth.perturb(seq.poses[f], rng, 0.3, 0.03)[:3].astype(np.float32).reshape(12) for _ in range(2)]
+                _same_lookups(A, B, scan, poses)
+        # the first sync uploads everything; while the map grows fast the table outgrows its headroom a few times,
+        # after that keyframes are patched in place
+        assert kinds[0] == -1
+        assert sum(p >= 0 for p in kinds[len(kinds) // 2:]) >= len(kinds) // 4, kinds
+    finally:
+        A.close()
+        B.close()
+
+
+def test_patch_capacity_falls_back_to_full_upload():
+    """Churn (a sensor jumping between two far places with a small radius) fills the table with tombstones: the
+    sync then re-uploads the whole map (-1) and lookups still agree."""
+    from lidar_odometry_amd.voxelmap import VoxelMap
+    sc = synth.patch_scene(n_patches=80, seed=11, extent=30.0)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A, B = _ctx(), _ctx()
+    try:
+        results = []
+        for k in range(12):
+            off = np.array([0.0 if k % 2 == 0 else 500.0, 0.0, 0.0], np.float32)
+            w = synth.sample_patches(sc, 40000, 100 + k, outlier_frac=0.0) + off
+            vm.update(w, off.astype(np.float64), 45.0, True)
+            results.append(_sync(A, vm))
+            _full(B, vm)
+            assert A.surfel_count() == B.surfel_count()
+        assert -1 in results[1:], results
+        q = synth.sample_patches(sc, 5000, 999, outlier_frac=0.0) + np.array([500.0, 0.0, 0.0], np.float32)
+        I = np.eye(3, 4, dtype=np.float32).reshape(12)
+        _same_lookups(A, B, q, [I])
+    finally:
+        A.close()
+        B.close()
