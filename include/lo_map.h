@@ -28,6 +28,10 @@ void         lo_voxelmap_destroy(lo_voxelmap* m);
 /* UpdateVoxelMap(new_cloud (world frame), sensor_position, max_distance, is_keyframe) */
 int          lo_voxelmap_update(lo_voxelmap* m, const float* world_xyz, size_t n, const double sensor[3],
                                 double max_distance, int is_keyframe);
+/* ApplyTransformAndRehash(T_correction) (VoxelMap.cpp:264-302; called after pose-graph optimisation, Estimator.cpp:877,
+ * :1181): every L0 centroid moved by T (row-major 3x4) and re-keyed, collisions merged, surfels recomputed.
+ * The next lo_map_sync_voxelmap uploads the whole map. */
+int          lo_voxelmap_apply_transform(lo_voxelmap* m, const float T[12]);
 size_t       lo_voxelmap_l0_count(const lo_voxelmap* m);
 size_t       lo_voxelmap_l1_count(const lo_voxelmap* m);
 size_t       lo_voxelmap_surfel_count(const lo_voxelmap* m);

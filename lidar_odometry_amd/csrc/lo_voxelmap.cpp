@@ -252,6 +252,86 @@ struct HostVoxelMap {
         }
     }
 
+    // The L1 voxel's children's L0 centroids in child order
+    void child_centroids(const L1& node, std::vector<float>& cs) const {
+        cs.clear();
+        for (size_t q = 0; q < node.children.size(); ++q) {
+            const int64_t c0 = l0.find(node.children.key_at(q));
+            if (c0 >= 0) cs.insert(cs.end(), l0.val_at(c0).c, l0.val_at(c0).c + 3);
+        }
+    }
+    // Surfel fit (VoxelMap.cpp:211-243): fp32 mean and covariance in child order, JacobiSVD<Matrix3f> (restated),
+    // normal = U.col(2); returns planarity = s2 / (s0 + 1e-6)
+    static float fit(const std::vector<float>& cs, float cen[3], float U[3][3]) {
+        const size_t m = cs.size() / 3;
+        cen[0] = cen[1] = cen[2] = 0.0f;
+        for (size_t q = 0; q < m; ++q) for (int a = 0; a < 3; ++a) cen[a] += cs[3 * q + a];
+        const float mf = static_cast<float>(m);
+        for (int a = 0; a < 3; ++a) cen[a] /= mf;
+        float cov[3][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+        for (size_t q = 0; q < m; ++q) {
+            const float d[3] = {cs[3 * q] - cen[0], cs[3 * q + 1] - cen[1], cs[3 * q + 2] - cen[2]};
+            for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) cov[r][c] += d[c] * d[r];
+        }
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) cov[r][c] /= mf;
+        float S[3];
+        jacobi_svd3(cov, U, S);
+        return S[2] / (S[0] + 1e-6f);
+    }
+
+    // VoxelMap::ApplyTransformAndRehash (VoxelMap.cpp:264-302), after a pose-graph correction: every L0 centroid
+    // moved by T (R c + t, Matrix3f * Vector3f order) and re-keyed in L0 order, colliding voxels merged by point
+    // count, the L1 level rebuilt from the new keys (RegisterToParent), then RecomputeAllSurfels (:304-366: at least
+    // 5 children, planarity failures lose the surfel without being erased).  The device tables need a full upload
+    // afterwards (the journal restarts).
+    void apply_transform(const float T[12]) {
+        const SE3f s = se3_from12(T);
+        std::vector<std::pair<Key3, L0>> tr;
+        tr.reserve(l0.size());
+        for (size_t i = 0; i < l0.size(); ++i) {
+            L0 nn = l0.val_at(i);
+            const float* c = l0.val_at(i).c;
+            for (int r = 0; r < 3; ++r) nn.c[r] = dot3e(s.R[r][0], s.R[r][1], s.R[r][2], c[0], c[1], c[2]) + s.t[r];
+            const Key3 k{static_cast<int32_t>(std::floor(nn.c[0] / voxel)), static_cast<int32_t>(std::floor(nn.c[1] / voxel)),
+                         static_cast<int32_t>(std::floor(nn.c[2] / voxel))};
+            tr.emplace_back(k, nn);
+        }
+        l0.clear();
+        l1.clear();
+        for (const auto& kn : tr) {
+            bool fresh = false;
+            const size_t i = l0.upsert(kn.first, &fresh);
+            L0& ex = l0.val_at(i);
+            if (ex.point_count == 0) {
+                ex = kn.second;
+            } else {
+                const float n1 = static_cast<float>(ex.point_count), n2 = static_cast<float>(kn.second.point_count);
+                for (int a = 0; a < 3; ++a) ex.c[a] = (ex.c[a] * n1 + kn.second.c[a] * n2) / (n1 + n2);
+                ex.point_count += kn.second.point_count;
+            }
+            const size_t j = l1.upsert(parent(kn.first), nullptr);
+            l1.val_at(j).children.upsert(kn.first, nullptr);
+        }
+        journal.clear();
+        ++epoch;
+        if (!compute_surfels) return;
+        std::vector<float> cs;
+        for (size_t t = 0; t < l1.size(); ++t) {
+            L1& node = l1.val_at(t);
+            const int cnt = static_cast<int>(node.children.size());
+            if (cnt < 5) { node.has_surfel = false; continue; }
+            child_centroids(node, cs);
+            if (cs.size() / 3 < 5) { node.has_surfel = false; continue; }
+            float U[3][3], cen[3];
+            const float planarity = fit(cs, cen, U);
+            if (planarity > planarity_thr) { node.has_surfel = false; continue; }
+            node.has_surfel = true;
+            for (int a = 0; a < 3; ++a) { node.normal[a] = U[a][2]; node.centroid[a] = cen[a]; }
+            node.planarity = planarity;
+            node.last_child_count = cnt;
+        }
+    }
+
     void update(const float* xyz, size_t n, const double sensor[3], double max_distance, bool keyframe) {
         if (!xyz || n == 0 || !keyframe) return;
         const float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
@@ -291,26 +371,10 @@ struct HostVoxelMap {
             }
             if (node.has_surfel && node.last_child_count == cnt) continue;
             note(k1);                                          // refitted, erased or losing its surfel below
-            cs.clear();
-            for (size_t q = 0; q < node.children.size(); ++q) {
-                const int64_t c0 = l0.find(node.children.key_at(q));
-                if (c0 >= 0) cs.insert(cs.end(), l0.val_at(c0).c, l0.val_at(c0).c + 3);
-            }
-            const size_t m = cs.size() / 3;
-            if (m < 3) { node.has_surfel = false; continue; }
-            float cen[3] = {0.0f, 0.0f, 0.0f};
-            for (size_t q = 0; q < m; ++q) for (int a = 0; a < 3; ++a) cen[a] += cs[3 * q + a];
-            const float mf = static_cast<float>(m);
-            for (int a = 0; a < 3; ++a) cen[a] /= mf;
-            float cov[3][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
-            for (size_t q = 0; q < m; ++q) {
-                const float d[3] = {cs[3 * q] - cen[0], cs[3 * q + 1] - cen[1], cs[3 * q + 2] - cen[2]};
-                for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) cov[r][c] += d[c] * d[r];
-            }
-            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) cov[r][c] /= mf;
-            float U[3][3], S[3];
-            jacobi_svd3(cov, U, S);
-            const float planarity = S[2] / (S[0] + 1e-6f);
+            child_centroids(node, cs);
+            if (cs.size() / 3 < 3) { node.has_surfel = false; continue; }
+            float U[3][3], cen[3];
+            const float planarity = fit(cs, cen, U);
             if (planarity > planarity_thr) {
                 node.has_surfel = false;
                 std::vector<Key3> kids;
@@ -348,6 +412,12 @@ lo_voxelmap* lo_voxelmap_create(float voxel_size, int hierarchy_factor, float pl
 }
 
 void lo_voxelmap_destroy(lo_voxelmap* m) { delete m; }
+
+int lo_voxelmap_apply_transform(lo_voxelmap* m, const float T[12]) {
+    if (!m || !T) return LO_ERR_ARG;
+    m->m.apply_transform(T);
+    return LO_OK;
+}
 
 int lo_voxelmap_update(lo_voxelmap* m, const float* xyz, size_t n, const double sensor[3], double max_distance, int is_keyframe) {
     if (!m || !sensor || (n > 0 && !xyz)) return LO_ERR_ARG;

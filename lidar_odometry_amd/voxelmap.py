@@ -56,6 +56,15 @@ class VoxelMap:
             raise RuntimeError(f"lo_voxelmap_update failed ({rc})")
         self.revision += 1
 
+    def apply_transform(self, T):
+        """VoxelMap::ApplyTransformAndRehash (VoxelMap.cpp:264-302): T = row-major 3x4 (or 4x4) correction."""
+        t = np.ascontiguousarray(np.asarray(T, np.float32)[:3, :] if np.asarray(T).ndim == 2 else
+                                 np.asarray(T, np.float32).reshape(12)).reshape(12)
+        rc = lib().lo_voxelmap_apply_transform(self._h, _f(t))
+        if rc < 0:
+            raise RuntimeError(f"lo_voxelmap_apply_transform failed ({rc})")
+        self.revision += 1
+
     def l0_count(self) -> int:
         return int(lib().lo_voxelmap_l0_count(self._h))
 

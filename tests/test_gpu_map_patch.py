@@ -95,3 +95,31 @@ def test_patch_capacity_falls_back_to_full_upload():
     finally:
         A.close()
         B.close()
+
+
+def test_sync_after_apply_transform_uploads_the_rehashed_map():
+    """ApplyTransformAndRehash restarts the map's journal: the next sync is a full upload, then patching resumes."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=30)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A, B = _ctx(), _ctx()
+    try:
+        for k in range(0, 21, 2):
+            vm.update(synth.transform(seq.poses[k], voxel_filter(seq.scan(k), 0.5, 8)), seq.poses[k][:3, 3], 120.0, True)
+            _sync(A, vm)
+        T = synth.se3(synth.rot_z(0.05), [0.4, -0.3, 0.02])
+        vm.apply_transform(T[:3].astype(np.float32))
+        assert _sync(A, vm) == -1
+        _full(B, vm)
+        f = 21
+        scan = voxel_filter(seq.scan(f), 0.5, 8)
+        Tf = (T @ seq.poses[f])[:3].astype(np.float32).reshape(12)
+        _same_lookups(A, B, scan, [Tf])
+        vm.update(synth.transform(T @ seq.poses[22], voxel_filter(seq.scan(22), 0.5, 8)), (T @ seq.poses[22])[:3, 3],
+                  120.0, True)
+        assert _sync(A, vm) >= 0
+        _full(B, vm)
+        _same_lookups(A, B, scan, [Tf])
+    finally:
+        A.close()
+        B.close()

@@ -116,3 +116,25 @@ def test_container_orders_match_unordered_dense_golden():
         np.testing.assert_array_equal(l1, g[f"cp{i}_l1"], err_msg=f"L1 order, checkpoint {i}")
         np.testing.assert_array_equal(cnt, g[f"cp{i}_cnt"], err_msg=f"children counts, checkpoint {i}")
         np.testing.assert_array_equal(ch, g[f"cp{i}_ch"], err_msg=f"children order, checkpoint {i}")
+
+
+@pytest.mark.parametrize("angle,shift", [(0.0, (0.0, 0.0, 0.0)), (0.02, (0.3, -0.2, 0.05)), (0.3, (5.0, 1.0, -0.4))])
+def test_apply_transform_and_rehash_bitwise(angle, shift):
+    """ApplyTransformAndRehash (VoxelMap.cpp:264-302) after a keyframe sequence, then further keyframes on the
+    corrected map: bit-identical to the oracle (re-keyed L0 order, merges, rebuilt L1, recomputed surfels)."""
+    seq = _data.kitti_seq()
+    a = VoxelMap(0.5, 3, 0.1, True)
+    b = oracle.VoxelMap(0.5, 3, 0.1, True)
+    for k in range(0, 13, 2):
+        w = synth.transform(seq.poses[k], voxel_filter(_data.kitti_scan(k), 0.5, 8))
+        a.update(w, seq.poses[k][:3, 3], 120.0, True)
+        b.update(w, seq.poses[k][:3, 3], 120.0, True)
+    T = synth.se3(synth.rot_z(angle), shift)[:3].astype(np.float32)
+    a.apply_transform(T)
+    b.apply_transform(T)
+    _compare_maps(a, b)
+    for k in range(14, 21, 2):
+        w = synth.transform(seq.poses[k], voxel_filter(_data.kitti_scan(k), 0.5, 8))
+        a.update(w, seq.poses[k][:3, 3], 120.0, True)
+        b.update(w, seq.poses[k][:3, 3], 120.0, True)
+        _compare_maps(a, b)
