@@ -138,6 +138,12 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * the one-iteration-at-a-time path.  Off by default: at KITTI size a candidate chain's sequential normal equations,
  * solve and correspondence sweeps inside one workgroup outweigh the EM overlap. */
 int lo_set_lookahead(lo_ctx* ctx, int enable);
+/* Reference-exact arithmetic (default off): H, g and the cost summed SEQUENTIALLY in fp32 over the correspondences
+ * in scan order, the iteration-0 scale from the sorted residuals, the fp32 LDLT and SO3 re-projection through
+ * JacobiSVD -- the reference's own operation order (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99),
+ * so the per-iteration logs equal the oracle restatement's bit for bit.  Slower (a sequential sum and two fp32 SVDs per
+ * GN iteration); scans of at most 16384 points (LO_ERR_CAPACITY beyond). */
+int lo_set_exact(lo_ctx* ctx, int enable);
 /* In-step timing: with enable, each optimize brackets its FIRST correspondence launch (k_correspond, or the KDTree
  * k_knn + k_knn_brute + k_plane) with HIP events on the context stream (up to 1024 scans; enabling resets them).
  * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */

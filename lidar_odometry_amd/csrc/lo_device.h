@@ -127,6 +127,8 @@ struct KParams {
     double* acc_part;         // speculative normal equations: [NA + 1 candidates][kFuseMaxBlocks][kNE] partials
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
+    float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms
+    int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     DevState* st;
 };

@@ -1,0 +1,275 @@
+// lo_exact.hip — reference-exact GN step (lo_set_exact): the reference's own fp32 arithmetic order where the fast
+// path reorders it.  IterativeClosestPointOptimizer.cpp:304-449 sums H, g and the cost SEQUENTIALLY in fp32 over the
+// correspondences in scan order, takes the iteration-0 scale from the SORTED residuals, solves with Eigen's fp32 LDLT
+// and re-projects SO3::Exp and the pose product through SO3(Matrix3f)'s JacobiSVD (MathUtils.cpp:23-39, :86-99).
+// The fast path (lo_kernels.hip / lo_pko.hip) sums in fixed-order trees with fp64 block partials, merges the scale
+// by Chan's formula and solves in fp64 with a Newton polar factor -- within 1e-7 of these, but not bit-equal, and over
+// long GN sequences such ~1e-7 differences can move a correspondence across a voxel face.  Here every operation is
+// the oracle's restatement (oracle/src/lo_oracle.cpp build_ne / iter0_scale / ldlt6_solve / so3_exp / se3_mul),
+// so a scan's per-iteration logs equal the oracle's bit for bit (tests/test_gpu_exact.py).  It costs a sequential
+// sum per iteration (~15 us at KITTI size) and two fp32 Jacobi SVDs per solve: a parity mode, not the default.
+// Scans up to kExactMaxPoints (the sort and the term buffer are sized for it).
+#include <cfloat>
+
+#include "lo_device.h"
+#include "lo_math.h"
+
+namespace lo {
+
+constexpr int kExactTerms = 43;        // H (36, full: the reference's H is not symmetrised), g (6), cost
+
+// ---- the reference's fp32 solve and pose update (restated exactly as the oracle states them) ----
+// LDLT<Matrix<float,6,6>> (Eigen ldlt_inplace<Lower>::unblocked with diagonal pivoting + LDLT::_solve_impl)
+__device__ inline void ldlt6_solve_f32(const float (&Hin)[36], const float (&b)[6], float (&x)[6]) {
+    float m[6][6];
+    for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) m[r][c] = Hin[r * 6 + c];
+    int transp[6];
+    float temp[6];
+    bool zero_all = false;
+    for (int k = 0; k < 6; ++k) {
+        int big = k;
+        float bv = fabsf(m[k][k]);
+        for (int i = k + 1; i < 6; ++i) if (fabsf(m[i][i]) > bv) { bv = fabsf(m[i][i]); big = i; }
+        transp[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; ++j) { const float t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
+            for (int i = big + 1; i < 6; ++i) { const float t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
+            { const float t = m[k][k]; m[k][k] = m[big][big]; m[big][big] = t; }
+            for (int i = k + 1; i < big; ++i) { const float t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
+            float acc = 0.0f;
+            for (int j = 0; j < k; ++j) acc += m[k][j] * temp[j];
+            m[k][k] -= acc;
+            for (int i = k + 1; i < 6; ++i) {
+                float a = 0.0f;
+                for (int j = 0; j < k; ++j) a += m[i][j] * temp[j];
+                m[i][k] -= a;
+            }
+        }
+        const float akk = m[k][k];
+        const bool valid = fabsf(akk) > 0.0f;
+        if (k == 0 && !valid) { zero_all = true; break; }
+        if (k < 5 && valid) for (int i = k + 1; i < 6; ++i) m[i][k] /= akk;
+    }
+    if (zero_all) { for (int i = 0; i < 6; ++i) x[i] = 0.0f; return; }
+    float d[6];
+    for (int i = 0; i < 6; ++i) d[i] = b[i];
+    for (int k = 0; k < 6; ++k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
+    for (int i = 0; i < 6; ++i) { float a = 0.0f; for (int j = 0; j < i; ++j) a += m[i][j] * d[j]; d[i] -= a; }
+    for (int i = 0; i < 6; ++i) d[i] = (fabsf(m[i][i]) > FLT_MIN) ? d[i] / m[i][i] : 0.0f;
+    for (int i = 5; i >= 0; --i) { float a = 0.0f; for (int j = i + 1; j < 6; ++j) a += m[j][i] * d[j]; d[i] -= a; }
+    for (int k = 5; k >= 0; --k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
+    for (int i = 0; i < 6; ++i) x[i] = d[i];
+}
+
+__device__ inline float norm3e(const float* v) { return sqrtf(dot3e(v[0], v[1], v[2], v[0], v[1], v[2])); }
+
+// SO3::Exp (MathUtils.cpp:23-39, kEps 1e-6f) with the SO3(Matrix3f) re-projection of its result; sin / cos are
+// evaluated in fp64 and rounded (the correctly rounded fp32 value; glibc's sinf agrees with it for 99.6 % of the
+// floats in [1e-7, 0.8], cosf for 99.99 %)
+__device__ inline void so3_exp_exact(const float w[3], float R[3][3]) {
+    const float theta = norm3e(w);
+    float M[3][3];
+    if (theta < 1e-6f) {
+        const float H[3][3] = {{0.0f, -w[2], w[1]}, {w[2], 0.0f, -w[0]}, {-w[1], w[0], 0.0f}};
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) M[r][c] = (r == c ? 1.0f : 0.0f) + H[r][c];
+    } else {
+        const float ti = 1.0f / theta;
+        const float k[3] = {w[0] * ti, w[1] * ti, w[2] * ti};
+        const float K[3][3] = {{0.0f, -k[2], k[1]}, {k[2], 0.0f, -k[0]}, {-k[1], k[0], 0.0f}};
+        const float s = static_cast<float>(sin(static_cast<double>(theta)));
+        const float omc = 1.0f - static_cast<float>(cos(static_cast<double>(theta)));
+        float sK[3][3], KK[3][3];
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) sK[r][c] = omc * K[r][c];
+        mul33e(sK, K, KK);
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) M[r][c] = ((r == c ? 1.0f : 0.0f) + s * K[r][c]) + KK[r][c];
+    }
+    so3_project_svd(M, R);
+}
+
+// ---- iteration 0: scale = sqrt(var) / 6 of the residuals sorted ascending, mean and variance summed in that order
+// (IterativeClosestPointOptimizer.cpp:304-316).  One workgroup: the residuals of the accepted points (+inf for the
+// rest) in dynamic LDS, bitonic sort, then one lane accumulates as std::accumulate does ----
+constexpr int kExactScaleThreads = 1024;
+__global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, int n2) {
+    DevState* st = P.st;
+    if (st->done) return;
+    extern __shared__ double s_r[];
+    const int tid = threadIdx.x, n = scan_n(P);
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    for (int i = tid; i < n2; i += kExactScaleThreads) {
+        double v = __builtin_inf();
+        if (i < n) {
+            const int s = P.slot[i];
+            if (s >= 0 && P.kd_res) {
+                v = P.kd_res[i];                           // KDTree variant: the plane distance it accepted
+            } else if (s >= 0) {
+                float wx, wy, wz;
+                transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], wx, wy, wz);
+                v = residual_f64(P.tab[s], wx, wy, wz);
+            }
+        }
+        s_r[i] = v;
+    }
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < n2; i += kExactScaleThreads) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const double a = s_r[i], b = s_r[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? (a > b) : (a < b)) { s_r[i] = b; s_r[l] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid != 0) return;
+    int cnt = 0;
+    double sum = 0.0;
+    while (cnt < n && s_r[cnt] != __builtin_inf()) sum += s_r[cnt++];
+    if (cnt == 0) return;                                  // too few correspondences: the PKO launch reports it
+    const double mean = sum / cnt;
+    double var = 0.0;
+    for (int i = 0; i < cnt; ++i) var += (s_r[i] - mean) * (s_r[i] - mean);
+    var /= cnt;
+    st->scale = sqrt(var) / 6.0;
+}
+
+// ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =
+// J[col] * (w J[row]) (all 36), g[j] = (w r) J[j], cost = (w r) r; zeros for points without a correspondence
+// (adding +0 to the running sums leaves them unchanged) ----
+__global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
+    DevState* st = P.st;
+    if (st->done) return;
+    __shared__ double s_alpha;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < kWave) {
+        const double a = P.use_pko ? pko_select_alpha(P) : P.robust_delta;
+        if (lane == 0) {
+            s_alpha = a;
+            if (blockIdx.x == 0) st->alpha = a;
+        }
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kBlock + tid;
+    if (i >= scan_n(P)) return;
+    float* out = P.ex_terms + static_cast<size_t>(i) * kExactTerms;
+    const int s = P.slot[i];
+    if (s < 0) {
+        for (int k = 0; k < kExactTerms; ++k) out[k] = 0.0f;
+        return;
+    }
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    const double scale = st->scale;
+    const float dl = static_cast<float>(s_alpha);
+    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+    const Slot sl = P.tab[s];
+    double r64;
+    if (P.kd_res) {
+        r64 = P.kd_res[i];
+    } else {
+        float wx, wy, wz;
+        transform_pt(T, px, py, pz, wx, wy, wz);
+        r64 = residual_f64(sl, wx, wy, wz);
+    }
+    const float nres = static_cast<float>(r64 / std_max(scale, 1e-6));
+    const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
+    const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
+    const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
+    const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
+    const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
+    float J[6];
+    J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
+    J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
+    J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
+    const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
+    const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
+    const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
+    J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
+    J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
+    J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
+    float w = 1.0f;
+    if (P.robust) {
+        const float an = fabsf(nres);
+        if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
+        else if (an > dl) w = dl / an;
+    }
+    float wJ[6];
+    for (int j = 0; j < 6; ++j) wJ[j] = w * J[j];
+    for (int row = 0; row < 6; ++row)
+        for (int col = 0; col < 6; ++col) out[row * 6 + col] = J[col] * wJ[row];
+    const float wr = w * res;
+    for (int j = 0; j < 6; ++j) out[36 + j] = wr * J[j];
+    out[42] = wr * res;
+}
+
+// ---- the running fp32 sums over the correspondences in scan order (one lane per H / g / cost entry), then the
+// reference's solve and right-update, convergence test and the iteration's log ----
+__global__ __launch_bounds__(kWave) void k_exact_solve(KParams P, int it) {
+    DevState* st = P.st;
+    if (st->done) return;
+    __shared__ float tot[kExactTerms];
+    const int lane = threadIdx.x, n = scan_n(P);
+    if (lane < kExactTerms) {
+        const float* col = P.ex_terms + lane;
+        float s = 0.0f;
+        int i = 0;
+        for (; i + 8 <= n; i += 8) {                         // 8 loads in flight, the adds in point order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = col[static_cast<size_t>(i + u) * kExactTerms];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; i < n; ++i) s += col[static_cast<size_t>(i) * kExactTerms];
+        tot[lane] = s;
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    float Hf[36], mg[6], delta[6];
+    for (int k = 0; k < 36; ++k) Hf[k] = tot[k];
+    for (int j = 0; j < 6; ++j) mg[j] = -tot[36 + j];
+    ldlt6_solve_f32(Hf, mg, delta);                            // :418
+    const float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
+    float Rd[3][3];
+    if (norm3e(dw) < 1e-10f) {                                 // :427-431
+        const float I[3][3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
+        so3_project_svd(I, Rd);
+    } else {
+        so3_exp_exact(dw, Rd);
+    }
+    float R[3][3], t[3], M[3][3], Rn[3][3];
+    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) R[r][c] = st->pose[r * 4 + c]; t[r] = st->pose[r * 4 + 3]; }
+    mul33e(R, Rd, M);                                           // SE3::operator* (MathUtils.h:144-147)
+    so3_project_svd(M, Rn);
+    float pn[12];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) pn[r * 4 + c] = Rn[r][c];
+        pn[r * 4 + 3] = t[r] + dot3e(R[r][0], R[r][1], R[r][2], dt[0], dt[1], dt[2]);
+    }
+    const bool conv = norm3e(dt) < P.tol_t && norm3e(dw) < P.tol_r;   // :443-448
+    for (int q = 0; q < 12; ++q) st->pose[q] = pn[q];
+    if (it < LO_MAX_ITERS) {
+        lo_iter_log& L = st->logs[it];
+        for (int q = 0; q < 12; ++q) L.pose[q] = pn[q];
+        L.n_corr = st->n_corr;
+        L.scale = st->scale;
+        L.alpha = st->alpha;
+        L.cost = tot[42];
+        int k = 0;
+        for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L.H[k++] = tot[r * 6 + c];
+        for (int j = 0; j < 6; ++j) { L.g[j] = tot[36 + j]; L.delta[j] = delta[j]; }
+    }
+    st->iter = it + 1;
+    if (conv) st->done = 1;
+}
+
+}  // namespace lo

@@ -49,6 +49,9 @@ __global__ void k_la(const KParams* Pp, LaParams L, int k, int G);
 struct MapPatchRec;
 __global__ void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n);
 __global__ void k_la_finish(const KParams* Pp, LaParams L, int k_next);
+__global__ void k_exact_scale(KParams P, int n2);
+__global__ void k_exact_terms(KParams P);
+__global__ void k_exact_solve(KParams P, int it);
 }  // namespace lo
 
 using namespace lo;
@@ -88,6 +91,8 @@ struct lo_ctx {
     void* d_la = nullptr;           //   one allocation behind them
     KParams* d_la_params = nullptr; //   the scan's parameters, stashed by its first k_correspond
     bool lookahead = false;         // lo_set_lookahead (measured slower at KITTI size: DESIGN.md §3)
+    bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
+    float* d_ex_terms = nullptr;
     size_t la_pad = 0;              //   dynamic LDS of k_la (prefix + padding to one workgroup per CU)
     double* d_js = nullptr;
     double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
@@ -455,7 +460,7 @@ void lo_destroy(lo_ctx* c) {
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
-                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la};
+                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la, c->d_ex_terms};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->d_raw) (void)hipFree(c->d_raw);
     vf_free(c->vf);
@@ -715,7 +720,8 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
     hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
 }
 
-static constexpr int kStageEvents = 1024;          // scans whose first correspondence launch is timed
+static constexpr int kStageEvents = 1024;
+static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: sort / term buffer capacity          // scans whose first correspondence launch is timed
 
 // A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
 // (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
@@ -748,6 +754,31 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         // small scan with PKO: the solve of iteration it runs fused with the correspondence search of it + 1
         // (k_solve_correspond; KDTree: k_solve_knn, then k_knn_brute + k_plane), the last solve alone (k_solve_pick)
         const bool fused = spec_ok(P) && g.max_iterations <= LO_MAX_ITERS;
+        if (c->exact) {
+            // reference-exact GN loop (lo_exact.hip): correspondences, (iteration 0) sorted-order scale, PKO,
+            // per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
+            if (n > static_cast<size_t>(kExactMaxPoints)) { c->err = "exact mode: at most 16384 points"; return LO_ERR_CAPACITY; }
+            if (!c->d_ex_terms) {
+                LO_HIP(c, hipMalloc(&c->d_ex_terms, static_cast<size_t>(kExactMaxPoints) * 43 * sizeof(float)));
+                LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kExactMaxPoints * 8));
+            }
+            P.ex_terms = c->d_ex_terms;
+            P.scale_given = 1;
+            int n2 = 1;
+            while (n2 < static_cast<int>(n)) n2 <<= 1;
+            for (int it = 0; it < g.max_iterations; ++it) {
+                launch_correspond(c, it == 0 ? P0 : P, 0, c->kd);
+                if (it == 0) hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
+                launch_pko(c, P, it);
+                hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
+                hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(kWave), 0, c->stream, P, it);
+            }
+            LO_HIP(c, hipGetLastError());
+            LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+            c->pending = true;
+            return LO_OK;
+        }
         if (fused && !c->kd && c->lookahead) {
             // two GN iterations per launch (lo_lookahead.hip): k_correspond, k_la(0), k_la(2), ..., k_la_finish
             const int rc2 = ensure_la(c);
@@ -1202,6 +1233,12 @@ int lo_stage_time(lo_ctx* c, double* avg_us, int* count) {
     }
     *avg_us = c->st_n > 0 ? tot * 1e3 / c->st_n : 0.0;
     if (count) *count = c->st_n;
+    return LO_OK;
+}
+
+int lo_set_exact(lo_ctx* c, int enable) {
+    if (!c) return LO_ERR_ARG;
+    c->exact = enable != 0;
     return LO_OK;
 }
 

@@ -6,20 +6,27 @@
 #include <cfloat>
 #include <cmath>
 
+// The SVD / SO(3) restatements below also run on the device (lo_exact.hip): host-device under HIP.
+#if defined(__HIP__)
+#define LO_HD __host__ __device__
+#else
+#define LO_HD
+#endif
+
 namespace lo {
 
 // ---------------------------------------------------------------------------------------------
 // Eigen JacobiSVD<Matrix3f>, square case (JacobiSVD.h compute(), real_2x2_jacobi_svd, makeJacobi)
 // ---------------------------------------------------------------------------------------------
 struct Rot { float c, s; };
-inline Rot rot_t(Rot r) { return {r.c, -r.s}; }
-inline Rot rot_mul(Rot a, Rot b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
-inline void rotate(float& x, float& y, Rot r) {
+LO_HD inline Rot rot_t(Rot r) { return {r.c, -r.s}; }
+LO_HD inline Rot rot_mul(Rot a, Rot b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
+LO_HD inline void rotate(float& x, float& y, Rot r) {
     const float xi = x, yi = y;
     x = r.c * xi + r.s * yi;
     y = -r.s * xi + r.c * yi;
 }
-inline Rot make_jacobi(float x, float y, float z) {
+LO_HD inline Rot make_jacobi(float x, float y, float z) {
     const float deno = 2.0f * std::fabs(y);
     if (deno < FLT_MIN) return {1.0f, 0.0f};
     const float tau = (x - z) / deno;
@@ -31,7 +38,7 @@ inline Rot make_jacobi(float x, float y, float z) {
 }
 
 // A row-major a[r][c]; U columns = left singular vectors, S descending.
-inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vout[3][3] = nullptr) {
+LO_HD inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vout[3][3] = nullptr) {
     float scale = 0.0f;                                               // maxCoeff<PropagateNaN>
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
         const float v = std::fabs(A[r][c]);
@@ -90,8 +97,11 @@ inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vo
         for (int k = i + 1; k < 3; ++k) if (S[k] > S[pos]) pos = k;
         if (S[pos] == 0.0f) break;
         if (pos != i) {
-            std::swap(S[i], S[pos]);
-            for (int r = 0; r < 3; ++r) { std::swap(U[r][i], U[r][pos]); std::swap(V[r][i], V[r][pos]); }
+            float tq = S[i]; S[i] = S[pos]; S[pos] = tq;
+            for (int r = 0; r < 3; ++r) {
+                tq = U[r][i]; U[r][i] = U[r][pos]; U[r][pos] = tq;
+                tq = V[r][i]; V[r][i] = V[r][pos]; V[r][pos] = tq;
+            }
         }
     }
     if (Vout) for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vout[r][c] = V[r][c];
@@ -101,20 +111,20 @@ inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vo
 // ---------------------------------------------------------------------------------------------
 // SO3 / SE3f (MathUtils.h:57-168, MathUtils.cpp:41-99)
 // ---------------------------------------------------------------------------------------------
-inline float dot3e(float a0, float a1, float a2, float b0, float b1, float b2) {   // Vector3f dot: e0 + (e1 + e2)
+LO_HD inline float dot3e(float a0, float a1, float a2, float b0, float b1, float b2) {   // Vector3f dot: e0 + (e1 + e2)
     const float e0 = a0 * b0, e1 = a1 * b1, e2 = a2 * b2;
     return e0 + (e1 + e2);
 }
-inline void mul33e(const float A[3][3], const float B[3][3], float C[3][3]) {     // Matrix3f * Matrix3f
+LO_HD inline void mul33e(const float A[3][3], const float B[3][3], float C[3][3]) {     // Matrix3f * Matrix3f
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) C[r][c] = dot3e(A[r][0], A[r][1], A[r][2], B[0][c], B[1][c], B[2][c]);
 }
-inline float det3e(const float m[3][3]) {                                         // Eigen bruteforce_det3_helper order
+LO_HD inline float det3e(const float m[3][3]) {                                         // Eigen bruteforce_det3_helper order
     auto h = [&](int a, int b, int c) { return m[0][a] * (m[1][b] * m[2][c] - m[1][c] * m[2][b]); };
     return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
 }
 // SO3(const Matrix3f&): U V^T of JacobiSVD, U.col(2) negated when det < 0 (MathUtils.cpp:86-99)
-inline void so3_project(const float M[3][3], float R[3][3]) {
+LO_HD inline void so3_project_svd(const float M[3][3], float R[3][3]) {
     float U[3][3], S[3], V[3][3], Vt[3][3];
     jacobi_svd3(M, U, S, V);
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vt[r][c] = V[c][r];
@@ -141,7 +151,7 @@ inline SE3f se3_mul(const SE3f& A, const SE3f& B) {
     SE3f o;
     float M[3][3];
     mul33e(A.R, B.R, M);
-    so3_project(M, o.R);
+    so3_project_svd(M, o.R);
     for (int r = 0; r < 3; ++r) o.t[r] = A.t[r] + dot3e(A.R[r][0], A.R[r][1], A.R[r][2], B.t[0], B.t[1], B.t[2]);
     return o;
 }
@@ -150,7 +160,7 @@ inline SE3f se3_inv(const SE3f& A) {
     SE3f o;
     float Rt[3][3];
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rt[r][c] = A.R[c][r];
-    so3_project(Rt, o.R);
+    so3_project_svd(Rt, o.R);
     for (int r = 0; r < 3; ++r) o.t[r] = dot3e(o.R[r][0], o.R[r][1], o.R[r][2], -A.t[0], -A.t[1], -A.t[2]);
     return o;
 }

@@ -125,7 +125,7 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
     // estimate_motion_dual_frame hands optimize SE3f(guess.R, guess.t), i.e. SO3(R) re-projected (:284), and
     // wraps the result the same way (:308); on failure it returns the guess itself (:304-307)
     SE3f g_in = guess;
-    lo::so3_project(guess.R, g_in.R);
+    lo::so3_project_svd(guess.R, g_in.R);
     float g12[12], p12[12];
     lo::se3_to12(g_in, g12);
     lo_iter_log logs[LO_MAX_ITERS];
@@ -142,7 +142,7 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
     if (rc == LO_OK) {
         const SE3f r = lo::se3_from12(p12);
         pose = r;
-        lo::so3_project(r.R, pose.R);
+        lo::so3_project_svd(r.R, pose.R);
     }
     lo::se3_to12(pose, p12);
     o->velocity = lo::se3_mul(lo::se3_inv(o->prev), pose);                    // :177
@@ -152,9 +152,9 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
     const float dist = std::sqrt(lo::dot3e(dt[0], dt[1], dt[2], dt[0], dt[1], dt[2]));
     float Rki[3][3], Rkt[3][3], Rrel[3][3], Rrel_p[3][3];
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rkt[r][c] = o->last_kf.R[c][r];
-    lo::so3_project(Rkt, Rki);                                                // SO3::Inverse -> SO3(R^T)
+    lo::so3_project_svd(Rkt, Rki);                                                // SO3::Inverse -> SO3(R^T)
     lo::mul33e(Rki, pose.R, Rrel);
-    lo::so3_project(Rrel, Rrel_p);                                            // SO3::operator*
+    lo::so3_project_svd(Rrel, Rrel_p);                                            // SO3::operator*
     const double ang = lo::so3_log_norm(Rrel_p);
     if (static_cast<double>(dist) > o->cfg.keyframe_distance || ang > o->cfg.keyframe_rotation) {
         const int krc = create_keyframe(o, pose, fi);

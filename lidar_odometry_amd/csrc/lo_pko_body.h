@@ -515,6 +515,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
     __shared__ int s_nc;
     __shared__ double s_scale, s_mean;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool calc = it == 0 && !P.scale_given;           // iteration 0 computes the scale (unless it is given)
     if (P.direct_res) {
         if (tid == 0) { s_nc = P.n; s_scale = 1.0; }
         __syncthreads();
@@ -528,7 +529,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
             const int c = B.blk_cnt[b];
             s_pre[b] = c;
             cnt += c;
-            if (it == 0) lsum += P.blk_sum[b];
+            if (calc) lsum += P.blk_sum[b];
         }
         cnt = wave_sum(cnt);
         lsum = wave_total(lsum);
@@ -552,7 +553,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
         double m2 = 0.0;
-        if (it == 0) {
+        if (calc) {
             const double mean = s_mean;
 #pragma unroll 4
             for (int b = tid; b < nb; b += NT) {
@@ -569,7 +570,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
             int run = 0;
             double M2 = 0.0;
             for (int w = 0; w < NW; ++w) { const int c = s_iscan[w]; s_iscan[w] = run; run += c; M2 += s_dscan[w]; }
-            if (it == 0) {
+            if (calc) {
                 const double var = s_nc > 0 ? M2 / s_nc : 0.0;
                 s_scale = sqrt(var) / 6.0;                      // IterativeClosestPointOptimizer.cpp:314-315
                 if (lead) st->scale = s_scale;

@@ -137,6 +137,12 @@ class IterativeClosestPointOptimizer:
         """Surfels in the device table (lo_map_surfel_count)."""
         return int(self._L.lo_map_surfel_count(self.ctx))
 
+    def set_exact(self, enable: bool = True):
+        """Reference-exact arithmetic order (sequential fp32 sums, sorted-order scale, fp32 LDLT / SVD SO3); default off."""
+        rc = self._L.lo_set_exact(self.ctx, int(bool(enable)))
+        if rc != 0:
+            raise RuntimeError(f"lo_set_exact failed ({rc})")
+
     def set_lookahead(self, enable: bool = True):
         """Two GN iterations per launch for small PKO scans (default off; bit-identical either way)."""
         rc = self._L.lo_set_lookahead(self.ctx, int(bool(enable)))
