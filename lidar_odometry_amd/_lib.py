@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
-    "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels",
+    "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
     # include/lo_io.h
     "lo_load_kitti_bin", "lo_load_ply", "lo_kitti_pose_line", "lo_save_trajectory_kitti",
 )
@@ -139,6 +139,7 @@ def lib():
     L.lo_odom_keyframe_count.argtypes = [vp]
     L.lo_odom_map_surfels.restype = C.c_size_t
     L.lo_odom_map_surfels.argtypes = [vp]
+    L.lo_odom_set_exact.argtypes = [vp, C.c_int]
     L.lo_load_kitti_bin.restype = C.c_longlong
     L.lo_load_kitti_bin.argtypes = [C.c_char_p, fp, C.c_size_t]
     L.lo_load_ply.restype = C.c_longlong

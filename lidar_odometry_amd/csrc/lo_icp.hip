@@ -732,6 +732,29 @@ static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
     if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n++ + 1], c->stream);
 }
 
+// Reference-exact mode (lo_exact.hip): device buffers on first use, then per GN iteration the correspondence stage,
+// (iteration 0) the sorted-order scale, the PKO, the per-point terms and the sequential sums + fp32 solve.
+static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
+    if (n > static_cast<size_t>(kExactMaxPoints)) { c->err = "exact mode: at most 16384 points"; return LO_ERR_CAPACITY; }
+    if (!c->d_ex_terms) {
+        LO_HIP(c, hipMalloc(&c->d_ex_terms, static_cast<size_t>(kExactMaxPoints) * 43 * sizeof(float)));
+        LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kExactMaxPoints * 8));
+    }
+    P.ex_terms = c->d_ex_terms;
+    P.scale_given = 1;
+    *n2 = 1;
+    while (*n2 < static_cast<int>(n)) *n2 <<= 1;
+    return LO_OK;
+}
+static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P0, int it, int n2, bool kd) {
+    launch_correspond(c, it == 0 ? P0 : P, 0, kd);
+    if (it == 0) hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
+    launch_pko(c, P, it);
+    hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
+    hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(kWave), 0, c->stream, P, it);
+}
+
 static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12], const int* n_dev = nullptr) {
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
@@ -757,23 +780,10 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         if (c->exact) {
             // reference-exact GN loop (lo_exact.hip): correspondences, (iteration 0) sorted-order scale, PKO,
             // per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
-            if (n > static_cast<size_t>(kExactMaxPoints)) { c->err = "exact mode: at most 16384 points"; return LO_ERR_CAPACITY; }
-            if (!c->d_ex_terms) {
-                LO_HIP(c, hipMalloc(&c->d_ex_terms, static_cast<size_t>(kExactMaxPoints) * 43 * sizeof(float)));
-                LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, kExactMaxPoints * 8));
-            }
-            P.ex_terms = c->d_ex_terms;
-            P.scale_given = 1;
             int n2 = 1;
-            while (n2 < static_cast<int>(n)) n2 <<= 1;
-            for (int it = 0; it < g.max_iterations; ++it) {
-                launch_correspond(c, it == 0 ? P0 : P, 0, c->kd);
-                if (it == 0) hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
-                launch_pko(c, P, it);
-                hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
-                hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(kWave), 0, c->stream, P, it);
-            }
+            const int rc3 = exact_prepare(c, P, n, &n2);
+            if (rc3 != LO_OK) return rc3;
+            for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
             LO_HIP(c, hipGetLastError());
             LO_HIP(c, hipEventRecord(c->ev1, c->stream));
             c->pending = true;
@@ -921,6 +931,8 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
         }
         P.Tlw[4 * r + 3] = static_cast<float>(tr);
     }
+    int n2 = 0;
+    if (c->exact && (rc = exact_prepare(c, P, n_curr, &n2)) != LO_OK) return rc;
     KParams P0 = P;
     P0.init = 1;
     std::memcpy(P0.T0, T_curr, sizeof(float) * 12);
@@ -929,6 +941,10 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     const size_t head = offsetof(DevState, logs);
     for (int it = 0; it < kLoopMaxIters;) {
         for (int k = 0; k < kLoopChunk && it < kLoopMaxIters; ++k, ++it) {
+            if (c->exact) {
+                launch_exact_iteration(c, P, P0, it, n2, true);
+                continue;
+            }
             launch_correspond(c, it == 0 ? P0 : P, it == 0 ? 1 : 0, true);
             launch_gn_tail(c, P, it);
         }

@@ -90,6 +90,11 @@ int lo_odom_set_initial_pose(lo_odometry* o, const float T[12]) {
     return LO_OK;
 }
 
+int lo_odom_set_exact(lo_odometry* o, int enable) {
+    if (!o) return LO_ERR_ARG;
+    return lo_set_exact(o->icp, enable);
+}
+
 int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12], lo_odom_frame* info) {
     if (!o || !T_out || (n > 0 && !raw)) return LO_ERR_ARG;
     lo_odom_frame local{};

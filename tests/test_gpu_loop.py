@@ -117,3 +117,51 @@ def test_loop_icp_on_kdtree_context():
         np.testing.assert_array_equal(np.asarray(A), np.asarray(B))
     finally:
         o.close()
+
+
+def _bits(a):
+    return np.asarray(a, np.float32).reshape(-1).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def exact_icp():
+    from lidar_odometry_amd import IterativeClosestPointOptimizer
+    o = IterativeClosestPointOptimizer(max_points=1 << 16)
+    o.set_exact(True)
+    yield o
+    o.close()
+
+
+@pytest.mark.parametrize("fa,fb,seed", [(2, 6, 0), (4, 7, 3), (10, 14, 5), (20, 23, 9)])
+def test_loop_icp_exact_bitwise(exact_icp, fa, fb, seed):
+    """Reference-exact mode (lo_set_exact): the loop ICP's every GN iteration bit-identical to the oracle (the same
+    sequential fp32 normal equations, sorted-order scale, fp32 LDLT and SVD re-projection as the odometry ICP,
+    tests/test_gpu_exact.py), hence the same iteration count, T_rel and inlier count -- no alpha-flip allowance."""
+    cur, Tc, mat, Tm, _ = _data.loop_case(fa, fb, seed)
+    ok_o, conv_o, Tr_o, inl_o, it_o, logs_o = oracle.icp_optimize_loop(cur, Tc, mat, Tm)
+    ok_g, Tr_g, inl_g = exact_icp.optimize_loop(cur, Tc, mat, Tm)
+    st = exact_icp.get_last_stats()
+    assert ok_g == ok_o and st.converged == conv_o and st.num_iterations == it_o
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        for key in ("pose", "H", "g", "delta"):
+            np.testing.assert_array_equal(_bits(lg[key]), _bits(lo[key]), err_msg=f"iter {k} {key}")
+        assert (lg["n_corr"], lg["scale"], lg["alpha"]) == (lo["n_corr"], lo["scale"], lo["alpha"]), k
+        assert np.float32(lg["cost"]) == np.float32(lo["cost"]), k
+    assert ok_g and conv_o
+    np.testing.assert_array_equal(_bits(Tr_g), _bits(Tr_o))
+    assert np.float32(inl_g) == np.float32(inl_o)
+
+
+def test_loop_icp_exact_far_keyframe_same_outcome(exact_icp):
+    """The near-singular case above (matched keyframe 500 m away): with the reference's fp32 LDLT the device now
+    takes the same steps as the oracle, iteration by iteration."""
+    cur, Tc, mat, Tm, _ = _data.loop_case(2, 6)
+    far = np.asarray(Tm, np.float32).copy()
+    far[3] += 500.0
+    ok_o, conv_o, Tr_o, inl_o, it_o, logs_o = oracle.icp_optimize_loop(cur, Tc, mat, far)
+    ok, Tr, inl = exact_icp.optimize_loop(cur, Tc, mat, far)
+    st = exact_icp.get_last_stats()
+    assert not ok_o and not ok
+    assert st.num_iterations == it_o and st.converged == conv_o
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        np.testing.assert_array_equal(_bits(lg["pose"]), _bits(lo["pose"]), err_msg=f"iter {k}")
