@@ -299,6 +299,16 @@ __device__ __forceinline__ double rcp64(double x) {
     e = fma(-x, r, 1.0);
     return fma(r, e, r);
 }
+// One Newton step (~2^-48 relative): the EM's per-iteration reciprocals, whose results only need the GMM's
+// tolerance (the fitted parameters are already tree sums, ~1e-9 from the reference), one dependent FMA pair shorter.
+__device__ __forceinline__ double rcp64_1n(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq64_1n(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    return fma(0.5 * y, fma(-x * y, y, 1.0), y);
+}
 __device__ __forceinline__ double rsq64(double x) {
     double y = __builtin_amdgcn_rsq(x);
     double e = fma(-x * y, y, 1.0);

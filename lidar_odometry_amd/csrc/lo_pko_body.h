@@ -272,7 +272,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
             double sr = sp[64 * s + lane];                 // pdfs are >= +0 (or NaN): 0 + p_0 == p_0
 #pragma unroll
             for (int q = 1; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
-            const double isr = have[s] ? rcp64(sr) : 0.0;
+            const double isr = have[s] ? rcp64_1n(sr) : 0.0;
             const double r = p[s] * isr;
             v[0] += r;
             v[1] += r * x[s];
@@ -280,7 +280,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         }
         wave_totals4<3>(v);
         const double Nk = v[0];
-        const double iN = rcp64(Nk);
+        const double iN = rcp64_1n(Nk);
         const double nmu = (jj == 0) ? 0.0 : v[1] * iN;
         const double dm = nmu - muj;
         double nv = v[2] * iN - dm * dm;
@@ -288,7 +288,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         wj = Nk * invS;
         muj = nmu;
         varj = nv;
-        const double rs = rsq64(nv);
+        const double rs = rsq64_1n(nv);
         ca = wj * (rs * kInvSqrt2Pi);
         cb = 0.5 * (rs * rs);
         if (j >= 1 && lane == 0) s_dm[buf * kMaxK + j] = fabs(dm);
@@ -399,7 +399,7 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
             double sr = p[0][s];                           // as gmm_fit_split: 0 + p_0 == p_0
 #pragma unroll
             for (int q = 1; q < K; ++q) sr += p[q][s];
-            const double isr = have[s] ? rcp64(sr) : 0.0;
+            const double isr = have[s] ? rcp64_1n(sr) : 0.0;
 #pragma unroll
             for (int q = 0; q < K; ++q) {
                 const double r = p[q][s] * isr;
@@ -413,7 +413,7 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             const double Nk = v[q];
-            const double iN = rcp64(Nk);
+            const double iN = rcp64_1n(Nk);
             const double nmu = (q == 0) ? 0.0 : v[K + q - 1] * iN;
             const double dm = nmu - mu[q];
             double nv = v[2 * K - 1 + q] * iN - dm * dm;
@@ -421,7 +421,7 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
             w[q] = Nk * invS;
             mu[q] = nmu;
             var[q] = nv;
-            const double rs = rsq64(nv);
+            const double rs = rsq64_1n(nv);
             ca[q] = w[q] * (rs * kInvSqrt2Pi);
             cb[q] = 0.5 * (rs * rs);
             if (q >= 1) change += fabs(dm);
