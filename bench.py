@@ -66,14 +66,16 @@ def _raycast_device(rank: int):
     return f"cuda:{int(os.environ.get('LOCAL_RANK', rank)) % max(torch.cuda.device_count(), 1)}"
 
 
-def build_kitti(rank: int, n_map: int = 300, name: str = ""):
+def build_kitti(rank: int, n_map: int = 660, name: str = "", city: bool = True):
     """KITTI-07-like workload: the surfel map after n_map frames of keyframing (a keyframe every
     2 frames ~ 1.2 m, kitti.yaml keyframe_distance 1.0; UpdateVoxelMap prunes to 1.2 x 100 m), then 20 scans from the
-    last 40 frames between keyframes with perturbed initial poses."""
+    last 40 frames between keyframes with perturbed initial poses.  city: the HDL-64-like scanner on a serpentine
+    through a street grid (synth.KittiCitySequence), so the 120 m radius holds several streets and the map reaches
+    ~10^4 L1 surfels; otherwise the single meandering street (KittiLikeSequence, the round-1 scene)."""
     from lidar_odometry_amd import synth
     from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
     dev = _raycast_device(rank)
-    seq = synth.KittiLikeSequence(seed=7, n_frames=n_map + 2)
+    seq = synth.KittiCitySequence(n_frames=n_map + 2) if city else synth.KittiLikeSequence(seed=7, n_frames=n_map + 2)
     vm = VoxelMap(0.5, 3, 0.1, True)
     kf = []
     for k in range(0, n_map + 1, 2):
@@ -88,15 +90,16 @@ def build_kitti(rank: int, n_map: int = 300, name: str = ""):
         scans.append(voxel_filter(seq.scan(f, device=dev), 0.5, 8))
         inits.append(synth.perturb(seq.poses[f], rng, 0.05, 0.01))
         gts.append(seq.poses[f])
-    return {"name": name or f"KITTI-07-like HDL-64 scan (stride 8, 0.5 m voxels) surfel ICP, config/kitti.yaml, map after "
-                            f"{n_map} frames",
+    return {"name": name or f"KITTI-07-like HDL-64 scan (stride 8, 0.5 m voxels) surfel ICP, config/kitti.yaml, city-grid "
+                            f"map after {n_map} frames",
             "voxel": 0.5, "max_dist": 120.0, "vm": vm, "scans": scans, "inits": inits, "gts": gts, "keyframes": kf,
             "seq": seq, "frames": frames, "raycast_device": dev}
 
 
 def build_kitti_small(rank: int):
     """Round-1 workload, kept as a labelled secondary line: the map after 42 frames (1.5k surfels)."""
-    return build_kitti(rank, n_map=40, name="KITTI-07-like HDL-64 scan surfel ICP, small map (42 frames, round-1 line)")
+    return build_kitti(rank, n_map=40, name="KITTI-07-like HDL-64 scan surfel ICP, small map (42 frames, round-1 line)",
+                       city=False)
 
 
 def build_mid360(rank: int):

@@ -32,6 +32,13 @@ int          lo_voxelmap_update(lo_voxelmap* m, const float* world_xyz, size_t n
  * :1181): every L0 centroid moved by T (row-major 3x4) and re-keyed, collisions merged, surfels recomputed.
  * The next lo_map_sync_voxelmap uploads the whole map. */
 int          lo_voxelmap_apply_transform(lo_voxelmap* m, const float T[12]);
+/* Device surfel fits: with enable, UpdateVoxelMap records each touched L1 voxel's refit
+ * (its children's centroids in child order) instead of fitting on the host; the next lo_map_sync_voxelmap of a
+ * context that mirrors this map runs them there (k_surfel_fit: the same fp32 mean / covariance / JacobiSVD code)
+ * and patches its table, and the results come back to the map before anything reads it -- surfel fields, or the
+ * planarity erase of the voxel and its children in the sequential loop's order.  Bit-identical to enable = 0.
+ * Without such a sync the map fits on the host when it is next read. */
+int          lo_voxelmap_set_device_fit(lo_voxelmap* m, int enable);
 size_t       lo_voxelmap_l0_count(const lo_voxelmap* m);
 size_t       lo_voxelmap_l1_count(const lo_voxelmap* m);
 size_t       lo_voxelmap_surfel_count(const lo_voxelmap* m);

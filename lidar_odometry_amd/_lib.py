@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
+    "lo_voxelmap_set_device_fit",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
     "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
@@ -196,6 +197,7 @@ def lib():
     L.lo_map_set_from_voxelmap.argtypes = [vp, vp]
     L.lo_map_sync_voxelmap.argtypes = [vp, vp, C.POINTER(C.c_int)]
     L.lo_voxelmap_apply_transform.argtypes = [vp, vp]
+    L.lo_voxelmap_set_device_fit.argtypes = [vp, C.c_int]
     L.lo_map_patch_surfels.argtypes = [vp, vp, vp, vp, vp, C.c_size_t]
     L.lo_voxel_filter.restype = C.c_size_t
     L.lo_voxel_filter.argtypes = [fp, C.c_size_t, C.c_float, C.c_int, fp]

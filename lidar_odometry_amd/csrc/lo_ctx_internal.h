@@ -9,4 +9,20 @@ namespace lo {
 // (lo_map_sync_voxelmap); src = 0 after any other table upload.
 void ctx_map_source(const lo_ctx* c, uint64_t* src, uint64_t* epoch, uint64_t* pos);
 void ctx_set_map_source(lo_ctx* c, uint64_t src, uint64_t epoch, uint64_t pos);
+
+// Device surfel fits for a host map's deferred jobs (lo_voxelmap_set_device_fit).  ctx_fit_surfels fits job j over
+// cs[3 * offs[j] ...) (children up to offs[j + 1], the last to n_cs) with k_surfel_fit on the context stream, which
+// patches the table (upsert when planarity <= thr, else erase) after any patch already enqueued, and copies the
+// results back asynchronously; *ticket identifies the launch.  LO_ERR_CAPACITY if the table could overflow (the
+// caller then fits on the host and uploads everything).  ctx_fit_results waits for that launch and returns its
+// results; LO_ERR_STATE if the context is gone or has launched other fits since (the caller fits on the host).
+struct FitResult {
+    float n[3];
+    float c[3];
+    float planarity;
+    uint32_t pad;
+};
+int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t n_jobs, const float* cs, size_t n_cs,
+                    float thr, uint64_t* ticket);
+int ctx_fit_results(lo_ctx* c, uint64_t ticket, FitResult* out, size_t n_jobs);
 }  // namespace lo

@@ -11,7 +11,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -48,6 +50,13 @@ __global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
 __global__ void k_la(const KParams* Pp, LaParams L, int k, int G);
 struct MapPatchRec;
 __global__ void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n);
+struct FitJob {
+    uint64_t key;
+    int32_t off, m;
+};
+struct FitOut;
+__global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
+                             FitOut* out);
 __global__ void k_la_finish(const KParams* Pp, LaParams L, int k_next);
 __global__ void k_exact_scale(KParams P, int n2);
 __global__ void k_exact_terms(KParams P);
@@ -114,6 +123,19 @@ struct lo_ctx {
     size_t patch_cap = 0;
     hipEvent_t ev_patch = nullptr;
     uint64_t map_src = 0, map_epoch = 0, map_pos = 0;
+    uint64_t tab_gen = 0;           // bumped by every full upload (a pending fit's results no longer apply to it)
+    // deferred surfel fits of a synced host map (lo::ctx_fit_surfels): pinned in / out staging, device copies
+    void* h_fit_in = nullptr;
+    void* d_fit_in = nullptr;
+    size_t fit_in_cap = 0;
+    FitResult* h_fit_out = nullptr;
+    FitResult* d_fit_out = nullptr;
+    size_t fit_out_cap = 0;
+    hipEvent_t ev_fit = nullptr;
+    uint64_t fit_ticket = 0;        // the launch whose results sit in h_fit_out (0: none)
+    uint64_t fit_gen = 0;           //   and the table generation it patched
+    std::vector<uint64_t> fit_keys; //   its packed keys, job order
+    float fit_thr = 0.0f;
     // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
     bool kd = false;
     PointGrid grid;                 // the map's L0 centroids (lo_map_set_points)
@@ -428,6 +450,11 @@ static int ctx_alloc(lo_ctx* c) {
     return LO_OK;
 }
 
+// Live contexts (a host map holding a deferred-fit ticket asks whether its context still exists).
+static std::mutex g_live_mu;
+static std::unordered_set<const lo_ctx*> g_live;
+static uint64_t g_ticket = 0;
+
 lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     std::string e;
     int rc = validate_config(cfg, e);
@@ -449,11 +476,19 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
         return nullptr;
     }
     if (err) *err = LO_OK;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        g_live.insert(c);
+    }
     return c;
 }
 
 void lo_destroy(lo_ctx* c) {
     if (!c) return;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        g_live.erase(c);
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part, c->d_acc_part,
@@ -471,6 +506,11 @@ void lo_destroy(lo_ctx* c) {
     if (c->ev_patch) (void)hipEventDestroy(c->ev_patch);
     if (c->h_patch) (void)hipHostFree(c->h_patch);
     if (c->d_patch) (void)hipFree(c->d_patch);
+    if (c->ev_fit) (void)hipEventDestroy(c->ev_fit);
+    if (c->h_fit_in) (void)hipHostFree(c->h_fit_in);
+    if (c->d_fit_in) (void)hipFree(c->d_fit_in);
+    if (c->h_fit_out) (void)hipHostFree(c->h_fit_out);
+    if (c->d_fit_out) (void)hipFree(c->d_fit_out);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -520,6 +560,7 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
     c->resident.swap(resident);
     c->n_tomb = 0;
     c->map_src = 0;                                      // no longer mirrors a synced host map
+    ++c->tab_gen;
     return LO_OK;
 }
 
@@ -538,6 +579,99 @@ void ctx_map_source(const lo_ctx* c, uint64_t* src, uint64_t* epoch, uint64_t* p
 }
 void ctx_set_map_source(lo_ctx* c, uint64_t src, uint64_t epoch, uint64_t pos) {
     c->map_src = src; c->map_epoch = epoch; c->map_pos = pos;
+}
+
+static int grow_pinned_pair(lo_ctx* c, void** h, void** d, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return LO_OK;
+    if (*h) LO_HIP(c, hipHostFree(*h));
+    if (*d) LO_HIP(c, hipFree(*d));
+    *h = *d = nullptr;
+    *cap = 0;
+    const size_t b = std::max<size_t>(2 * bytes, 64 * 1024);
+    LO_HIP(c, hipHostMalloc(h, b, hipHostMallocDefault));
+    LO_HIP(c, hipMalloc(d, b));
+    *cap = b;
+    return LO_OK;
+}
+
+int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t n_jobs, const float* cs, size_t n_cs,
+                    float thr, uint64_t* ticket) {
+    if (!c || !ticket || (n_jobs > 0 && (!keys || !offs || !cs))) return LO_ERR_ARG;
+    if (!c->d_tab) { c->err = "no surfel table to patch"; return LO_ERR_STATE; }
+    if (n_jobs > static_cast<size_t>(INT32_MAX) || n_cs > static_cast<size_t>(INT32_MAX / 3)) return LO_ERR_CAPACITY;
+    // worst case for the table: every job not resident inserts, every resident one leaves a tombstone
+    std::vector<uint64_t> pk(n_jobs);
+    size_t ins = 0, ers = 0;
+    for (size_t j = 0; j < n_jobs; ++j) {
+        for (int a = 0; a < 3; ++a) {
+            const int32_t v = keys[3 * j + a];
+            if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
+        }
+        pk[j] = pack_key_host(keys[3 * j], keys[3 * j + 1], keys[3 * j + 2]);
+        if (c->resident.count(pk[j])) ++ers; else ++ins;
+    }
+    const size_t cap = size_t(1) << c->log2cap;
+    if (c->resident.size() + ins + c->n_tomb + ers > cap / 2) { c->err = "table full"; return LO_ERR_CAPACITY; }
+    LO_HIP(c, hipSetDevice(c->device));
+    if (!c->ev_fit) LO_HIP(c, hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming));
+    else LO_HIP(c, hipEventSynchronize(c->ev_fit));     // the previous fit has left the staging buffers
+    const size_t jb = n_jobs * sizeof(FitJob), in_bytes = jb + n_cs * 3 * sizeof(float);
+    int rc = grow_pinned_pair(c, &c->h_fit_in, &c->d_fit_in, &c->fit_in_cap, in_bytes);
+    if (rc != LO_OK) return rc;
+    void* ho = c->h_fit_out;
+    void* dv = c->d_fit_out;
+    rc = grow_pinned_pair(c, &ho, &dv, &c->fit_out_cap, n_jobs * sizeof(FitResult));
+    c->h_fit_out = static_cast<FitResult*>(ho);
+    c->d_fit_out = static_cast<FitResult*>(dv);
+    if (rc != LO_OK) return rc;
+    FitJob* J = static_cast<FitJob*>(c->h_fit_in);
+    for (size_t j = 0; j < n_jobs; ++j) {
+        const int32_t end = j + 1 < n_jobs ? offs[j + 1] : static_cast<int32_t>(n_cs);
+        J[j].key = pk[j];
+        J[j].off = offs[j];
+        J[j].m = end - offs[j];
+    }
+    std::memcpy(static_cast<char*>(c->h_fit_in) + jb, cs, n_cs * 3 * sizeof(float));
+    LO_HIP(c, hipMemcpyAsync(c->d_fit_in, c->h_fit_in, in_bytes, hipMemcpyHostToDevice, c->stream));
+    if (n_jobs > 0)
+        hipLaunchKernelGGL(k_surfel_fit, dim3(static_cast<unsigned>((n_jobs + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           c->stream, static_cast<const FitJob*>(c->d_fit_in),
+                           reinterpret_cast<const float*>(static_cast<const char*>(c->d_fit_in) + jb),
+                           static_cast<int>(n_jobs), thr, c->d_tab, c->log2cap, reinterpret_cast<FitOut*>(c->d_fit_out));
+    LO_HIP(c, hipGetLastError());
+    LO_HIP(c, hipMemcpyAsync(c->h_fit_out, c->d_fit_out, n_jobs * sizeof(FitResult), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipEventRecord(c->ev_fit, c->stream));
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        c->fit_ticket = ++g_ticket;
+    }
+    c->fit_gen = c->tab_gen;
+    c->fit_keys.swap(pk);
+    c->fit_thr = thr;
+    // until the results are collected the mirror counts every job key as resident (erases are then always sent)
+    for (uint64_t k : c->fit_keys) c->resident.insert(k);
+    c->n_tomb += ers;
+    c->n_surfels = c->resident.size();
+    *ticket = c->fit_ticket;
+    return LO_OK;
+}
+
+int ctx_fit_results(lo_ctx* c, uint64_t ticket, FitResult* out, size_t n_jobs) {
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        if (!c || !g_live.count(c) || c->fit_ticket != ticket || ticket == 0) return LO_ERR_STATE;
+    }
+    if (c->fit_keys.size() != n_jobs) return LO_ERR_STATE;
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipEventSynchronize(c->ev_fit));
+    std::memcpy(out, c->h_fit_out, n_jobs * sizeof(FitResult));
+    if (c->fit_gen == c->tab_gen)                        // the table still holds what the kernel patched
+        for (size_t j = 0; j < n_jobs; ++j)
+            if (out[j].planarity > c->fit_thr) c->resident.erase(c->fit_keys[j]);
+    c->n_surfels = c->resident.size();
+    c->fit_ticket = 0;
+    c->fit_keys.clear();
+    return LO_OK;
 }
 }  // namespace lo
 

@@ -21,6 +21,7 @@
 // reference's fp32/fp64 expressions (DESIGN.md "fp order").  Sums are fixed-order trees (run-to-run
 // deterministic), not the reference's sequential order.
 #include "lo_device.h"
+#include "lo_math.h"
 #include "lo_solve.h"
 
 #include <cfloat>
@@ -321,10 +322,7 @@ struct MapPatchRec {
     uint32_t pad;
 };
 
-__global__ __launch_bounds__(kBlock) void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const MapPatchRec r = rec[i];
+__device__ void patch_slot(Slot* tab, uint32_t log2cap, const MapPatchRec& r) {
     const uint32_t mask = (1u << log2cap) - 1u;
     uint32_t h = hash_slot(r.key, log2cap);
     for (uint32_t p = 0; p <= mask; ++p) {
@@ -350,6 +348,43 @@ __global__ __launch_bounds__(kBlock) void k_map_patch(Slot* tab, uint32_t log2ca
         }
         h = (h + 1u) & mask;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    patch_slot(tab, log2cap, rec[i]);
+}
+
+// k_surfel_fit: the deferred refits of a host map's touched L1 voxels (VoxelMap.cpp:211-243, surfel_fit in lo_math.h,
+// the host's own code), one thread per voxel: result back to the host map, and the table patched in place -- the
+// surfel upserted, or erased when the planarity test fails (:239-247).
+struct FitJob {
+    uint64_t key;
+    int32_t off, m;
+};
+struct FitOut {
+    float n[3], c[3], planarity;
+    uint32_t pad;
+};
+__global__ __launch_bounds__(kBlock) void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab,
+                                                       uint32_t log2cap, FitOut* out) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const FitJob J = jobs[i];
+    float cen[3], U[3][3];
+    const float pl = surfel_fit(cs + 3 * static_cast<size_t>(J.off), J.m, cen, U);
+    FitOut o;
+    for (int a = 0; a < 3; ++a) { o.n[a] = U[a][2]; o.c[a] = cen[a]; }
+    o.planarity = pl;
+    o.pad = 0;
+    out[i] = o;
+    MapPatchRec r;
+    r.key = J.key;
+    r.op = (pl > thr) ? 0u : 1u;                        // NaN planarity keeps the surfel, as the host comparison
+    r.pad = 0;
+    for (int a = 0; a < 3; ++a) { r.n[a] = o.n[a]; r.c[a] = o.c[a]; }
+    patch_slot(tab, log2cap, r);
 }
 
 // ====================================================================================================

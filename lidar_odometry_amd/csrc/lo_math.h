@@ -107,6 +107,24 @@ LO_HD inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], fl
     if (Vout) for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Vout[r][c] = V[r][c];
 }
 
+// Surfel fit of one L1 voxel (VoxelMap.cpp:211-243) over its m children's L0 centroids cs (xyz, child order): fp32
+// mean and covariance in child order, JacobiSVD<Matrix3f>, normal = U.col(2); returns planarity = s2 / (s0 + 1e-6).
+// One definition for the host map (lo_voxelmap.cpp) and the device fit (k_surfel_fit), so the two agree bit for bit.
+LO_HD inline float surfel_fit(const float* cs, int m, float cen[3], float U[3][3]) {
+    cen[0] = cen[1] = cen[2] = 0.0f;
+    for (int q = 0; q < m; ++q) for (int a = 0; a < 3; ++a) cen[a] += cs[3 * q + a];
+    const float mf = static_cast<float>(m);
+    for (int a = 0; a < 3; ++a) cen[a] /= mf;
+    float cov[3][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+    for (int q = 0; q < m; ++q) {
+        const float d[3] = {cs[3 * q] - cen[0], cs[3 * q + 1] - cen[1], cs[3 * q + 2] - cen[2]};
+        for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) cov[r][c] += d[c] * d[r];
+    }
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) cov[r][c] /= mf;
+    float S[3];
+    jacobi_svd3(cov, U, S);
+    return S[2] / (S[0] + 1e-6f);
+}
 
 // ---------------------------------------------------------------------------------------------
 // SO3 / SE3f (MathUtils.h:57-168, MathUtils.cpp:41-99)

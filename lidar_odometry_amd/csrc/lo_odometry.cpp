@@ -71,6 +71,7 @@ lo_odometry* lo_odom_create(const lo_odom_config* cfg, int device, int* err) {
     o->map = lo_voxelmap_create(cfg->icp.voxel_size, cfg->icp.hierarchy_factor, cfg->planarity_threshold,
                                 cfg->icp.use_surfel_correspondence ? 1 : 0);   // SetComputeSurfels (Estimator.cpp:79)
     if (!o->map) { lo_destroy(o->icp); delete o; if (err) *err = LO_ERR_ARG; return nullptr; }
+    if (cfg->icp.use_surfel_correspondence) lo_voxelmap_set_device_fit(o->map, 1);   // refits run in the sync's patch
     if (err) *err = LO_OK;
     return o;
 }

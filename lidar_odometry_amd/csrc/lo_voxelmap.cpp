@@ -263,20 +263,56 @@ struct HostVoxelMap {
     // Surfel fit (VoxelMap.cpp:211-243): fp32 mean and covariance in child order, JacobiSVD<Matrix3f> (restated),
     // normal = U.col(2); returns planarity = s2 / (s0 + 1e-6)
     static float fit(const std::vector<float>& cs, float cen[3], float U[3][3]) {
-        const size_t m = cs.size() / 3;
-        cen[0] = cen[1] = cen[2] = 0.0f;
-        for (size_t q = 0; q < m; ++q) for (int a = 0; a < 3; ++a) cen[a] += cs[3 * q + a];
-        const float mf = static_cast<float>(m);
-        for (int a = 0; a < 3; ++a) cen[a] /= mf;
-        float cov[3][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
-        for (size_t q = 0; q < m; ++q) {
-            const float d[3] = {cs[3 * q] - cen[0], cs[3 * q + 1] - cen[1], cs[3 * q + 2] - cen[2]};
-            for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) cov[r][c] += d[c] * d[r];
+        return surfel_fit(cs.data(), static_cast<int>(cs.size() / 3), cen, U);
+    }
+
+    // Deferred fits (lo_voxelmap_set_device_fit): the touched loop of update() records each refit as a job (L1 key,
+    // child count, child centroids in child order) instead of fitting; lo_map_sync_voxelmap runs the jobs on the
+    // device (k_surfel_fit, which also patches the synced table), and resolve() applies the results in job order --
+    // surfel fields, or on a planarity failure the erase of the voxel and its children, exactly where the sequential
+    // loop would have done it (no other structural change happens in that loop, and the jobs' inputs are per voxel).
+    // Every reader of the map resolves first; without a device result the jobs are fitted here.
+    bool defer_fit = false;
+    std::vector<Key3> job_key;
+    std::vector<int32_t> job_cnt, job_off;               // child count; offset into job_cs (floats / 3)
+    std::vector<float> job_cs;
+    lo_ctx* fit_ctx = nullptr;                           // the context whose k_surfel_fit holds the results
+    uint64_t fit_id = 0;                                 // its ticket
+    void resolve() {
+        if (job_key.empty()) return;
+        const size_t nj = job_key.size();
+        std::vector<FitResult> res(nj);
+        bool have = fit_ctx && ctx_fit_results(fit_ctx, fit_id, res.data(), nj) == LO_OK;
+        if (!have) {
+            for (size_t j = 0; j < nj; ++j) {
+                const int m = (j + 1 < nj ? job_off[j + 1] : static_cast<int32_t>(job_cs.size() / 3)) - job_off[j];
+                float U[3][3];
+                res[j].planarity = surfel_fit(job_cs.data() + 3 * job_off[j], m, res[j].c, U);
+                for (int a = 0; a < 3; ++a) res[j].n[a] = U[a][2];
+            }
         }
-        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) cov[r][c] /= mf;
-        float S[3];
-        jacobi_svd3(cov, U, S);
-        return S[2] / (S[0] + 1e-6f);
+        for (size_t j = 0; j < nj; ++j) {
+            const int64_t li = l1.find(job_key[j]);
+            if (li < 0) continue;                           // cannot happen: jobs are unique, nothing erased them
+            L1& node = l1.val_at(li);
+            if (res[j].planarity > planarity_thr) {
+                node.has_surfel = false;
+                std::vector<Key3> kids;
+                for (size_t q = 0; q < node.children.size(); ++q) kids.push_back(node.children.key_at(q));
+                for (const Key3& k : kids) l0.erase(k);
+                l1.erase(job_key[j]);
+                continue;
+            }
+            node.has_surfel = true;
+            for (int a = 0; a < 3; ++a) { node.normal[a] = res[j].n[a]; node.centroid[a] = res[j].c[a]; }
+            node.planarity = res[j].planarity;
+            node.last_child_count = job_cnt[j];
+        }
+        job_key.clear();
+        job_cnt.clear();
+        job_off.clear();
+        job_cs.clear();
+        fit_ctx = nullptr;
     }
 
     // VoxelMap::ApplyTransformAndRehash (VoxelMap.cpp:264-302), after a pose-graph correction: every L0 centroid
@@ -285,6 +321,7 @@ struct HostVoxelMap {
     // 5 children, planarity failures lose the surfel without being erased).  The device tables need a full upload
     // afterwards (the journal restarts).
     void apply_transform(const float T[12]) {
+        resolve();
         const SE3f s = se3_from12(T);
         std::vector<std::pair<Key3, L0>> tr;
         tr.reserve(l0.size());
@@ -333,6 +370,7 @@ struct HostVoxelMap {
     }
 
     void update(const float* xyz, size_t n, const double sensor[3], double max_distance, bool keyframe) {
+        resolve();
         if (!xyz || n == 0 || !keyframe) return;
         const float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
         const float rsq = static_cast<float>(max_distance * max_distance);
@@ -373,6 +411,14 @@ struct HostVoxelMap {
             note(k1);                                          // refitted, erased or losing its surfel below
             child_centroids(node, cs);
             if (cs.size() / 3 < 3) { node.has_surfel = false; continue; }
+            if (defer_fit) {                                   // resolve() finishes this voxel
+                job_key.push_back(k1);
+                job_cnt.push_back(cnt);
+                job_off.push_back(static_cast<int32_t>(job_cs.size() / 3));
+                job_cs.insert(job_cs.end(), cs.begin(), cs.end());
+                node.has_surfel = false;
+                continue;
+            }
             float U[3][3], cen[3];
             const float planarity = fit(cs, cen, U);
             if (planarity > planarity_thr) {
@@ -398,6 +444,13 @@ using lo::HostVoxelMap;
 struct lo_voxelmap {
     HostVoxelMap m;
 };
+
+// Readers see the map as the sequential UpdateVoxelMap leaves it: pending device fits are applied first.
+static const HostVoxelMap& resolved(const lo_voxelmap* m) {
+    HostVoxelMap& h = const_cast<lo_voxelmap*>(m)->m;
+    h.resolve();
+    return h;
+}
 
 extern "C" {
 
@@ -425,22 +478,31 @@ int lo_voxelmap_update(lo_voxelmap* m, const float* xyz, size_t n, const double 
     return LO_OK;
 }
 
-size_t lo_voxelmap_l0_count(const lo_voxelmap* m) { return m ? m->m.l0.size() : 0; }
-size_t lo_voxelmap_l1_count(const lo_voxelmap* m) { return m ? m->m.l1.size() : 0; }
+size_t lo_voxelmap_l0_count(const lo_voxelmap* m) { return m ? resolved(m).l0.size() : 0; }
+size_t lo_voxelmap_l1_count(const lo_voxelmap* m) { return m ? resolved(m).l1.size() : 0; }
 size_t lo_voxelmap_surfel_count(const lo_voxelmap* m) {
     if (!m) return 0;
+    const HostVoxelMap& h = resolved(m);
     size_t c = 0;
-    for (size_t i = 0; i < m->m.l1.size(); ++i) c += m->m.l1.val_at(i).has_surfel ? 1 : 0;
+    for (size_t i = 0; i < h.l1.size(); ++i) c += h.l1.val_at(i).has_surfel ? 1 : 0;
     return c;
+}
+
+int lo_voxelmap_set_device_fit(lo_voxelmap* m, int enable) {
+    if (!m) return LO_ERR_ARG;
+    m->m.resolve();
+    m->m.defer_fit = enable != 0;
+    return LO_OK;
 }
 
 size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* normals, float* centroids, float* planarity, size_t cap) {
     if (!m) return 0;
+    const HostVoxelMap& h = resolved(m);
     size_t c = 0;
-    for (size_t i = 0; i < m->m.l1.size() && c < cap; ++i) {
-        const auto& n = m->m.l1.val_at(i);
+    for (size_t i = 0; i < h.l1.size() && c < cap; ++i) {
+        const auto& n = h.l1.val_at(i);
         if (!n.has_surfel) continue;
-        const auto& k = m->m.l1.key_at(i);
+        const auto& k = h.l1.key_at(i);
         if (keys) { keys[3 * c] = k.x; keys[3 * c + 1] = k.y; keys[3 * c + 2] = k.z; }
         for (int a = 0; a < 3; ++a) {
             if (normals) normals[3 * c + a] = n.normal[a];
@@ -454,8 +516,9 @@ size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* norma
 
 size_t lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap) {
     if (!m || !xyz) return 0;
+    const HostVoxelMap& h = resolved(m);
     size_t c = 0;
-    for (; c < m->m.l0.size() && c < cap; ++c) std::memcpy(xyz + 3 * c, m->m.l0.val_at(c).c, sizeof(float) * 3);
+    for (; c < h.l0.size() && c < cap; ++c) std::memcpy(xyz + 3 * c, h.l0.val_at(c).c, sizeof(float) * 3);
     return c;
 }
 
@@ -464,13 +527,18 @@ int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
     if (patched) *patched = -1;
     lo_config cfg;
     if (lo_get_config(ctx, &cfg) != LO_OK) return LO_ERR_ARG;
-    const HostVoxelMap& H = m->m;
+    HostVoxelMap& H = const_cast<lo_voxelmap*>(m)->m;
     if (cfg.use_surfel_correspondence) {
         uint64_t src = 0, epoch = 0, pos = 0;
         lo::ctx_map_source(ctx, &src, &epoch, &pos);
+        if (H.fit_ctx) H.resolve();                     // fits already handed to a context: collect them first
         if (src == reinterpret_cast<uint64_t>(m) && epoch == H.epoch && pos <= H.journal.size()) {
-            lo::OrderedMap<lo::Key3, lo::NoValue, lo::HashKey3> keys;      // the changed L1 keys, once each
-            for (size_t i = pos; i < H.journal.size(); ++i) keys.upsert(H.journal[i], nullptr);
+            // the changed L1 keys, once each; keys with a pending fit job are patched by k_surfel_fit after these
+            lo::OrderedMap<lo::Key3, lo::NoValue, lo::HashKey3> jobs;
+            for (const lo::Key3& k : H.job_key) jobs.upsert(k, nullptr);
+            lo::OrderedMap<lo::Key3, lo::NoValue, lo::HashKey3> keys;
+            for (size_t i = pos; i < H.journal.size(); ++i)
+                if (jobs.find(H.journal[i]) < 0) keys.upsert(H.journal[i], nullptr);
             const size_t cnt = keys.size();
             std::vector<int32_t> k(3 * std::max<size_t>(cnt, 1));
             std::vector<float> nn(3 * std::max<size_t>(cnt, 1)), cc(3 * std::max<size_t>(cnt, 1));
@@ -486,15 +554,25 @@ int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
                     cc[3 * i + a] = has ? H.l1.val_at(li).centroid[a] : 0.0f;
                 }
             }
-            const int rc = lo_map_patch_surfels(ctx, k.data(), nn.data(), cc.data(), present.data(), cnt);
+            int rc = lo_map_patch_surfels(ctx, k.data(), nn.data(), cc.data(), present.data(), cnt);
+            if (rc == LO_OK && !H.job_key.empty()) {
+                const size_t nj = H.job_key.size();
+                std::vector<int32_t> jk(3 * nj);
+                for (size_t j = 0; j < nj; ++j) { jk[3 * j] = H.job_key[j].x; jk[3 * j + 1] = H.job_key[j].y; jk[3 * j + 2] = H.job_key[j].z; }
+                uint64_t id = 0;
+                rc = lo::ctx_fit_surfels(ctx, jk.data(), H.job_off.data(), nj, H.job_cs.data(), H.job_cs.size() / 3,
+                                         H.planarity_thr, &id);
+                if (rc == LO_OK) { H.fit_ctx = ctx; H.fit_id = id; }
+            }
             if (rc == LO_OK) {
                 lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());
-                if (patched) *patched = static_cast<int>(cnt);
+                if (patched) *patched = static_cast<int>(cnt + H.job_key.size());
                 return LO_OK;
             }
             if (rc != LO_ERR_CAPACITY) return rc;           // capacity: the table is rebuilt below
         }
     }
+    H.resolve();                                         // a full upload needs the fitted surfels on the host
     const int rc = lo_map_set_from_voxelmap(ctx, m);
     if (rc == LO_OK && cfg.use_surfel_correspondence)
         lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());

@@ -280,6 +280,86 @@ class KittiLikeSequence:
         return pts.astype(np.float32)
 
 
+class KittiCitySequence(KittiLikeSequence):
+    """The same HDL-64E-like scanner driving a serpentine through a city grid: legs of `leg` m along parallel
+    streets `spacing` m apart, joined by 90 degree turns (radius 8 m) through cross streets, facades, parked cars,
+    poles and trees along every street.  Unlike the single meandering street of KittiLikeSequence, the 120 m
+    pruning radius then holds several streets at once, so the keyframed map reaches the surfel count of an urban
+    KITTI drive (~10^4 L1 surfels).  Benchmark data only."""
+
+    def __init__(self, seed: int = 7, n_frames: int = 900, leg: float = 110.0, spacing: float = 44.0):
+        self.seed = seed
+        self.n_frames = n_frames
+        rng = np.random.default_rng(seed + 500)
+        dt, r_turn = 1.0 / self.HZ, 8.0
+        t = np.arange(n_frames) * dt
+        speed = 6.0 + 1.0 * np.sin(2 * np.pi * t / 37.0)
+        s_frames = np.concatenate([[0.0], np.cumsum(speed[:-1] * dt)])
+        total = s_frames[-1] + 1.0
+        # path: straight leg, two quarter turns the same way, next leg back; alternate left / right
+        segs, length, k = [], 0.0, 0
+        while length < total:
+            turn = 1.0 if k % 2 == 0 else -1.0
+            for seg in ((leg, 0.0), (0.5 * np.pi * r_turn, turn / r_turn), (spacing - 2 * r_turn, 0.0),
+                        (0.5 * np.pi * r_turn, turn / r_turn)):
+                segs.append(seg)
+                length += seg[0]
+            k += 1
+        n_legs = k + 1
+        ds = 0.05
+        xs, ys, hs = [0.0], [0.0], [0.0]
+        for L, curv in segs:
+            for _ in range(int(round(L / ds))):
+                h = hs[-1] + curv * ds
+                hm = 0.5 * (hs[-1] + h)
+                xs.append(xs[-1] + ds * math.cos(hm))
+                ys.append(ys[-1] + ds * math.sin(hm))
+                hs.append(h)
+        sp = np.arange(len(xs)) * ds
+        x = np.interp(s_frames, sp, xs)
+        y = np.interp(s_frames, sp, ys)
+        heading = np.interp(s_frames, sp, hs)
+        self.poses = [se3(rot_z(heading[i]), [x[i], y[i], self.SENSOR_H]) for i in range(n_frames)]
+        # scene: along every horizontal street y = j * spacing, x in [-70, leg + 70], cross streets at the turns
+        boxes, cyls = [], []
+        cross = (-r_turn, leg + r_turn)
+        max_back = spacing / 2 - 1.0
+        for j in range(-1, n_legs + 1):
+            y0 = j * spacing
+            for side in (-1.0, 1.0):
+                xa = -70.0
+                while xa < leg + 70.0:
+                    L = rng.uniform(8.0, 22.0)
+                    if rng.random() < 0.12 or any(xa - 12.0 < c < xa + L + 12.0 for c in cross):
+                        xa += L + rng.uniform(2.0, 8.0)
+                        continue
+                    off = rng.uniform(9.0, 12.0)
+                    D = rng.uniform(6.0, max_back - off)
+                    H = rng.uniform(4.0, 20.0)
+                    boxes.append([xa + L / 2, y0 + side * (off + D / 2), H / 2, L / 2, D / 2, H / 2, rng.normal(0.0, 0.04)])
+                    xa += L + rng.uniform(1.0, 6.0)
+                xa = -70.0 + rng.uniform(0.0, 10.0)
+                while xa < leg + 70.0:                # parked cars, poles, trees
+                    u = rng.random()
+                    if any(abs(xa - c) < 10.0 for c in cross):
+                        pass
+                    elif u < 0.45:
+                        boxes.append([xa, y0 + side * rng.uniform(3.6, 4.4), 0.75, 2.25, 0.9, 0.75, rng.normal(0.0, 0.05)])
+                    elif u < 0.65:
+                        cyls.append([xa, y0 + side * rng.uniform(5.0, 7.0), rng.uniform(0.12, 0.3), 0.0, rng.uniform(4, 9)])
+                    else:
+                        cx, cy = xa, y0 + side * rng.uniform(5.5, 7.5)
+                        cyls.append([cx, cy, rng.uniform(0.15, 0.4), 0.0, rng.uniform(2.0, 4.0)])
+                        cr = rng.uniform(1.0, 2.5)
+                        boxes.append([cx, cy, rng.uniform(3.5, 5.5), cr, cr, rng.uniform(0.8, 1.8), rng.uniform(0, np.pi)])
+                    xa += rng.uniform(5.0, 14.0)
+        self.scene = Scene(np.array(boxes, dtype=np.float64), np.array(cyls, dtype=np.float64))
+        elev = np.deg2rad(np.linspace(-24.9, 2.0, 64))
+        az = np.linspace(0.0, 2 * np.pi, 1800, endpoint=False)
+        E, A = np.meshgrid(elev, az, indexing="ij")
+        self.dirs = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
+
+
 # ----------------------------------------------------------------------------------------------------
 # MID360-like scan (C3)
 # ----------------------------------------------------------------------------------------------------

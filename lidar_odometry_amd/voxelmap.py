@@ -56,6 +56,13 @@ class VoxelMap:
             raise RuntimeError(f"lo_voxelmap_update failed ({rc})")
         self.revision += 1
 
+    def set_device_fit(self, enable: bool = True):
+        """Defer the surfel refits of update() to the next lo_map_sync_voxelmap of a context mirroring this map
+        (k_surfel_fit on the device); bit-identical to host fits (include/lo_map.h)."""
+        rc = lib().lo_voxelmap_set_device_fit(self._h, int(bool(enable)))
+        if rc < 0:
+            raise RuntimeError(f"lo_voxelmap_set_device_fit failed ({rc})")
+
     def apply_transform(self, T):
         """VoxelMap::ApplyTransformAndRehash (VoxelMap.cpp:264-302): T = row-major 3x4 (or 4x4) correction."""
         t = np.ascontiguousarray(np.asarray(T, np.float32)[:3, :] if np.asarray(T).ndim == 2 else

@@ -50,6 +50,28 @@ def kitti_case(frame: int, seed: int = 42, last_kf: int = 20, n_frames: int = 40
 
 
 @functools.lru_cache(maxsize=None)
+def city_map(n_map: int = 300, device: str | None = None):
+    """Oracle VoxelMap of the city-grid sequence (bench.py's KITTI map, shorter): keyframes 0, 2, ..., n_map;
+    device: raycast with torch there (GPU tests; the numpy raycast of a few hundred frames takes minutes)."""
+    seq = synth.KittiCitySequence(n_frames=n_map + 42)
+    m = oracle.VoxelMap(0.5, 3, 0.1, True)
+    for k in range(0, n_map + 1, 2):
+        pts = oracle.voxel_filter(seq.scan(k, device=device), 0.5, 8)
+        T = seq.poses[k]
+        m.update(synth.transform(T, pts), T[:3, 3], 120.0, True)
+    return seq, m
+
+
+def city_case(frame: int, n_map: int = 300, device: str | None = None, seed: int = 42):
+    """(map, filtered scan points, perturbed initial pose 12, ground-truth pose 12) on the city-grid map."""
+    seq, m = city_map(n_map, device)
+    pts = oracle.voxel_filter(seq.scan(frame, device=device), 0.5, 8)
+    rng = np.random.default_rng(seed + frame)
+    Ti = synth.perturb(seq.poses[frame], rng, 0.05, 0.01)
+    return m, pts, pose12(Ti), pose12(seq.poses[frame])
+
+
+@functools.lru_cache(maxsize=None)
 def mid360_case(frame: int = 3):
     """MID360-like (C3): voxel 0.4 (L1 = fp32(0.4f*3)), stride 4, surfel correspondence forced on."""
     sc = synth.mid360_scene()

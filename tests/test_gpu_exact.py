@@ -79,6 +79,16 @@ def test_exact_all_iterations_bitwise(max_iters, pko):
         o.close()
 
 
+@pytest.mark.parametrize("frame", [281, 295, 313, 331])
+def test_exact_city_map_bitwise(exact, frame):
+    """The city-grid map (bench.py's KITTI workload, here after 300 frames: ~6k surfels, several streets in the
+    120 m radius), scans between and beyond its keyframes, including the turns."""
+    m, pts, Ti, _ = _data.city_case(frame, device="cuda")
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    _bitwise(exact, m, pts, Ti)
+
+
 def test_exact_mid360_bitwise():
     from lidar_odometry_amd import IterativeClosestPointOptimizer, MapGeometry
     m, pts, Ti, _ = _data.mid360_case()

@@ -123,3 +123,37 @@ def test_sync_after_apply_transform_uploads_the_rehashed_map():
     finally:
         A.close()
         B.close()
+
+
+def test_device_fit_matches_host_fit():
+    """lo_voxelmap_set_device_fit: the touched voxels' refits run on the device inside the sync (k_surfel_fit patches
+    the table) and come back to the host map.  Against a map fitting on the host and fully re-uploaded each
+    keyframe: identical host maps (surfel keys / normals / centroids / planarity bitwise, L0 and L1 counts) and
+    identical lookups, across keyframes that insert, refit, lose and prune surfels."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
+    va, vb = VoxelMap(0.5, 3, 0.1, True), VoxelMap(0.5, 3, 0.1, True)
+    va.set_device_fit(True)
+    A, B = _ctx(), _ctx()
+    try:
+        patched = []
+        for k in range(0, 41, 2):
+            T = seq.poses[k]
+            w = synth.transform(T, voxel_filter(seq.scan(k), 0.5, 8))
+            va.update(w, T[:3, 3], 60.0, True)
+            vb.update(w, T[:3, 3], 60.0, True)
+            patched.append(_sync(A, va))
+            _full(B, vb)
+            if k % 8 == 0:
+                f = k + 1
+                scan = voxel_filter(seq.scan(f), 0.5, 8)
+                _same_lookups(A, B, scan, [seq.poses[f][:3].astype(np.float32).reshape(12)])
+            sa, sb = va.surfels(), vb.surfels()
+            for x, y in zip(sa, sb):
+                np.testing.assert_array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
+            assert (va.l0_count(), va.l1_count()) == (vb.l0_count(), vb.l1_count())
+            assert A.surfel_count() == B.surfel_count() == vb.surfel_count()
+        assert sum(p > 0 for p in patched[1:]) >= len(patched) // 2, patched
+    finally:
+        A.close()
+        B.close()

@@ -167,6 +167,19 @@ def test_optimize_kitti_like_per_iteration(icp, frame):
     _compare_optimize(icp, m, pts, Ti)
 
 
+@pytest.mark.parametrize("frame", [281, 313])
+def test_optimize_city_map_per_iteration(icp, frame):
+    """bench.py's KITTI map kind (city grid, several streets inside the 120 m radius; here after 300 frames)."""
+    m, pts, Ti, _ = _data.city_case(frame, device="cuda")
+    _load_map(icp, m)
+    n_o, v_o, r_o = oracle.find_correspondences(m, pts, Ti)
+    n_g, v_g, r_g = icp.find_correspondences(pts, Ti)
+    assert n_g == n_o
+    np.testing.assert_array_equal(v_g, v_o)
+    np.testing.assert_array_equal(r_g.view(np.uint64), r_o.view(np.uint64))
+    _compare_optimize(icp, m, pts, Ti)
+
+
 @pytest.mark.parametrize("max_iters,tol,pko", [(1, 0.005, True), (2, 1e-9, True), (6, 1e-9, True), (6, 1e-9, False)])
 def test_optimize_launch_shapes(max_iters, tol, pko):
     """Every GN-loop launch shape of a small scan against the oracle with the same config.  With PKO: the first

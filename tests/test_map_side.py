@@ -138,3 +138,20 @@ def test_apply_transform_and_rehash_bitwise(angle, shift):
         a.update(w, seq.poses[k][:3, 3], 120.0, True)
         b.update(w, seq.poses[k][:3, 3], 120.0, True)
         _compare_maps(a, b)
+
+
+def test_deferred_fit_resolved_on_host_is_bitwise():
+    """lo_voxelmap_set_device_fit without a syncing context: the recorded refits are fitted on the host when the
+    map is next read, and the map equals the oracle's at every keyframe (same L0 / L1 orders after the deferred
+    planarity erases, same surfels)."""
+    seq = _data.kitti_seq()
+    a = VoxelMap(0.5, 3, 0.1, True)
+    a.set_device_fit(True)
+    b = oracle.VoxelMap(0.5, 3, 0.1, True)
+    for k in range(0, 21, 2):
+        w = synth.transform(seq.poses[k], voxel_filter(_data.kitti_scan(k), 0.5, 8))
+        a.update(w, seq.poses[k][:3, 3], 60.0, True)          # 60 m: pruning runs too
+        b.update(w, seq.poses[k][:3, 3], 60.0, True)
+        if k % 4 == 0:
+            _compare_maps(a, b)
+    _compare_maps(a, b)
