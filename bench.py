@@ -240,6 +240,67 @@ def read_pmc_traffic(workload_key: str):
         return None
 
 
+def pmc_child(path: str):
+    """--pmc-child: the isolated k_correspond launches of a case the parent bench wrote (scan, pose, scale/alpha,
+    surfel map), nothing else -- the program rocprofv3 --pmc runs for live_pmc."""
+    import torch
+    from lidar_odometry_amd import lib
+    from lidar_odometry_amd.icp import IterativeClosestPointOptimizer, MapGeometry
+    z = np.load(path)
+    pts = np.ascontiguousarray(z["pts"], np.float32)
+    icp = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=float(z["voxel"])), max_points=len(pts))
+    icp.set_surfels(z["keys"], z["normals"], z["centroids"])
+    d = torch.from_numpy(pts).cuda()
+    T = np.ascontiguousarray(z["T"], np.float32)
+    ms = C.c_float(0.0)
+    rc = lib().lo_bench_kernel(icp.ctx, C.c_void_p(d.data_ptr()), len(pts), T.ctypes.data_as(C.POINTER(C.c_float)),
+                               C.c_double(float(z["scale"])), C.c_double(float(z["alpha"])), 0, int(z["reps"]),
+                               C.byref(ms))
+    torch.cuda.synchronize()
+    icp.close()
+    sys.exit(0 if rc == 0 else 1)
+
+
+def live_pmc(case: dict, reps: int = 200):
+    """HBM traffic of one k_correspond launch, measured in this run: two rocprofv3 passes (--pmc FETCH_SIZE, then
+    --pmc WRITE_SIZE, each counter in a run of its own) over `reps` isolated launches of the bench's largest scan,
+    in child processes (this process has initialised the GPU).  MI355X_MICROARCH.md §HBM: the counters are KiB;
+    FETCH_SIZE counts half of a wide coalesced stream's bytes on gfx950, so the read side is taken x2 (the raw
+    values are kept).  Returns None when rocprofv3 is absent or a pass fails."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from pmc_summary import per_launch
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="lo_pmc_") as tmp:
+        np.savez(os.path.join(tmp, "case.npz"), reps=reps, **case)
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", counter, "--kernel-trace",
+                   "--kernel-include-regex", "k_correspond", "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", os.path.join(tmp, "case.npz")]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, cwd=ROOT)
+            if r.returncode != 0:
+                log(f"live PMC pass {counter} failed (rc {r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
+                return None
+            try:
+                iso, n_iso, _, _ = per_launch(d, counter, "k_correspond", min_run=20)
+            except SystemExit as e:
+                log(f"live PMC pass {counter}: {e}")
+                return None
+            out[counter] = (iso, n_iso)
+    fetch_kib, nf = out["FETCH_SIZE"]
+    write_kib, nw = out["WRITE_SIZE"]
+    return {"hbm_bytes_per_launch": 2.0 * fetch_kib * 1024.0 + write_kib * 1024.0,
+            "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib, "launches": [nf, nw],
+            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md §HBM); memory-side counters, Infinity-Cache "
+                          "hits included"}
+
+
 def read_pko_latency():
     """The dominant kernel's latency roofline (k_pko_t: a strictly sequential fp64 EM chain, neither HBM- nor
     MFMA-bound): measured cycles per EM iteration against the floor from measured instruction costs, from the
@@ -507,6 +568,10 @@ def main():
     ap.add_argument("--sequences", type=int, default=8,
                     help="extra measurement: independent sequences sharing this GPU, one context + HIP stream each "
                          "(0 = skip); reported as multi_sequence, never as value")
+    ap.add_argument("--pmc", default="live", choices=["live", "off"],
+                    help="HBM traffic of the roofline kernel: live rocprofv3 --pmc passes in child processes (rank 0, "
+                         "1 GPU), or off (the committed profiles/pmc_traffic.json figure)")
+    ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--batch", type=str, default="64,256,1024,2048,4096",
                     help="extra measurement: comma list of B for the scan-parallel batch (lo_batch_*: B independent "
                          "contexts advanced in lockstep, one launch per kernel per GN iteration); '' = skip; "
@@ -514,6 +579,8 @@ def main():
     args = ap.parse_args()
     global ORDER
     ORDER = args.order
+    if args.pmc_child:
+        pmc_child(args.pmc_child)
 
     if args.gpus < 1:
         sys.exit(f"--gpus must be >= 1 (got {args.gpus})")
@@ -708,6 +775,16 @@ def main():
     ws_bytes = float(n0 * (12 + 4 + 32))
     achieved = alg_bytes / t_corr / 1e9
     traffic = read_pmc_traffic(args.config + ("_random" if args.config == "patch1m" and ORDER == "random" else ""))
+    traffic_source = "profiles/pmc_traffic.json (separate rocprofv3 --pmc passes, earlier run)"
+    traffic_live = None
+    if not kd and rank == 0 and world == 1 and args.pmc == "live":
+        keys, normals, cents, _ = wl["vm"].surfels()
+        traffic_live = live_pmc({"pts": wl["scans"][i0], "T": inits[i0], "scale": scale0, "alpha": alpha0,
+                                 "keys": keys, "normals": normals, "centroids": cents, "voxel": wl["voxel"]})
+        if traffic_live is not None:
+            traffic = traffic_live["hbm_bytes_per_launch"]
+            traffic_source = ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this run (child processes, "
+                              "200 isolated launches of the same scan and map)")
     # where a step's device time goes: isolated kernel time x launches per scan (working launches only)
     gi = float(np.mean(iters))
     # small scans with PKO (<= 64 accumulate blocks): the accumulate runs inside the k_pko launch (one candidate
@@ -881,7 +958,7 @@ def main():
                            "path": "lo_icp_optimize on host buffers (H2D points, D2H pose+logs, sync per scan)"},
         "roofline": {"kernel": corr_kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": "profiles/pmc_traffic.json (separate rocprofv3 --pmc passes)",
+                     "traffic": traffic, "traffic_source": traffic_source, "traffic_live": traffic_live,
                      "alg_bytes_per_launch": alg_bytes, "points_per_launch": int(n0), "valid_fraction": v,
                      "timing": "isolated: back-to-back launches of the largest scan (lo_bench_kernel, HIP events)",
                      "kernel_us": kern_us[stage0],

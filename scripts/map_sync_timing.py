@@ -1,7 +1,9 @@
 """Host cost of a keyframe's map update and of bringing the device table up to date: full re-upload
 (lo_map_set_from_voxelmap: host re-hash of every surfel + blocking copy of the whole table) against the in-place
 patch (lo_map_sync_voxelmap: the L1 voxels the update changed, async).  KITTI-like sequence, keyframe every 2 frames,
-pruning radius 120 m; times per keyframe over the second half (the map at its steady size)."""
+pruning radius 120 m; times per keyframe over the second half (the map at its steady size).  Third column: the
+same map with device surfel fits (lo_voxelmap_set_device_fit: update without fits + patch + k_surfel_fit, the
+results applied at the next update)."""
 import ctypes as C
 import os
 import sys
@@ -20,8 +22,11 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 dev = "cuda:0" if torch.cuda.is_available() else None
 seq = synth.KittiLikeSequence(seed=7, n_frames=n + 2)
 vm = VoxelMap(0.5, 3, 0.1, True)
+vd = VoxelMap(0.5, 3, 0.1, True)
+vd.set_device_fit(True)
 A, B = IterativeClosestPointOptimizer(max_points=1 << 16), IterativeClosestPointOptimizer(max_points=1 << 16)
-t_upd, t_full, t_patch, kinds = [], [], [], []
+D = IterativeClosestPointOptimizer(max_points=1 << 16)
+t_upd, t_full, t_patch, kinds, t_dev = [], [], [], [], []
 patched = C.c_int(0)
 for k in range(0, n + 1, 2):
     T = seq.poses[k]
@@ -34,10 +39,18 @@ for k in range(0, n + 1, 2):
     assert lib().lo_map_sync_voxelmap(A.ctx, vm.handle, C.byref(patched)) == 0
     lib().lo_sync(A.ctx)
     t3 = time.perf_counter()
+    t4 = time.perf_counter()
+    vd.update(w, T[:3, 3], 120.0, True)
+    assert lib().lo_map_sync_voxelmap(D.ctx, vd.handle, C.byref(patched)) == 0
+    lib().lo_sync(D.ctx)
+    t5 = time.perf_counter()
     t_upd.append(t1 - t0); t_full.append(t2 - t1); t_patch.append(t3 - t2); kinds.append(patched.value)
+    t_dev.append(t5 - t4)
 h = len(t_upd) // 2
 ms = lambda v: 1e3 * float(np.mean(v[h:]))  # noqa: E731
 print(f"keyframes {len(t_upd)}, surfels {vm.surfel_count()}, L0 {vm.l0_count()}: per keyframe (second half) "
       f"host map update {ms(t_upd):.3f} ms, full upload {ms(t_full):.3f} ms, patch {ms(t_patch):.3f} ms "
       f"(incl. stream sync); patched voxels per keyframe {np.mean([p for p in kinds[h:] if p >= 0]):.0f}, "
-      f"full re-uploads in the second half {sum(p < 0 for p in kinds[h:])}")
+      f"full re-uploads in the second half {sum(p < 0 for p in kinds[h:])}; with device fits: update + sync "
+      f"{ms(t_dev):.3f} ms (host fits: {ms(t_upd) + ms(t_patch):.3f} ms)")
+assert vd.surfel_count() == vm.surfel_count()
