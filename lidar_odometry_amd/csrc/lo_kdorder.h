@@ -40,11 +40,15 @@ public:
         if (m_ == 0) return;
         acc_.resize(m_);
         for (size_t i = 0; i < m_; ++i) acc_[i] = static_cast<uint32_t>(i);
+        for (int d = 0; d < 3; ++d) {                       // coordinates by vAcc_ position, permuted alongside it
+            co_[d].resize(m_);
+            for (size_t i = 0; i < m_; ++i) co_[d][i] = p_[3 * i + d];
+        }
         Box bb;                                             // computeBoundingBox (:1845-1880)
-        for (int d = 0; d < 3; ++d) bb.lo[d] = bb.hi[d] = at(acc_[0], d);
+        for (int d = 0; d < 3; ++d) bb.lo[d] = bb.hi[d] = at(0, d);
         for (size_t k = 1; k < m_; ++k)
             for (int d = 0; d < 3; ++d) {
-                const float v = at(acc_[k], d);
+                const float v = at(k, d);
                 if (v < bb.lo[d]) bb.lo[d] = v;
                 if (v > bb.hi[d]) bb.hi[d] = v;
             }
@@ -58,19 +62,24 @@ private:
     const float* p_;
     size_t m_;
     std::vector<uint32_t> acc_;
+    std::vector<float> co_[3];                             // co_[d][k] = coordinate d of point acc_[k]
     std::vector<KdNode>* nodes_ = nullptr;
 
-    float at(uint32_t i, int d) const { return p_[3 * static_cast<size_t>(i) + d]; }
+    float at(size_t k, int d) const { return co_[d][k]; }   // by position in acc_
+    void swap_at(size_t a, size_t b) {
+        std::swap(acc_[a], acc_[b]);
+        for (int d = 0; d < 3; ++d) std::swap(co_[d][a], co_[d][b]);
+    }
 
     int divide(size_t left, size_t right, Box& bb) {
         std::vector<KdNode>& N = *nodes_;
         const int id = static_cast<int>(N.size());
         N.push_back(KdNode{-1, -1, 0, 0, 0.0f, 0.0f});
         if (right - left <= 10) {                           // leaf: its points' extent
-            for (int d = 0; d < 3; ++d) bb.lo[d] = bb.hi[d] = at(acc_[left], d);
+            for (int d = 0; d < 3; ++d) bb.lo[d] = bb.hi[d] = at(left, d);
             for (size_t k = left + 1; k < right; ++k)
                 for (int d = 0; d < 3; ++d) {
-                    const float v = at(acc_[k], d);
+                    const float v = at(k, d);
                     if (bb.lo[d] > v) bb.lo[d] = v;
                     if (bb.hi[d] < v) bb.hi[d] = v;
                 }
@@ -109,11 +118,12 @@ private:
         f = 0;
         for (int d = 0; d < 3; ++d) {
             if (!(bb.hi[d] - bb.lo[d] >= (1 - eps) * max_span)) continue;
-            float mn = at(acc_[ind], d), mx = mn;
+            const float* c = co_[d].data() + ind;
+            float mn = c[0], mx = mn;
             for (size_t k = 1; k < count; ++k) {
-                const float v = at(acc_[ind + k], d);
-                if (v < mn) mn = v;
-                if (v > mx) mx = v;
+                const float v = c[k];
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
             }
             if (mx - mn > best_spread) { f = d; best_spread = mx - mn; mn_f = mn; mx_f = mx; }
         }
@@ -126,13 +136,14 @@ private:
 
     // planeSplit: [< cut | == cut | > cut] by two in-place swap passes (the swap pattern fixes vAcc_ order)
     void partition(size_t ind, size_t count, int f, float cut, size_t& lim1, size_t& lim2) {
-        auto v = [&](size_t k) { return at(acc_[ind + k], f); };
+        const float* c = co_[f].data() + ind;
+        auto v = [&](size_t k) { return c[k]; };
         size_t l = 0, r = count - 1;
         for (;;) {
             while (l <= r && v(l) < cut) ++l;
             while (r && l <= r && v(r) >= cut) --r;
             if (l > r || !r) break;
-            std::swap(acc_[ind + l], acc_[ind + r]);
+            swap_at(ind + l, ind + r);
             ++l;
             --r;
         }
@@ -142,7 +153,7 @@ private:
             while (l <= r && v(l) <= cut) ++l;
             while (r && l <= r && v(r) > cut) --r;
             if (l > r || !r) break;
-            std::swap(acc_[ind + l], acc_[ind + r]);
+            swap_at(ind + l, ind + r);
             ++l;
             --r;
         }

@@ -38,6 +38,7 @@ struct Top5 {
     int id[5];      // original centroid index (tie-break)
     int pos[5];     // position in kd_pts
     int n;
+    int tie;        // fast order only: two different points compared at equal distance (the result may differ)
 };
 
 // The query and the reference tree's order, for ties.
@@ -67,29 +68,41 @@ __device__ __noinline__ bool kd_visit_before(const KnnQ& Q, int a, int b) {
     return pa < pb;
 }
 
-__device__ __forceinline__ bool lex_less(const KnnQ& Q, float da, int ia, float db, int ib) {
-    return da < db || (da == db && ia != ib && kd_visit_before(Q, ia, ib));
+// Two orders over (distance, point).  EX: nanoflann's (distance, visit order) -- the reference's result.  Fast:
+// (distance, index), which differs only between points at EQUAL distance, and every such comparison raises
+// t.tie; a query that raised it is answered again in the exact order (k_knn hands it to k_knn_brute, which reruns
+// it with EX), so the visit-order walk stays out of the hot loops.
+template <bool EX>
+__device__ __forceinline__ bool lex_less(const KnnQ& Q, Top5& t, float da, int ia, float db, int ib) {
+    if constexpr (EX) {
+        return da < db || (da == db && ia != ib && kd_visit_before(Q, ia, ib));
+    } else {
+        t.tie |= (da == db && ia != ib) ? 1 : 0;
+        return da < db || (da == db && ia < ib);
+    }
 }
 
 __device__ __forceinline__ void top5_init(Top5& t) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) { t.d[k] = __builtin_inff(); t.id[k] = 0x7fffffff; t.pos[k] = -1; }
     t.n = 0;
+    t.tie = 0;
 }
 
 // KNNResultSet::addPoint behind searchLevel's `dist < worstDist` (worstDist = FLT_MAX until 5 are held),
 // with (dist, visit order) order; unrolled compare-swaps keep the list in VGPRs.
+template <bool EX>
 __device__ __forceinline__ void top5_insert(const KnnQ& Q, Top5& t, float d, int id, int pos) {
     if (t.n < 5) {
         if (!(d < FLT_MAX)) return;
         ++t.n;
-    } else if (!lex_less(Q, d, id, t.d[4], t.id[4])) {
+    } else if (!lex_less<EX>(Q, t, d, id, t.d[4], t.id[4])) {
         return;
     }
     t.d[4] = d; t.id[4] = id; t.pos[4] = pos;
 #pragma unroll
     for (int k = 4; k > 0; --k) {
-        if (lex_less(Q, t.d[k], t.id[k], t.d[k - 1], t.id[k - 1])) {
+        if (lex_less<EX>(Q, t, t.d[k], t.id[k], t.d[k - 1], t.id[k - 1])) {
             const float fd = t.d[k]; t.d[k] = t.d[k - 1]; t.d[k - 1] = fd;
             const int fi = t.id[k]; t.id[k] = t.id[k - 1]; t.id[k - 1] = fi;
             const int fp = t.pos[k]; t.pos[k] = t.pos[k - 1]; t.pos[k - 1] = fp;
@@ -105,7 +118,7 @@ __device__ __forceinline__ float l2sq(float qx, float qy, float qz, const float4
 // Merge of disjoint top-5 lists across the kKnnGroup = 16 lanes of a query: a hypercube over the 16-lane DPP row
 // (quad_perm xor 1, quad_perm xor 2, row_half_mirror i <-> 7-i, row_mirror i <-> 15-i) -- VALU moves, no LDS
 // round trips -- after which every lane of the row holds the (dist, index)-smallest five of the group's union.
-template <int CTRL>
+template <int CTRL, bool EX>
 __device__ __forceinline__ void top5_merge_dpp(const KnnQ& Q, Top5& t) {
     Top5 u;
 #pragma unroll
@@ -115,18 +128,20 @@ __device__ __forceinline__ void top5_merge_dpp(const KnnQ& Q, Top5& t) {
         u.pos[k] = __builtin_amdgcn_mov_dpp(t.pos[k], CTRL, 0xf, 0xf, false);
     }
     u.n = __builtin_amdgcn_mov_dpp(t.n, CTRL, 0xf, 0xf, false);
+    t.tie |= __builtin_amdgcn_mov_dpp(t.tie, CTRL, 0xf, 0xf, false);
 #pragma unroll
     for (int k = 0; k < 5; ++k)
-        if (k < u.n) top5_insert(Q, t, u.d[k], u.id[k], u.pos[k]);
+        if (k < u.n) top5_insert<EX>(Q, t, u.d[k], u.id[k], u.pos[k]);
 }
 
+template <bool EX>
 __device__ __forceinline__ Top5 group_merge(const KnnQ& Q, const Top5& own) {
     static_assert(kKnnGroup == 16, "the DPP hypercube spans one 16-lane row");
     Top5 t = own;
-    top5_merge_dpp<0xB1>(Q, t);     // quad_perm [1,0,3,2]
-    top5_merge_dpp<0x4E>(Q, t);     // quad_perm [2,3,0,1]
-    top5_merge_dpp<0x141>(Q, t);    // row_half_mirror
-    top5_merge_dpp<0x140>(Q, t);    // row_mirror
+    top5_merge_dpp<0xB1, EX>(Q, t);     // quad_perm [1,0,3,2]
+    top5_merge_dpp<0x4E, EX>(Q, t);     // quad_perm [2,3,0,1]
+    top5_merge_dpp<0x141, EX>(Q, t);    // row_half_mirror
+    top5_merge_dpp<0x140, EX>(Q, t);    // row_mirror
     return t;
 }
 
@@ -142,7 +157,7 @@ __device__ __forceinline__ void scan_range8(const KParams& P, const KnnQ& Q, uin
         for (int u = 0; u < 8; ++u) v[u] = (p + u < e) ? P.kd_pts[p + u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (p + u < e) top5_insert(Q, t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
+            if (p + u < e) top5_insert<false>(Q, t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
     }
 }
 
@@ -201,7 +216,7 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
 #pragma unroll
             for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, Q, rs[j], re[j], qx, qy, qz, own);
         }
-        grp = group_merge(Q, own);
+        grp = group_merge<false>(Q, own);
         // every unscanned centroid lies outside the cube of cells [c - r, c + r]
         bool all = true;
         double b = DBL_MAX;
@@ -220,7 +235,7 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
         }
     }
     if (g != 0) return;
-    if (!done) {
+    if (!done || grp.tie) {                                   // not certified, or an equal-distance comparison
         out[0] = -2;
         P.kd_unres[atomicAdd(&P.st->kd_unres_n, 1u)] = i;
         return;
@@ -277,6 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
 // ====================================================================================================
 constexpr int kBruteThreads = 1024;
 
+template <bool EX>
 __device__ __forceinline__ void top5_merge_xor(const KnnQ& Q, Top5& t, int o) {
     Top5 u;
 #pragma unroll
@@ -286,9 +302,56 @@ __device__ __forceinline__ void top5_merge_xor(const KnnQ& Q, Top5& t, int o) {
         u.pos[k] = __shfl_xor(t.pos[k], o, 64);
     }
     u.n = __shfl_xor(t.n, o, 64);
+    t.tie |= __shfl_xor(t.tie, o, 64);
 #pragma unroll
     for (int k = 0; k < 5; ++k)
-        if (k < u.n) top5_insert(Q, t, u.d[k], u.id[k], u.pos[k]);
+        if (k < u.n) top5_insert<EX>(Q, t, u.d[k], u.id[k], u.pos[k]);
+}
+
+// One query over the whole map by a 1024-thread workgroup: every lane scans a strided share with 8 loads in flight,
+// then the wave / workgroup merges; wave 0 lane 0 returns the five (and, fast order, whether any tie was seen).
+template <bool EX>
+__device__ __forceinline__ Top5 brute_query(const KParams& P, const KnnQ& Q, float (&s_d)[16][5], int (&s_id)[16][5],
+                                            int (&s_pos)[16][5], int (&s_n)[16], int (&s_tie)[16]) {
+    constexpr int kBT = 1024;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const float qx = Q.q[0], qy = Q.q[1], qz = Q.q[2];
+    Top5 t;
+    top5_init(t);
+    for (int p0 = tid; p0 < P.kd_m; p0 += 8 * kBT) {           // 8 loads in flight per lane
+        float4 v[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const int p = p0 + w * kBT;
+            v[w] = p < P.kd_m ? P.kd_pts[p] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const int p = p0 + w * kBT;
+            if (p < P.kd_m) top5_insert<EX>(Q, t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
+        }
+    }
+    t = group_merge<EX>(Q, t);                             // 16-lane rows
+    top5_merge_xor<EX>(Q, t, 16);
+    top5_merge_xor<EX>(Q, t, 32);                          // the wave's five
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { s_d[wid][k] = t.d[k]; s_id[wid][k] = t.id[k]; s_pos[wid][k] = t.pos[k]; }
+        s_n[wid] = t.n;
+        s_tie[wid] = t.tie;
+    }
+    __syncthreads();
+    Top5 a;
+    top5_init(a);
+    if (wid == 0 && lane < 16) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { a.d[k] = s_d[lane][k]; a.id[k] = s_id[lane][k]; a.pos[k] = s_pos[lane][k]; }
+        a.n = s_n[lane];
+        a.tie = s_tie[lane];
+    }
+    if (wid == 0) a = group_merge<EX>(Q, a);               // lanes 16-63 merge empty lists (discarded)
+    __syncthreads();
+    return a;
 }
 
 __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
@@ -301,7 +364,9 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     __shared__ int s_id[kW][5];
     __shared__ int s_pos[kW][5];
     __shared__ int s_n[kW];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ int s_tie[kW];
+    __shared__ int s_redo;
+    const int tid = threadIdx.x;
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
@@ -310,43 +375,17 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         float qx, qy, qz;
         transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
         const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
-        Top5 t;
-        top5_init(t);
-        for (int p0 = tid; p0 < P.kd_m; p0 += 8 * kBruteThreads) {           // 8 loads in flight per lane
-            float4 v[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const int p = p0 + w * kBruteThreads;
-                v[w] = p < P.kd_m ? P.kd_pts[p] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const int p = p0 + w * kBruteThreads;
-                if (p < P.kd_m) top5_insert(Q, t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
-            }
-        }
-        t = group_merge(Q, t);                             // 16-lane rows
-        top5_merge_xor(Q, t, 16);
-        top5_merge_xor(Q, t, 32);                          // the wave's five
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) { s_d[wid][k] = t.d[k]; s_id[wid][k] = t.id[k]; s_pos[wid][k] = t.pos[k]; }
-            s_n[wid] = t.n;
-        }
+        Top5 a = brute_query<false>(P, Q, s_d, s_id, s_pos, s_n, s_tie);
+        if (tid == 0) s_redo = a.tie;
         __syncthreads();
-        if (wid == 0 && lane < 16) {
-            Top5 a;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) { a.d[k] = s_d[lane][k]; a.id[k] = s_id[lane][k]; a.pos[k] = s_pos[lane][k]; }
-            a.n = s_n[lane];
-            a = group_merge(Q, a);
-            if (lane == 0) {
-                int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
-                if (a.n < 5) out[0] = -1;
-                else for (int k = 0; k < 5; ++k) out[k] = a.pos[k];
-            }
-        }
+        const bool redo = s_redo != 0;
         __syncthreads();
+        if (redo) a = brute_query<true>(P, Q, s_d, s_id, s_pos, s_n, s_tie);   // equal distances: nanoflann's order
+        if (tid == 0) {
+            int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+            if (a.n < 5) out[0] = -1;
+            else for (int k = 0; k < 5; ++k) out[k] = a.pos[k];
+        }
     }
 }
 
