@@ -16,14 +16,18 @@ all=(
   "bench_kd:600:python bench.py --config kitti_kdtree --cpu-budget 10 > gpurun_out/bench_kitti_kdtree.json"
   "bench_mid360:600:python bench.py --config mid360 --cpu-budget 10 > gpurun_out/bench_mid360.json"
   "stats_kd:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kd -o run --output-format csv -- python bench.py --config kitti_kdtree --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
-  "stats_kitti:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
+  "stats_kitti:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off --batch 1024 --sequences 0"
   "stats_e2e:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_e2e -o run --output-format csv -- python bench.py --config kitti_e2e --steps 240 --no-cpu-baseline --pmc off"
+  "stats_loop:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_loop -o run --output-format csv -- python bench.py --config kitti_loop --steps 100 --warmup 12 --no-cpu-baseline --pmc off"
   "stats_1m:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
   "pmcf_kitti:600:rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
   "pmcw_kitti:600:rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
   "pmcf_1m:600:rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
   "pmcw_1m:600:rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
 )
+# post: summaries of the traces / PMC passes into gpurun_out/summ/, then the raw CSVs are deleted (gpurun merges
+# at most 64 MiB of gpurun_out/ back)
+all+=("post:300:scripts/profile_post.sh")
 steps=()
 for spec in "${all[@]}"; do
     if [ $# -eq 0 ]; then steps+=("$spec"); continue; fi
