@@ -127,6 +127,8 @@ struct KParams {
     double* acc_part;         // speculative normal equations: [NA + 1 candidates][kFuseMaxBlocks][kNE] partials
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
+    double* res_out;          // nullable: per-point fp64 residual of the accepted correspondences (k_correspond /
+                              //   k_solve_correspond), read back by the PKO sample instead of recomputing it
     float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
@@ -168,9 +170,10 @@ struct ScanBufs {
     double* js;
     DevState* st;
     const float* pose_in;             // the iteration's pose (nullable: st->pose)
+    const double* res;                // the correspondences' residuals (nullable: recomputed from slot + pose)
 };
 __device__ __forceinline__ ScanBufs own_bufs(const KParams& P) {
-    return ScanBufs{P.slot, P.wmask, P.blk_cnt, P.js, P.st, nullptr};
+    return ScanBufs{P.slot, P.wmask, P.blk_cnt, P.js, P.st, nullptr, P.res_out};
 }
 
 // ---------------------------------------------------------------------------------------------------

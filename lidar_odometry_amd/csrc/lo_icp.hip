@@ -93,6 +93,7 @@ struct lo_ctx {
     // scan buffers
     float* d_pts = nullptr;
     int32_t* d_slot = nullptr;
+    double* d_res_pko = nullptr;    // per-point residual of the accepted correspondences (the PKO sample reads it)
     uint64_t* d_wmask = nullptr;
     int32_t* d_blk_cnt = nullptr;
     double* d_blk_sum = nullptr;
@@ -321,6 +322,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.acc_part = c->d_acc_part;
     P.js = c->d_js;
     P.res_dbg = nullptr;
+    P.res_out = c->d_res_pko;
     P.direct_res = nullptr;
     P.st = c->d_st;
     if (c->kd) set_kd_params(c, P, c->grid);             // KDTree path: downstream kernels read per-point planes
@@ -407,6 +409,7 @@ static int ctx_alloc(lo_ctx* c) {
     const size_t NB = (N + kBlock - 1) / kBlock;
     LO_HIP(c, hipMalloc(&c->d_pts, N * 3 * sizeof(float)));
     LO_HIP(c, hipMalloc(&c->d_slot, NB * kBlock * sizeof(int32_t)));
+    LO_HIP(c, hipMalloc(&c->d_res_pko, NB * kBlock * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_wmask, NB * kWavesPerBlock * sizeof(uint64_t)));
     LO_HIP(c, hipMalloc(&c->d_blk_cnt, NB * sizeof(int32_t)));
     LO_HIP(c, hipMalloc(&c->d_blk_sum, NB * sizeof(double)));
@@ -498,7 +501,7 @@ void lo_destroy(lo_ctx* c) {
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
-                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la, c->d_ex_terms};
+                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la, c->d_ex_terms, c->d_res_pko};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
     if (c->lgrid.h_stage) (void)hipHostFree(c->lgrid.h_stage);

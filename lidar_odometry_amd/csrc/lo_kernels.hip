@@ -49,6 +49,7 @@ __device__ __forceinline__ void correspond_tail(const KParams& P, const float (&
         }
         P.slot[i] = slot;
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
+        if (P.res_out) P.res_out[i] = r;
     }
     corr_epilogue(P, slot >= 0, r, with_stats, blk);
 }

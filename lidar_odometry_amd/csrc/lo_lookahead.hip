@@ -197,6 +197,7 @@ __device__ void la_chain(const KParams& P, const ScanBufs& Bk, const LaParams& L
 #pragma unroll
     for (int q = 0; q < 12; ++q) T1[q] = s_pose[0][q];
     ScanBufs Bx;
+    Bx.res = nullptr;                                      // la_correspond stores no residuals
     Bx.slot = L.slotX + static_cast<size_t>(c) * L.n_cap;
     Bx.wmask = L.wmaskX + static_cast<size_t>(c) * (L.n_cap / kWave);
     Bx.blk_cnt = L.blkX + static_cast<size_t>(c) * kFuseMaxBlocks;
@@ -284,6 +285,7 @@ __global__ __launch_bounds__(kLaThreads) void k_la(const KParams* __restrict__ P
         Bk.wmask = L.wmaskO + set * (L.n_cap / kWave);
         Bk.blk_cnt = L.blkO + set * kFuseMaxBlocks;
         Bk.pose_in = L.rec[set].log[1].pose;               // the pose after iteration k - 1
+        Bk.res = nullptr;                                  // a chain's correspondences: no stored residuals
     } else if (P.st->done) {
         return;
     }

@@ -693,6 +693,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             const int pidx = b * kBlock + w * kWave + bit;
             if (P.kd_res) {
                 v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
+            } else if (B.res) {
+                v = B.res[pidx] / sden;                          // stored by the correspondence launch (same bits)
             } else {
                 float T[12];
 #pragma unroll
