@@ -533,8 +533,9 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
 
 // optimize_loop's inlier ratio (:206-238): the curr cloud at the converged pose (t + R p, :220-221), each point an
 // inlier when its nearest matched-map point is closer than 1 m: sqrt of nanoflann's fp32 (dx^2 + dy^2) + dz^2 < 1.
-// Every map point within 1 m lies in the cells spanned by q +- 1 m (one extra cell each side against rounding of
-// the cell index), so the grid answers the 1-NN threshold test exactly.  One lane per point, early exit on a hit.
+// Every map point within 1 m lies in the cells spanned by q +- (1 m + kKnnMargin) (the margin covers the fp32
+// rounding of q / h and of the grid's own cell index), so the grid answers the 1-NN threshold test exactly.  One
+// lane per point, a row's points 8 loads at a time, early exit on a hit.
 __global__ __launch_bounds__(kBlock) void k_inlier(KParams P) {
     DevState* st = P.st;
     const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -551,7 +552,8 @@ __global__ __launch_bounds__(kBlock) void k_inlier(KParams P) {
             bool any = true;
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const float fl = floorf((q[a] - 1.0f) / P.kd_h) - 1.0f, fh = floorf((q[a] + 1.0f) / P.kd_h) + 1.0f;
+                const float rr = 1.0f + static_cast<float>(kKnnMargin);
+                const float fl = floorf((q[a] - rr) / P.kd_h), fh = floorf((q[a] + rr) / P.kd_h);
                 const float o = static_cast<float>(P.kd_org[a]), d = static_cast<float>(P.kd_dim[a]);
                 const float l = fmaxf(fl - o, 0.0f), h = fminf(fh - o, d - 1.0f);
                 if (!(l <= h)) any = false;
@@ -562,11 +564,16 @@ __global__ __launch_bounds__(kBlock) void k_inlier(KParams P) {
                 for (int y = lo[1]; !in && y <= hi[1]; ++y) {
                     const size_t row = (static_cast<size_t>(z) * P.kd_dim[1] + y) * P.kd_dim[0];
                     const uint32_t b = P.kd_start[row + lo[0]], e = P.kd_start[row + hi[0] + 1];
-                    for (uint32_t p = b; p < e; ++p) {
-                        const float4 v = P.kd_pts[p];
-                        const float d0 = q[0] - v.x, d1 = q[1] - v.y, d2 = q[2] - v.z;
-                        const float d = (d0 * d0 + d1 * d1) + d2 * d2;
-                        if (sqrtf(d) < 1.0f) { in = true; break; }
+                    for (uint32_t p0 = b; !in && p0 < e; p0 += 8) {
+                        float4 v[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v[u] = (p0 + u < e) ? P.kd_pts[p0 + u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            const float d0 = q[0] - v[u].x, d1 = q[1] - v[u].y, d2 = q[2] - v[u].z;
+                            const float d = (d0 * d0 + d1 * d1) + d2 * d2;
+                            in = in || (p0 + u < e && sqrtf(d) < 1.0f);
+                        }
                     }
                 }
         }
