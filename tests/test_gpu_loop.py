@@ -165,3 +165,30 @@ def test_loop_icp_exact_far_keyframe_same_outcome(exact_icp):
     assert st.num_iterations == it_o and st.converged == conv_o
     for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
         np.testing.assert_array_equal(_bits(lg["pose"]), _bits(lo["pose"]), err_msg=f"iter {k}")
+
+
+def test_loop_icp_lattice_ties_rerun_with_visit_order(exact_icp):
+    """The matched keyframe's grid is built without the kd visit order; queries midway between lattice points
+    meet exact distance ties, the solve is flagged and rerun with the order (nanoflann's tie-break), so every
+    iteration still matches the oracle bit for bit."""
+    g = np.arange(-8.0, 8.0, 0.5, dtype=np.float32)
+    X, Y = np.meshgrid(g, g, indexing="ij")
+    floor = np.stack([X.ravel(), Y.ravel(), np.zeros(X.size, np.float32)], 1)
+    wall = np.stack([np.full(X.size, 8.0, np.float32), X.ravel(), Y.ravel() * 0.25 + 2.0], 1)
+    wall2 = np.stack([X.ravel(), np.full(X.size, -8.0, np.float32), Y.ravel() * 0.25 + 2.0], 1)
+    mat = np.concatenate([floor, wall, wall2]).astype(np.float32)
+    cur = (mat + np.array([0.25, 0.0, 0.0], np.float32)).astype(np.float32)      # midway along x: ties
+    I = np.eye(3, 4, dtype=np.float32).reshape(12)
+    Tc = I.copy()
+    Tc[3] = 0.02
+    ok_o, conv_o, Tr_o, inl_o, it_o, logs_o = oracle.icp_optimize_loop(cur, Tc, mat, I)
+    ok_g, Tr_g, inl_g = exact_icp.optimize_loop(cur, Tc, mat, I)
+    st = exact_icp.get_last_stats()
+    assert ok_g == ok_o and st.num_iterations == it_o and st.converged == conv_o
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        for key in ("pose", "H", "g", "delta"):
+            np.testing.assert_array_equal(_bits(lg[key]), _bits(lo[key]), err_msg=f"iter {k} {key}")
+        assert lg["n_corr"] == lo["n_corr"], k
+    if conv_o:
+        np.testing.assert_array_equal(_bits(Tr_g), _bits(Tr_o))
+        assert np.float32(inl_g) == np.float32(inl_o)
