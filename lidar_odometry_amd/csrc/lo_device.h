@@ -55,6 +55,7 @@ struct DevState {
     unsigned int acc_arrive;        // k_accumulate last-block-done counter (reset by the last block)
     unsigned int kd_unres_n;        // KDTree path: queries the grid search could not certify (k_knn_brute)
     unsigned int inliers;           // loop closure: points whose nearest matched-map point is < 1 m (k_inlier)
+    unsigned int kd_tie;            // KDTree grid without its kd visit order: a query met a deciding distance tie
     double H_out[36];
     double g_out[6];
     double cost_out;
@@ -385,6 +386,7 @@ __device__ __forceinline__ void scan_pose(const KParams& P, int init, int blk, f
             st->status = LO_OK;
             st->acc_arrive = 0;
             st->inliers = 0;
+            st->kd_tie = 0;
             // kd_unres_n is NOT reset here: other blocks of the same k_knn launch may already be appending
             // (k_plane zeroes it after every use; k_init / lo_create start it at 0)
         }

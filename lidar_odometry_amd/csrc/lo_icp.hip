@@ -77,6 +77,7 @@ struct PointGrid {
     size_t vpos_cap = 0;
     KdNode* d_nodes = nullptr;      //   and the tree's nodes (root = 0)
     size_t nodes_cap = 0;
+    bool has_order = false;         // d_vpos / d_nodes hold the visit order of the current points
     void* h_stage = nullptr;        // pinned upload staging (grid_build)
     size_t stage_cap = 0;
     int m = 0;
@@ -144,6 +145,7 @@ struct lo_ctx {
     bool kd = false;
     PointGrid grid;                 // the map's L0 centroids (lo_map_set_points)
     PointGrid lgrid;                // loop closure: the matched keyframe's local map (lo_icp_optimize_loop)
+    uint64_t loop_reruns = 0;       //   solves rerun with the kd visit order (a deciding distance tie)
     int32_t* d_kd_nbr = nullptr;
     int32_t* d_kd_unres = nullptr;
     double* d_kd_res = nullptr;
@@ -269,8 +271,8 @@ static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
     P.tab = c->d_kd_plane;
     P.kd_pts = G.d_pts;
     P.kd_start = G.d_start;
-    P.kd_vpos = G.d_vpos;
-    P.kd_nodes = G.d_nodes;
+    P.kd_vpos = G.has_order ? G.d_vpos : nullptr;
+    P.kd_nodes = G.has_order ? G.d_nodes : nullptr;
     P.kd_m = G.m;
     for (int a = 0; a < 3; ++a) { P.kd_org[a] = G.org[a]; P.kd_dim[a] = G.dim[a]; }
     P.kd_h = G.h;
@@ -752,7 +754,9 @@ size_t lo_map_surfel_count(const lo_ctx* c) { return c ? c->n_surfels : 0; }
 // index order inside a cell; kd_start[cell] = first point, kd_start[ncell] = m.
 static constexpr size_t kKdMaxCells = size_t(1) << 26;
 
-static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
+// with_order: also the reference kd-tree's visit order (the tie-break of equal distances); without it the kNN
+// kernels flag a deciding tie in DevState::kd_tie instead of ranking it (the loop-closure ICP then rebuilds with it).
+static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool with_order = true) {
     if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
     if (m > static_cast<size_t>(INT32_MAX / 2)) { c->err = "too many map points"; return LO_ERR_CAPACITY; }
     for (size_t i = 0; i < 3 * m; ++i)
@@ -762,7 +766,7 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
     // ~0.3 ms for a 3.6k-point keyframe cloud, as the reference's own buildIndex per loop-closure call)
     std::vector<KdNode> nodes;
     std::vector<uint32_t> vpos;
-    std::thread order_thread([&] { KdOrderBuilder(xyz, m).build(nodes, vpos); });
+    std::thread order_thread([&] { if (with_order) KdOrderBuilder(xyz, m).build(nodes, vpos); });
     struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } joiner{order_thread};
     float h = 2.0f * c->cfg.voxel_size;
     int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
@@ -852,6 +856,7 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
     LO_HIP(c, hipMemcpyAsync(G.d_vpos, hs + b_pts + b_start, b_vpos, hipMemcpyHostToDevice, c->stream));
     LO_HIP(c, hipMemcpyAsync(G.d_nodes, hs + b_pts + b_start + b_vpos, b_nodes, hipMemcpyHostToDevice, c->stream));
     G.m = static_cast<int>(m);
+    G.has_order = with_order;
     G.h = h;
     for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
     return LO_OK;
@@ -1075,8 +1080,13 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     const lo::SE3f Tm = lo::se3_from12(T_matched);
     std::vector<float> lmap(3 * std::max<size_t>(n_matched, 1));
     if (n_matched > 0) lo::transform_points(Tm, matched, n_matched, lmap.data());
-    rc = grid_build(c, c->lgrid, lmap.data(), n_matched);
+    // the matched cloud's grid first without the kd visit order (building it is ~0.3 ms of host work per call and
+    // it only ranks exact distance ties that decide a query's five neighbours or their order, which keyframe
+    // centroids rarely produce); a solve that met one is rerun with the order below
+    bool with_order = false;
+    rc = grid_build(c, c->lgrid, lmap.data(), n_matched, with_order);
     if (rc != LO_OK) return rc;
+retry:
     if (st) { std::memset(st, 0, sizeof(*st)); st->status = LO_INSUFFICIENT; }
     if (n_curr == 0 || n_matched == 0) return LO_INSUFFICIENT;       // empty clouds: 0 correspondences (:477-483)
     if ((rc = ensure_acc_part(c)) != LO_OK) return rc;
@@ -1123,6 +1133,13 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     const size_t bytes = head + sizeof(lo_iter_log) * static_cast<size_t>(LO_MAX_ITERS);
     LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
     LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->h_st->kd_tie && !with_order) {               // a deciding tie was ranked by index: redo with the order
+        with_order = true;
+        ++c->loop_reruns;
+        rc = grid_build(c, c->lgrid, lmap.data(), n_matched, true);
+        if (rc != LO_OK) return rc;
+        goto retry;
+    }
     const DevState* hs = c->h_st;
     bool success = false;
     if (converged) {

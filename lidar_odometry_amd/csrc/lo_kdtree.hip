@@ -38,7 +38,8 @@ struct Top5 {
     int id[5];      // original centroid index (tie-break)
     int pos[5];     // position in kd_pts
     int n;
-    int tie;        // fast order only: two different points compared at equal distance (the result may differ)
+    float tie;      // fast order only: the smallest distance at which two different points compared equal (+inf:
+                    // none); the result can differ from nanoflann's only if tie <= the final fifth distance
 };
 
 // The query and the reference tree's order, for ties.
@@ -77,7 +78,7 @@ __device__ __forceinline__ bool lex_less(const KnnQ& Q, Top5& t, float da, int i
     if constexpr (EX) {
         return da < db || (da == db && ia != ib && kd_visit_before(Q, ia, ib));
     } else {
-        t.tie |= (da == db && ia != ib) ? 1 : 0;
+        if (da == db && ia != ib) t.tie = fminf(t.tie, da);
         return da < db || (da == db && ia < ib);
     }
 }
@@ -86,7 +87,7 @@ __device__ __forceinline__ void top5_init(Top5& t) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) { t.d[k] = __builtin_inff(); t.id[k] = 0x7fffffff; t.pos[k] = -1; }
     t.n = 0;
-    t.tie = 0;
+    t.tie = __builtin_inff();
 }
 
 // KNNResultSet::addPoint behind searchLevel's `dist < worstDist` (worstDist = FLT_MAX until 5 are held),
@@ -128,7 +129,7 @@ __device__ __forceinline__ void top5_merge_dpp(const KnnQ& Q, Top5& t) {
         u.pos[k] = __builtin_amdgcn_mov_dpp(t.pos[k], CTRL, 0xf, 0xf, false);
     }
     u.n = __builtin_amdgcn_mov_dpp(t.n, CTRL, 0xf, 0xf, false);
-    t.tie |= __builtin_amdgcn_mov_dpp(t.tie, CTRL, 0xf, 0xf, false);
+    t.tie = fminf(t.tie, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t.tie), CTRL, 0xf, 0xf, false)));
 #pragma unroll
     for (int k = 0; k < 5; ++k)
         if (k < u.n) top5_insert<EX>(Q, t, u.d[k], u.id[k], u.pos[k]);
@@ -235,7 +236,8 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
         }
     }
     if (g != 0) return;
-    if (!done || grp.tie) {                                   // not certified, or an equal-distance comparison
+    if (!done || (grp.n == 5 && grp.tie <= grp.d[4]) || (grp.n < 5 && grp.tie < __builtin_inff())) {
+        // not certified, or a tie that can decide the five or their order
         out[0] = -2;
         P.kd_unres[atomicAdd(&P.st->kd_unres_n, 1u)] = i;
         return;
@@ -302,7 +304,7 @@ __device__ __forceinline__ void top5_merge_xor(const KnnQ& Q, Top5& t, int o) {
         u.pos[k] = __shfl_xor(t.pos[k], o, 64);
     }
     u.n = __shfl_xor(t.n, o, 64);
-    t.tie |= __shfl_xor(t.tie, o, 64);
+    t.tie = fminf(t.tie, __shfl_xor(t.tie, o, 64));
 #pragma unroll
     for (int k = 0; k < 5; ++k)
         if (k < u.n) top5_insert<EX>(Q, t, u.d[k], u.id[k], u.pos[k]);
@@ -312,7 +314,7 @@ __device__ __forceinline__ void top5_merge_xor(const KnnQ& Q, Top5& t, int o) {
 // then the wave / workgroup merges; wave 0 lane 0 returns the five (and, fast order, whether any tie was seen).
 template <bool EX>
 __device__ __forceinline__ Top5 brute_query(const KParams& P, const KnnQ& Q, float (&s_d)[16][5], int (&s_id)[16][5],
-                                            int (&s_pos)[16][5], int (&s_n)[16], int (&s_tie)[16]) {
+                                            int (&s_pos)[16][5], int (&s_n)[16], float (&s_tie)[16]) {
     constexpr int kBT = 1024;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const float qx = Q.q[0], qy = Q.q[1], qz = Q.q[2];
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     __shared__ int s_id[kW][5];
     __shared__ int s_pos[kW][5];
     __shared__ int s_n[kW];
-    __shared__ int s_tie[kW];
+    __shared__ float s_tie[kW];
     __shared__ int s_redo;
     const int tid = threadIdx.x;
     float T[12];
@@ -376,11 +378,14 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
         const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
         Top5 a = brute_query<false>(P, Q, s_d, s_id, s_pos, s_n, s_tie);
-        if (tid == 0) s_redo = a.tie;
+        if (tid == 0) s_redo = (a.n == 5 && a.tie <= a.d[4]) || (a.n < 5 && a.tie < __builtin_inff());
         __syncthreads();
         const bool redo = s_redo != 0;
         __syncthreads();
-        if (redo) a = brute_query<true>(P, Q, s_d, s_id, s_pos, s_n, s_tie);   // equal distances: nanoflann's order
+        if (redo) {                                        // a deciding tie: nanoflann's visit order ranks it
+            if (P.kd_nodes) a = brute_query<true>(P, Q, s_d, s_id, s_pos, s_n, s_tie);
+            else if (tid == 0) atomicOr(&st->kd_tie, 1u);  // no visit order built: the host reruns with it
+        }
         if (tid == 0) {
             int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
             if (a.n < 5) out[0] = -1;

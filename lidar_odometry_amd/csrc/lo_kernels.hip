@@ -406,6 +406,7 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
         st->acc_arrive = 0;
         st->kd_unres_n = 0;
         st->inliers = 0;
+        st->kd_tie = 0;
     }
 }
 
