@@ -196,6 +196,9 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
 #pragma unroll
     for (int q = 0; q < K; ++q) cnt[q] = 0.0;
     // ---- k-means until the means repeat exactly (:351-389) ----
+    // Component 0's mean is pinned, so only its count is needed, and counts are small integers (exact in fp64):
+    // it is S minus the others' counts, and the 2(K - 1) remaining totals fit the 4-value butterfly (each total
+    // bit-identical to wave_totals8's, so the fit still equals gmm_fit_1w's).
     for (int guard = 0; guard < 100000; ++guard) {
         double v[2 * K - 1];
 #pragma unroll
@@ -207,13 +210,23 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
 #pragma unroll
             for (int q = 0; q < K; ++q) { const double d = fabs(x[s] - mu[q]); if (d < md) { md = d; ci = q; } }
 #pragma unroll
-            for (int q = 0; q < K; ++q) {
+            for (int q = 1; q < K; ++q) {
                 const bool mine = have[s] && ci == q;
                 v[q] += mine ? 1.0 : 0.0;
-                if (q > 0) v[K + q - 1] += mine ? x[s] : 0.0;
+                v[K + q - 1] += mine ? x[s] : 0.0;
             }
         }
-        wave_totals8<2 * K - 1>(v);
+        if constexpr (K > 1) {
+            double u[2 * K - 2];
+#pragma unroll
+            for (int q = 0; q < 2 * K - 2; ++q) u[q] = v[q + 1];
+            wave_totals4<2 * K - 2>(u);
+#pragma unroll
+            for (int q = 0; q < 2 * K - 2; ++q) v[q + 1] = u[q];
+        }
+        v[0] = static_cast<double>(S);
+#pragma unroll
+        for (int q = 1; q < K; ++q) v[0] -= v[q];
         bool eq = true;
         double nm[K];
 #pragma unroll
