@@ -686,7 +686,7 @@ def main():
     for i in range(len(d_scans)):
         nv_i, _, _ = icp.find_correspondences(wl["scans"][i], inits[i])
         ni = len(wl["scans"][i])
-        scan_alg_bytes.append(ni * (12 + 80 + 40 + 4 + 0.125) + 40 * nv_i if kd else ni * (12 + 8 + 4 + 0.125) + 24 * nv_i)
+        scan_alg_bytes.append(ni * (12 + 80 + 40 + 4 + 0.125) + 40 * nv_i if kd else ni * (12 + 8 + 4 + 8 + 0.125) + 24 * nv_i)
     L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
     for k in range(args.warmup):
         step(k)
@@ -763,8 +763,9 @@ def main():
     n_valid, valid, _ = icp.find_correspondences(wl["scans"][i0], inits[i0])
     v = n_valid / n0
     # algorithmic bytes per k_correspond launch: per point 12 B point + 8 B key probe + 24 B payload on a hit
-    # (lower-bounded by the accepted fraction v) + 4 B slot index written + 1/8 B validity ballot
-    alg_bytes = n0 * (12 + 8 + 24 * v + 4 + 0.125)
+    # (lower-bounded by the accepted fraction v) + 4 B slot index and 8 B fp64 residual written (the PKO sample
+    # reads the residual back) + 1/8 B validity ballot
+    alg_bytes = n0 * (12 + 8 + 24 * v + 4 + 8 + 0.125)
     corr_kernel = "k_correspond"
     if kd:
         # KDTree stage (k_knn + k_knn_brute + k_plane): per point 12 B point + 5 x 16 B neighbour centroids +
@@ -856,7 +857,7 @@ def main():
         scan_bytes = []
         for i in range(len(d_scans)):
             nv, _, _ = icp.find_correspondences(wl["scans"][i], inits[i])
-            scan_bytes.append(len(wl["scans"][i]) * (12 + 8 + 4 + 0.125) + 24 * nv)
+            scan_bytes.append(len(wl["scans"][i]) * (12 + 8 + 4 + 8 + 0.125) + 24 * nv)
         for B in sizes:
             while len(pool) < B:
                 o = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
