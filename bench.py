@@ -247,6 +247,36 @@ def pmc_child(path: str):
     from lidar_odometry_amd import lib
     from lidar_odometry_amd.icp import IterativeClosestPointOptimizer, MapGeometry
     z = np.load(path)
+    if "batch" in z:                       # the batched launch: B contexts (own map copy each), private scan copies
+        from lidar_odometry_amd import BatchOptimizer
+        B, nd = int(z["batch"]), int(z["n_scans"])
+        scans = [np.ascontiguousarray(z[f"scan_{i}"], np.float32) for i in range(nd)]
+        inits = np.ascontiguousarray(z["inits"], np.float32).reshape(nd, 12)
+        mp = max(len(x) for x in scans)
+        ctxs = []
+        for _ in range(B):
+            o = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=float(z["voxel"])), max_points=mp)
+            o.set_surfels(z["keys"], z["normals"], z["centroids"])
+            ctxs.append(o)
+        bo = BatchOptimizer(ctxs)
+        sel = [j % nd for j in range(B)]
+        job = [torch.from_numpy(scans[i]).cuda() for i in sel]
+        c_ptrs = (C.c_void_p * B)(*[t.data_ptr() for t in job])
+        c_cnts = (C.c_size_t * B)(*[t.shape[0] for t in job])
+        c_T = np.ascontiguousarray(np.stack([inits[i] for i in sel]))
+        from lidar_odometry_amd._lib import LoBatchRec
+        recs = (LoBatchRec * B)()
+        ms = C.c_double(0.0)
+        L = lib()
+        rc = L.lo_batch_optimize_async(bo._b, c_ptrs, c_cnts, c_T.ctypes.data_as(C.POINTER(C.c_float)))
+        rc |= L.lo_batch_result(bo._b, recs, C.byref(ms))
+        cms = C.c_float(0.0)
+        rc |= L.lo_batch_bench_correspond(bo._b, int(z["reps"]), C.byref(cms))
+        torch.cuda.synchronize()
+        bo.close()
+        for o in ctxs:
+            o.close()
+        sys.exit(0 if rc == 0 else 1)
     pts = np.ascontiguousarray(z["pts"], np.float32)
     icp = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=float(z["voxel"])), max_points=len(pts))
     icp.set_surfels(z["keys"], z["normals"], z["centroids"])
@@ -261,7 +291,7 @@ def pmc_child(path: str):
     sys.exit(0 if rc == 0 else 1)
 
 
-def live_pmc(case: dict, reps: int = 200):
+def live_pmc(case: dict, reps: int = 200, kernel: str = "k_correspond"):
     """HBM traffic of one k_correspond launch, measured in this run: two rocprofv3 passes (--pmc FETCH_SIZE, then
     --pmc WRITE_SIZE, each counter in a run of its own) over `reps` isolated launches of the bench's largest scan,
     in child processes (this process has initialised the GPU).  MI355X_MICROARCH.md §HBM: the counters are KiB;
@@ -280,15 +310,15 @@ def live_pmc(case: dict, reps: int = 200):
         env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, counter)
-            cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", counter, "--kernel-trace",
-                   "--kernel-include-regex", "k_correspond", "-d", d, "-o", "run", "--output-format", "csv", "--",
+            cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "--kernel-trace",
+                   "--kernel-include-regex", kernel, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", os.path.join(tmp, "case.npz")]
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, cwd=ROOT)
             if r.returncode != 0:
                 log(f"live PMC pass {counter} failed (rc {r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
                 return None
             try:
-                iso, n_iso, _, _ = per_launch(d, counter, "k_correspond", min_run=20)
+                iso, n_iso, _, _ = per_launch(d, counter, kernel, min_run=20)
             except SystemExit as e:
                 log(f"live PMC pass {counter}: {e}")
                 return None
@@ -912,6 +942,17 @@ def main():
                                                "points_per_launch": npts, "working_set_bytes": wsb,
                                                "in_cache": wsb <= MALL_BYTES,
                                                "traffic": read_pmc_traffic(f"{args.config}_batch{B}")}
+            if args.pmc == "live" and B == sizes[-1]:
+                # the largest batch (beyond the 256 MB Infinity Cache at B >= 2048): HBM traffic measured live
+                keys, normals, cents, _ = wl["vm"].surfels()
+                case = {"batch": B, "n_scans": nd, "inits": np.stack(inits), "keys": keys, "normals": normals,
+                        "centroids": cents, "voxel": wl["voxel"]}
+                for i in range(nd):
+                    case[f"scan_{i}"] = wl["scans"][i]
+                tl = live_pmc(case, reps=50, kernel="k_correspond_b")
+                if tl is not None:
+                    batched["runs"][-1]["roofline"]["traffic"] = tl["hbm_bytes_per_launch"]
+                    batched["runs"][-1]["roofline"]["traffic_live"] = tl
             del job_scans
             log(f"[batch] B={B}: {B * K3 / el3:.0f} scans/s, {el3 / K3 * 1e3:.3f} ms/batch "
                 f"(device {np.mean(dev_ms):.3f} ms)")
