@@ -47,9 +47,10 @@ __device__ __forceinline__ void correspond_tail(const KParams& P, const float (&
             r = residual_f64(P.tab[s], wx, wy, wz);
             if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, :630)
         }
-        P.slot[i] = slot;
+        // streaming stores: read back only by the next kernels (PKO sample, accumulate), not by this launch
+        __builtin_nontemporal_store(slot, &P.slot[i]);
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
-        if (P.res_out) P.res_out[i] = r;
+        if (P.res_out) __builtin_nontemporal_store(r, &P.res_out[i]);
     }
     corr_epilogue(P, slot >= 0, r, with_stats, blk);
 }
