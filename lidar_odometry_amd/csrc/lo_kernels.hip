@@ -70,6 +70,15 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
     correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
 }
 
+// XCD-aware block order: the hardware hands consecutive workgroups to the 8 XCDs round-robin; logical block
+// xcd_block(h) gives XCD x (= h % 8) one contiguous run of the scan's blocks, so spatially coherent points (scans in
+// acquisition order) probe the same surfel-table lines through one L2 instead of eight.  A bijection on [0, nb).
+__device__ __forceinline__ int xcd_block(int h, int nb) {
+    constexpr int kXcd = 8;
+    const int q = nb / kXcd, r = nb % kXcd, x = h % kXcd, k = h / kXcd;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
     if (P.init && P.stash && blockIdx.x == 0) {          // the scan's parameters for the k_la launches (lo_icp.hip)
         constexpr int kWords = sizeof(KParams) / 4;
@@ -80,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
         __syncthreads();
         if (threadIdx.x == 0) P.stash->init = 0;
     }
-    correspond_body(P, with_stats, P.init, blockIdx.x);
+    correspond_body(P, with_stats, P.init, xcd_block(blockIdx.x, gridDim.x));
 }
 
 // Batched launch (lo_batch_*): blockIdx.y = job (one context each: own scan, map and GN state); the grid is
