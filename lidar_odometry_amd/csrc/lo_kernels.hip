@@ -94,10 +94,15 @@ __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats
 
 // Batched launch (lo_batch_*): blockIdx.y = job (one context each: own scan, map and GN state); the grid is
 // sized for the largest job and a job's surplus blocks leave before touching any of its buffers.
+// Batched: the (block, job) grid is linearised and put in XCD-aware order, so each XCD takes whole jobs and a
+// job's surfel table is cached by one L2.
 __global__ __launch_bounds__(kBlock) void k_correspond_b(const KParams* __restrict__ PB, int with_stats, int init) {
-    const KParams& P = PB[blockIdx.y];
-    if (static_cast<int>(blockIdx.x) >= P.nb) return;
-    correspond_body(P, with_stats, init, blockIdx.x);
+    const int total = static_cast<int>(gridDim.x * gridDim.y);
+    const int lin = xcd_block(static_cast<int>(blockIdx.x + blockIdx.y * gridDim.x), total);
+    const int job = lin / static_cast<int>(gridDim.x), blk = lin - job * static_cast<int>(gridDim.x);
+    const KParams& P = PB[job];
+    if (blk >= P.nb) return;
+    correspond_body(P, with_stats, init, blk);
 }
 
 // ====================================================================================================
