@@ -140,11 +140,7 @@ __device__ __forceinline__ void accumulate_body(const KParams& P, int it, int fu
     // wave / block trees; the partial count k_solve reduces stays <= kAccBlocks
     const int n = scan_n(P);
     for (int i = blk * kBlock + tid; i < n; i += P.nb_acc * kBlock) acc_point(P, T, scale, dl, i, acc);
-#pragma unroll
-    for (int k = 0; k < kNE; ++k) {
-        const float v = wave_total(acc[k]);
-        if (lane == 0) s_acc[wid][k] = v;
-    }
+    wave_totals_f32<kNE>(acc, s_acc[wid]);
     __syncthreads();
     if (tid < kNE) {
         double v = 0.0;
@@ -303,11 +299,7 @@ __global__ __launch_bounds__(kAcc1Threads) void k_accumulate_b1(const KParams* _
 #pragma unroll
         for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
         if (vb < nb && i < n) acc_point(P, T, scale, dl, i, acc);
-#pragma unroll
-        for (int k = 0; k < kNE; ++k) {
-            const float v = wave_total(acc[k]);
-            if (lane == 0) s_acc[wid][k] = v;
-        }
+        wave_totals_f32<kNE>(acc, s_acc[wid]);
         __syncthreads();
         if (tid < kW / kWavesPerBlock * kNE) {
             const int q = tid / kNE, k = tid - q * kNE;

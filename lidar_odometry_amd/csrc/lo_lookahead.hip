@@ -47,11 +47,7 @@ __device__ __forceinline__ void la_accumulate(const KParams& P, const int32_t* s
 #pragma unroll
         for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
         if (vb < nb && i < n) acc_point(P, slot, T, scale, dl, i, acc);
-#pragma unroll
-        for (int k = 0; k < kNE; ++k) {
-            const float v = wave_total(acc[k]);
-            if (lane == 0) s_acc[wid][k] = v;
-        }
+        wave_totals_f32<kNE>(acc, s_acc[wid]);
         __syncthreads();
         if (tid < kG * kNE) {
             const int q = tid / kNE, k = tid - q * kNE;

@@ -484,7 +484,7 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
     if (c > P.NA) return;
     const float dl = static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
     __shared__ float s_acc[kWavesPerBlock][kNE];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, wid = tid >> 6;
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
@@ -497,11 +497,7 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
         for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
         const int i = vb * kBlock + tid;
         if (i < n) acc_point(P, T, scale, dl, i, acc);
-#pragma unroll
-        for (int k = 0; k < kNE; ++k) {
-            const float v = wave_total(acc[k]);
-            if (lane == 0) s_acc[wid][k] = v;
-        }
+        wave_totals_f32<kNE>(acc, s_acc[wid]);
         __syncthreads();
         if (tid < kNE) {
             double v = 0.0;
