@@ -516,7 +516,7 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // NW.  lead: this workgroup publishes the iteration-0 scale.
 template <int NW>
 __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, int it, bool lead, int* s_pre,
-                                           int& nc_out, double& scale_out) {
+                                           int& nc_out, double& scale_out, uint64_t* s_wm = nullptr) {
     constexpr int NT = NW * 64;
     DevState* st = B.st;
     __shared__ int s_iscan[NW];
@@ -527,6 +527,45 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
     const bool calc = it == 0 && !P.scale_given;           // iteration 0 computes the scale (unless it is given)
     if (P.direct_res) {
         if (tid == 0) { s_nc = P.n; s_scale = 1.0; }
+        __syncthreads();
+    } else if (P.nb <= 64) {
+        // one wave, lane b = block b, one barrier: the same per-lane values and wave trees as the general path below
+        // (with nb <= 64 every block sits in wave 0 there too), so the same bits.  s_wm (nullable): the blocks'
+        // validity ballots prefetched into LDS for the sample phase.
+        if (wid == 0) {
+            const int nb = P.nb;
+            const int c = lane < nb ? B.blk_cnt[lane] : 0;
+            const double bs = (calc && lane < nb) ? 0.0 + P.blk_sum[lane] : 0.0;   // as `lsum += ...` from +0
+            const double bm = (calc && lane < nb) ? P.blk_m2[lane] : 0.0;
+            if (s_wm) {
+#pragma unroll
+                for (int q = 0; q < kWavesPerBlock; ++q) {
+                    const int w = q * 64 + lane;
+                    if (w < nb * kWavesPerBlock) s_wm[w] = B.wmask[w];
+                }
+            }
+            int inc = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) { const int t = __shfl_up(inc, o, 64); if (lane >= o) inc += t; }
+            const int total = __shfl(inc, 63, 64);
+            if (lane < nb) s_pre[lane] = inc - c;
+            double scale;
+            if (calc) {
+                const double mean = total > 0 ? (0.0 + wave_total(bs)) / total : 0.0;
+                double m2 = 0.0;
+                if (c > 0) { const double dm = bs / c - mean; m2 = 0.0 + (bm + c * (dm * dm)); }
+                const double M2 = 0.0 + wave_total(m2);
+                const double var = total > 0 ? M2 / total : 0.0;
+                scale = sqrt(var) / 6.0;                       // IterativeClosestPointOptimizer.cpp:314-315
+            } else {
+                scale = st->scale;
+            }
+            if (lane == 0) {
+                s_nc = total;
+                s_scale = scale;
+                if (calc && lead) st->scale = scale;
+            }
+        }
         __syncthreads();
     } else {
         const int nb = P.nb;
@@ -643,7 +682,9 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
     int nc;
     double s_scale;
-    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale);
+    __shared__ uint64_t s_wm[kWavesPerBlock * 64];             // ballots of <= 64 blocks, prefetched by the prefix
+    const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? s_wm : nullptr;
+    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm);
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
         if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
         return;
@@ -689,7 +730,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             int k = rank - s_pre[b];
             uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
 #pragma unroll
-            for (int q = 0; q < kWavesPerBlock; ++q) m4[q] = B.wmask[b * kWavesPerBlock + q];
+            for (int q = 0; q < kWavesPerBlock; ++q)
+                m4[q] = s_wmask ? s_wmask[b * kWavesPerBlock + q] : B.wmask[b * kWavesPerBlock + q];
             int w = 0;
             uint64_t mk = m4[0];
 #pragma unroll
