@@ -260,19 +260,22 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
 // the pose from it -- and the old pose comes from the previous iteration's log (the initial pose for it = 0).
 __global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
     DevState* st = P.st;
-    if (st->done) return;
+    const int done = st->done;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    __shared__ int s_c, s_done;
+    __shared__ int s_c, s_done, s_skip;
     __shared__ double tot[kNE];
     __shared__ float s_T[12];
-    if (tid < kWave) {
-        const int bi = pko_select_index(P);
-        if (tid == 0) {
+    int bi = 0;
+    if (tid < kWave) bi = pko_select_index(P);
+    if (tid == 0) {                              // thread 0's view of the flag decides for the whole block (block 0
+        s_skip = done;                           // of this launch may set it while other blocks start)
+        if (!done) {
             s_c = bi > 0 ? bi - 1 : P.NA;
             if (blk == 0) st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
         }
     }
     __syncthreads();
+    if (s_skip) return;
     solve_sums<kBlock>(P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc, tot);
     if (tid == 0) {
         const float* pose_old = it == 0 ? P.T0 : st->logs[it - 1].pose;

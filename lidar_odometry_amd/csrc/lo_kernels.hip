@@ -207,16 +207,19 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(KParams P, int it, int 
 // have formed, reduced here with the same solve_tail<kBlock> pattern -- bit-identical, one launch fewer.
 __global__ __launch_bounds__(kBlock) void k_solve_pick(KParams P, int it) {
     DevState* st = P.st;
-    if (st->done) return;
-    __shared__ int s_c;
-    if (threadIdx.x < kWave) {
-        const int bi = pko_select_index(P);
-        if (threadIdx.x == 0) {
+    const int done = st->done;                   // loaded together with the JS grid
+    __shared__ int s_c, s_skip;
+    int bi = 0;
+    if (threadIdx.x < kWave) bi = pko_select_index(P);
+    if (threadIdx.x == 0) {
+        s_skip = done;
+        if (!done) {
             s_c = bi > 0 ? bi - 1 : P.NA;
             st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
         }
     }
     __syncthreads();
+    if (s_skip) return;
     solve_tail<kBlock>(P, it, 0, P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc);
 }
 
@@ -228,22 +231,27 @@ __global__ __launch_bounds__(kBlock) void k_solve_pick(KParams P, int it) {
 __global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) {
     DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    if (st->done) return;                        // before any other load: an early exit costs one round trip
+    // the done flag, the points and the JS grid are loaded together (one round trip, not two); a converged scan
+    // leaves after it without writing anything
+    const int done = st->done;
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;       // in flight during the solve
     if (i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
-    __shared__ int s_c, s_done;
+    __shared__ int s_c, s_done, s_skip;
     __shared__ double tot[kNE];
     __shared__ float s_T[12];
-    if (tid < kWave) {
-        const int bi = pko_select_index(P);
-        if (tid == 0) {
+    int bi = 0;
+    if (tid < kWave) bi = pko_select_index(P);
+    if (tid == 0) {                              // thread 0's view of the flag decides for the whole block (block 0
+        s_skip = done;                           // of this launch may set it while other blocks start)
+        if (!done) {
             s_c = bi > 0 ? bi - 1 : P.NA;
             if (blk == 0) st->alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
         }
     }
     __syncthreads();
+    if (s_skip) return;
     solve_sums<kBlock>(P.acc_part + static_cast<size_t>(s_c) * kFuseMaxBlocks * kNE, P.nb_acc, tot);
     if (tid == 0) {
         const float* pose_old = it == 0 ? P.T0 : st->logs[it - 1].pose;
