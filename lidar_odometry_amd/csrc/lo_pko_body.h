@@ -727,7 +727,9 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             int lo = 0, hi = P.nb - 1;                          // last block with prefix <= rank
             while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (s_pre[mid] <= rank) lo = mid; else hi = mid - 1; }
             const int b = lo;
-            int k = rank - s_pre[b];
+            // clamped: in-range for any data, so a workgroup that read a half-written state (a wave that saw the
+            // lead's INSUFFICIENT flag after the others started) cannot index outside the block or loop long
+            int k = min(max(rank - s_pre[b], 0), kBlock - 1);
             uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
 #pragma unroll
             for (int q = 0; q < kWavesPerBlock; ++q)
@@ -740,7 +742,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
                 if (w == q && k >= c) { k -= c; w = q + 1; mk = m4[q + 1]; }
             }
             for (int q = 0; q < k; ++q) mk &= mk - 1;
-            const int bit = __ffsll(static_cast<unsigned long long>(mk)) - 1;
+            const int bit = max(__ffsll(static_cast<unsigned long long>(mk)) - 1, 0);
             const int pidx = b * kBlock + w * kWave + bit;
             if (P.kd_res) {
                 v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
