@@ -1520,7 +1520,10 @@ int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out) {
 // loads); they are rebuilt on the host every call but uploaded only when a job's scan pointer, size or map
 // table changed.  The initial poses travel in a separate 12-float-per-job array (KParams::T0p).
 static constexpr int kBatchPkoWGs = 256;    // PKO workgroups per launch over all jobs (>= 1 per job; measured best)
-static constexpr int kBatchOneWaveMin = 2048; // from this many jobs, PKO is one single-wave workgroup per job (measured)
+// one single-wave PKO workgroup per job (k_pko_tb<1, true>) is opt-in (LO_BATCH_ONE_WAVE=1): with the JS phase's
+// LDS alpha table the four-wave split wins at every measured size (2048 jobs 946k vs 828k scans/s, 4096 1.039M vs
+// 1.021M); the one-wave variant stays tested (tests/test_gpu_batch.py) for batches beyond the measured range
+static constexpr int kBatchOneWaveMin = 0x7fffffff;
 
 struct lo_batch {
     std::vector<lo_ctx*> ctx;

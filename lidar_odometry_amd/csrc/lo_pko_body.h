@@ -21,6 +21,7 @@
 // so no in-launch hand-off is needed.
 #pragma once
 #include "lo_device.h"
+#include "lo_math.h"
 
 #include <cfloat>
 
@@ -782,8 +783,22 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
 
     // ---- 4. JS divergence for this workgroup's alphas (calculate_js_divergence :710-787) ----
+    // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
+    // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25).  The
+    // pass's alphas and Z sit in LDS (s_az), loaded by the summing threads while the previous pass is summed, so
+    // the term loop issues no global load and its iterations are independent chains the compiler interleaves.
+    constexpr int kJsPass = kPbuf / 100;
+    constexpr int kTerms = kJsPass * 100;
+    __shared__ double s_az[2 * kJsPass];
+    double* s_jsd = s_p;
     const int K = P.K;
     const double dr = P.trunc / 100.0;
+    const int a_step = G * kJsPass;
+    if (!one_alpha && tid < kJsPass) {
+        const int ai = 1 + wg + tid * G;
+        s_az[tid] = ai <= P.NA ? P.alphas[ai] : 0.0;
+        s_az[kJsPass + tid] = ai <= P.NA ? P.Z[ai] : 0.0;
+    }
     for (int b = tid; b < 100; b += NT) {
         const double r = dr * (1 + static_cast<double>(b));
         double g[kMaxK];                                         // independent pdf chains, then the ordered sum
@@ -795,26 +810,26 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
         s_P[b] = Pr + 1e-10;
     }
     __syncthreads();
-    // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
-    // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25)
-    constexpr int kJsPass = kPbuf / 100;
-    double* s_jsd = s_p;
-    for (int a0 = 1 + wg; a0 <= P.NA; a0 += G * kJsPass) {
-        for (int idx = tid; idx < kJsPass * 100; idx += NT) {
+    for (int a0 = 1 + wg; a0 <= P.NA; a0 += a_step) {
+        const int n_terms = one_alpha ? 100 : min(kJsPass, (P.NA - a0) / G + 1) * 100;   // this pass's alphas
+#pragma unroll 4
+        for (int q = 0; q < (kTerms + NT - 1) / NT; ++q) {
+            const int idx = tid + q * NT;
+            if (idx >= n_terms) break;
             const int a = idx / 100, b = idx - a * 100;
-            const int ai = a0 + a * G;
-            if (ai > P.NA) continue;
-            const double alpha = one_alpha ? pf_alpha : P.alphas[ai];
-            const double pf = one_alpha ? pf_Z : P.Z[ai];
+            const double alpha = one_alpha ? pf_alpha : s_az[a];
+            const double pf = one_alpha ? pf_Z : s_az[kJsPass + a];
             const double r = dr * (1 + static_cast<double>(b));
             const double Pr = s_P[b];
             const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
             const double M = 0.5 * (Pr + Q);
-            s_jsd[idx] = 0.5 * (Pr * log(Pr / M) + Q * log(Q / M));
+            s_jsd[idx] = 0.5 * (Pr * log_pos(Pr / M) + Q * log_pos(Q / M));   // lo_math.h, <= 1 ulp from log
         }
         __syncthreads();
         if (tid < kJsPass) {
-            const int ai = a0 + tid * G;
+            const int ai = a0 + tid * G, an = ai + a_step;
+            double nx_a = 0.0, nx_z = 0.0;                       // next pass's alpha and Z, in flight during the sum
+            if (!one_alpha && an <= P.NA) { nx_a = P.alphas[an]; nx_z = P.Z[an]; }
             if (ai <= P.NA) {
                 double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
                 const double* row = s_jsd + tid * 100;
@@ -835,6 +850,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
                 }
                 B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }
+            if (!one_alpha) { s_az[tid] = nx_a; s_az[kJsPass + tid] = nx_z; }
         }
         __syncthreads();
     }

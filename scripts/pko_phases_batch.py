@@ -45,6 +45,14 @@ for B in [int(a) for a in sys.argv[1:]] or [64, 1024]:
     dt = np.array([t[i + 1] - t[i] for i in range(6)], dtype=np.float64)
     print(f"B={B}: batch {ms.value:.3f} ms, job 0 last PKO: em_iters={out[8]} km_iters={out[9]} "
           + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, dt)) + f" total={t[6] - t[0]} cyc", flush=True)
+    tot, em = [], []
+    for o in ctxs:
+        L.lo_debug_counters(o.ctx, out)
+        tot.append(out[6] - out[0])
+        em.append(out[8])
+    tot, em = np.array(tot, dtype=np.float64), np.array(em)
+    print(f"  all jobs: total cyc mean {tot.mean():.0f} max {tot.max():.0f}; em_iters per case "
+          + " ".join(str(int(e)) for e in em[:len(cases)]) + f"; em max {em.max()}", flush=True)
     bo.close()
     for o in ctxs:
         o.close()

@@ -65,7 +65,7 @@ def _check_equal(res, singles):
 
 @pytest.fixture(params=["split", "one_wave"])
 def pko_mode(request, monkeypatch):
-    """The batch's two PKO launch shapes (k_pko_tb<4, false> below 2048 jobs, <1, true> from 2048): forced."""
+    """The batch's two PKO launch shapes (k_pko_tb<4, false> by default, <1, true> with LO_BATCH_ONE_WAVE=1): forced."""
     monkeypatch.setenv("LO_BATCH_ONE_WAVE", "1" if request.param == "one_wave" else "0")
     return request.param
 
