@@ -45,7 +45,8 @@ __global__ void k_inlier(KParams P);
 __global__ void k_correspond_b(const KParams* PB, int with_stats, int init);
 template <int NW, bool ONE_WAVE> __global__ void k_pko_tb(const KParams* PB, int it);
 __global__ void k_accumulate_b(const KParams* PB, int it);
-__global__ void k_accumulate_b1(const KParams* PB, int it);
+template <bool SOLVE> __global__ void k_accumulate_b1(const KParams* PB, int it);
+__global__ void k_solve_b1(const KParams* PB, int it);
 __global__ void k_solve_b(const KParams* PB, int it);
 __global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
 __global__ void k_la(const KParams* Pp, LaParams L, int k, int G);
@@ -1524,6 +1525,10 @@ static constexpr int kBatchPkoWGs = 256;    // PKO workgroups per launch over al
 // LDS alpha table the four-wave split wins at every measured size (2048 jobs 946k vs 828k scans/s, 4096 1.039M vs
 // 1.021M); the one-wave variant stays tested (tests/test_gpu_batch.py) for batches beyond the measured range
 static constexpr int kBatchOneWaveMin = 0x7fffffff;
+// from this many small jobs the accumulate and the solve are two launches (k_accumulate_b1<false> + k_solve_b1):
+// the fused form's fp64 solve holds the 8-wave accumulate at 128 VGPRs (2 workgroups per CU; split: 70, 3 per CU).
+// Measured: 4096 jobs 1.037M -> 1.090M scans/s, 1024 857k -> 875k; at 64-256 jobs the extra launch costs ~1 %.
+static constexpr int kBatchSplitSolveMin = 1024;
 
 struct lo_batch {
     std::vector<lo_ctx*> ctx;
@@ -1532,6 +1537,7 @@ struct lo_batch {
     int pko_max = 1;                 // min over contexts of the single-scan PKO grid
     int pko_budget = kBatchPkoWGs;   // PKO workgroups per launch over all jobs (LO_BATCH_PKO_WGS overrides)
     int one_wave_min = kBatchOneWaveMin;   // jobs from which PKO runs one wave per job (LO_BATCH_ONE_WAVE=0/1 forces)
+    int split_solve_min = kBatchSplitSolveMin;   // jobs from which k_solve_b1 solves (LO_BATCH_FUSED_SOLVE=0/1 forces)
     hipStream_t stream = nullptr;
     std::string err;
     KParams* d_P = nullptr;
@@ -1604,6 +1610,7 @@ lo_batch* lo_batch_create(lo_ctx* const* ctxs, int count, int* err) {
     for (const lo_ctx* c : b->ctx) b->pko_max = std::min(b->pko_max, pko_grid(c->cfg));
     if (const char* e = std::getenv("LO_BATCH_PKO_WGS")) b->pko_budget = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LO_BATCH_ONE_WAVE")) b->one_wave_min = std::atoi(e) ? 1 : 0x7fffffff;
+    if (const char* e = std::getenv("LO_BATCH_FUSED_SOLVE")) b->split_solve_min = std::atoi(e) ? 0x7fffffff : 1;
     const int rc = batch_alloc(b);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_batch_create: %s\n", b->err.c_str());
@@ -1678,7 +1685,12 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
             else
                 hipLaunchKernelGGL((k_pko_tb<4, false>), dim3(pko_wgs, nact), dim3(256), pre_bytes, b->stream, b->d_P, it);
             if (max_acc <= kFuseMaxBlocks) {           // small jobs: one 8-wave workgroup accumulates + solves
-                hipLaunchKernelGGL(k_accumulate_b1, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
+                if (nact < b->split_solve_min) {
+                    hipLaunchKernelGGL(k_accumulate_b1<true>, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
+                } else {
+                    hipLaunchKernelGGL(k_accumulate_b1<false>, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
+                    hipLaunchKernelGGL(k_solve_b1, dim3(nact), dim3(kBlock), 0, b->stream, b->d_P, it);
+                }
             } else {
                 hipLaunchKernelGGL(k_accumulate_b, dim3(max_acc, nact), blk, 0, b->stream, b->d_P, it);
                 hipLaunchKernelGGL(k_solve_b, dim3(nact), dim3(kSolveThreads), 0, b->stream, b->d_P, it);

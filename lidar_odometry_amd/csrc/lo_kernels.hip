@@ -279,7 +279,11 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve_b(const KParams* __rest
 // sum and per-block fp64 partial is formed exactly as in the multi-block launch; the partials stay in LDS and the
 // same workgroup solves.  No inter-workgroup hand-off: no atomics and no agent-scope fences (whose L2 write-back
 // and invalidate per workgroup dominated the multi-block form once thousands of workgroups were in flight).
+// SOLVE = false (the default batch form): the per-block partials go to the job's blk_part and k_solve_b1 solves --
+// the fp64 solve's registers then size neither launch (fused, the solve pins this 8-wave kernel at 128 VGPRs plus
+// scratch spills, 2 workgroups per CU).
 constexpr int kAcc1Threads = 512;
+template <bool SOLVE>
 __global__ __launch_bounds__(kAcc1Threads) void k_accumulate_b1(const KParams* __restrict__ PB, int it) {
     const KParams& P = PB[blockIdx.y];
     DevState* st = P.st;
@@ -320,7 +324,21 @@ __global__ __launch_bounds__(kAcc1Threads) void k_accumulate_b1(const KParams* _
         }
         __syncthreads();
     }
-    solve_tail<kBlock>(P, it, 0, s_part, nb);
+    if (SOLVE) {
+        solve_tail<kBlock>(P, it, 0, s_part, nb);
+    } else {
+        for (int k = tid; k < nb * kNE; k += kAcc1Threads) P.blk_part[k] = s_part[k];
+    }
+}
+template __global__ void k_accumulate_b1<true>(const KParams*, int);
+template __global__ void k_accumulate_b1<false>(const KParams*, int);
+
+// The solve after k_accumulate_b1<false>: one 256-thread workgroup per job, the same solve_tail<kBlock> over the same
+// partials as the fused form (bit-identical), with a 256-thread register budget.
+__global__ __launch_bounds__(kBlock) void k_solve_b1(const KParams* __restrict__ PB, int it) {
+    const KParams& P = PB[blockIdx.x];
+    if (P.st->done) return;
+    solve_tail<kBlock>(P, it, 0, P.blk_part, P.nb_acc);
 }
 
 // ====================================================================================================

@@ -63,10 +63,13 @@ def _check_equal(res, singles):
             assert r.alpha == alpha, f"job {j}: alpha {r.alpha} vs {alpha}"
 
 
-@pytest.fixture(params=["split", "one_wave"])
+@pytest.fixture(params=["split", "one_wave", "split_solve"])
 def pko_mode(request, monkeypatch):
-    """The batch's two PKO launch shapes (k_pko_tb<4, false> by default, <1, true> with LO_BATCH_ONE_WAVE=1): forced."""
+    """The batch's launch shapes, forced: the two PKO forms (k_pko_tb<4, false> by default, <1, true> with
+    LO_BATCH_ONE_WAVE=1) with the fused accumulate + solve, and the four-wave PKO with the separate k_solve_b1 (the
+    default from 1024 jobs, LO_BATCH_FUSED_SOLVE=0)."""
     monkeypatch.setenv("LO_BATCH_ONE_WAVE", "1" if request.param == "one_wave" else "0")
+    monkeypatch.setenv("LO_BATCH_FUSED_SOLVE", "0" if request.param == "split_solve" else "1")
     return request.param
 
 
