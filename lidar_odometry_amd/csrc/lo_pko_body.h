@@ -277,15 +277,21 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         if (j >= 0) s_p[j * kStride + 64 * s + lane] = p[s];
     }
     __syncthreads();
+    // every component's pdfs of the current iteration, read right after the barrier TOGETHER with the change test's
+    // s_dm values (one LDS round trip per iteration instead of two: the compare no longer gates these reads)
+    double pv[K][SPL];
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) pv[q][s] = s_p[q * kStride + 64 * s + lane];
     int buf = 0;
     for (int em = 0; em < 100; ++em) {
-        const double* sp = s_p + buf * kBuf;
         double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-            double sr = sp[64 * s + lane];                 // pdfs are >= +0 (or NaN): 0 + p_0 == p_0
+            double sr = pv[0][s];                          // pdfs are >= +0 (or NaN): 0 + p_0 == p_0
 #pragma unroll
-            for (int q = 1; q < K; ++q) sr += sp[q * kStride + 64 * s + lane];
+            for (int q = 1; q < K; ++q) sr += pv[q][s];
             const double isr = have[s] ? rcp64_1n(sr) : 0.0;
             const double r = p[s] * isr;
             v[0] += r;
@@ -314,9 +320,22 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
             if (j >= 0) spn[j * kStride + 64 * s + lane] = p[s];
         }
         __syncthreads();
+        double dmv[kMaxK];
+#pragma unroll
+        for (int q = 1; q < K; ++q) dmv[q] = s_dm[buf * kMaxK + q];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) pv[q][s] = spn[q * kStride + 64 * s + lane];
+        // pin the pdf reads above the exit branch (the compiler would otherwise sink them below it, behind the
+        // s_dm round trip)
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) asm volatile("" : "+v"(pv[q][s]));
         double change = 0.0;
 #pragma unroll
-        for (int q = 1; q < K; ++q) change += s_dm[buf * kMaxK + q];
+        for (int q = 1; q < K; ++q) change += dmv[q];
         LO_COUNT(dbg, 8, em + 1);
         if (change < 1e-6) break;
         buf ^= 1;
