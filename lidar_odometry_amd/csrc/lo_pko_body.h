@@ -294,9 +294,11 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
             for (int q = 1; q < K; ++q) sr += pv[q][s];
             const double isr = have[s] ? rcp64_1n(sr) : 0.0;
             const double r = p[s] * isr;
-            v[0] += r;
-            v[1] += r * x[s];
-            v[2] += (r * d[s]) * d[s];
+            // the first sample's terms start the sums (no "0 + t": r >= +0, so only the sign of an all-zero
+            // total could differ, and no value downstream depends on it)
+            v[0] = s == 0 ? r : v[0] + r;
+            v[1] = s == 0 ? r * x[s] : v[1] + r * x[s];
+            v[2] = s == 0 ? (r * d[s]) * d[s] : v[2] + (r * d[s]) * d[s];
         }
         wave_totals4<3>(v);
         const double Nk = v[0];
@@ -435,10 +437,10 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
             const double isr = have[s] ? rcp64_1n(sr) : 0.0;
 #pragma unroll
             for (int q = 0; q < K; ++q) {
-                const double r = p[q][s] * isr;
-                v[q] += r;
-                if (q > 0) v[K + q - 1] += r * x[s];
-                v[2 * K - 1 + q] += (r * d[q][s]) * d[q][s];
+                const double r = p[q][s] * isr;       // first sample starts the sums, as gmm_fit_split
+                v[q] = s == 0 ? r : v[q] + r;
+                if (q > 0) v[K + q - 1] = s == 0 ? r * x[s] : v[K + q - 1] + r * x[s];
+                v[2 * K - 1 + q] = s == 0 ? (r * d[q][s]) * d[q][s] : v[2 * K - 1 + q] + (r * d[q][s]) * d[q][s];
             }
         }
         wave_totals8<3 * K - 1>(v);
