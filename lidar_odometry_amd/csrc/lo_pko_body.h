@@ -801,6 +801,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
         }
     }
     __syncthreads();
+    LO_STAMP(dbg, 12);
     if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
 
     // ---- 4. JS divergence for this workgroup's alphas (calculate_js_divergence :710-787) ----
@@ -811,10 +812,12 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     constexpr int kJsPass = kPbuf / 100;
     constexpr int kTerms = kJsPass * 100;
     __shared__ double s_az[2 * kJsPass];
+    __shared__ int s_nan[kJsPass];                              // NaN terms per row of the current pass
     double* s_jsd = s_p;
     const int K = P.K;
     const double dr = P.trunc / 100.0;
     const int a_step = G * kJsPass;
+    if (tid < kJsPass) s_nan[tid] = 0;                          // ordered by the barrier after the bins
     if (!one_alpha && tid < kJsPass) {
         const int ai = 1 + wg + tid * G;
         s_az[tid] = ai <= P.NA ? P.alphas[ai] : 0.0;
@@ -831,6 +834,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
         s_P[b] = Pr + 1e-10;
     }
     __syncthreads();
+    LO_STAMP(dbg, 10);
     for (int a0 = 1 + wg; a0 <= P.NA; a0 += a_step) {
         const int n_terms = one_alpha ? 100 : min(kJsPass, (P.NA - a0) / G + 1) * 100;   // this pass's alphas
 #pragma unroll 4
@@ -844,34 +848,39 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             const double Pr = s_P[b];
             const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
             const double M = 0.5 * (Pr + Q);
-            s_jsd[idx] = 0.5 * (Pr * log_pos(Pr / M) + Q * log_pos(Q / M));   // lo_math.h, <= 1 ulp from log
+            const double t = 0.5 * (Pr * log_pos(Pr / M) + Q * log_pos(Q / M));   // lo_math.h, <= 1 ulp from log
+            // the reference skips NaN terms in its sum and count: the term is stored as +0 (adding +0 to the sum,
+            // which starts at +0, is the same as skipping it) and counted here, so the sequential sum below is a
+            // plain chain of adds
+            const bool bad = isnan(t);
+            if (bad) atomicAdd(&s_nan[a], 1);
+            s_jsd[idx] = bad ? 0.0 : t;
         }
         __syncthreads();
+        LO_STAMP(dbg, 11);
         if (tid < kJsPass) {
             const int ai = a0 + tid * G, an = ai + a_step;
             double nx_a = 0.0, nx_z = 0.0;                       // next pass's alpha and Z, in flight during the sum
             if (!one_alpha && an <= P.NA) { nx_a = P.alphas[an]; nx_z = P.Z[an]; }
             if (ai <= P.NA) {
-                double cost = 0.0, cnt = 0.0;                    // sequential, bin order, NaN skipped
+                double cost = 0.0;                               // sequential, bin order (NaN terms are +0)
+                const double cnt = static_cast<double>(100 - s_nan[tid]);
                 const double* row = s_jsd + tid * 100;
-                double vb[10], vn[10];                           // LDS reads of the next 10 bins in flight while
+                double vb[20], vn[20];                           // LDS reads of the next 20 bins in flight while
 #pragma unroll                                                   // the serial adds consume the current ones
-                for (int q = 0; q < 10; ++q) vb[q] = row[q];
-                for (int b0 = 0; b0 < 100; b0 += 10) {
+                for (int q = 0; q < 20; ++q) vb[q] = row[q];
+                for (int b0 = 0; b0 < 100; b0 += 20) {
 #pragma unroll
-                    for (int q = 0; q < 10; ++q) vn[q] = (b0 + 10 < 100) ? row[b0 + 10 + q] : 0.0;
+                    for (int q = 0; q < 20; ++q) vn[q] = (b0 + 20 < 100) ? row[b0 + 20 + q] : 0.0;
 #pragma unroll
-                    for (int q = 0; q < 10; ++q) {
-                        const bool ok = !isnan(vb[q]);
-                        cost += ok ? vb[q] : 0.0;                // cost starts at +0: adding +0 == skipping
-                        cnt += ok ? 1.0 : 0.0;
-                    }
+                    for (int q = 0; q < 20; ++q) cost += vb[q];
 #pragma unroll
-                    for (int q = 0; q < 10; ++q) vb[q] = vn[q];
+                    for (int q = 0; q < 20; ++q) vb[q] = vn[q];
                 }
                 B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }
             if (!one_alpha) { s_az[tid] = nx_a; s_az[kJsPass + tid] = nx_z; }
+            s_nan[tid] = 0;                                      // read above; the next pass counts after the barrier
         }
         __syncthreads();
     }

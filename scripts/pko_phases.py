@@ -37,5 +37,7 @@ for f in (11, 13, 17, 21, 25, 31):
     tot += dt
     print(f"frame {f}: n={len(pts)} em_iters={out[8]} km_iters={out[9]} launch={ms.value * 1e3:.1f} us "
           + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, dt)) + f" total={t[6] - t[0]} cyc"
-          + f" | per EM iter {dt[4] / max(out[8], 1):.0f} cyc", flush=True)
+          + f" | per EM iter {dt[4] / max(out[8], 1):.0f} cyc"
+          + f" | JS: post-EM barrier {out[12] - t[5]} gpdf {out[10] - out[12]} terms {out[11] - out[10]}"
+          + f" sum {t[6] - out[11]}", flush=True)
 print("mean share: " + " ".join(f"{nm}={v / tot.sum():.2f}" for nm, v in zip(names, tot)))
