@@ -536,9 +536,32 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // per-block (count, sum, M2) by a Chan merge about the global mean (IterativeClosestPointOptimizer.cpp:304-316);
 // later iterations: DevState::scale.  With nb <= 64 every block sits in wave 0, so the result does not depend on
 // NW.  lead: this workgroup publishes the iteration-0 scale.
+// The single-wave prefix's global loads (nb <= 64, wave 0, lane = block), issued by pko_body in the same round trip
+// as the done flag instead of after it.
+struct PrefixLoads {
+    int c;
+    double bs, bm, sc;
+    uint64_t wm[kWavesPerBlock];
+};
+
+__device__ __forceinline__ void prefix_loads(const KParams& P, const ScanBufs& B, int it, PrefixLoads& pl) {
+    const int lane = threadIdx.x & 63, nb = P.nb;
+    const bool calc = it == 0 && !P.scale_given;
+    pl.c = lane < nb ? B.blk_cnt[lane] : 0;
+    pl.bs = (calc && lane < nb) ? 0.0 + P.blk_sum[lane] : 0.0;   // as `lsum += ...` from +0
+    pl.bm = (calc && lane < nb) ? P.blk_m2[lane] : 0.0;
+#pragma unroll
+    for (int q = 0; q < kWavesPerBlock; ++q) {
+        const int w = q * 64 + lane;
+        pl.wm[q] = w < nb * kWavesPerBlock ? B.wmask[w] : 0;
+    }
+    pl.sc = calc ? 0.0 : B.st->scale;
+}
+
 template <int NW>
 __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, int it, bool lead, int* s_pre,
-                                           int& nc_out, double& scale_out, uint64_t* s_wm = nullptr) {
+                                           int& nc_out, double& scale_out, uint64_t* s_wm = nullptr,
+                                           const PrefixLoads* pre = nullptr) {
     constexpr int NT = NW * 64;
     DevState* st = B.st;
     __shared__ int s_iscan[NW];
@@ -556,14 +579,16 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
         // validity ballots prefetched into LDS for the sample phase.
         if (wid == 0) {
             const int nb = P.nb;
-            const int c = lane < nb ? B.blk_cnt[lane] : 0;
-            const double bs = (calc && lane < nb) ? 0.0 + P.blk_sum[lane] : 0.0;   // as `lsum += ...` from +0
-            const double bm = (calc && lane < nb) ? P.blk_m2[lane] : 0.0;
+            PrefixLoads own;
+            if (!pre) prefix_loads(P, B, it, own);
+            const PrefixLoads& L = pre ? *pre : own;
+            const int c = L.c;
+            const double bs = L.bs, bm = L.bm;
             if (s_wm) {
 #pragma unroll
                 for (int q = 0; q < kWavesPerBlock; ++q) {
                     const int w = q * 64 + lane;
-                    if (w < nb * kWavesPerBlock) s_wm[w] = B.wmask[w];
+                    if (w < nb * kWavesPerBlock) s_wm[w] = L.wm[q];
                 }
             }
             int inc = c;
@@ -580,7 +605,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
                 const double var = total > 0 ? M2 / total : 0.0;
                 scale = sqrt(var) / 6.0;                       // IterativeClosestPointOptimizer.cpp:314-315
             } else {
-                scale = st->scale;
+                scale = L.sc;
             }
             if (lane == 0) {
                 s_nc = total;
@@ -664,7 +689,12 @@ template <int NW, bool ONE_WAVE>
 __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, int it, int wg, int G) {
     constexpr int NT = NW * 64;
     DevState* st = B.st;
-    if (st->done) return;
+    // the done flag, the single-wave prefix's loads and the prefetch below go out in one round trip; the flag is
+    // tested once they are in flight (a converged scan leaves without writing anything)
+    const int done0 = st->done;
+    PrefixLoads pl;
+    const bool wave_prefix = !P.direct_res && P.nb <= 64;
+    if (wave_prefix && threadIdx.x < 64) prefix_loads(P, B, it, pl);
     unsigned long long* dbg = nullptr;
 #ifdef LO_PKO_STAMPS
     if (wg == 0) dbg = st->dbg;
@@ -700,13 +730,14 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     const bool one_alpha = G >= P.NA;                       // the single-scan launch: alpha 1 + wg only
     double pf_alpha = 0.0, pf_Z = 0.0;
     if (one_alpha && 1 + wg <= P.NA) { pf_alpha = P.alphas[1 + wg]; pf_Z = P.Z[1 + wg]; }
+    if (done0) return;
 
     // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
     int nc;
     double s_scale;
     __shared__ uint64_t s_wm[kWavesPerBlock * 64];             // ballots of <= 64 blocks, prefetched by the prefix
     const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? s_wm : nullptr;
-    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm);
+    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm, wave_prefix ? &pl : nullptr);
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
         if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
         return;
