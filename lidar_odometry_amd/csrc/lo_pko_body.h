@@ -59,9 +59,18 @@ __device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {
 #ifdef LO_PKO_STAMPS
 #define LO_STAMP(dbg, i) do { if ((dbg) && threadIdx.x == 0) (dbg)[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #define LO_COUNT(dbg, i, v) do { if ((dbg) && threadIdx.x == 0) (dbg)[i] = (v); } while (0)
+// a stamp after this wave's outstanding loads have landed
+#define LO_STAMP_WAIT(dbg, i, cond)                                                        \
+    do {                                                                                   \
+        if ((dbg) && (cond)) {                                                             \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                    \
+            (dbg)[i] = __builtin_amdgcn_s_memtime();                                       \
+        }                                                                                  \
+    } while (0)
 #else
 #define LO_STAMP(dbg, i) do { } while (0)
 #define LO_COUNT(dbg, i, v) do { } while (0)
+#define LO_STAMP_WAIT(dbg, i, cond) do { } while (0)
 #endif
 
 // exp(y) for y <= 0 or NaN (the E-step exponent -(d^2) * 0.5 / var): Cody-Waite reduction by ln2 and the
@@ -737,7 +746,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     double s_scale;
     __shared__ uint64_t s_wm[kWavesPerBlock * 64];             // ballots of <= 64 blocks, prefetched by the prefix
     const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? s_wm : nullptr;
-    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm, wave_prefix ? &pl : nullptr);
+    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm, &pl);   // pl is set where it is read (nb <= 64)
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
         if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
         return;
@@ -773,6 +782,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
         } else {
             rank = pko_sample(P, nc, sidx);
         }
+        LO_STAMP_WAIT(dbg, 13, sidx == 0);
         double v;
         if (P.direct_res) {
             v = P.direct_res[rank];
@@ -810,6 +820,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
                 v = residual_f64(P.tab[B.slot[pidx]], wx, wy, wz) / sden;   // :321-326
             }
         }
+        LO_STAMP_WAIT(dbg, 14, sidx == 0);
         s_sd[sidx] = v;
     }
     __syncthreads();

@@ -39,5 +39,6 @@ for f in (11, 13, 17, 21, 25, 31):
           + " ".join(f"{nm}={int(v)}" for nm, v in zip(names, dt)) + f" total={t[6] - t[0]} cyc"
           + f" | per EM iter {dt[4] / max(out[8], 1):.0f} cyc"
           + f" | JS: post-EM barrier {out[12] - t[5]} gpdf {out[10] - out[12]} terms {out[11] - out[10]}"
-          + f" sum {t[6] - out[11]}", flush=True)
+          + f" sum {t[6] - out[11]}"
+          + f" | sample: events {out[13] - t[1]} residual {out[14] - out[13]} barrier {t[2] - out[14]}", flush=True)
 print("mean share: " + " ".join(f"{nm}={v / tot.sum():.2f}" for nm, v in zip(names, tot)))
