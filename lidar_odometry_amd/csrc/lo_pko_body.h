@@ -804,8 +804,15 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
                 const int c = __popcll(mk);
                 if (w == q && k >= c) { k -= c; w = q + 1; mk = m4[q + 1]; }
             }
-            for (int q = 0; q < k; ++q) mk &= mk - 1;
-            const int bit = max(__ffsll(static_cast<unsigned long long>(mk)) - 1, 0);
+            // position of the k-th set bit of mk by halving windows (6 popcounts) instead of clearing k bits one
+            // at a time (up to 63 dependent steps, the wave waits for its largest k); same bit
+            int bit = 0;
+#pragma unroll
+            for (int wdt = 32; wdt >= 1; wdt >>= 1) {
+                const int c = __popcll(mk & ((1ull << wdt) - 1));
+                if (k >= c) { k -= c; mk >>= wdt; bit += wdt; }
+            }
+            bit = min(bit, kWave - 1);
             const int pidx = b * kBlock + w * kWave + bit;
             if (P.kd_res) {
                 v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
