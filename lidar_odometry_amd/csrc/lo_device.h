@@ -36,6 +36,8 @@ constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
 constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP row)
 constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
+constexpr int kGnSyncWords = 2048;  // persistent GN launch (lo_persist.hip): arrival counters per context
+constexpr int kGnCandWords = 48;    //   and the words of one candidate's solved-step record
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;
@@ -136,6 +138,26 @@ struct KParams {
     DevState* st;
 };
 
+// Persistent GN launch (lo_persist.hip).  Correspondence sets of the candidates (the next iteration's correspondences at each candidate's pose),
+// [parity][NA + 1] sets of cs_pts points each.
+struct GnSets {
+    int32_t* slot;
+    double* res;
+    uint64_t* wmask;
+    int32_t* cnt;
+    int cs_pts;                                             // points per set (a multiple of kBlock)
+};
+// Kernel arguments besides the scan's KParams.
+struct GnArgs {
+    unsigned* sync;
+    float* cand;                                            // [2][NA + 1][kCandWords]
+    GnSets sets;
+    int G;                                                  // PKO workgroups (one alpha of the JS grid each)
+    int W;                                                  // workgroups per alpha candidate
+    int per;                                                // 256-point blocks per candidate workgroup
+    int skip_corr0;                                         // the first correspondence search ran as its own launch
+};
+
 // Lookahead launches (lo_lookahead.hip): one candidate chain's results for GN iterations k, k + 1 of a launch.
 struct LaRec {
     lo_iter_log log[2];
@@ -176,6 +198,47 @@ struct ScanBufs {
 __device__ __forceinline__ ScanBufs own_bufs(const KParams& P) {
     return ScanBufs{P.slot, P.wmask, P.blk_cnt, P.js, P.st, nullptr, P.res_out};
 }
+
+// ---------------------------------------------------------------------------------------------------
+// Memory policy of the buffers one workgroup hands to another INSIDE a launch (the persistent GN loop k_gn,
+// lo_persist.hip).  Mem<false>: plain loads / stores (the hand-off is a kernel boundary).  Mem<true>: agent-scope
+// relaxed atomic loads / stores on the global address space -- `global_load/store ... sc1`: stores write through
+// the XCD's L2, loads bypass the CU's L1 -- so a consumer that saw the producer's counter after the producer drained
+// its stores (s_waitcnt vmcnt(0)) reads the fresh bytes on any XCD without release / acquire fences
+// (MI355X_MICROARCH.md "inter-workgroup visibility", the one-lane-signals / sc1-poll row).  Every load of a handed-off
+// word in such a launch must go through Mem<true> (never the scalar path).
+// ---------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+
+template <bool SC1> struct Mem;
+template <> struct Mem<false> {
+    template <typename T> __device__ static __forceinline__ T ld(const T* p) { return *p; }
+    template <typename T> __device__ static __forceinline__ void st(T* p, T v) { *p = v; }
+    template <typename T> __device__ static __forceinline__ void st_stream(T* p, T v) { __builtin_nontemporal_store(v, p); }
+};
+template <> struct Mem<true> {
+    template <typename T> __device__ static __forceinline__ T ld(const T* p) {
+        static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte words");
+        if constexpr (sizeof(T) == 4) {
+            const uint32_t u = __hip_atomic_load((g_u32*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_bit_cast(T, u);
+        } else {
+            const unsigned long long u = __hip_atomic_load((g_u64*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_bit_cast(T, u);
+        }
+    }
+    template <typename T> __device__ static __forceinline__ void st(T* p, T v) {
+        static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte words");
+        if constexpr (sizeof(T) == 4)
+            __hip_atomic_store((g_u32*)(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_store((g_u64*)(p), __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // hand-off stores are never non-temporal (write-through is what makes them visible)
+    template <typename T> __device__ static __forceinline__ void st_stream(T* p, T v) { st(p, v); }
+};
 
 // ---------------------------------------------------------------------------------------------------
 // Bit-faithful scalar numerics (compiled with -ffp-contract=off; see DESIGN.md "fp order")
@@ -379,12 +442,13 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 // calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the index of the FIRST alpha with
 // the strictly smallest JS cost, 0 (min_scale_factor) if none is below DBL_MAX.  Every wave computes it
 // redundantly from P.js (lexicographic (cost, index) minimum == first strict minimum).
+template <bool SC1 = false>
 __device__ __forceinline__ int pko_select_index(const KParams& P, const double* js) {
     const int lane = threadIdx.x & 63;
     double bv = 1.7976931348623157e308;
     int bi = 0x7fffffff;
     for (int i = 1 + lane; i <= P.NA; i += 64) {
-        const double v = js[i];
+        const double v = Mem<SC1>::ld(js + i);
         if (v < bv) { bv = v; bi = i; }
     }
 #pragma unroll
@@ -445,16 +509,33 @@ __device__ __forceinline__ void scan_pose(const KParams& P, int init, int blk, f
     }
 }
 
+// Where a correspondence pass writes: per point the accepted slot and fp64 residual, per wave the validity ballot, per
+// block the accepted count and (iteration 0) the residual sum / M2.  The context's own buffers (corr_out(P)), or an
+// alpha candidate's set in the persistent launch (lo_persist.hip: the next iteration's correspondences at the
+// candidate's pose).
+struct CorrOut {
+    int32_t* slot;
+    double* res;                      // nullable
+    uint64_t* wmask;
+    int32_t* blk_cnt;
+    double* blk_sum;                  // with_stats only
+    double* blk_m2;
+};
+__device__ __forceinline__ CorrOut corr_out(const KParams& P) {
+    return CorrOut{P.slot, P.res_out, P.wmask, P.blk_cnt, P.blk_sum, P.blk_m2};
+}
+
 // Per-wave validity ballots, per-block accepted count and (iteration 0, with_stats) the per-block
 // (count, sum, M2) of the accepted fp64 residuals for the stable merge of the residual variance.
-__device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, double r, int with_stats, int vb) {
+template <bool SC1 = false>
+__device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, double r, int with_stats, int vb) {
     __shared__ double s_red[kWavesPerBlock];
     __shared__ int s_cnt[kWavesPerBlock];
     __shared__ double s_mean;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t m = __ballot(valid);
     if (lane == 0) {
-        P.wmask[vb * kWavesPerBlock + wid] = m;
+        Mem<SC1>::st(O.wmask + vb * kWavesPerBlock + wid, static_cast<uint64_t>(m));
         s_cnt[wid] = __popcll(m);
     }
     if (!with_stats) {
@@ -462,7 +543,7 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
         if (tid == 0) {
             int c = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) c += s_cnt[w];
-            P.blk_cnt[vb] = c;
+            Mem<SC1>::st(O.blk_cnt + vb, c);
         }
         return;
     }
@@ -473,8 +554,8 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
         int c = 0;
         double sum = 0.0;
         for (int w = 0; w < kWavesPerBlock; ++w) { c += s_cnt[w]; sum += s_red[w]; }
-        P.blk_cnt[vb] = c;
-        P.blk_sum[vb] = sum;
+        Mem<SC1>::st(O.blk_cnt + vb, c);
+        Mem<SC1>::st(O.blk_sum + vb, sum);
         s_mean = c > 0 ? sum / c : 0.0;
     }
     __syncthreads();
@@ -487,16 +568,51 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
     if (tid == 0) {
         double m2 = 0.0;
         for (int w = 0; w < kWavesPerBlock; ++w) m2 += s_red[w];
-        P.blk_m2[vb] = m2;
+        Mem<SC1>::st(O.blk_m2 + vb, m2);
     }
+}
+template <bool SC1 = false>
+__device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, double r, int with_stats, int vb) {
+    corr_epilogue<SC1>(corr_out(P), valid, r, with_stats, vb);
+}
+
+// find_correspondences' per-point step (IterativeClosestPointOptimizer.cpp:606-641) for point i at pose T, then the
+// block's ballots / count / (iteration 0) residual stats.
+// SC1: the persistent launch (lo_persist.hip) -- slot / residual / ballots / counts are handed to other workgroups of
+// the same launch, so they are stored write-through (Mem<true>) instead of streaming.
+template <bool SC1>
+__device__ __forceinline__ void correspond_tail(const KParams& P, const CorrOut& O, const float (&T)[12], float px,
+                                                float py, float pz, int i, int n, int with_stats, int blk) {
+    int slot = -1;
+    double r = 0.0;
+    if (i < n) {
+        float wx, wy, wz;
+        transform_pt(T, px, py, pz, wx, wy, wz);
+        const int s = lookup_surfel(P.tab, P.log2cap, P.l1scale, wx, wy, wz);
+        if (s >= 0) {
+            r = residual_f64(P.tab[s], wx, wy, wz);
+            if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, :630)
+        }
+        // streaming stores: read back only by the next kernels (PKO sample, accumulate), not by this launch
+        Mem<SC1>::st_stream(O.slot + i, slot);
+        if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
+        if (O.res) Mem<SC1>::st_stream(O.res + i, r);
+    }
+    corr_epilogue<SC1>(O, slot >= 0, r, with_stats, blk);
+}
+template <bool SC1>
+__device__ __forceinline__ void correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
+                                                int i, int n, int with_stats, int blk) {
+    correspond_tail<SC1>(P, corr_out(P), T, px, py, pz, i, n, with_stats, blk);
 }
 
 // ---------------------------------------------------------------------------------------------------
 // One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
 // fp32 products fl(fl(w J_i) J_j) as the reference forms them.
+template <bool SC1 = false>
 __device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot, const float (&T)[12], double scale,
                                           float dl, int i, float (&acc)[kNE]) {
-    const int s = slot[i];
+    const int s = Mem<SC1>::ld(slot + i);
     if (s < 0) return;
     const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
     const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i

@@ -35,26 +35,6 @@ namespace lo {
 // the kernel argument (T0 / T0p), block 0 writes the fresh DevState that the later kernels of the scan read.
 // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
 // instead of serialising at the start of every wave.
-__device__ __forceinline__ void correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
-                                                int i, int n, int with_stats, int blk) {
-    int slot = -1;
-    double r = 0.0;
-    if (i < n) {
-        float wx, wy, wz;
-        transform_pt(T, px, py, pz, wx, wy, wz);
-        const int s = lookup_surfel(P.tab, P.log2cap, P.l1scale, wx, wy, wz);
-        if (s >= 0) {
-            r = residual_f64(P.tab[s], wx, wy, wz);
-            if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, :630)
-        }
-        // streaming stores: read back only by the next kernels (PKO sample, accumulate), not by this launch
-        __builtin_nontemporal_store(slot, &P.slot[i]);
-        if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
-        if (P.res_out) __builtin_nontemporal_store(r, &P.res_out[i]);
-    }
-    corr_epilogue(P, slot >= 0, r, with_stats, blk);
-}
-
 __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats, int init, int blk) {
     const int i = blk * kBlock + threadIdx.x;
     const int n = scan_n(P);
@@ -67,7 +47,7 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
     for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
     if (!init && done) return;
     scan_pose(P, init, blk, T);
-    correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
+    correspond_tail<false>(P, T, px, py, pz, i, n, with_stats, blk);
 }
 
 // XCD-aware block order: the hardware hands consecutive workgroups to the 8 XCDs round-robin; logical block
@@ -262,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) 
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_T[k];
-    correspond_tail(P, T, px, py, pz, i, n, 0, blk);
+    correspond_tail<false>(P, T, px, py, pz, i, n, 0, blk);
 }
 
 // Batched solve (jobs with more than kFuseMaxBlocks accumulate blocks present): one block per job, with the

@@ -508,36 +508,45 @@ __device__ __forceinline__ void gmm_fit_1w_dispatch(const double* s_sd, int S, c
 // takes candidate wgi / W (W = ceil(nb_acc / kSpecBlocksPerWG)) and its kSpecBlocksPerWG 256-point blocks
 // starting at kSpecBlocksPerWG * (wgi % W); each block's partial is formed exactly as accumulate_body forms it
 // (one point per thread, fp32 wave_total, fp64 sum over the 4 waves), so the solve is bit-identical.
-__device__ void acc_candidate(const KParams& P, double scale, int wgi) {
-    const int nb = P.nb_acc;
-    const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
-    const int c = wgi / W, part = wgi - c * W;
-    if (c > P.NA) return;
-    const float dl = static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
+// The normal-equation partials of blocks [vb0, vb1) with Huber delta dl into dst[vb][kNE], each block's partial formed
+// exactly as accumulate_body forms it (one point per thread, fp32 wave_total, fp64 sum over the 4 waves).  SC1 (the
+// persistent launch): the slots are read and the partials written through Mem<true>.
+template <bool SC1>
+__device__ void acc_blocks(const KParams& P, const int32_t* slot, const float (&T)[12], double scale, float dl, int vb0,
+                           int vb1, double* dst) {
     __shared__ float s_acc[kWavesPerBlock][kNE];
     const int tid = threadIdx.x, wid = tid >> 6;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
     const int n = scan_n(P);
-    double* dst = P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE;
-    const int vb1 = min(nb, (part + 1) * kSpecBlocksPerWG);
-    for (int vb = part * kSpecBlocksPerWG; vb < vb1; ++vb) {
+    for (int vb = vb0; vb < vb1; ++vb) {
         float acc[kNE];
 #pragma unroll
         for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
         const int i = vb * kBlock + tid;
-        if (i < n) acc_point(P, T, scale, dl, i, acc);
+        if (i < n) acc_point<SC1>(P, slot, T, scale, dl, i, acc);
         wave_totals_f32<kNE>(acc, s_acc[wid]);
         __syncthreads();
         if (tid < kNE) {
             double v = 0.0;
 #pragma unroll
             for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
-            dst[static_cast<size_t>(vb) * kNE + tid] = v;
+            Mem<SC1>::st(dst + static_cast<size_t>(vb) * kNE + tid, v);
         }
         __syncthreads();
     }
+}
+__device__ __forceinline__ float cand_delta(const KParams& P, int c) {
+    return static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
+}
+__device__ void acc_candidate(const KParams& P, double scale, int wgi) {
+    const int nb = P.nb_acc;
+    const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
+    const int c = wgi / W, part = wgi - c * W;
+    if (c > P.NA) return;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+    acc_blocks<false>(P, P.slot, T, scale, cand_delta(P, c), part * kSpecBlocksPerWG, min(nb, (part + 1) * kSpecBlocksPerWG),
+                      P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE);
 }
 
 // Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts
@@ -553,18 +562,22 @@ struct PrefixLoads {
     uint64_t wm[kWavesPerBlock];
 };
 
+// SC1 (the persistent launch): the counts / sums / ballots were handed over inside the launch (Mem<true> loads), and
+// the scale of later iterations is the caller's (pl.sc is left 0).
+template <bool SC1 = false>
 __device__ __forceinline__ void prefix_loads(const KParams& P, const ScanBufs& B, int it, PrefixLoads& pl) {
+    using M = Mem<SC1>;
     const int lane = threadIdx.x & 63, nb = P.nb;
     const bool calc = it == 0 && !P.scale_given;
-    pl.c = lane < nb ? B.blk_cnt[lane] : 0;
-    pl.bs = (calc && lane < nb) ? 0.0 + P.blk_sum[lane] : 0.0;   // as `lsum += ...` from +0
-    pl.bm = (calc && lane < nb) ? P.blk_m2[lane] : 0.0;
+    pl.c = lane < nb ? M::ld(B.blk_cnt + lane) : 0;
+    pl.bs = (calc && lane < nb) ? 0.0 + M::ld(P.blk_sum + lane) : 0.0;   // as `lsum += ...` from +0
+    pl.bm = (calc && lane < nb) ? M::ld(P.blk_m2 + lane) : 0.0;
 #pragma unroll
     for (int q = 0; q < kWavesPerBlock; ++q) {
         const int w = q * 64 + lane;
-        pl.wm[q] = w < nb * kWavesPerBlock ? B.wmask[w] : 0;
+        pl.wm[q] = w < nb * kWavesPerBlock ? M::ld(B.wmask + w) : 0;
     }
-    pl.sc = calc ? 0.0 : B.st->scale;
+    pl.sc = (calc || SC1) ? 0.0 : B.st->scale;
 }
 
 template <int NW>
@@ -691,77 +704,64 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
     scale_out = s_scale;
 }
 
-// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
-// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate).
-// ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
-template <int NW, bool ONE_WAVE>
-__device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, int it, int wg, int G) {
-    constexpr int NT = NW * 64;
-    DevState* st = B.st;
-    // the done flag, the single-wave prefix's loads and the prefetch below go out in one round trip; the flag is
-    // tested once they are in flight (a converged scan leaves without writing anything)
-    const int done0 = st->done;
-    PrefixLoads pl;
-    const bool wave_prefix = !P.direct_res && P.nb <= 64;
-    if (wave_prefix && threadIdx.x < 64) prefix_loads(P, B, it, pl);
-    unsigned long long* dbg = nullptr;
-#ifdef LO_PKO_STAMPS
-    if (wg == 0) dbg = st->dbg;
-#endif
-    LO_STAMP(dbg, 0);
-    extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
-    // s_p: the split EM's per-sample pdfs of each component (double-buffered), then the JS terms (>= 20 alphas)
-    constexpr int kPbuf = (2 * kMaxK * 64 * NW > 2000) ? 2 * kMaxK * 64 * NW : 2000;
-    __shared__ double s_sd[kMaxS];
-    __shared__ double s_gmm[3 * kMaxK];
-    __shared__ double s_P[100];
-    __shared__ double s_p[kPbuf];
-    __shared__ double s_dm[2 * kMaxK];
+// LDS of the PKO phases (one instance per workgroup: pko_body, or the persistent launch).
+template <int NW>
+struct PkoLds {
+    // p: the split EM's per-sample pdfs of each component (double-buffered), then the JS terms (>= 20 alphas)
+    static constexpr int kPbuf = (2 * kMaxK * 64 * NW > 2000) ? 2 * kMaxK * 64 * NW : 2000;
+    static constexpr int kJsPass = kPbuf / 100;
+    double sd[kMaxS];
+    double gmm[3 * kMaxK];
+    double Pbin[100];
+    double p[kPbuf];
+    double dm[2 * kMaxK];
+    double az[2 * kJsPass];
+    int nan[kJsPass];                              // NaN terms per row of the current JS pass
+    uint64_t wm[kWavesPerBlock * 64];              // ballots of <= 64 blocks, prefetched by the prefix
+    int32_t draws[kMaxK];                          // k-means draws for S = P.S
+};
 
+// Phase 0: what later phases need but does not depend on n_c, so its latency hides behind the prefix phase: this
+// thread's sample slot (s = tid) event-list bounds and base value for the three shuffle modes, the k-means draws for
+// S = P.S, and (one alpha per workgroup) this alpha and Z.
+struct PkoPrefetch {
+    int lo[3], hi[3], base[3];
+    double alpha, Z;
+};
+template <int NW>
+__device__ __forceinline__ void pko_prefetch(const KParams& P, int wg, int G, PkoPrefetch& pf, PkoLds<NW>& L) {
     const int tid = threadIdx.x;
-    const bool lead = wg == 0;
-
-    // ---- 0. prefetch what later phases need but does not depend on n_c, so its latency hides behind the
-    //         prefix phase: this thread's sample slot (s = tid) event-list bounds and base value for the three
-    //         shuffle modes, the k-means draws for S = P.S, and (one alpha per workgroup) this alpha and Z ----
-    __shared__ int32_t s_draws[kMaxK];
-    int pf_lo[3] = {0, 0, 0}, pf_hi[3] = {0, 0, 0}, pf_base[3] = {0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 3; ++m) { pf.lo[m] = 0; pf.hi[m] = 0; pf.base[m] = 0; }
     if (tid < P.S) {
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
-            pf_lo[m] = P.ev_off[m * (P.S + 1) + tid];
-            pf_hi[m] = P.ev_off[m * (P.S + 1) + tid + 1];
-            pf_base[m] = P.base[m * P.S + tid];
+            pf.lo[m] = P.ev_off[m * (P.S + 1) + tid];
+            pf.hi[m] = P.ev_off[m * (P.S + 1) + tid + 1];
+            pf.base[m] = P.base[m * P.S + tid];
         }
     }
     const int D0 = P.K > 1 ? P.K - 1 : 1;
-    if (tid < D0) s_draws[tid] = P.km_draws[P.S * D0 + tid];
-    const bool one_alpha = G >= P.NA;                       // the single-scan launch: alpha 1 + wg only
-    double pf_alpha = 0.0, pf_Z = 0.0;
-    if (one_alpha && 1 + wg <= P.NA) { pf_alpha = P.alphas[1 + wg]; pf_Z = P.Z[1 + wg]; }
-    if (done0) return;
+    if (tid < D0) L.draws[tid] = P.km_draws[P.S * D0 + tid];
+    pf.alpha = 0.0;
+    pf.Z = 0.0;
+    if (G >= P.NA && 1 + wg <= P.NA) { pf.alpha = P.alphas[1 + wg]; pf.Z = P.Z[1 + wg]; }
+}
 
-    // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
-    int nc;
-    double s_scale;
-    __shared__ uint64_t s_wm[kWavesPerBlock * 64];             // ballots of <= 64 blocks, prefetched by the prefix
-    const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? s_wm : nullptr;
-    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, s_wm, &pl);   // pl is set where it is read (nb <= 64)
-    if (!P.direct_res && nc < P.min_corr) {                     // :298-302
-        if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
-        return;
-    }
-    if constexpr (NW == 4 && !ONE_WAVE) {
-        if (wg >= G) {                                          // after the scale: the candidates need it
-            acc_candidate(P, s_scale, wg - G);
-            return;
-        }
-    }
-    if (lead && tid == 0) st->n_corr = nc;
-    if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
-    const double scale = s_scale;
-    const double sden = (scale < 1e-6) ? 1e-6 : scale;         // std::max(scale, 1e-6)
-    LO_STAMP(dbg, 1);
+// Phases 2-4 of the PKO for n_c >= 1 correspondences with normalisation scale `scale`: the reference's GMM sample,
+// the GMM fit and this workgroup's slice of the JS grid (written to B.js).  SC1 (the persistent launch): the stored
+// residuals / slots are read and the JS costs written through Mem<true>.
+template <int NW, bool ONE_WAVE, bool SC1>
+__device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, int wg, int G, int nc, double scale,
+                                           const PkoPrefetch& pf, const int* s_pre, const uint64_t* s_wmask,
+                                           PkoLds<NW>& L, unsigned long long* dbg) {
+    using M = Mem<SC1>;
+    constexpr int NT = NW * 64;
+    DevState* st = B.st;
+    const int tid = threadIdx.x;
+    const bool lead = wg == 0;
+    const bool one_alpha = G >= P.NA;                       // the single-scan launch: alpha 1 + wg only
+    const double sden = (scale < 1e-6) ? 1e-6 : scale;     // std::max(scale, 1e-6)
 
     // ---- 2. the reference's GMM sample ----
     const int S = min(P.S, nc);
@@ -769,9 +769,9 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
         int rank;
         if (sidx == tid && nc >= P.S && sidx < P.S) {          // prefetched bounds: one round of event loads
             const int mode = (nc <= 65535) ? ((nc & 1) ? 0 : 1) : 2;
-            const int lo0 = mode == 0 ? pf_lo[0] : (mode == 1 ? pf_lo[1] : pf_lo[2]);
-            const int hi0 = mode == 0 ? pf_hi[0] : (mode == 1 ? pf_hi[1] : pf_hi[2]);
-            rank = mode == 0 ? pf_base[0] : (mode == 1 ? pf_base[1] : pf_base[2]);
+            const int lo0 = mode == 0 ? pf.lo[0] : (mode == 1 ? pf.lo[1] : pf.lo[2]);
+            const int hi0 = mode == 0 ? pf.hi[0] : (mode == 1 ? pf.hi[1] : pf.hi[2]);
+            rank = mode == 0 ? pf.base[0] : (mode == 1 ? pf.base[1] : pf.base[2]);
             for (int e0 = lo0; e0 < hi0; e0 += 8) {             // ascending steps: the last one <= n - 1 wins
                 int ev[8];
 #pragma unroll
@@ -796,7 +796,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
 #pragma unroll
             for (int q = 0; q < kWavesPerBlock; ++q)
-                m4[q] = s_wmask ? s_wmask[b * kWavesPerBlock + q] : B.wmask[b * kWavesPerBlock + q];
+                m4[q] = s_wmask ? s_wmask[b * kWavesPerBlock + q] : M::ld(B.wmask + b * kWavesPerBlock + q);
             int w = 0;
             uint64_t mk = m4[0];
 #pragma unroll
@@ -817,70 +817,68 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             if (P.kd_res) {
                 v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
             } else if (B.res) {
-                v = B.res[pidx] / sden;                          // stored by the correspondence launch (same bits)
+                v = M::ld(B.res + pidx) / sden;                  // stored by the correspondence launch (same bits)
             } else {
                 float T[12];
 #pragma unroll
                 for (int q = 0; q < 12; ++q) T[q] = B.pose_in ? B.pose_in[q] : st->pose[q];
                 float wx, wy, wz;
                 transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
-                v = residual_f64(P.tab[B.slot[pidx]], wx, wy, wz) / sden;   // :321-326
+                v = residual_f64(P.tab[M::ld(B.slot + pidx)], wx, wy, wz) / sden;   // :321-326
             }
         }
         LO_STAMP_WAIT(dbg, 14, sidx == 0);
-        s_sd[sidx] = v;
+        L.sd[sidx] = v;
     }
     __syncthreads();
     LO_STAMP(dbg, 2);
 
     // ---- 3. GMM ----
     const int D = P.K > 1 ? P.K - 1 : 1;
-    const int32_t* draws = (S == P.S) ? s_draws : P.km_draws + S * D;
+    const int32_t* draws = (S == P.S) ? L.draws : P.km_draws + S * D;
     if (ONE_WAVE) {                                             // wave 0 alone: see gmm_fit_1w
         switch (P.K) {
-            case 1: gmm_fit_1w_dispatch<1>(s_sd, S, draws, s_gmm); break;
-            case 2: gmm_fit_1w_dispatch<2>(s_sd, S, draws, s_gmm); break;
-            default: gmm_fit_1w_dispatch<3>(s_sd, S, draws, s_gmm); break;
+            case 1: gmm_fit_1w_dispatch<1>(L.sd, S, draws, L.gmm); break;
+            case 2: gmm_fit_1w_dispatch<2>(L.sd, S, draws, L.gmm); break;
+            default: gmm_fit_1w_dispatch<3>(L.sd, S, draws, L.gmm); break;
         }
     } else {
         switch (P.K) {                                          // every wave: see gmm_fit_split
-            case 1: gmm_fit_dispatch<1>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
-            case 2: gmm_fit_dispatch<2>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
-            default: gmm_fit_dispatch<3>(s_sd, S, draws, s_gmm, s_p, s_dm, dbg); break;
+            case 1: gmm_fit_dispatch<1>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
+            case 2: gmm_fit_dispatch<2>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
+            default: gmm_fit_dispatch<3>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
         }
     }
     __syncthreads();
     LO_STAMP(dbg, 12);
-    if (lead && tid < 3 * P.K) st->gmm_out[tid] = s_gmm[tid];
+    if (lead && tid < 3 * P.K) st->gmm_out[tid] = L.gmm[tid];
 
     // ---- 4. JS divergence for this workgroup's alphas (calculate_js_divergence :710-787) ----
     // the EM's pdf buffers are dead now: they hold the terms of kJsPass alphas x 100 bins per pass (a single
     // workgroup per scan -- the batched launch -- needs 5 passes for the 100-alpha grid instead of 25).  The
-    // pass's alphas and Z sit in LDS (s_az), loaded by the summing threads while the previous pass is summed, so
+    // pass's alphas and Z sit in LDS (L.az), loaded by the summing threads while the previous pass is summed, so
     // the term loop issues no global load and its iterations are independent chains the compiler interleaves.
-    constexpr int kJsPass = kPbuf / 100;
+    constexpr int kJsPass = PkoLds<NW>::kJsPass;
     constexpr int kTerms = kJsPass * 100;
-    __shared__ double s_az[2 * kJsPass];
-    __shared__ int s_nan[kJsPass];                              // NaN terms per row of the current pass
-    double* s_jsd = s_p;
+    double* s_jsd = L.p;
     const int K = P.K;
     const double dr = P.trunc / 100.0;
     const int a_step = G * kJsPass;
-    if (tid < kJsPass) s_nan[tid] = 0;                          // ordered by the barrier after the bins
+    if (tid < kJsPass) L.nan[tid] = 0;                          // ordered by the barrier after the bins
     if (!one_alpha && tid < kJsPass) {
         const int ai = 1 + wg + tid * G;
-        s_az[tid] = ai <= P.NA ? P.alphas[ai] : 0.0;
-        s_az[kJsPass + tid] = ai <= P.NA ? P.Z[ai] : 0.0;
+        L.az[tid] = ai <= P.NA ? P.alphas[ai] : 0.0;
+        L.az[kJsPass + tid] = ai <= P.NA ? P.Z[ai] : 0.0;
     }
     for (int b = tid; b < 100; b += NT) {
         const double r = dr * (1 + static_cast<double>(b));
         double g[kMaxK];                                         // independent pdf chains, then the ordered sum
 #pragma unroll
-        for (int m = 0; m < kMaxK; ++m) g[m] = m < K ? s_gmm[m] * gpdf(r, s_gmm[K + m], s_gmm[2 * K + m]) : 0.0;
+        for (int m = 0; m < kMaxK; ++m) g[m] = m < K ? L.gmm[m] * gpdf(r, L.gmm[K + m], L.gmm[2 * K + m]) : 0.0;
         double Pr = 0.0;
 #pragma unroll
         for (int m = 0; m < kMaxK; ++m) if (m < K) Pr += g[m];
-        s_P[b] = Pr + 1e-10;
+        L.Pbin[b] = Pr + 1e-10;
     }
     __syncthreads();
     LO_STAMP(dbg, 10);
@@ -891,18 +889,18 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             const int idx = tid + q * NT;
             if (idx >= n_terms) break;
             const int a = idx / 100, b = idx - a * 100;
-            const double alpha = one_alpha ? pf_alpha : s_az[a];
-            const double pf = one_alpha ? pf_Z : s_az[kJsPass + a];
+            const double alpha = one_alpha ? pf.alpha : L.az[a];
+            const double pz = one_alpha ? pf.Z : L.az[kJsPass + a];
             const double r = dr * (1 + static_cast<double>(b));
-            const double Pr = s_P[b];
-            const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pf + 1e-10) + 1e-10;
-            const double M = 0.5 * (Pr + Q);
-            const double t = 0.5 * (Pr * log_pos(Pr / M) + Q * log_pos(Q / M));   // lo_math.h, <= 1 ulp from log
+            const double Pr = L.Pbin[b];
+            const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pz + 1e-10) + 1e-10;
+            const double Mx = 0.5 * (Pr + Q);
+            const double t = 0.5 * (Pr * log_pos(Pr / Mx) + Q * log_pos(Q / Mx));   // lo_math.h, <= 1 ulp from log
             // the reference skips NaN terms in its sum and count: the term is stored as +0 (adding +0 to the sum,
             // which starts at +0, is the same as skipping it) and counted here, so the sequential sum below is a
             // plain chain of adds
             const bool bad = isnan(t);
-            if (bad) atomicAdd(&s_nan[a], 1);
+            if (bad) atomicAdd(&L.nan[a], 1);
             s_jsd[idx] = bad ? 0.0 : t;
         }
         __syncthreads();
@@ -913,7 +911,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
             if (!one_alpha && an <= P.NA) { nx_a = P.alphas[an]; nx_z = P.Z[an]; }
             if (ai <= P.NA) {
                 double cost = 0.0;                               // sequential, bin order (NaN terms are +0)
-                const double cnt = static_cast<double>(100 - s_nan[tid]);
+                const double cnt = static_cast<double>(100 - L.nan[tid]);
                 const double* row = s_jsd + tid * 100;
                 double vb[20], vn[20];                           // LDS reads of the next 20 bins in flight while
 #pragma unroll                                                   // the serial adds consume the current ones
@@ -926,14 +924,60 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
 #pragma unroll
                     for (int q = 0; q < 20; ++q) vb[q] = vn[q];
                 }
-                B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
+                M::st(B.js + ai, cnt == 0.0 ? DBL_MAX : cost / cnt);
             }
-            if (!one_alpha) { s_az[tid] = nx_a; s_az[kJsPass + tid] = nx_z; }
-            s_nan[tid] = 0;                                      // read above; the next pass counts after the barrier
+            if (!one_alpha) { L.az[tid] = nx_a; L.az[kJsPass + tid] = nx_z; }
+            L.nan[tid] = 0;                                      // read above; the next pass counts after the barrier
         }
         __syncthreads();
     }
     LO_STAMP(dbg, 6);
+}
+
+// wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
+// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate).
+// ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
+template <int NW, bool ONE_WAVE>
+__device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, int it, int wg, int G) {
+    DevState* st = B.st;
+    // the done flag, the single-wave prefix's loads and the prefetch below go out in one round trip; the flag is
+    // tested once they are in flight (a converged scan leaves without writing anything)
+    const int done0 = st->done;
+    PrefixLoads pl;
+    const bool wave_prefix = !P.direct_res && P.nb <= 64;
+    if (wave_prefix && threadIdx.x < 64) prefix_loads(P, B, it, pl);
+    unsigned long long* dbg = nullptr;
+#ifdef LO_PKO_STAMPS
+    if (wg == 0) dbg = st->dbg;
+#endif
+    LO_STAMP(dbg, 0);
+    extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
+    __shared__ PkoLds<NW> L;
+    PkoPrefetch pf;
+    pko_prefetch<NW>(P, wg, G, pf, L);
+    if (done0) return;
+
+    const int tid = threadIdx.x;
+    const bool lead = wg == 0;
+    // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
+    int nc;
+    double s_scale;
+    const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? L.wm : nullptr;
+    pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, L.wm, &pl);   // pl is set where it is read (nb <= 64)
+    if (!P.direct_res && nc < P.min_corr) {                     // :298-302
+        if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
+        return;
+    }
+    if constexpr (NW == 4 && !ONE_WAVE) {
+        if (wg >= G) {                                          // after the scale: the candidates need it
+            acc_candidate(P, s_scale, wg - G);
+            return;
+        }
+    }
+    if (lead && tid == 0) st->n_corr = nc;
+    if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
+    LO_STAMP(dbg, 1);
+    pko_fit_js<NW, ONE_WAVE, false>(P, B, wg, G, nc, s_scale, pf, s_pre, s_wmask, L, dbg);
 }
 
 }  // namespace lo

@@ -150,7 +150,7 @@ __device__ inline void ldlt6_solve(const double* Hin, const double* b, double* x
 
 // NT fixes the summation pattern of the nrows x kNE block partials (part_src: global or LDS) into tot[kNE] (LDS);
 // the calling block may be larger than NT (its extra threads only join the barriers).
-template <int NT>
+template <int NT, bool SC1 = false>
 __device__ __forceinline__ void solve_sums(const double* part_src, int nrows, double* tot) {
     constexpr int kQ = NT / kNE;                     // partial rows per entry (36 for 1024 threads, 9 for 256)
     __shared__ double part[kQ][kNE];
@@ -165,9 +165,9 @@ __device__ __forceinline__ void solve_sums(const double* part_src, int nrows, do
         int j = 0;
         for (; j + 8 <= nrow; j += 8) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) a[u] += src[static_cast<size_t>(j + u) * kStride];
+            for (int u = 0; u < 8; ++u) a[u] += Mem<SC1>::ld(src + static_cast<size_t>(j + u) * kStride);
         }
-        for (; j < nrow; ++j) a[0] += src[static_cast<size_t>(j) * kStride];
+        for (; j < nrow; ++j) a[0] += Mem<SC1>::ld(src + static_cast<size_t>(j) * kStride);
         part[q][k] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
     __syncthreads();
