@@ -38,6 +38,15 @@ extern "C" {
 
 #define LO_MAX_ITERS      64
 
+/* PKO kernel types (AdaptiveMEstimatorConfig::pko_kernel_type, AdaptiveMEstimator.h:40; the weights of
+ * pko_kernel_weight, AdaptiveMEstimator.cpp:99-156).  Any other name selects Cauchy there, as lo_pko_kernel_from_name. */
+#define LO_PKO_HUBER          0
+#define LO_PKO_CAUCHY         1
+#define LO_PKO_TUKEY          2
+#define LO_PKO_WELSCH         3
+#define LO_PKO_GEMAN_MCCLURE  4
+#define LO_PKO_PSEUDO_HUBER   5
+
 /* ICPConfig (IterativeClosestPointOptimizer.h:55-76, wired by Estimator.cpp:62-70) +
  * AdaptiveMEstimatorConfig (AdaptiveMEstimator.h:24-41, built at Estimator.cpp:49-59) +
  * the map geometry the surfel lookup needs (VoxelMap::GetVoxelSize/GetHierarchyFactor, VoxelMap.h:204-205). */
@@ -57,7 +66,7 @@ typedef struct lo_config {
     double truncated_threshold;          /* 10.0 */
     int    gmm_components;               /* 3 (1..3 supported) */
     int    gmm_sample_size;              /* 100 (1..256 supported) */
-    int    pko_kernel_cauchy;            /* 0: "huber" (kitti.yaml:51) */
+    int    pko_kernel;                   /* LO_PKO_*: pko_kernel_type, "huber" in kitti.yaml:51 / mid360.yaml:51 */
     float  voxel_size;                   /* map_voxel_size 0.5 */
     int    hierarchy_factor;             /* 3 */
     int    use_surfel_correspondence;    /* 1: L1 surfel lookup; 0: KDTree variant (5-NN plane fit, :647-767) */
@@ -89,6 +98,9 @@ typedef struct lo_stats {
 typedef struct lo_ctx lo_ctx;
 
 void        lo_config_default_kitti(lo_config* cfg);
+/* pko_kernel_type string -> LO_PKO_* exactly as pko_kernel_weight dispatches (AdaptiveMEstimator.cpp:128-156):
+ * "huber", "cauchy", "tukey", "welsch", "gemanMcClure", "pseudoHuber"; anything else (NULL included) -> Cauchy. */
+int         lo_pko_kernel_from_name(const char* name);
 void        lo_config_default_mid360(lo_config* cfg);
 lo_ctx*     lo_create(const lo_config* cfg, int device, int* err);
 void        lo_destroy(lo_ctx* ctx);

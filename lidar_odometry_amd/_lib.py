@@ -24,7 +24,7 @@ LO_MAX_ITERS = 64
 
 # Every symbol include/lo_icp.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
-    "lo_config_default_kitti", "lo_config_default_mid360", "lo_create", "lo_destroy", "lo_last_error",
+    "lo_config_default_kitti", "lo_config_default_mid360", "lo_pko_kernel_from_name", "lo_create", "lo_destroy", "lo_last_error",
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
@@ -52,7 +52,7 @@ class LoConfig(C.Structure):
         ("use_robust_loss", C.c_int), ("robust_loss_delta", C.c_double), ("loss_cauchy", C.c_int),
         ("use_adaptive_m_estimator", C.c_int), ("min_scale_factor", C.c_double), ("max_scale_factor", C.c_double),
         ("num_alpha_segments", C.c_int), ("truncated_threshold", C.c_double), ("gmm_components", C.c_int),
-        ("gmm_sample_size", C.c_int), ("pko_kernel_cauchy", C.c_int), ("voxel_size", C.c_float),
+        ("gmm_sample_size", C.c_int), ("pko_kernel", C.c_int), ("voxel_size", C.c_float),
         ("hierarchy_factor", C.c_int), ("use_surfel_correspondence", C.c_int), ("max_points", C.c_int),
     ]
 
@@ -150,6 +150,8 @@ def lib():
     L.lo_save_trajectory_kitti.restype = C.c_int
     L.lo_save_trajectory_kitti.argtypes = [C.c_char_p, fp, C.c_size_t]
     L.lo_get_config.restype = C.c_int
+    L.lo_pko_kernel_from_name.restype = C.c_int
+    L.lo_pko_kernel_from_name.argtypes = [C.c_char_p]
     L.lo_get_config.argtypes = [vp, C.POINTER(LoConfig)]
     L.lo_icp_optimize.argtypes = [vp, fp, C.c_size_t, fp, fp, C.POINTER(LoIterLog), C.POINTER(LoStats)]
     L.lo_icp_optimize_async.argtypes = [vp, C.c_void_p, C.c_size_t, fp]

@@ -110,7 +110,7 @@ struct KParams {
     int use_pko;
     int alpha_given;          // 1: take the Huber delta from DevState::alpha (normal-equation entry point)
     // PKO config + tables
-    int S, K, NA, pko_cauchy;
+    int S, K, NA, pko_kernel;           // pko_kernel: LO_PKO_*
     double min_scale, trunc;
     const double* alphas;
     const double* Z;

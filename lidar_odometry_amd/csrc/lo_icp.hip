@@ -315,7 +315,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.S = g.gmm_sample_size;
     P.K = g.gmm_components;
     P.NA = g.num_alpha_segments;
-    P.pko_cauchy = g.pko_kernel_cauchy;
+    P.pko_kernel = g.pko_kernel;
     P.min_scale = g.min_scale_factor;
     P.trunc = g.truncated_threshold;
     P.alphas = c->d_alphas;
@@ -350,6 +350,7 @@ static int validate_config(const lo_config* g, std::string& err) {
     if (g->min_correspondence_points < 1) { err = "min_correspondence_points must be >= 1"; return LO_ERR_ARG; }
     if (g->gmm_sample_size < 1 || g->gmm_sample_size > kMaxS) { err = "gmm_sample_size out of [1, 256]"; return LO_ERR_ARG; }
     if (g->gmm_components < 1 || g->gmm_components > 3) { err = "gmm_components out of [1, 3]"; return LO_ERR_ARG; }
+    if (g->pko_kernel < LO_PKO_HUBER || g->pko_kernel > LO_PKO_PSEUDO_HUBER) { err = "pko_kernel out of [0, 5]"; return LO_ERR_ARG; }
     if (g->num_alpha_segments < 1 || g->num_alpha_segments > kMaxAlpha) { err = "num_alpha_segments out of [1, 1000]"; return LO_ERR_ARG; }
     if (!(g->voxel_size > 0.0f)) { err = "voxel_size must be positive"; return LO_ERR_ARG; }   // VoxelMap.cpp:28-30
     if (g->hierarchy_factor <= 0 || g->hierarchy_factor % 2 == 0) { err = "hierarchy_factor must be positive and odd"; return LO_ERR_ARG; }
@@ -376,11 +377,23 @@ void lo_config_default_kitti(lo_config* c) {
     c->truncated_threshold = 10.0;
     c->gmm_components = 3;
     c->gmm_sample_size = 100;
-    c->pko_kernel_cauchy = 0;
+    c->pko_kernel = LO_PKO_HUBER;
     c->voxel_size = 0.5f;
     c->hierarchy_factor = 3;
     c->use_surfel_correspondence = 1;
     c->max_points = 1 << 17;
+}
+
+int lo_pko_kernel_from_name(const char* name) {
+    if (!name) return LO_PKO_CAUCHY;
+    const std::string k(name);
+    if (k == "huber") return LO_PKO_HUBER;
+    if (k == "cauchy") return LO_PKO_CAUCHY;
+    if (k == "tukey") return LO_PKO_TUKEY;
+    if (k == "welsch") return LO_PKO_WELSCH;
+    if (k == "gemanMcClure") return LO_PKO_GEMAN_MCCLURE;
+    if (k == "pseudoHuber") return LO_PKO_PSEUDO_HUBER;
+    return LO_PKO_CAUCHY;                                  // "Default to Cauchy" (AdaptiveMEstimator.cpp:150-155)
 }
 
 void lo_config_default_mid360(lo_config* c) {
@@ -442,7 +455,7 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMemset(c->d_tab, 0xff, c->tab_cap * sizeof(Slot)));
     // PKO tables
     build_pko_tables(c->tables, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
-                     g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel_cauchy != 0);
+                     g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel);
     const PkoTables& t = c->tables;
     LO_HIP(c, hipMalloc(&c->d_alphas, t.alphas.size() * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_Z, t.Z.size() * sizeof(double)));

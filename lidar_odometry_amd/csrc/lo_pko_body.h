@@ -48,10 +48,21 @@ __device__ __forceinline__ double gpdf(double x, double mean, double variance) {
     return norm * exp(expo);
 }
 
-__device__ __forceinline__ double pko_kernel_w(double r, double d, int cauchy) {   // :128-156
-    if (!cauchy) { const double a = fabs(r); return a <= d ? 1.0 : d / a; }
-    const double e2 = r * r, d2 = d * d;
-    return d2 / (d2 + e2);
+// pko_kernel_weight (AdaptiveMEstimator.cpp:128-156) with tukey_weight / welsch_weight / geman_mcclure_weight /
+// pseudo_huber_weight (:99-126), the same operation order; kernel = LO_PKO_* (unknown names map to Cauchy on the host)
+__device__ __forceinline__ double pko_kernel_w(double r, double d, int kernel) {
+    switch (kernel) {
+        case LO_PKO_HUBER: { const double a = fabs(r); return a <= d ? 1.0 : d / a; }
+        case LO_PKO_TUKEY: {
+            const double a = fabs(r);
+            if (a < d) { const double x = a / d, x2 = x * x; return (1 - x2) * (1 - x2); }
+            return 0.0;
+        }
+        case LO_PKO_WELSCH: { const double e2 = r * r, d2 = d * d; return exp(-e2 / d2 / 2.0); }
+        case LO_PKO_GEMAN_MCCLURE: { const double e2 = r * r, d2 = d * d; return r * d2 / (d2 + e2) / (d2 + e2); }
+        case LO_PKO_PSEUDO_HUBER: { const double e = r, d2 = d * d; return d2 / pow(d2 + e * e, 1.5); }
+        default: { const double e2 = r * r, d2 = d * d; return d2 / (d2 + e2); }   // cauchy
+    }
 }
 
 // Diagnostic build only (-DLO_PKO_STAMPS): workgroup 0 / thread 0 stores s_memtime at phase boundaries
@@ -893,7 +904,7 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
             const double pz = one_alpha ? pf.Z : L.az[kJsPass + a];
             const double r = dr * (1 + static_cast<double>(b));
             const double Pr = L.Pbin[b];
-            const double Q = pko_kernel_w(r, alpha, P.pko_cauchy) / (pz + 1e-10) + 1e-10;
+            const double Q = pko_kernel_w(r, alpha, P.pko_kernel) / (pz + 1e-10) + 1e-10;
             const double Mx = 0.5 * (Pr + Q);
             const double t = 0.5 * (Pr * log_pos(Pr / Mx) + Q * log_pos(Q / Mx));   // lo_math.h, <= 1 ulp from log
             // the reference skips NaN terms in its sum and count: the term is stored as +0 (adding +0 to the sum,

@@ -79,13 +79,23 @@ static void full_perm(int n, std::vector<int32_t>& out) {
 }
 
 void build_pko_tables(PkoTables& t, int S, int K, int max_n, double min_scale, double max_scale, int nseg,
-                      double trunc, bool cauchy_kernel) {
+                      double trunc, int kernel_type) {
     t.S = S; t.K = K; t.max_n = max_n;
-    // ---- alpha grid + partition functions (AdaptiveMEstimator.cpp:218-241, :692-708) ----
-    auto kernel = [&](double r, double d) {
-        if (!cauchy_kernel) { double a = std::fabs(r); return a <= d ? 1.0 : d / a; }
-        double e2 = r * r, d2 = d * d;
-        return d2 / (d2 + e2);
+    // ---- alpha grid + partition functions (AdaptiveMEstimator.cpp:218-241, :692-708) with pko_kernel_weight
+    //      (:99-156, glibc exp / pow as the reference) ----
+    auto kernel = [&](double r, double d) -> double {
+        switch (kernel_type) {
+            case 0: { double a = std::fabs(r); return a <= d ? 1.0 : d / a; }                 // huber
+            case 2: {                                                                          // tukey
+                double a = std::fabs(r);
+                if (a < d) { double x = a / d, x2 = x * x; return (1 - x2) * (1 - x2); }
+                return 0.0;
+            }
+            case 3: { double e2 = r * r, d2 = d * d; return std::exp(-e2 / d2 / 2.0); }      // welsch
+            case 4: { double e2 = r * r, d2 = d * d; return r * d2 / (d2 + e2) / (d2 + e2); } // gemanMcClure
+            case 5: { double d2 = d * d; return d2 / std::pow(d2 + r * r, 1.5); }             // pseudoHuber
+            default: { double e2 = r * r, d2 = d * d; return d2 / (d2 + e2); }                // cauchy
+        }
     };
     auto partition = [&](double alpha) {
         double integral = 0.0;

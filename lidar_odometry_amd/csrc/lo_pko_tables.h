@@ -44,7 +44,7 @@ struct PkoTables {
 };
 
 void build_pko_tables(PkoTables& t, int S, int K, int max_n, double min_scale, double max_scale, int nseg,
-                      double trunc, bool cauchy_kernel);
+                      double trunc, int kernel);   // kernel: LO_PKO_*
 int32_t pko_sample_host(const PkoTables& t, int n, int s);
 
 }  // namespace lo

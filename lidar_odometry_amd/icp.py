@@ -72,9 +72,8 @@ def make_config(icp: ICPConfig, pko: AdaptiveMEstimatorConfig, geom: MapGeometry
     c.truncated_threshold = pko.truncated_threshold
     c.gmm_components = pko.gmm_components
     c.gmm_sample_size = pko.gmm_sample_size
-    if pko.pko_kernel_type not in ("huber", "cauchy"):
-        raise ValueError(f"pko_kernel_type {pko.pko_kernel_type!r} not supported (huber, cauchy)")
-    c.pko_kernel_cauchy = int(pko.pko_kernel_type == "cauchy")
+    # every pko_kernel_type of AdaptiveMEstimator.cpp:128-156; an unknown name is Cauchy there, and here
+    c.pko_kernel = lib().lo_pko_kernel_from_name(pko.pko_kernel_type.encode())
     c.voxel_size = geom.voxel_size
     c.hierarchy_factor = geom.hierarchy_factor
     c.use_surfel_correspondence = int(icp.use_surfel_correspondence)

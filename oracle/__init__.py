@@ -38,6 +38,14 @@ class IterLog(C.Structure):
                 ("g", C.c_float * 6), ("delta", C.c_float * 6)]
 
 
+# pko_kernel_type -> PkoCfg.kernel (AdaptiveMEstimator.cpp:128-156: any other name is Cauchy)
+PKO_KERNELS = {"huber": 0, "cauchy": 1, "tukey": 2, "welsch": 3, "gemanMcClure": 4, "pseudoHuber": 5}
+
+
+def pko_kernel_id(name: str) -> int:
+    return PKO_KERNELS.get(name, 1)
+
+
 def kitti_pko_cfg() -> PkoCfg:
     """config/kitti.yaml:41-51 robust_estimation block (same values in mid360.yaml)."""
     return PkoCfg(0.1, 10.0, 100, 10.0, 3, 100, 0)

@@ -7,6 +7,8 @@
 // file, writes the reference's alpha and fitted GMM parameters (AdaptiveMEstimator.cpp:243-485), plus the
 // libstdc++ std::shuffle(mt19937(42)) sample prefix and the k-means seed draws the reference consumes.
 //
+// An optional third argument selects pko_kernel_type (default "huber", as kitti.yaml); the other kernels
+// (AdaptiveMEstimator.cpp:99-156) feed tests/golden/pko_golden_kernels.jsonl.
 // Input (binary): int32 ncases; per case: int32 n, then n float64.
 // Output: JSON lines, one per case, doubles printed with 17 significant digits (exact round trip).
 #define private public   // read the fitted GMM (m_gmm_*) without modifying the reference source
@@ -32,13 +34,14 @@ static void put_vec(FILE* f, const char* name, const std::vector<double>& v) {
 }
 
 int main(int argc, char** argv) {
-    if (argc < 3) { std::fprintf(stderr, "usage: %s input.bin output.jsonl\n", argv[0]); return 2; }
+    if (argc < 3) { std::fprintf(stderr, "usage: %s input.bin output.jsonl [pko_kernel_type]\n", argv[0]); return 2; }
+    const char* kernel = argc > 3 ? argv[3] : "huber";   // AdaptiveMEstimatorConfig::pko_kernel_type
     FILE* in = std::fopen(argv[1], "rb");
     FILE* out = std::fopen(argv[2], "w");
     if (!in || !out) return 3;
     int32_t ncases = 0;
     if (std::fread(&ncases, 4, 1, in) != 1) return 4;
-    lidar_slam::optimization::AdaptiveMEstimator est(true, "huber", 0.1, 10.0, 100, 10.0, 3, 100, "huber");
+    lidar_slam::optimization::AdaptiveMEstimator est(true, "huber", 0.1, 10.0, 100, 10.0, 3, 100, kernel);
     for (int c = 0; c < ncases; ++c) {
         int32_t n = 0;
         if (std::fread(&n, 4, 1, in) != 1) return 5;

@@ -886,13 +886,22 @@ struct PKO {
     std::vector<double> alphas, Z;
     std::vector<double> w, mu, var;
 
-    double kernel(double r, double delta) const {   // pko_kernel_weight :128-156
-        if (cfg.kernel == 0) {
-            double a = std::fabs(r);
-            return a <= delta ? 1.0 : delta / a;
+    double kernel(double r, double delta) const {   // pko_kernel_weight :128-156 (+ :99-126)
+        switch (cfg.kernel) {
+            case 0: {                                                            // "huber"
+                double a = std::fabs(r);
+                return a <= delta ? 1.0 : delta / a;
+            }
+            case 2: {                                                            // tukey_weight :99-108
+                double a = std::fabs(r);
+                if (a < delta) { double x = a / delta, x2 = x * x; return (1 - x2) * (1 - x2); }
+                return 0.0;
+            }
+            case 3: { double e2 = r * r, d2 = delta * delta; return std::exp(-e2 / d2 / 2.0); }       // :110-114
+            case 4: { double e2 = r * r, d2 = delta * delta; return r * d2 / (d2 + e2) / (d2 + e2); } // :116-120
+            case 5: { double e = r, d2 = delta * delta; return d2 / std::pow(d2 + e * e, 1.5); }      // :122-126
+            default: { double e2 = r * r, d2 = delta * delta; return d2 / (d2 + e2); }               // "cauchy" / other
         }
-        double e2 = r * r, d2 = delta * delta;
-        return d2 / (d2 + e2);
     }
     double partition(double alpha) const {          // :692-708
         const double bound = cfg.truncated_threshold, step = 0.01;

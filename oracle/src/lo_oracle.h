@@ -32,7 +32,7 @@ typedef struct or_pko_cfg {
     double truncated_threshold;   /* 10.0 */
     int    gmm_components;        /* 3    */
     int    gmm_sample_size;       /* 100  */
-    int    kernel;                /* 0 = huber, 1 = cauchy (pko_kernel_type) */
+    int    kernel;                /* pko_kernel_type: 0 huber, 1 cauchy, 2 tukey, 3 welsch, 4 gemanMcClure, 5 pseudoHuber */
 } or_pko_cfg;
 
 /* ICP configuration (ICPConfig, IterativeClosestPointOptimizer.h:55-76 as wired by Estimator.cpp:62-70). */

@@ -6,12 +6,14 @@ compiled in place from /root/reference by ``make -C oracle ref``) on seeded resi
   tests/golden/pko_inputs.npz     residual vectors (inputs), keys case_<i>
   tests/golden/pko_golden.jsonl   reference outputs: alpha, GMM weights/means/variances, alpha grid, Z,
                                   std::shuffle(mt19937(42)) sample prefix and k-means seed draws
+  tests/golden/pko_golden_kernels.jsonl  the same for the other pko_kernel_type values on a subset of the cases
 
 Usage:  make -C oracle ref && python tests/golden/make_pko_golden.py
 The fixtures are data only; the reference source never leaves /root/reference.
 """
 from __future__ import annotations
 
+import json
 import os
 import struct
 import subprocess
@@ -52,19 +54,46 @@ def cases():
     return out
 
 
+# pko_kernel_type values of AdaptiveMEstimator.cpp:128-156 besides kitti.yaml's "huber"; "robust" is not a kernel
+# name, so the reference falls back to Cauchy for it.  Run on a subset of the cases.
+KERNELS = ("cauchy", "tukey", "welsch", "gemanMcClure", "pseudoHuber", "robust")
+KERNEL_CASES = ("halfnormal_100", "halfnormal_1000", "mixture_999", "exponential_3000", "heavy_tail_2000",
+                "icp_like_9000", "halfnormal_12000")
+
+
+def _write_inputs(path, vecs):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<i", len(vecs)))
+        for v in vecs:
+            v = np.ascontiguousarray(v, dtype="<f8")
+            f.write(struct.pack("<i", len(v)))
+            f.write(v.tobytes())
+
+
 def main():
     if not os.path.exists(DRIVER):
         sys.exit(f"missing {DRIVER}: run `make -C oracle ref` (needs /root/reference)")
     cs = cases()
     inp = os.path.join(HERE, "_pko_in.bin")
     outp = os.path.join(HERE, "pko_golden.jsonl")
-    with open(inp, "wb") as f:
-        f.write(struct.pack("<i", len(cs)))
-        for _, v in cs:
-            v = np.ascontiguousarray(v, dtype="<f8")
-            f.write(struct.pack("<i", len(v)))
-            f.write(v.tobytes())
+    _write_inputs(inp, [v for _, v in cs])
     subprocess.run([DRIVER, inp, outp], check=True, stdout=subprocess.DEVNULL)
+    # the other PKO kernels: one JSON line per (kernel, case), "case" indexing pko_inputs.npz
+    names = [c[0] for c in cs]
+    sel = [names.index(n) for n in KERNEL_CASES]
+    _write_inputs(inp, [cs[i][1] for i in sel])
+    tmp = os.path.join(HERE, "_pko_kernel.jsonl")
+    with open(os.path.join(HERE, "pko_golden_kernels.jsonl"), "w") as out:
+        for kern in KERNELS:
+            subprocess.run([DRIVER, inp, tmp, kern], check=True, stdout=subprocess.DEVNULL)
+            with open(tmp) as f:
+                for j, line in enumerate(f):
+                    rec = json.loads(line)
+                    rec["case"] = sel[j]
+                    rec["name"] = names[sel[j]]
+                    rec["kernel"] = kern
+                    out.write(json.dumps(rec) + "\n")
+    os.remove(tmp)
     os.remove(inp)
     np.savez_compressed(os.path.join(HERE, "pko_inputs.npz"),
                         names=np.array([c[0] for c in cs]),

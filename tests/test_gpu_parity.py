@@ -115,6 +115,29 @@ def test_pko_alpha_matches_reference_golden(icp):
     assert not mism, f"alpha mismatches: {mism}"
 
 
+def test_pko_other_kernels_match_reference_golden():
+    """Device PKO with pko_kernel_type tukey / welsch / gemanMcClure / pseudoHuber / cauchy / unknown (-> Cauchy)
+    against the reference's own AdaptiveMEstimator.cpp outputs: alpha identical, GMM within 1e-9."""
+    from lidar_odometry_amd import AdaptiveMEstimatorConfig, IterativeClosestPointOptimizer
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "pko_inputs.npz"))
+    recs = [json.loads(l) for l in open(os.path.join(os.path.dirname(__file__), "golden", "pko_golden_kernels.jsonl"))]
+    mism = []
+    for kern in sorted({d["kernel"] for d in recs}):
+        o = IterativeClosestPointOptimizer(adaptive=AdaptiveMEstimatorConfig(pko_kernel_type=kern), max_points=1 << 15)
+        try:
+            for d in (d for d in recs if d["kernel"] == kern):
+                a, gmm = o.pko_scale_factor(z[f"case_{d['case']}"])
+                if a != d["alpha"]:
+                    mism.append((kern, d["name"], a, d["alpha"]))
+                    continue
+                for k in ("w", "mu", "var"):
+                    np.testing.assert_allclose(gmm[k], np.array(d[k], np.float64), rtol=1e-9, atol=1e-12,
+                                               equal_nan=True, err_msg=f"{kern} {d['name']} {k}")
+        finally:
+            o.close()
+    assert not mism, f"alpha mismatches: {mism}"
+
+
 def test_pko_sample_indices_device_tables(icp):
     for n in (1, 5, 99, 100, 101, 4000, 65535, 65536, 100001):
         np.testing.assert_array_equal(icp.pko_sample_indices(n), oracle.shuffle_prefix(n, 100))

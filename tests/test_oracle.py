@@ -28,6 +28,33 @@ def test_pko_matches_reference_golden_bitwise(case):
         np.testing.assert_array_equal(g[k], np.array(d[k], dtype=np.float64))
 
 
+def _kernel_golden():
+    z = np.load(os.path.join(GOLD, "pko_inputs.npz"))
+    with open(os.path.join(GOLD, "pko_golden_kernels.jsonl")) as f:
+        for line in f:
+            d = json.loads(line)
+            yield d, z[f"case_{d['case']}"]
+
+
+_KG = [(d["kernel"], d["name"]) for d, _ in _kernel_golden()]
+
+
+@pytest.mark.parametrize("kernel,name", _KG)
+def test_pko_other_kernels_match_reference_golden_bitwise(kernel, name):
+    """pko_kernel_type tukey / welsch / gemanMcClure / pseudoHuber / cauchy and an unknown name (-> Cauchy),
+    AdaptiveMEstimator.cpp:99-156, against the reference's own compiled AdaptiveMEstimator.cpp."""
+    d, r = next((d, r) for d, r in _kernel_golden() if d["kernel"] == kernel and d["name"] == name)
+    cfg = oracle.kitti_pko_cfg()
+    cfg.kernel = oracle.pko_kernel_id(kernel)
+    a, g = oracle.pko_scale_factor(r, cfg)
+    assert a == d["alpha"]
+    for k in ("w", "mu", "var"):
+        np.testing.assert_array_equal(g[k], np.array(d[k], dtype=np.float64))
+    al, z = oracle.pko_tables(cfg)
+    np.testing.assert_array_equal(al, np.array(d["alphas"]))
+    np.testing.assert_array_equal(z, np.array(d["Z"]))
+
+
 def test_pko_tables_match_reference():
     d, _ = next(iter(_golden()))
     a, z = oracle.pko_tables()
