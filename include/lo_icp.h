@@ -150,12 +150,6 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * the one-iteration-at-a-time path.  Off by default: at KITTI size a candidate chain's sequential normal equations,
  * solve and correspondence sweeps inside one workgroup outweigh the EM overlap. */
 int lo_set_lookahead(lo_ctx* ctx, int enable);
-/* Persistent GN loop (default on): a small scan with PKO (<= 64 blocks of 256 points, surfel correspondences, default
- * arithmetic) runs its whole optimize() as ONE launch whose workgroups hand the stages to each other in place --
- * a converged scan leaves the launch instead of falling through the remaining per-iteration launches.  Results are
- * bit-identical to the launch-per-stage form (enable = 0), which stays for A/B runs and for grids the device cannot
- * hold co-resident (checked against the occupancy query per context). */
-int lo_set_persistent(lo_ctx* ctx, int enable);
 /* Reference-exact arithmetic (default off): H, g and the cost summed SEQUENTIALLY in fp32 over the correspondences
  * in scan order, the iteration-0 scale from the sorted residuals, the fp32 LDLT and SO3 re-projection through
  * JacobiSVD -- the reference's own operation order (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99),

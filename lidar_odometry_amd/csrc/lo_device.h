@@ -36,8 +36,8 @@ constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
 constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP row)
 constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
-constexpr int kGnSyncWords = 2048;  // persistent GN launch (lo_persist.hip): arrival counters per context
-constexpr int kGnCandWords = 48;    //   and the words of one candidate's solved-step record
+constexpr int kCandWords = 48;      // a candidate's solved GN step: pose[12] | cost | H[21] | g[6] | delta[6] | conv | pad
+constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv = 46;
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;
@@ -128,6 +128,9 @@ struct KParams {
     double* blk_m2;
     double* blk_part;
     double* acc_part;         // speculative normal equations: [NA + 1 candidates][kFuseMaxBlocks][kNE] partials
+    float* cand_rec;          // nullable: each candidate's solved GN step [NA + 1][kCandWords] (pre-solved in the PKO
+                              //   launch while the EM runs; k_pick_correspond / k_pick select one)
+    unsigned* cand_cnt;       //   per-candidate arrivals of its W workgroups (the last one solves and re-zeroes it)
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
     double* res_out;          // nullable: per-point fp64 residual of the accepted correspondences (k_correspond /
@@ -136,26 +139,6 @@ struct KParams {
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     DevState* st;
-};
-
-// Persistent GN launch (lo_persist.hip).  Correspondence sets of the candidates (the next iteration's correspondences at each candidate's pose),
-// [parity][NA + 1] sets of cs_pts points each.
-struct GnSets {
-    int32_t* slot;
-    double* res;
-    uint64_t* wmask;
-    int32_t* cnt;
-    int cs_pts;                                             // points per set (a multiple of kBlock)
-};
-// Kernel arguments besides the scan's KParams.
-struct GnArgs {
-    unsigned* sync;
-    float* cand;                                            // [2][NA + 1][kCandWords]
-    GnSets sets;
-    int G;                                                  // PKO workgroups (one alpha of the JS grid each)
-    int W;                                                  // workgroups per alpha candidate
-    int per;                                                // 256-point blocks per candidate workgroup
-    int skip_corr0;                                         // the first correspondence search ran as its own launch
 };
 
 // Lookahead launches (lo_lookahead.hip): one candidate chain's results for GN iterations k, k + 1 of a launch.
@@ -200,8 +183,9 @@ __device__ __forceinline__ ScanBufs own_bufs(const KParams& P) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Memory policy of the buffers one workgroup hands to another INSIDE a launch (the persistent GN loop k_gn,
-// lo_persist.hip).  Mem<false>: plain loads / stores (the hand-off is a kernel boundary).  Mem<true>: agent-scope
+// Memory policy of the buffers one workgroup hands to another INSIDE a launch (a speculative candidate's W > 1
+// workgroups, whose last arrival solves: lo_pko_body.h acc_candidate).  Mem<false>: plain loads / stores (the
+// hand-off is a kernel boundary).  Mem<true>: agent-scope
 // relaxed atomic loads / stores on the global address space -- `global_load/store ... sc1`: stores write through
 // the XCD's L2, loads bypass the CU's L1 -- so a consumer that saw the producer's counter after the producer drained
 // its stores (s_waitcnt vmcnt(0)) reads the fresh bytes on any XCD without release / acquire fences
@@ -215,7 +199,6 @@ template <bool SC1> struct Mem;
 template <> struct Mem<false> {
     template <typename T> __device__ static __forceinline__ T ld(const T* p) { return *p; }
     template <typename T> __device__ static __forceinline__ void st(T* p, T v) { *p = v; }
-    template <typename T> __device__ static __forceinline__ void st_stream(T* p, T v) { __builtin_nontemporal_store(v, p); }
 };
 template <> struct Mem<true> {
     template <typename T> __device__ static __forceinline__ T ld(const T* p) {
@@ -236,8 +219,6 @@ template <> struct Mem<true> {
             __hip_atomic_store((g_u64*)(p), __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
-    // hand-off stores are never non-temporal (write-through is what makes them visible)
-    template <typename T> __device__ static __forceinline__ void st_stream(T* p, T v) { st(p, v); }
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -442,13 +423,12 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 // calculate_pko_scale_factor's selection (AdaptiveMEstimator.cpp:256-275): the index of the FIRST alpha with
 // the strictly smallest JS cost, 0 (min_scale_factor) if none is below DBL_MAX.  Every wave computes it
 // redundantly from P.js (lexicographic (cost, index) minimum == first strict minimum).
-template <bool SC1 = false>
 __device__ __forceinline__ int pko_select_index(const KParams& P, const double* js) {
     const int lane = threadIdx.x & 63;
     double bv = 1.7976931348623157e308;
     int bi = 0x7fffffff;
     for (int i = 1 + lane; i <= P.NA; i += 64) {
-        const double v = Mem<SC1>::ld(js + i);
+        const double v = js[i];
         if (v < bv) { bv = v; bi = i; }
     }
 #pragma unroll
@@ -510,9 +490,8 @@ __device__ __forceinline__ void scan_pose(const KParams& P, int init, int blk, f
 }
 
 // Where a correspondence pass writes: per point the accepted slot and fp64 residual, per wave the validity ballot, per
-// block the accepted count and (iteration 0) the residual sum / M2.  The context's own buffers (corr_out(P)), or an
-// alpha candidate's set in the persistent launch (lo_persist.hip: the next iteration's correspondences at the
-// candidate's pose).
+// block the accepted count and (iteration 0) the residual sum / M2: the context's own buffers (corr_out(P)) or
+// another set.
 struct CorrOut {
     int32_t* slot;
     double* res;                      // nullable
@@ -527,7 +506,6 @@ __device__ __forceinline__ CorrOut corr_out(const KParams& P) {
 
 // Per-wave validity ballots, per-block accepted count and (iteration 0, with_stats) the per-block
 // (count, sum, M2) of the accepted fp64 residuals for the stable merge of the residual variance.
-template <bool SC1 = false>
 __device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, double r, int with_stats, int vb) {
     __shared__ double s_red[kWavesPerBlock];
     __shared__ int s_cnt[kWavesPerBlock];
@@ -535,7 +513,7 @@ __device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, doub
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t m = __ballot(valid);
     if (lane == 0) {
-        Mem<SC1>::st(O.wmask + vb * kWavesPerBlock + wid, static_cast<uint64_t>(m));
+        O.wmask[vb * kWavesPerBlock + wid] = m;
         s_cnt[wid] = __popcll(m);
     }
     if (!with_stats) {
@@ -543,7 +521,7 @@ __device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, doub
         if (tid == 0) {
             int c = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) c += s_cnt[w];
-            Mem<SC1>::st(O.blk_cnt + vb, c);
+            O.blk_cnt[vb] = c;
         }
         return;
     }
@@ -554,8 +532,8 @@ __device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, doub
         int c = 0;
         double sum = 0.0;
         for (int w = 0; w < kWavesPerBlock; ++w) { c += s_cnt[w]; sum += s_red[w]; }
-        Mem<SC1>::st(O.blk_cnt + vb, c);
-        Mem<SC1>::st(O.blk_sum + vb, sum);
+        O.blk_cnt[vb] = c;
+        O.blk_sum[vb] = sum;
         s_mean = c > 0 ? sum / c : 0.0;
     }
     __syncthreads();
@@ -568,19 +546,15 @@ __device__ __forceinline__ void corr_epilogue(const CorrOut& O, bool valid, doub
     if (tid == 0) {
         double m2 = 0.0;
         for (int w = 0; w < kWavesPerBlock; ++w) m2 += s_red[w];
-        Mem<SC1>::st(O.blk_m2 + vb, m2);
+        O.blk_m2[vb] = m2;
     }
 }
-template <bool SC1 = false>
 __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, double r, int with_stats, int vb) {
-    corr_epilogue<SC1>(corr_out(P), valid, r, with_stats, vb);
+    corr_epilogue(corr_out(P), valid, r, with_stats, vb);
 }
 
 // find_correspondences' per-point step (IterativeClosestPointOptimizer.cpp:606-641) for point i at pose T, then the
 // block's ballots / count / (iteration 0) residual stats.
-// SC1: the persistent launch (lo_persist.hip) -- slot / residual / ballots / counts are handed to other workgroups of
-// the same launch, so they are stored write-through (Mem<true>) instead of streaming.
-template <bool SC1>
 __device__ __forceinline__ void correspond_tail(const KParams& P, const CorrOut& O, const float (&T)[12], float px,
                                                 float py, float pz, int i, int n, int with_stats, int blk) {
     int slot = -1;
@@ -594,25 +568,23 @@ __device__ __forceinline__ void correspond_tail(const KParams& P, const CorrOut&
             if (!(r > P.maxd)) slot = s;     // reference rejects only residual > max (NaN kept, :630)
         }
         // streaming stores: read back only by the next kernels (PKO sample, accumulate), not by this launch
-        Mem<SC1>::st_stream(O.slot + i, slot);
+        __builtin_nontemporal_store(slot, &O.slot[i]);
         if (P.res_dbg) P.res_dbg[i] = slot >= 0 ? r : 0.0;
-        if (O.res) Mem<SC1>::st_stream(O.res + i, r);
+        if (O.res) __builtin_nontemporal_store(r, &O.res[i]);
     }
-    corr_epilogue<SC1>(O, slot >= 0, r, with_stats, blk);
+    corr_epilogue(O, slot >= 0, r, with_stats, blk);
 }
-template <bool SC1>
 __device__ __forceinline__ void correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
                                                 int i, int n, int with_stats, int blk) {
-    correspond_tail<SC1>(P, corr_out(P), T, px, py, pz, i, n, with_stats, blk);
+    correspond_tail(P, corr_out(P), T, px, py, pz, i, n, with_stats, blk);
 }
 
 // ---------------------------------------------------------------------------------------------------
 // One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
 // fp32 products fl(fl(w J_i) J_j) as the reference forms them.
-template <bool SC1 = false>
 __device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot, const float (&T)[12], double scale,
                                           float dl, int i, float (&acc)[kNE]) {
-    const int s = Mem<SC1>::ld(slot + i);
+    const int s = slot[i];
     if (s < 0) return;
     const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
     const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i

@@ -34,6 +34,8 @@ __global__ void k_solve(KParams P, int it, int ne_only);
 __global__ void k_solve_pick(KParams P, int it);
 __global__ void k_solve_correspond(KParams P, int it);
 __global__ void k_solve_knn(KParams P, int it);
+__global__ void k_pick_correspond(KParams P, int it);
+__global__ void k_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
@@ -63,7 +65,6 @@ __global__ void k_la_finish(const KParams* Pp, LaParams L, int k_next);
 __global__ void k_exact_scale(KParams P, int n2);
 __global__ void k_exact_terms(KParams P);
 __global__ void k_exact_solve(KParams P, int it);
-__global__ void k_gn(KParams P, GnArgs A);
 }  // namespace lo
 
 using namespace lo;
@@ -103,18 +104,14 @@ struct lo_ctx {
     double* d_blk_m2 = nullptr;
     double* d_blk_part = nullptr;
     double* d_acc_part = nullptr;   // speculative normal equations (allocated on the first PKO optimize)
+    float* d_cand_rec = nullptr;    //   and each candidate's solved GN step [NA + 1][kCandWords]
+    unsigned* d_cand_cnt = nullptr; //   per-candidate workgroup arrivals (zero between launches)
+    bool presolve = true;           //   candidates solve inside the PKO launch (LO_PRESOLVE=0: k_solve_* instead)
     LaParams la{};                  // lookahead launch buffers (allocated on the first small PKO optimize)
     void* d_la = nullptr;           //   one allocation behind them
     KParams* d_la_params = nullptr; //   the scan's parameters, stashed by its first k_correspond
     bool lookahead = false;         // lo_set_lookahead (measured slower at KITTI size: DESIGN.md §3)
     bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
-    bool persist = true;            // lo_set_persistent: small PKO scans run the GN loop as one launch (k_gn)
-    int gn_cap = -1;                //   co-resident k_gn workgroups on this device (occupancy query, -1: not asked)
-    unsigned* d_sync = nullptr;     //   k_gn's arrival counters (lo_persist.hip), zeroed at creation
-    float* d_cand = nullptr;        //   k_gn's solved candidate steps [2][NA + 1][kGnCandWords]
-    void* d_gn_cs = nullptr;        //   k_gn's candidate correspondence sets [2][NA + 1] (allocated on first use)
-    GnSets gn_sets{};
-    int gn_parts = 4;               //   workgroups per alpha candidate (LO_GN_PARTS)
     float* d_ex_terms = nullptr;
     size_t la_pad = 0;              //   dynamic LDS of k_la (prefix + padding to one workgroup per CU)
     double* d_js = nullptr;
@@ -272,9 +269,10 @@ static int ensure_la(lo_ctx* c) {
 static int ensure_acc_part(lo_ctx* c) {
     if (c->d_acc_part || !c->cfg.use_adaptive_m_estimator) return LO_OK;
     const size_t cand = static_cast<size_t>(c->cfg.num_alpha_segments) + 1;
-    // two sets: the persistent launch double-buffers the candidates by GN-iteration parity (lo_persist.hip)
-    LO_HIP(c, hipMalloc(&c->d_acc_part, 2 * cand * kFuseMaxBlocks * kNE * sizeof(double)));
-    LO_HIP(c, hipMalloc(&c->d_cand, 2 * cand * kGnCandWords * sizeof(float)));
+    LO_HIP(c, hipMalloc(&c->d_acc_part, cand * kFuseMaxBlocks * kNE * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_cand_rec, cand * kCandWords * sizeof(float)));
+    LO_HIP(c, hipMalloc(&c->d_cand_cnt, cand * sizeof(unsigned)));
+    LO_HIP(c, hipMemset(c->d_cand_cnt, 0, cand * sizeof(unsigned)));
     return LO_OK;
 }
 
@@ -333,6 +331,8 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.blk_m2 = c->d_blk_m2;
     P.blk_part = c->d_blk_part;
     P.acc_part = c->d_acc_part;
+    P.cand_rec = (c->kd || !c->presolve) ? nullptr : c->d_cand_rec;   // surfel path: candidates pre-solve (k_pick*)
+    P.cand_cnt = c->d_cand_cnt;
     P.js = c->d_js;
     P.res_dbg = nullptr;
     P.res_out = c->d_res_pko;
@@ -441,9 +441,7 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_blk_sum, NB * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_blk_m2, NB * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_blk_part, NB * kNE * sizeof(double)));
-    LO_HIP(c, hipMalloc(&c->d_js, 2 * (kMaxAlpha + 1) * sizeof(double)));   // two sets (k_gn's parity buffers)
-    LO_HIP(c, hipMalloc(&c->d_sync, kGnSyncWords * sizeof(unsigned)));
-    LO_HIP(c, hipMemset(c->d_sync, 0, kGnSyncWords * sizeof(unsigned)));
+    LO_HIP(c, hipMalloc(&c->d_js, (kMaxAlpha + 1) * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_st, sizeof(DevState)));
     LO_HIP(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
     std::memset(c->h_st, 0, sizeof(DevState));
@@ -502,8 +500,7 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     lo_ctx* c = new lo_ctx();
     c->cfg = *cfg;
     c->device = device;
-    if (const char* pe = std::getenv("LO_PERSISTENT")) c->persist = std::atoi(pe) != 0;   // A/B runs (lo_set_persistent)
-    if (const char* pe = std::getenv("LO_GN_PARTS")) c->gn_parts = std::max(1, std::atoi(pe));
+    if (const char* pe = std::getenv("LO_PRESOLVE")) c->presolve = std::atoi(pe) != 0;   // A/B runs
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
@@ -532,7 +529,7 @@ void lo_destroy(lo_ctx* c) {
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la, c->d_ex_terms, c->d_res_pko,
-                    c->d_sync, c->d_cand, c->d_gn_cs};
+                    c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
     if (c->lgrid.h_stage) (void)hipHostFree(c->lgrid.h_stage);
@@ -986,54 +983,6 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             c->pending = true;
             return LO_OK;
         }
-        if (fused && !c->kd && !c->lookahead && c->persist) {
-            // the whole GN loop as one persistent launch (lo_persist.hip): G PKO workgroups + (NA + 1) x W candidate
-            // workgroups, W of them per alpha candidate
-            GnArgs A{};
-            A.G = pko_grid(g);
-            A.per = (P.nb + std::min(c->gn_parts, P.nb) - 1) / std::min(c->gn_parts, P.nb);
-            A.W = (P.nb + A.per - 1) / A.per;
-            const int nwg = A.G + (P.NA + 1) * A.W;
-            const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
-            if (c->gn_cap < 0) {
-                int per_cu = 0, n_cu = 0;
-                LO_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_gn),
-                                                                      kBlock, kFuseMaxBlocks * sizeof(int)));
-                LO_HIP(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
-                // two thirds of the device (k_gn: 166 VGPRs, 103 SGPRs -> 3 workgroups per CU; the SGPR rule of
-                // MI355X_MICROARCH.md "residency" admits 6): other streams' kernels may hold CUs meanwhile; a grid that
-                // still finds no room fails its bounded waits (status LO_ERR_HIP) instead of hanging
-                c->gn_cap = std::max(0, per_cu * n_cu * 2 / 3);
-            }
-            if (nwg <= c->gn_cap && !c->d_gn_cs) {
-                const size_t cs_pts = static_cast<size_t>(std::min(kFuseMaxBlocks, (c->cfg.max_points + kBlock - 1) / kBlock)) * kBlock;
-                const size_t nset = 2 * (static_cast<size_t>(g.num_alpha_segments) + 1);
-                const size_t b_slot = nset * cs_pts * 4, b_res = nset * cs_pts * 8, b_wm = nset * cs_pts / kWave * 8;
-                const size_t b_cnt = nset * cs_pts / kBlock * 4;
-                LO_HIP(c, hipMalloc(&c->d_gn_cs, b_slot + b_res + b_wm + b_cnt));
-                char* base = static_cast<char*>(c->d_gn_cs);
-                c->gn_sets.res = reinterpret_cast<double*>(base);
-                c->gn_sets.wmask = reinterpret_cast<uint64_t*>(base + b_res);
-                c->gn_sets.slot = reinterpret_cast<int32_t*>(base + b_res + b_wm);
-                c->gn_sets.cnt = reinterpret_cast<int32_t*>(base + b_res + b_wm + b_slot);
-                c->gn_sets.cs_pts = static_cast<int>(cs_pts);
-            }
-            if (nwg <= c->gn_cap && P.nb * kBlock <= c->gn_sets.cs_pts) {
-                A.skip_corr0 = 0;
-                if (c->stage_timing && c->st_n < kStageEvents) {   // the first correspondence launch, timed apart
-                    launch_correspond_first(c, P0, false);
-                    A.skip_corr0 = 1;
-                }
-                A.sync = c->d_sync;
-                A.cand = c->d_cand;
-                A.sets = c->gn_sets;
-                hipLaunchKernelGGL(k_gn, dim3(nwg), dim3(kBlock), pre_bytes, c->stream, P, A);
-                LO_HIP(c, hipGetLastError());
-                LO_HIP(c, hipEventRecord(c->ev1, c->stream));
-                c->pending = true;
-                return LO_OK;
-            }
-        }
         if (fused && !c->kd && c->lookahead) {
             // two GN iterations per launch (lo_lookahead.hip): k_correspond, k_la(0), k_la(2), ..., k_la_finish
             const int rc2 = ensure_la(c);
@@ -1064,14 +1013,18 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             if (it == 0) launch_correspond_first(c, P0, c->kd);
             launch_pko_spec(c, P, it);
             if (it + 1 < g.max_iterations && !c->kd) {
-                hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
+                if (P.cand_rec) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
+                else hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
             } else if (it + 1 < g.max_iterations) {
                 hipLaunchKernelGGL(k_solve_knn, dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock),
                                    dim3(kBlock), 0, c->stream, P, it);
                 hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, P);
                 hipLaunchKernelGGL(k_plane, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
-            } else
+            } else if (P.cand_rec) {
+                hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, c->stream, P, it);
+            } else {
                 hipLaunchKernelGGL(k_solve_pick, dim3(1), dim3(kBlock), 0, c->stream, P, it);
+            }
         }
         LO_HIP(c, hipGetLastError());
     }
@@ -1098,7 +1051,6 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     c->pending = false;
     const DevState* hs = c->h_st;
     int status = c->last_n == 0 ? LO_INSUFFICIENT : hs->status;
-    if (status < 0) c->err = "persistent GN launch: a hand-off wait timed out (grid not co-resident)";
     const int iters = hs->iter;
     if (T_out) {
         if (status == LO_OK) std::memcpy(T_out, hs->pose, sizeof(float) * 12);
@@ -1513,12 +1465,6 @@ int lo_stage_time(lo_ctx* c, double* avg_us, int* count) {
 int lo_set_exact(lo_ctx* c, int enable) {
     if (!c) return LO_ERR_ARG;
     c->exact = enable != 0;
-    return LO_OK;
-}
-
-int lo_set_persistent(lo_ctx* c, int enable) {
-    if (!c) return LO_ERR_ARG;
-    c->persist = enable != 0;
     return LO_OK;
 }
 

@@ -47,7 +47,7 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
     for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
     if (!init && done) return;
     scan_pose(P, init, blk, T);
-    correspond_tail<false>(P, T, px, py, pz, i, n, with_stats, blk);
+    correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
 }
 
 // XCD-aware block order: the hardware hands consecutive workgroups to the 8 XCDs round-robin; logical block
@@ -242,8 +242,63 @@ __global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) 
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_T[k];
-    correspond_tail<false>(P, T, px, py, pz, i, n, 0, blk);
+    correspond_tail(P, T, px, py, pz, i, n, 0, blk);
 }
+
+// The selection of GN iteration it (pko_select_index: the reference's first strict JS minimum,
+// AdaptiveMEstimator.cpp:256-275) applied to the candidates the PKO launch already solved (acc_candidate with
+// P.cand_rec): the selected record is the iteration's pose, log and convergence test (:417-448), block 0 publishes
+// the GN state, and with CORR every block then searches its 256 points at the new pose for iteration it + 1 -- the
+// fp64 solve is no longer between the EM's end and the next correspondence search.  Same record = same bits as
+// k_solve_pick / k_solve_correspond.
+template <bool CORR>
+__device__ __forceinline__ void pick_body(const KParams& P, int it) {
+    DevState* st = P.st;
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    const int done = st->done;                    // loaded with the points and the JS grid (one round trip)
+    const int i = blk * kBlock + tid;
+    const int n = scan_n(P);
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    if (CORR && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    __shared__ float s_rec[kCandWords];
+    __shared__ int s_skip;
+    __shared__ double s_alpha;
+    if (tid < kWave) {
+        const int bi = pko_select_index(P, P.js);
+        const int c = bi > 0 ? bi - 1 : P.NA;
+        if (tid < kCandWords) s_rec[tid] = P.cand_rec[static_cast<size_t>(c) * kCandWords + tid];
+        if (tid == 0) {                           // thread 0's view of the flag decides for the whole block
+            s_skip = done;
+            s_alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
+        }
+    }
+    __syncthreads();
+    if (s_skip) return;
+    const bool conv = s_rec[kCandConv] != 0.0f;
+    if (blk == 0 && tid == 0) {
+        lo_iter_log& L = st->logs[it];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) { st->pose[q] = s_rec[q]; L.pose[q] = s_rec[q]; }
+        L.n_corr = st->n_corr;
+        L.scale = st->scale;
+        L.alpha = s_alpha;
+        L.cost = s_rec[kCandCost];
+#pragma unroll
+        for (int q = 0; q < 21; ++q) L.H[q] = s_rec[kCandH + q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) { L.g[q] = s_rec[kCandG + q]; L.delta[q] = s_rec[kCandD + q]; }
+        st->alpha = s_alpha;
+        st->iter = it + 1;
+        if (conv) st->done = 1;
+    }
+    if (!CORR || conv) return;                    // converged: the later launches of the scan see DevState::done
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
+    correspond_tail(P, T, px, py, pz, i, n, 0, blk);
+}
+__global__ __launch_bounds__(kBlock) void k_pick_correspond(KParams P, int it) { pick_body<true>(P, it); }
+__global__ __launch_bounds__(kBlock) void k_pick(KParams P, int it) { pick_body<false>(P, it); }
 
 // Batched solve (jobs with more than kFuseMaxBlocks accumulate blocks present): one block per job, with the
 // partial-sum pattern the single-scan path uses for that job's size, so every job stays bit-identical to it.

@@ -22,6 +22,7 @@
 #pragma once
 #include "lo_device.h"
 #include "lo_math.h"
+#include "lo_solve.h"
 
 #include <cfloat>
 
@@ -520,8 +521,8 @@ __device__ __forceinline__ void gmm_fit_1w_dispatch(const double* s_sd, int S, c
 // starting at kSpecBlocksPerWG * (wgi % W); each block's partial is formed exactly as accumulate_body forms it
 // (one point per thread, fp32 wave_total, fp64 sum over the 4 waves), so the solve is bit-identical.
 // The normal-equation partials of blocks [vb0, vb1) with Huber delta dl into dst[vb][kNE], each block's partial formed
-// exactly as accumulate_body forms it (one point per thread, fp32 wave_total, fp64 sum over the 4 waves).  SC1 (the
-// persistent launch): the slots are read and the partials written through Mem<true>.
+// exactly as accumulate_body forms it (one point per thread, fp32 wave_total, fp64 sum over the 4 waves).  SC1: the
+// partials are stored through Mem<true>, for a reader in another workgroup of the same launch.
 template <bool SC1>
 __device__ void acc_blocks(const KParams& P, const int32_t* slot, const float (&T)[12], double scale, float dl, int vb0,
                            int vb1, double* dst) {
@@ -533,7 +534,7 @@ __device__ void acc_blocks(const KParams& P, const int32_t* slot, const float (&
 #pragma unroll
         for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
         const int i = vb * kBlock + tid;
-        if (i < n) acc_point<SC1>(P, slot, T, scale, dl, i, acc);
+        if (i < n) acc_point(P, slot, T, scale, dl, i, acc);
         wave_totals_f32<kNE>(acc, s_acc[wid]);
         __syncthreads();
         if (tid < kNE) {
@@ -548,16 +549,62 @@ __device__ void acc_blocks(const KParams& P, const int32_t* slot, const float (&
 __device__ __forceinline__ float cand_delta(const KParams& P, int c) {
     return static_cast<float>(c < P.NA ? P.alphas[c + 1] : P.min_scale);
 }
+// Candidate workgroup wgi: part (wgi % W) of candidate c = wgi / W's partials.  With P.cand_rec the candidate's GN step
+// is also solved here, while the EM still runs (:417-448: solve_sums + solve_step over the same partials the fused
+// k_accumulate / k_solve_pick would reduce, so the same bits): W = 1 in this workgroup; W > 1 by the candidate's last
+// workgroup to arrive -- the parts' partials are stored write-through and drained before an agent-scope add on the
+// candidate's counter (MI355X_MICROARCH.md "inter-workgroup visibility", the one-lane-signals row), and the last
+// arrival reads them past L1 and re-zeroes the counter for the next launch.  The record [kCandWords] is read by
+// k_pick_correspond / k_pick after the launch, so the selected solve leaves the iteration's critical path.
 __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
     const int nb = P.nb_acc;
     const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
     const int c = wgi / W, part = wgi - c * W;
     if (c > P.NA) return;
+    const int tid = threadIdx.x;
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
-    acc_blocks<false>(P, P.slot, T, scale, cand_delta(P, c), part * kSpecBlocksPerWG, min(nb, (part + 1) * kSpecBlocksPerWG),
-                      P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE);
+    double* part_c = P.acc_part + static_cast<size_t>(c) * kFuseMaxBlocks * kNE;
+    const int vb0 = part * kSpecBlocksPerWG, vb1 = min(nb, (part + 1) * kSpecBlocksPerWG);
+    const bool handoff = P.cand_rec && W > 1;
+    if (handoff) acc_blocks<true>(P, P.slot, T, scale, cand_delta(P, c), vb0, vb1, part_c);
+    else acc_blocks<false>(P, P.slot, T, scale, cand_delta(P, c), vb0, vb1, part_c);
+    if (!P.cand_rec) return;
+    __shared__ int s_last;
+    __shared__ double s_tot[kNE];
+    __shared__ float s_rec[kCandWords];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave: its partials have left
+    __syncthreads();
+    if (handoff) {
+        if (tid == 0) {
+            unsigned* cnt = P.cand_cnt + c;
+            const unsigned old = __hip_atomic_fetch_add((g_u32*)(cnt), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old + 1u == static_cast<unsigned>(W) ? 1 : 0;
+            if (s_last) Mem<true>::st(cnt, 0u);               // every part has arrived: ready for the next launch
+        }
+        __syncthreads();
+        if (!s_last) return;
+        solve_sums<kBlock, true>(part_c, nb, s_tot);
+    } else {
+        solve_sums<kBlock, false>(part_c, nb, s_tot);
+    }
+    if (tid == 0) {
+        float Tn[12];
+        lo_iter_log lg;
+        const bool conv = solve_step(P, s_tot, T, Tn, &lg);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) s_rec[q] = Tn[q];
+        s_rec[kCandCost] = lg.cost;
+#pragma unroll
+        for (int q = 0; q < 21; ++q) s_rec[kCandH + q] = lg.H[q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) { s_rec[kCandG + q] = lg.g[q]; s_rec[kCandD + q] = lg.delta[q]; }
+        s_rec[kCandConv] = conv ? 1.0f : 0.0f;
+        s_rec[kCandConv + 1] = 0.0f;
+    }
+    __syncthreads();
+    if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
 }
 
 // Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts
@@ -573,22 +620,18 @@ struct PrefixLoads {
     uint64_t wm[kWavesPerBlock];
 };
 
-// SC1 (the persistent launch): the counts / sums / ballots were handed over inside the launch (Mem<true> loads), and
-// the scale of later iterations is the caller's (pl.sc is left 0).
-template <bool SC1 = false>
 __device__ __forceinline__ void prefix_loads(const KParams& P, const ScanBufs& B, int it, PrefixLoads& pl) {
-    using M = Mem<SC1>;
     const int lane = threadIdx.x & 63, nb = P.nb;
     const bool calc = it == 0 && !P.scale_given;
-    pl.c = lane < nb ? M::ld(B.blk_cnt + lane) : 0;
-    pl.bs = (calc && lane < nb) ? 0.0 + M::ld(P.blk_sum + lane) : 0.0;   // as `lsum += ...` from +0
-    pl.bm = (calc && lane < nb) ? M::ld(P.blk_m2 + lane) : 0.0;
+    pl.c = lane < nb ? B.blk_cnt[lane] : 0;
+    pl.bs = (calc && lane < nb) ? 0.0 + P.blk_sum[lane] : 0.0;   // as `lsum += ...` from +0
+    pl.bm = (calc && lane < nb) ? P.blk_m2[lane] : 0.0;
 #pragma unroll
     for (int q = 0; q < kWavesPerBlock; ++q) {
         const int w = q * 64 + lane;
-        pl.wm[q] = w < nb * kWavesPerBlock ? M::ld(B.wmask + w) : 0;
+        pl.wm[q] = w < nb * kWavesPerBlock ? B.wmask[w] : 0;
     }
-    pl.sc = (calc || SC1) ? 0.0 : B.st->scale;
+    pl.sc = calc ? 0.0 : B.st->scale;
 }
 
 template <int NW>
@@ -715,7 +758,7 @@ __device__ __forceinline__ void pko_prefix(const KParams& P, const ScanBufs& B, 
     scale_out = s_scale;
 }
 
-// LDS of the PKO phases (one instance per workgroup: pko_body, or the persistent launch).
+// LDS of the PKO phases (one instance per workgroup).
 template <int NW>
 struct PkoLds {
     // p: the split EM's per-sample pdfs of each component (double-buffered), then the JS terms (>= 20 alphas)
@@ -760,13 +803,11 @@ __device__ __forceinline__ void pko_prefetch(const KParams& P, int wg, int G, Pk
 }
 
 // Phases 2-4 of the PKO for n_c >= 1 correspondences with normalisation scale `scale`: the reference's GMM sample,
-// the GMM fit and this workgroup's slice of the JS grid (written to B.js).  SC1 (the persistent launch): the stored
-// residuals / slots are read and the JS costs written through Mem<true>.
-template <int NW, bool ONE_WAVE, bool SC1>
+// the GMM fit and this workgroup's slice of the JS grid (written to B.js).
+template <int NW, bool ONE_WAVE>
 __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, int wg, int G, int nc, double scale,
                                            const PkoPrefetch& pf, const int* s_pre, const uint64_t* s_wmask,
                                            PkoLds<NW>& L, unsigned long long* dbg) {
-    using M = Mem<SC1>;
     constexpr int NT = NW * 64;
     DevState* st = B.st;
     const int tid = threadIdx.x;
@@ -807,7 +848,7 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
             uint64_t m4[kWavesPerBlock];                        // the block's ballots: independent loads in flight
 #pragma unroll
             for (int q = 0; q < kWavesPerBlock; ++q)
-                m4[q] = s_wmask ? s_wmask[b * kWavesPerBlock + q] : M::ld(B.wmask + b * kWavesPerBlock + q);
+                m4[q] = s_wmask ? s_wmask[b * kWavesPerBlock + q] : B.wmask[b * kWavesPerBlock + q];
             int w = 0;
             uint64_t mk = m4[0];
 #pragma unroll
@@ -828,14 +869,14 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
             if (P.kd_res) {
                 v = P.kd_res[pidx] / sden;                       // KDTree path: stored fp64 distance
             } else if (B.res) {
-                v = M::ld(B.res + pidx) / sden;                  // stored by the correspondence launch (same bits)
+                v = B.res[pidx] / sden;                          // stored by the correspondence launch (same bits)
             } else {
                 float T[12];
 #pragma unroll
                 for (int q = 0; q < 12; ++q) T[q] = B.pose_in ? B.pose_in[q] : st->pose[q];
                 float wx, wy, wz;
                 transform_pt(T, P.pts[3 * pidx], P.pts[3 * pidx + 1], P.pts[3 * pidx + 2], wx, wy, wz);
-                v = residual_f64(P.tab[M::ld(B.slot + pidx)], wx, wy, wz) / sden;   // :321-326
+                v = residual_f64(P.tab[B.slot[pidx]], wx, wy, wz) / sden;   // :321-326
             }
         }
         LO_STAMP_WAIT(dbg, 14, sidx == 0);
@@ -935,7 +976,7 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
 #pragma unroll
                     for (int q = 0; q < 20; ++q) vb[q] = vn[q];
                 }
-                M::st(B.js + ai, cnt == 0.0 ? DBL_MAX : cost / cnt);
+                B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }
             if (!one_alpha) { L.az[tid] = nx_a; L.az[kJsPass + tid] = nx_z; }
             L.nan[tid] = 0;                                      // read above; the next pass counts after the barrier
@@ -988,7 +1029,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     if (lead && tid == 0) st->n_corr = nc;
     if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
     LO_STAMP(dbg, 1);
-    pko_fit_js<NW, ONE_WAVE, false>(P, B, wg, G, nc, s_scale, pf, s_pre, s_wmask, L, dbg);
+    pko_fit_js<NW, ONE_WAVE>(P, B, wg, G, nc, s_scale, pf, s_pre, s_wmask, L, dbg);
 }
 
 }  // namespace lo

@@ -142,12 +142,6 @@ class IterativeClosestPointOptimizer:
         if rc != 0:
             raise RuntimeError(f"lo_set_exact failed ({rc})")
 
-    def set_persistent(self, enable: bool = True):
-        """The whole GN loop of a small PKO scan as one persistent launch (default on; bit-identical either way)."""
-        rc = self._L.lo_set_persistent(self.ctx, int(bool(enable)))
-        if rc != 0:
-            raise RuntimeError(f"lo_set_persistent failed ({rc})")
-
     def set_lookahead(self, enable: bool = True):
         """Two GN iterations per launch for small PKO scans (default off; bit-identical either way)."""
         rc = self._L.lo_set_lookahead(self.ctx, int(bool(enable)))
