@@ -145,11 +145,6 @@ void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
 /* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again (a fresh
  * hipStreamNonBlocking stream -- so the legacy default stream, handle 0, cannot be selected: pass a created stream). */
 int lo_set_stream(lo_ctx* ctx, void* hip_stream);
-/* Lookahead launches for small scans with PKO (default off): every alpha candidate's next GN iteration -- its whole
- * PKO included -- runs while the current iteration's PKO runs, two iterations per launch, results bit-identical to
- * the one-iteration-at-a-time path.  Off by default: at KITTI size a candidate chain's sequential normal equations,
- * solve and correspondence sweeps inside one workgroup outweigh the EM overlap. */
-int lo_set_lookahead(lo_ctx* ctx, int enable);
 /* Reference-exact arithmetic (default off): H, g and the cost summed SEQUENTIALLY in fp32 over the correspondences
  * in scan order, the iteration-0 scale from the sorted residuals, the fp32 LDLT and SO3 re-projection through
  * JacobiSVD -- the reference's own operation order (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99),

@@ -77,8 +77,6 @@ struct KParams {
     int init;                         // k_correspond: first launch of a scan resets DevState (pose = T0)
     float T0[12];
     const float* T0p;                 // batched launches: the job's initial pose in device memory (else T0)
-    KParams* stash;                   // nullable: the first k_correspond of a scan copies these parameters here (init
-                                      // cleared) for kernels that read them from memory (k_la: no kernarg SGPR pressure)
     // KDTree correspondence path (use_surfel_correspondence = 0; lo_kdtree.hip)
     const float4* kd_pts;             // L0 centroids sorted by grid cell: x, y, z, original index (int bits)
     const uint32_t* kd_start;         // cell -> first point (dense grid, ncell + 1 entries)
@@ -141,34 +139,8 @@ struct KParams {
     DevState* st;
 };
 
-// Lookahead launches (lo_lookahead.hip): one candidate chain's results for GN iterations k, k + 1 of a launch.
-struct LaRec {
-    lo_iter_log log[2];
-    int n_exec;                       // iterations the chain executed: 1 (converged / max_iterations) or 2
-    int conv0, conv1;                 // convergence after iteration k / k + 1
-    int status1;                      // LO_INSUFFICIENT: iteration k + 1 found too few correspondences
-};
-constexpr int kLaThreads = 512;       // lookahead workgroup (8 waves: 2 blocks per pass in the chains' sweeps)
-
-// Per-context lookahead buffers (host-allocated once; candidates c = 0..NA).
-struct LaParams {
-    int n_cap;                        // points per candidate buffer (kFuseMaxBlocks x kBlock)
-    int32_t* slotX;                   // [NA+1][n_cap]      chain-private correspondences of iteration k + 1
-    uint64_t* wmaskX;                 // [NA+1][n_cap/64]
-    int32_t* blkX;                    // [NA+1][kFuseMaxBlocks]
-    int32_t* slotO;                   // [2][NA+1][n_cap]   correspondences of iteration k + 2 (next launch's input)
-    uint64_t* wmaskO;                 // [2][NA+1][n_cap/64]
-    int32_t* blkO;                    // [2][NA+1][kFuseMaxBlocks]
-    double* jsC;                      // [NA+1][NA+1]       each chain's JS grid of iteration k + 1
-    double* jsM;                      // [2][NA+1]          the main JS grid of iteration k
-    DevState* stC;                    // [NA+1]             each chain's GN state for its PKO
-    LaRec* rec;                       // [2][NA+1]
-    unsigned long long* stamp;        // diagnostic build: chain 0's stage timestamps (DevState::dbg + 8)
-};
-
-// The per-iteration buffers a PKO / accumulate / correspondence pass works on: the context's own (own_bufs), or a
-// lookahead chain's (lo_lookahead.hip).  Passed beside the kernel-argument KParams, so a kernel that works on several
-// buffer sets holds a few pointers instead of several KParams copies.
+// The per-iteration buffers a PKO pass works on (own_bufs: the context's own), passed beside the kernel-argument
+// KParams.
 struct ScanBufs {
     int32_t* slot;
     uint64_t* wmask;

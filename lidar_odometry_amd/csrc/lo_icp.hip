@@ -51,7 +51,6 @@ template <bool SOLVE> __global__ void k_accumulate_b1(const KParams* PB, int it)
 __global__ void k_solve_b1(const KParams* PB, int it);
 __global__ void k_solve_b(const KParams* PB, int it);
 __global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
-__global__ void k_la(const KParams* Pp, LaParams L, int k, int G);
 struct MapPatchRec;
 __global__ void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n);
 struct FitJob {
@@ -61,7 +60,6 @@ struct FitJob {
 struct FitOut;
 __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
                              FitOut* out);
-__global__ void k_la_finish(const KParams* Pp, LaParams L, int k_next);
 __global__ void k_exact_scale(KParams P, int n2);
 __global__ void k_exact_terms(KParams P);
 __global__ void k_exact_solve(KParams P, int it);
@@ -107,13 +105,8 @@ struct lo_ctx {
     float* d_cand_rec = nullptr;    //   and each candidate's solved GN step [NA + 1][kCandWords]
     unsigned* d_cand_cnt = nullptr; //   per-candidate workgroup arrivals (zero between launches)
     bool presolve = true;           //   candidates solve inside the PKO launch (LO_PRESOLVE=0: k_solve_* instead)
-    LaParams la{};                  // lookahead launch buffers (allocated on the first small PKO optimize)
-    void* d_la = nullptr;           //   one allocation behind them
-    KParams* d_la_params = nullptr; //   the scan's parameters, stashed by its first k_correspond
-    bool lookahead = false;         // lo_set_lookahead (measured slower at KITTI size: DESIGN.md §3)
     bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
     float* d_ex_terms = nullptr;
-    size_t la_pad = 0;              //   dynamic LDS of k_la (prefix + padding to one workgroup per CU)
     double* d_js = nullptr;
     double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
     size_t res_cap = 0;
@@ -225,45 +218,6 @@ static void launch_gn_tail(lo_ctx* c, const KParams& P, int it) {
         hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, it, 0);
         hipLaunchKernelGGL(k_solve, dim3(1), dim3(kSolveThreads), 0, c->stream, P, it, 0);
     }
-}
-
-// Lookahead buffers (lo_lookahead.hip): per candidate c = 0..NA, chain-private correspondences, the double-buffered
-// next-iteration correspondences, a JS grid, a scratch GN state and the two records; ~200 KB per candidate.
-static int ensure_la(lo_ctx* c) {
-    if (c->d_la) return LO_OK;
-    hipFuncAttributes fa{};
-    LO_HIP(c, hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_la)));
-    const size_t half = 80 * 1024 + 256;              // > half of the CU's 160 KB LDS: one workgroup per CU
-    c->la_pad = fa.sharedSizeBytes < half ? half - fa.sharedSizeBytes : 0;
-    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_la), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(std::max<size_t>(c->la_pad, kMaxBlocks * sizeof(int)))));
-    const size_t nc1 = static_cast<size_t>(c->cfg.num_alpha_segments) + 1;
-    const size_t ncap = static_cast<size_t>(kFuseMaxBlocks) * kBlock, nw = ncap / kWave;
-    size_t off = 0;
-    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-    const size_t o_slotX = take(nc1 * ncap * 4), o_wmX = take(nc1 * nw * 8), o_blkX = take(nc1 * kFuseMaxBlocks * 4);
-    const size_t o_slotO = take(2 * nc1 * ncap * 4), o_wmO = take(2 * nc1 * nw * 8), o_blkO = take(2 * nc1 * kFuseMaxBlocks * 4);
-    const size_t o_jsC = take(nc1 * nc1 * 8), o_jsM = take(2 * nc1 * 8), o_stC = take(nc1 * sizeof(DevState));
-    const size_t o_rec = take(2 * nc1 * sizeof(LaRec));
-    const size_t o_par = take(sizeof(KParams));
-    LO_HIP(c, hipMalloc(&c->d_la, off));
-    LO_HIP(c, hipMemsetAsync(c->d_la, 0, off, c->stream));
-    char* b = static_cast<char*>(c->d_la);
-    LaParams& L = c->la;
-    L.n_cap = static_cast<int>(ncap);
-    L.slotX = reinterpret_cast<int32_t*>(b + o_slotX);
-    L.wmaskX = reinterpret_cast<uint64_t*>(b + o_wmX);
-    L.blkX = reinterpret_cast<int32_t*>(b + o_blkX);
-    L.slotO = reinterpret_cast<int32_t*>(b + o_slotO);
-    L.wmaskO = reinterpret_cast<uint64_t*>(b + o_wmO);
-    L.blkO = reinterpret_cast<int32_t*>(b + o_blkO);
-    L.jsC = reinterpret_cast<double*>(b + o_jsC);
-    L.jsM = reinterpret_cast<double*>(b + o_jsM);
-    L.stC = reinterpret_cast<DevState*>(b + o_stC);
-    L.rec = reinterpret_cast<LaRec*>(b + o_rec);
-    c->d_la_params = reinterpret_cast<KParams*>(b + o_par);
-    L.stamp = c->d_st->dbg + 8;
-    return LO_OK;
 }
 
 static int ensure_acc_part(lo_ctx* c) {
@@ -528,7 +482,7 @@ void lo_destroy(lo_ctx* c) {
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
-                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_la, c->d_ex_terms, c->d_res_pko,
+                    c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_ex_terms, c->d_res_pko,
                     c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
@@ -978,26 +932,6 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             const int rc3 = exact_prepare(c, P, n, &n2);
             if (rc3 != LO_OK) return rc3;
             for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
-            LO_HIP(c, hipGetLastError());
-            LO_HIP(c, hipEventRecord(c->ev1, c->stream));
-            c->pending = true;
-            return LO_OK;
-        }
-        if (fused && !c->kd && c->lookahead) {
-            // two GN iterations per launch (lo_lookahead.hip): k_correspond, k_la(0), k_la(2), ..., k_la_finish
-            const int rc2 = ensure_la(c);
-            if (rc2 != LO_OK) return rc2;
-            P0.stash = c->d_la_params;                    // k_correspond copies the parameters for k_la
-            launch_correspond_first(c, P0, false);
-            const int G = pko_grid(g);
-            // dynamic LDS: the prefix (nb ints), padded so that one workgroup fills a CU's LDS -- the 201 workgroups
-            // then sit on 201 CUs and no two EM chains share a SIMD
-            const size_t pre_bytes = std::max<size_t>(static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int), c->la_pad);
-            int k = 0;
-            for (; k < g.max_iterations; k += 2)
-                hipLaunchKernelGGL(k_la, dim3(G + P.NA + 1), dim3(kLaThreads), pre_bytes, c->stream, c->d_la_params, c->la,
-                                   k, G);
-            hipLaunchKernelGGL(k_la_finish, dim3(1), dim3(kWave), 0, c->stream, c->d_la_params, c->la, k);
             LO_HIP(c, hipGetLastError());
             LO_HIP(c, hipEventRecord(c->ev1, c->stream));
             c->pending = true;
@@ -1465,12 +1399,6 @@ int lo_stage_time(lo_ctx* c, double* avg_us, int* count) {
 int lo_set_exact(lo_ctx* c, int enable) {
     if (!c) return LO_ERR_ARG;
     c->exact = enable != 0;
-    return LO_OK;
-}
-
-int lo_set_lookahead(lo_ctx* c, int enable) {
-    if (!c) return LO_ERR_ARG;
-    c->lookahead = enable != 0;
     return LO_OK;
 }
 

@@ -60,15 +60,6 @@ __device__ __forceinline__ int xcd_block(int h, int nb) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_correspond(KParams P, int with_stats) {
-    if (P.init && P.stash && blockIdx.x == 0) {          // the scan's parameters for the k_la launches (lo_icp.hip)
-        constexpr int kWords = sizeof(KParams) / 4;
-        static_assert(sizeof(KParams) % 4 == 0, "KParams copy by dwords");
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&P);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(P.stash);
-        for (int w = threadIdx.x; w < kWords; w += kBlock) dst[w] = src[w];
-        __syncthreads();
-        if (threadIdx.x == 0) P.stash->init = 0;
-    }
     correspond_body(P, with_stats, P.init, xcd_block(blockIdx.x, gridDim.x));
 }
 

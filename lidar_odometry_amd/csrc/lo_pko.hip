@@ -1,5 +1,5 @@
 // lo_pko.hip — the PKO kernels (k_pko_t single scan, k_pko_tb batched, k_pko_finish); the device code lives in
-// lo_pko_body.h (shared with the lookahead launch, lo_lookahead.hip).
+// lo_pko_body.h.
 #include "lo_pko_body.h"
 
 namespace lo {

@@ -142,12 +142,6 @@ class IterativeClosestPointOptimizer:
         if rc != 0:
             raise RuntimeError(f"lo_set_exact failed ({rc})")
 
-    def set_lookahead(self, enable: bool = True):
-        """Two GN iterations per launch for small PKO scans (default off; bit-identical either way)."""
-        rc = self._L.lo_set_lookahead(self.ctx, int(bool(enable)))
-        if rc != 0:
-            raise RuntimeError(f"lo_set_lookahead failed ({rc})")
-
     def close(self):
         h = getattr(self, "_ctx", None)
         if h:
