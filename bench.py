@@ -173,27 +173,82 @@ def pose12(T):
 # --------------------------------------------------------------------------------------------------
 # CPU baseline: oracle restatement of the reference ICP, 1 thread, bounded sample
 # --------------------------------------------------------------------------------------------------
-def cpu_baseline(wl, budget_s: float):
+def _rot_diff(A12, B12) -> float:
+    """Rotation difference (rad) of two row-major 3x4 poses: ||Ra - Rb||_F / sqrt(2) ~ the angle."""
+    a = np.asarray(A12, np.float64).reshape(3, 4)[:, :3]
+    b = np.asarray(B12, np.float64).reshape(3, 4)[:, :3]
+    return float(np.linalg.norm(a - b) / np.sqrt(2.0))
+
+
+def parity_vs_oracle(gpu, cpu) -> dict:
+    """The GPU's optimize() results against the oracle's on the same scans (north_star: 1e-4 m / 1e-4 rad per
+    iteration on identical inputs).  gpu / cpu: per scan {"ok", "T" (12), "logs" (per-iteration dicts)}."""
+    dt = dr = dt_it = dr_it = 0.0
+    same_iters = same_alpha0 = same_alpha_all = same_ok = 0
+    for g, c in zip(gpu, cpu):
+        same_ok += int(g["ok"] == c["ok"])
+        dt = max(dt, float(np.abs(np.asarray(g["T"], np.float64).reshape(3, 4)[:, 3]
+                                  - np.asarray(c["T"], np.float64).reshape(3, 4)[:, 3]).max()))
+        dr = max(dr, _rot_diff(g["T"], c["T"]))
+        same_iters += int(len(g["logs"]) == len(c["logs"]))
+        if g["logs"] and c["logs"]:
+            same_alpha0 += int(g["logs"][0]["alpha"] == c["logs"][0]["alpha"])
+        same_alpha_all += int(len(g["logs"]) == len(c["logs"]) and
+                              all(a["alpha"] == b["alpha"] for a, b in zip(g["logs"], c["logs"])))
+        for a, b in zip(g["logs"], c["logs"]):
+            dt_it = max(dt_it, float(np.abs(np.asarray(a["pose"], np.float64).reshape(3, 4)[:, 3]
+                                            - np.asarray(b["pose"], np.float64).reshape(3, 4)[:, 3]).max()))
+            dr_it = max(dr_it, _rot_diff(a["pose"], b["pose"]))
+    n = len(gpu)
+    return {"scans": n, "max_abs_dt_m": dt, "max_abs_dR_rad": dr, "per_iteration_max_dt_m": dt_it,
+            "per_iteration_max_dR_rad": dr_it, "within_1e-4": bool(dt_it <= 1e-4 and dr_it <= 1e-4),
+            "status_equal": same_ok, "iteration_count_equal": same_iters, "alpha_iter0_equal": same_alpha0,
+            "alpha_every_iteration_equal": same_alpha_all}
+
+
+def cpu_baseline(wl, budget_s: float, gpu=None, gpu_exact=None):
+    """The oracle port timed on this host (1 thread, bounded sample); its first pass over the distinct scans is also
+    the parity reference for the GPU results of the same scans (gpu: default mode, gpu_exact: reference-exact mode,
+    compared bit for bit)."""
     import oracle
     m = oracle.VoxelMap(wl["voxel"], 3, 0.1, True)
     for w, s in wl["keyframes"]:
         m.update(w, s, wl["max_dist"], True)
     scans, inits = wl["scans"], [pose12(T) for T in wl["inits"]]
     n_scans = n_iters = 0
+    ref = []
     t0 = time.perf_counter()
     while True:
         i = n_scans % len(scans)
         pts_i = oracle.voxel_filter(wl["raw_scans"][i], 0.5, 8) if wl.get("raw") else scans[i]
-        ok, To, it, _ = oracle.icp_optimize(m, pts_i, inits[i], kdtree=wl.get("kdtree", False))
+        ok, To, it, logs = oracle.icp_optimize(m, pts_i, inits[i], kdtree=wl.get("kdtree", False))
+        if n_scans < len(scans):
+            ref.append({"ok": ok, "T": np.asarray(To if ok else inits[i], np.float32), "logs": logs})
         n_scans += 1
         n_iters += it
         el = time.perf_counter() - t0
         if el >= budget_s and n_scans >= len(scans):
             break
-    return {"value": n_scans / el, "unit": "scans/s", "cores": 1, "kind": "port",
-            "gn_iters_per_sec": n_iters / el,
-            "sample": f"{n_scans} optimize() calls over {len(scans)} distinct scans in {el:.1f} s "
-                      f"(oracle/liblo_oracle.so, single thread, g++ -O3, same synthetic inputs)"}
+    out = {"value": n_scans / el, "unit": "scans/s", "cores": 1, "kind": "port",
+           "gn_iters_per_sec": n_iters / el,
+           "sample": f"{n_scans} optimize() calls over {len(scans)} distinct scans in {el:.1f} s "
+                     f"(oracle/liblo_oracle.so, single thread, g++ -O3, same synthetic inputs)"}
+    if gpu is not None:
+        out["parity"] = parity_vs_oracle(gpu, ref)
+        out["parity"]["mode"] = "default (fp64 tree sums, fp64 LDLT + polar SO3)"
+    if gpu_exact is not None:
+        bitwise = sum(int(g["ok"] == c["ok"] and np.array_equal(np.asarray(g["T"], np.float32).view(np.uint32),
+                                                                   np.asarray(c["T"], np.float32).view(np.uint32))
+                          and len(g["logs"]) == len(c["logs"])
+                          and all(np.array_equal(a["pose"].view(np.uint32), b["pose"].view(np.uint32)) and
+                                  a["alpha"] == b["alpha"] and a["n_corr"] == b["n_corr"]
+                                  for a, b in zip(g["logs"], c["logs"])))
+                      for g, c in zip(gpu_exact, ref))
+        out["parity_exact"] = {"scans": len(ref), "bitwise_equal": bitwise,
+                               "mode": "lo_set_exact: the reference's fp32 operation order (sequential sums, fp32 "
+                                       "LDLT, JacobiSVD SO3); every iteration's pose, alpha and n_corr compared bit "
+                                       "for bit"}
+    return out
 
 
 def cpu_baseline_replicas(wl, budget_s: float, threads: int):
@@ -331,15 +386,125 @@ def live_pmc(case: dict, reps: int = 200, kernel: str = "k_correspond"):
                           "hits included"}
 
 
-def read_pko_latency():
+def pko_roofline(em_live):
     """The dominant kernel's latency roofline (k_pko_t: a strictly sequential fp64 EM chain, neither HBM- nor
-    MFMA-bound): measured cycles per EM iteration against the floor from measured instruction costs, from the
-    committed profiles/pko_latency.json (scripts/pko_stamps.py + scripts/lat_bench.hip on the GPU box)."""
+    MFMA-bound): cycles per EM iteration measured in this run (em_live: the lead PKO workgroup's s_memtime around its
+    EM loop inside the bench's GN loop) against the issue floor of the loop's own instruction stream (the ISA count
+    and measured instruction costs committed in profiles/pko_latency.json: scripts/pko_em_isa.py over the gfx950
+    assembly, scripts/lat_bench.hip on the MI355X)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pko_latency.json")) as f:
-            return json.load(f)
+            floor = json.load(f)
     except Exception:
-        return None
+        floor = {}
+    achieved = em_live.get("cycles_per_em_iteration")
+    peak = floor.get("peak")
+    return {"kernel": "k_pko_t", "bound": "latency", "unit": "cycles per EM iteration",
+            "achieved": achieved, "peak": peak, "frac": (peak / achieved) if (achieved and peak) else None,
+            "measured_live": em_live,
+            "floor_model": {k: floor.get(k) for k in ("floor_model", "isa_counts", "issue_cost_cycles", "isa_by")},
+            "note": "lower is better: frac = issue floor / measured cycles; the EM must stay fp64 with the reference's "
+                    "iteration count for alpha to stay identical"}
+
+
+def c5_hbm_leg(local: int, dev, n_scans: int):
+    """C5's data at one GPU's scale (BASELINE.json configs[4]: synthetic 1M-point scans, 1000 planar patches + 10 %
+    outliers): n_scans DISTINCT scans, each on its own context (its own slot / residual outputs and table copy),
+    launched round-robin on one stream.  Between two launches of a scan the other n_scans - 1 move their own ~24 MB
+    each, so the working set exceeds the 256 MB Infinity Cache and every correspondence launch reads its scan from
+    HBM.  Reports k_correspond against the HBM roofline (isolated single launches with no set-up pass, and in-step:
+    each scan's first correspondence launch inside its GN loop) and the 1M-point optimize rate."""
+    import torch
+
+    from lidar_odometry_amd import lib, synth
+    from lidar_odometry_amd.icp import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
+    from lidar_odometry_amd.voxelmap import VoxelMap
+    L = lib()
+    t0 = time.perf_counter()
+    sc = synth.patch_scene(1000, 1000)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    vm.update(synth.sample_patches(sc, 1_500_000, 1007, sigma=0.01, outlier_frac=0.0), np.zeros(3), 1e4, True)
+    rng = np.random.default_rng(1000)
+    stream = torch.cuda.Stream(dev)
+    fptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))   # noqa: E731
+    ctxs, d_scans, scans, inits = [], [], [], []
+    for f in range(n_scans):
+        T = synth.se3(synth.rot_z(0.2 + 0.05 * f), [1.0 + 0.3 * f, -2.0, 0.5])
+        pts = synth.azimuth_order(synth.transform(np.linalg.inv(T), synth.sample_patches(sc, 1_000_000, 2011 + f)))
+        o = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=0.5),
+                                           device=local, max_points=len(pts))
+        assert L.lo_map_set_from_voxelmap(o.ctx, vm.handle) == 0
+        ctxs.append(o)
+        scans.append(pts)
+        inits.append(pose12(synth.perturb(T, rng, 0.05, 0.01)))
+        d_scans.append(torch.from_numpy(pts).to(dev))
+    log(f"[c5] {n_scans} distinct 1M-point scans built in {time.perf_counter() - t0:.1f} s, "
+        f"{vm.surfel_count()} surfels")
+    alg, it0, iters = [], [], []
+    for o, p, Ti in zip(ctxs, scans, inits):
+        o.optimize(None, p, Ti)
+        st = o.get_last_stats()
+        it0.append((float(st.iterations[0]["scale"]), float(st.iterations[0]["alpha"])))
+        iters.append(st.num_iterations)
+        nv, _, _ = o.find_correspondences(p, Ti)
+        alg.append(len(p) * (12 + 8 + 4 + 8 + 0.125) + 24 * nv)
+    for o in ctxs:
+        L.lo_set_stream(o.ctx, C.c_void_p(stream.cuda_stream))
+    # working set between two launches of one scan: every scan's points + its context's outputs + its table copy
+    tab_bytes = 32 * 4 * vm.surfel_count()
+    ws = sum(len(p) * (12 + 4 + 8) for p in scans) + n_scans * tab_bytes
+    # isolated: one launch per call, no set-up pass, round-robin over the scans (each last touched n_scans - 1 ago)
+    iso_us, iso_bytes = [], []
+    for r in range(4):
+        for i, o in enumerate(ctxs):
+            ms = C.c_float(0.0)
+            assert L.lo_bench_kernel(o.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]),
+                                     C.c_double(it0[i][0]), C.c_double(it0[i][1]), 4, 1, C.byref(ms)) == 0
+            if r > 0:
+                iso_us.append(ms.value * 1e3)
+                iso_bytes.append(alg[i])
+    iso_t = float(np.mean(iso_us))
+    iso_ach = float(np.mean(iso_bytes)) / (iso_t * 1e-6) / 1e9
+
+    def enqueue_round():
+        for i, o in enumerate(ctxs):
+            assert L.lo_icp_optimize_async(o.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0],
+                                           fptr(inits[i])) == 0
+    enqueue_round()
+    torch.cuda.synchronize(dev)
+    rounds = 6
+    t1 = time.perf_counter()
+    for _ in range(rounds):
+        enqueue_round()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t1
+    # in-step: each scan's first correspondence launch inside its GN loop (a separate pass with stage timing)
+    for o in ctxs:
+        L.lo_set_stage_timing(o.ctx, 1)
+    for _ in range(3):
+        enqueue_round()
+    tot_us = n_in = 0.0
+    for o in ctxs:
+        us, cnt = C.c_double(0.0), C.c_int(0)
+        assert L.lo_stage_time(o.ctx, C.byref(us), C.byref(cnt)) == 0
+        tot_us += us.value * cnt.value
+        n_in += cnt.value
+        L.lo_set_stage_timing(o.ctx, 0)
+    in_t = tot_us / max(n_in, 1)
+    in_ach = float(np.mean(alg)) / (in_t * 1e-6) / 1e9
+    for o in ctxs:
+        o.close()
+    return {"workload": "C5 synthetic 1M-point scans (1000 planar patches + 10 % outliers, azimuth order), "
+                        f"{n_scans} distinct scans, one context each, round-robin on one stream",
+            "value": rounds * n_scans / el, "unit": "scans/s (1M points)", "gn_iters_per_scan_avg": float(np.mean(iters)),
+            "working_set_bytes": float(ws), "in_cache": bool(ws <= MALL_BYTES), "map_surfels": vm.surfel_count(),
+            "roofline": {"kernel": "k_correspond", "bound": "hbm", "achieved": iso_ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": iso_ach / HBM_PEAK_GBS, "kernel_us": iso_t,
+                         "alg_bytes_per_launch": float(np.mean(alg)), "launches": len(iso_us),
+                         "timing": "single launches (lo_bench_kernel id 4: no set-up pass), HIP events, each scan "
+                                   f"last touched {n_scans - 1} scans earlier"},
+            "in_step": {"kernel_us": in_t, "achieved": in_ach, "frac": in_ach / HBM_PEAK_GBS, "scans": int(n_in),
+                        "timing": "each scan's first correspondence launch inside its GN loop (HIP events)"}}
 
 
 # --------------------------------------------------------------------------------------------------
@@ -593,6 +758,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS) + ["kitti_e2e", "kitti_loop"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work for cpu_baseline")
+    ap.add_argument("--c5", type=int, default=12,
+                    help="extra measurement with --config kitti: this many distinct 1M-point scans (C5), one context "
+                         "each, rotated so each launch reads its scan from HBM; 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--order", default="azimuth", choices=["azimuth", "random"], help="patch1m scan point order")
     ap.add_argument("--sequences", type=int, default=8,
@@ -704,13 +872,15 @@ def main():
             L.lo_icp_export_pose(icp.ctx, C.c_void_p(rec_log[n_step[0]].data_ptr()))
         n_step[0] += 1
 
-    # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them)
-    iters, errs = [], []
+    # per-scan GN iteration counts + accuracy vs ground truth (deterministic, so the timed pass repeats them); the
+    # results are also compared with the oracle's in cpu_baseline (parity of the measured workload itself)
+    iters, errs, gpu_res = [], [], []
     for i in range(len(d_scans)):
         ok, To = icp.optimize(None, wl["scans"][i], inits[i])
         st = icp.get_last_stats()
         iters.append(st.num_iterations)
         errs.append(float(np.linalg.norm(To[:, 3] - wl["gts"][i][:3, 3])))
+        gpu_res.append({"ok": bool(ok), "T": np.asarray(To, np.float32).reshape(12).copy(), "logs": st.iterations})
     # algorithmic bytes of each scan's first correspondence pass at its initial pose (formula: see alg_bytes below)
     scan_alg_bytes = []
     for i in range(len(d_scans)):
@@ -775,6 +945,8 @@ def main():
     # in-step duration of each scan's first correspondence launch (HIP events on the context stream around that
     # launch inside the real GN loop), over a separate pass of the same steps (events would perturb the timed pass)
     n_in = min(args.steps, 200)
+    em0 = (C.c_ulonglong * 3)()
+    assert L.lo_pko_em_stats(icp.ctx, em0, 1) == 0               # zero the EM clock sums
     L.lo_set_stage_timing(icp.ctx, 1)
     in_bytes = 0.0
     for k in range(n_in):
@@ -789,6 +961,13 @@ def main():
     in_us, in_cnt = C.c_double(0.0), C.c_int(0)
     assert L.lo_stage_time(icp.ctx, C.byref(in_us), C.byref(in_cnt)) == 0
     L.lo_set_stage_timing(icp.ctx, 0)
+    # the dominant kernel (k_pko_t) measured in the same pass: the lead workgroup clocks its EM loop (s_memtime)
+    em = (C.c_ulonglong * 3)()
+    assert L.lo_pko_em_stats(icp.ctx, em, 1) == 0
+    em_live = {"cycles_per_em_iteration": em[0] / em[1] if em[1] else None,
+               "em_iterations_per_fit": em[1] / em[2] if em[2] else None, "fits": int(em[2]),
+               "scans": in_cnt.value,
+               "timing": "s_memtime around the EM loop of the lead PKO workgroup, inside the GN loop of this pass"}
     n0 = d_scans[i0].shape[0]
     n_valid, valid, _ = icp.find_correspondences(wl["scans"][i0], inits[i0])
     v = n_valid / n0
@@ -832,6 +1011,42 @@ def main():
         i = k % len(d_scans)
         icp.optimize(None, wl["scans"][i], inits[i])
     pcie_rate = n_pc / (time.perf_counter() - t1)
+
+    # reference-exact arithmetic (lo_set_exact: sequential fp32 sums in the reference's order, fp32 LDLT, JacobiSVD
+    # SO3): the same steps timed, and every scan's result kept for the bit-for-bit comparison with the oracle
+    exact, gpu_exact = None, None
+    if world == 1 and max_pts <= 16384:
+        icp.set_exact(True)
+        gpu_exact = []
+        for i in range(len(d_scans)):
+            ok, To = icp.optimize(None, wl["scans"][i], inits[i])
+            st = icp.get_last_stats()
+            gpu_exact.append({"ok": bool(ok), "T": np.asarray(To, np.float32).reshape(12).copy(), "logs": st.iterations})
+        L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
+        n_ex = min(args.steps, 300)
+
+        def exact_step(k):
+            i = k % len(d_scans)
+            if raw:
+                rc = L.lo_icp_optimize_raw_async(icp.ctx, C.c_void_p(d_raw[i].data_ptr()), d_raw[i].shape[0], 8,
+                                                 C.c_float(0.5), fptr(inits[i]))
+            else:
+                rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0],
+                                             fptr(inits[i]))
+            assert rc == 0, rc
+        for k in range(10):
+            exact_step(k)
+        torch.cuda.synchronize(dev)
+        t4 = time.perf_counter()
+        for k in range(n_ex):
+            exact_step(k)
+        torch.cuda.synchronize(dev)
+        el4 = time.perf_counter() - t4
+        icp.set_exact(False)
+        exact = {"value": n_ex / el4, "unit": "scans/s", "steps": n_ex,
+                 "gn_iters_per_sec": sum(iters[k % len(iters)] for k in range(n_ex)) / el4,
+                 "note": "lo_set_exact: the reference's own fp32 operation order, bit-identical to the oracle "
+                         "(cpu_baseline.parity_exact); timed like value, never value"}
 
     # independent sequences sharing the GPU (serving many sensors / logs): B contexts, one HIP stream each,
     # scans enqueued round-robin without host syncs; aggregate scans/s.  Never `value`.
@@ -1012,11 +1227,14 @@ def main():
                      "working_set_bytes": ws_bytes, "in_cache": ws_bytes <= MALL_BYTES,
                      "in_cache_note": "working set (points + slot writes + one 32-B table sector per point) within the "
                                       "256 MB Infinity Cache: the fraction measures cache, not HBM, bandwidth"},
-        "roofline_dominant": read_pko_latency(),
+        "roofline_dominant": pko_roofline(em_live),
+        "exact_mode": exact,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
+        result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget, gpu_res, gpu_exact)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
+    if rank == 0 and world == 1 and args.config == "kitti" and args.c5 > 0:
+        result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5)
     icp.close()
     if rank == 0:
         emit(result)

@@ -156,11 +156,16 @@ int lo_set_exact(lo_ctx* ctx, int enable);
  * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */
 int lo_set_stage_timing(lo_ctx* ctx, int enable);
 int lo_stage_time(lo_ctx* ctx, double* avg_us, int* count);
+/* With stage timing on, the lead PKO workgroup also clocks its EM loop (s_memtime): out = {cycles, EM iterations, fits}
+ * summed over the optimize calls since the last reset (the dominant kernel's cycles per EM iteration, measured in the
+ * running GN loop).  Syncs the stream; reset != 0 zeroes the sums. */
+int lo_pko_em_stats(lo_ctx* ctx, unsigned long long out[3], int reset);
 /* Enqueue a copy of the current GN state into device memory: 16 floats = pose[12], status, iterations,
  * n_corr, 0.  For the scan-parallel pose gather (RCCL all-gather of these 16 floats per rank). */
 int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);
-/* Timing harness: reps back-to-back launches of one kernel (0 correspond, 1 accumulate, 2 pko, 3 solve)
- * on a device-resident scan at pose T; writes the average device time per launch (HIP events). */
+/* Timing harness: reps back-to-back launches of one kernel (0 correspond, 1 accumulate, 2 pko, 3 solve; 4 correspond
+ * without the set-up pass the others get, so a scan last touched long ago is read from HBM) on a device-resident scan
+ * at pose T; writes the average device time per launch (HIP events). */
 int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
                     int kernel_id, int reps, float* avg_ms);
 

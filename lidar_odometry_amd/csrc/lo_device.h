@@ -63,6 +63,7 @@ struct DevState {
     double cost_out;
     double gmm_out[3 * kMaxK];
     unsigned long long dbg[16];     // diagnostic build only (-DLO_PKO_STAMPS): phase timestamps / counters
+    unsigned long long em_stat[3];  // with stage timing: EM s_memtime cycles, EM iterations, fits (lead workgroup)
     lo_iter_log logs[LO_MAX_ITERS];
 };
 
@@ -136,6 +137,7 @@ struct KParams {
     float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
+    unsigned long long* em_stat;  // nullable (stage timing on): DevState::em_stat, the lead PKO workgroup's EM timing
     DevState* st;
 };
 

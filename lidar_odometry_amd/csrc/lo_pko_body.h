@@ -183,9 +183,11 @@ __device__ __forceinline__ void wave_totals4(double (&v)[NV]) {
 // the VALU issue on the critical path.  k-means and the initial variance run redundantly in every wave (identical inputs and code,
 // so identical results, no exchange).  All NW waves execute the loop (waves >= K only join the barriers), and
 // the convergence test reads the same LDS values everywhere, so every wave leaves at the same iteration.
+// emst (nullable, one workgroup): s_memtime cycles of the EM loop, its iterations and one fit are added there.
 template <int K, int SPL>
 __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const int32_t* draws, double* gmm,
-                                              double* s_p, double* s_dm, unsigned long long* dbg) {
+                                              double* s_p, double* s_dm, unsigned long long* dbg,
+                                              unsigned long long* emst) {
     static_assert(3 * K - 1 <= 8, "partials");
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int j = wid < K ? wid : -1;                      // this wave's component (-1: barriers only)
@@ -283,6 +285,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
     double ca = (iv <= 0.0) ? 0.0 : wj * (rs0 * kInvSqrt2Pi);
     double cb = (iv <= 0.0) ? 0.0 : 0.5 * (rs0 * rs0);
     LO_STAMP(dbg, 4);
+    const unsigned long long em_t0 = emst ? __builtin_amdgcn_s_memtime() : 0ull;
 
     // One barrier per iteration: after its M-step each wave evaluates the NEXT iteration's pdfs with the updated
     // parameters (speculatively) into the other half of the double-buffered s_p / s_dm, then the barrier; if
@@ -306,6 +309,7 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
 #pragma unroll
         for (int s = 0; s < SPL; ++s) pv[q][s] = s_p[q * kStride + 64 * s + lane];
     int buf = 0;
+    int n_em = 100;
     for (int em = 0; em < 100; ++em) {
         double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
@@ -360,10 +364,15 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
 #pragma unroll
         for (int q = 1; q < K; ++q) change += dmv[q];
         LO_COUNT(dbg, 8, em + 1);
-        if (change < 1e-6) break;
+        if (change < 1e-6) { n_em = em + 1; break; }
         buf ^= 1;
     }
     LO_STAMP(dbg, 5);
+    if (emst && threadIdx.x == 0) {                        // wave 0 (component 0): the loop's own clock
+        atomicAdd(emst, __builtin_amdgcn_s_memtime() - em_t0);
+        atomicAdd(emst + 1, static_cast<unsigned long long>(n_em));
+        atomicAdd(emst + 2, 1ull);
+    }
     if (j >= 0 && lane == 0) { gmm[j] = wj; gmm[K + j] = muj; gmm[2 * K + j] = varj; }
 }
 
@@ -499,10 +508,11 @@ __device__ __forceinline__ void gmm_fit_1w(const double* s_sd, int S, const int3
 
 template <int K>
 __device__ __forceinline__ void gmm_fit_dispatch(const double* s_sd, int S, const int32_t* draws, double* gmm,
-                                                 double* s_p, double* s_dm, unsigned long long* dbg) {
-    if (S <= 64) gmm_fit_split<K, 1>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
-    else if (S <= 128) gmm_fit_split<K, 2>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
-    else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg);
+                                                 double* s_p, double* s_dm, unsigned long long* dbg,
+                                                 unsigned long long* emst) {
+    if (S <= 64) gmm_fit_split<K, 1>(s_sd, S, draws, gmm, s_p, s_dm, dbg, emst);
+    else if (S <= 128) gmm_fit_split<K, 2>(s_sd, S, draws, gmm, s_p, s_dm, dbg, emst);
+    else gmm_fit_split<K, 4>(s_sd, S, draws, gmm, s_p, s_dm, dbg, emst);
 }
 
 template <int K>
@@ -895,10 +905,11 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
             default: gmm_fit_1w_dispatch<3>(L.sd, S, draws, L.gmm); break;
         }
     } else {
+        unsigned long long* emst = lead ? P.em_stat : nullptr;
         switch (P.K) {                                          // every wave: see gmm_fit_split
-            case 1: gmm_fit_dispatch<1>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
-            case 2: gmm_fit_dispatch<2>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
-            default: gmm_fit_dispatch<3>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg); break;
+            case 1: gmm_fit_dispatch<1>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg, emst); break;
+            case 2: gmm_fit_dispatch<2>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg, emst); break;
+            default: gmm_fit_dispatch<3>(L.sd, S, draws, L.gmm, L.p, L.dm, dbg, emst); break;
         }
     }
     __syncthreads();
