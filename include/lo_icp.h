@@ -176,7 +176,8 @@ int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12]
  * (blockIdx.y = job).  Each job computes exactly what lo_icp_optimize computes on its context (bit-identical:
  * same kernels, same per-job reductions).  The reference has no batch entry point; this is the multi-sequence
  * form of IterativeClosestPointOptimizer::optimize (IterativeClosestPointOptimizer.cpp:255-463) called once
- * per sequence.  Requirements: surfel correspondence mode, one device, equal max_iterations.  The batch runs
+ * per sequence.  Requirements: surfel correspondence mode, one device, equal max_iterations, reference-exact mode
+ * off (lo_set_exact has no batched form: create and optimize refuse such a context).  The batch runs
  * on its own stream; the contexts must be idle while it runs and each context's lo_icp_result() is not valid
  * for a batched scan (use lo_batch_result). */
 typedef struct lo_batch lo_batch;

@@ -8,6 +8,8 @@
  *
  * Results are bit-identical to the reference's fp32 arithmetic (insertion-ordered containers with
  * unordered_dense's swap-with-last erase, Eigen JacobiSVD<Matrix3f> restated), checked against the oracle.
+ * Every lo_voxelmap_* call (the const readers included: they apply pending device fits) locks the map's recursive
+ * mutex, as the reference's VoxelMap does, so one map may be used from several threads.
  */
 #ifndef LO_MAP_H
 #define LO_MAP_H

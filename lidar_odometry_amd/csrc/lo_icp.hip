@@ -139,6 +139,7 @@ struct lo_ctx {
     uint64_t fit_ticket = 0;        // the launch whose results sit in h_fit_out (0: none)
     uint64_t fit_gen = 0;           //   and the table generation it patched
     std::vector<uint64_t> fit_keys; //   its packed keys, job order
+    bool fit_reconciled = false;    //   its planarity failures already removed from `resident`
     float fit_thr = 0.0f;
     // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
     bool kd = false;
@@ -587,10 +588,27 @@ static int grow_pinned_pair(lo_ctx* c, void** h, void** d, size_t* cap, size_t b
     return LO_OK;
 }
 
+// The pending fit launch's planarity failures leave the resident mirror (the kernel erased them from the table), once:
+// before a count is reported, before another patch or fit reads the mirror, and when the map collects the results.
+static int reconcile_fit(lo_ctx* c) {
+    if (c->fit_ticket == 0 || c->fit_reconciled) return LO_OK;
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipEventSynchronize(c->ev_fit));
+    const FitResult* out = c->h_fit_out;
+    if (c->fit_gen == c->tab_gen)                        // the table still holds what the kernel patched
+        for (size_t j = 0; j < c->fit_keys.size(); ++j)
+            if (out[j].planarity > c->fit_thr) c->resident.erase(c->fit_keys[j]);
+    c->n_surfels = c->resident.size();
+    c->fit_reconciled = true;
+    return LO_OK;
+}
+
 int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t n_jobs, const float* cs, size_t n_cs,
                     float thr, uint64_t* ticket) {
     if (!c || !ticket || (n_jobs > 0 && (!keys || !offs || !cs))) return LO_ERR_ARG;
     if (!c->d_tab) { c->err = "no surfel table to patch"; return LO_ERR_STATE; }
+    int rc0 = reconcile_fit(c);                          // a superseded ticket's failures must not stay resident
+    if (rc0 != LO_OK) return rc0;
     if (n_jobs > static_cast<size_t>(INT32_MAX) || n_cs > static_cast<size_t>(INT32_MAX / 3)) return LO_ERR_CAPACITY;
     // worst case for the table: every job not resident inserts, every resident one leaves a tombstone
     std::vector<uint64_t> pk(n_jobs);
@@ -640,6 +658,7 @@ int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t 
     }
     c->fit_gen = c->tab_gen;
     c->fit_keys.swap(pk);
+    c->fit_reconciled = false;
     c->fit_thr = thr;
     // until the results are collected the mirror counts every job key as resident (erases are then always sent)
     for (uint64_t k : c->fit_keys) c->resident.insert(k);
@@ -655,13 +674,9 @@ int ctx_fit_results(lo_ctx* c, uint64_t ticket, FitResult* out, size_t n_jobs) {
         if (!c || !g_live.count(c) || c->fit_ticket != ticket || ticket == 0) return LO_ERR_STATE;
     }
     if (c->fit_keys.size() != n_jobs) return LO_ERR_STATE;
-    LO_HIP(c, hipSetDevice(c->device));
-    LO_HIP(c, hipEventSynchronize(c->ev_fit));
+    const int rc = reconcile_fit(c);
+    if (rc != LO_OK) return rc;
     std::memcpy(out, c->h_fit_out, n_jobs * sizeof(FitResult));
-    if (c->fit_gen == c->tab_gen)                        // the table still holds what the kernel patched
-        for (size_t j = 0; j < n_jobs; ++j)
-            if (out[j].planarity > c->fit_thr) c->resident.erase(c->fit_keys[j]);
-    c->n_surfels = c->resident.size();
     c->fit_ticket = 0;
     c->fit_keys.clear();
     return LO_OK;
@@ -680,13 +695,24 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     if (m == 0) return LO_OK;
     if (!keys || !normals || !centroids || !present) { c->err = "null patch arrays"; return LO_ERR_ARG; }
     if (!c->d_tab) { c->err = "no surfel table to patch"; return LO_ERR_STATE; }
-    size_t ins = 0, ers = 0;
+    const int rc0 = reconcile_fit(c);
+    if (rc0 != LO_OK) return rc0;
+    // a key given more than once: its last record wins (as lo_map_set_surfels), the earlier ones are dropped, so the
+    // device patch (one thread per record) never races two records of one key
+    std::unordered_map<uint64_t, size_t> last;
+    last.reserve(2 * m);
     for (size_t i = 0; i < m; ++i) {
         for (int a = 0; a < 3; ++a) {
             const int32_t v = keys[3 * i + a];
             if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
         }
-        const bool res = c->resident.count(pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2])) != 0;
+        last[pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2])] = i;
+    }
+    size_t ins = 0, ers = 0;
+    for (size_t i = 0; i < m; ++i) {
+        const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        if (last[key] != i) continue;
+        const bool res = c->resident.count(key) != 0;
         ins += (present[i] && !res) ? 1 : 0;
         ers += (!present[i] && res) ? 1 : 0;
     }
@@ -710,6 +736,7 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     int n_rec = 0;
     for (size_t i = 0; i < m; ++i) {
         const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
+        if (last[key] != i) continue;                      // superseded by a later record of the key
         const bool res = c->resident.count(key) != 0;
         if (!present[i] && !res) continue;                 // nothing on the device to remove
         MapPatchRec& q = r[n_rec++];
@@ -730,7 +757,12 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     return LO_OK;
 }
 
-size_t lo_map_surfel_count(const lo_ctx* c) { return c ? c->n_surfels : 0; }
+size_t lo_map_surfel_count(const lo_ctx* c) {
+    if (!c) return 0;
+    lo_ctx* w = const_cast<lo_ctx*>(c);
+    if (reconcile_fit(w) != LO_OK) return 0;             // pending device fits: count their planarity failures out
+    return w->n_surfels;
+}
 
 // VoxelMap::RebuildKdTree (VoxelMap.cpp:420-438) equivalent: a dense uniform grid (cell = 2 x voxel, doubled
 // until it fits kKdMaxCells) over the L0 centroids in GetPointCloud order; points sorted by cell (x fastest),
@@ -872,7 +904,7 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
 }
 
 static constexpr int kStageEvents = 1024;
-static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: sort / term buffer capacity          // scans whose first correspondence launch is timed
+static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: sort / term buffer capacity
 
 // A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
 // (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
@@ -1572,6 +1604,7 @@ lo_batch* lo_batch_create(lo_ctx* const* ctxs, int count, int* err) {
         const lo_ctx* c = ctxs[j];
         if (!c) return fail(LO_ERR_ARG, "null context");
         if (c->kd) return fail(LO_ERR_ARG, "batched optimize needs surfel-mode contexts");
+        if (c->exact) return fail(LO_ERR_ARG, "batched optimize has no reference-exact mode (lo_set_exact)");
         if (c->device != ctxs[0]->device) return fail(LO_ERR_ARG, "contexts on different devices");
         if (c->cfg.max_iterations != ctxs[0]->cfg.max_iterations) return fail(LO_ERR_ARG, "max_iterations differ");
         for (int k = 0; k < j; ++k) if (ctxs[k] == c) return fail(LO_ERR_ARG, "a context appears twice");
@@ -1617,8 +1650,10 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
     if (!b || !n || !T_init) return LO_ERR_ARG;
     if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }
     const int B = static_cast<int>(b->ctx.size());
-    for (int j = 0; j < B; ++j)
+    for (int j = 0; j < B; ++j) {
         if (n[j] > static_cast<size_t>(b->ctx[j]->cfg.max_points)) { b->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+        if (b->ctx[j]->exact) { b->err = "a context has reference-exact mode on (no batched form)"; return LO_ERR_STATE; }
+    }
     LO_BHIP(b, hipSetDevice(b->device));
     std::memcpy(b->T_in.data(), T_init, sizeof(float) * 12 * B);
     b->act.clear();

@@ -13,6 +13,8 @@
 //  * the surfel normal is U.col(2) of Eigen's 2-sided Jacobi SVD of the fp32 covariance (restated below),
 //    planarity = s2 / (s0 + 1e-6f) (:239-243).
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -441,9 +443,17 @@ struct HostVoxelMap {
 
 using lo::HostVoxelMap;
 
+// Every entry point locks the map's recursive mutex, as the reference guards VoxelMap (VoxelMap.h: m_mutex): the
+// const readers resolve pending device fits (erasing voxels, syncing an event), so they mutate too.  id is unique
+// per map for the life of the process (a context's incremental sync names its source by it: an address can be
+// recycled by the next map).
+static std::atomic<uint64_t> g_map_ids{1};
 struct lo_voxelmap {
     HostVoxelMap m;
+    std::recursive_mutex mu;
+    const uint64_t id = g_map_ids.fetch_add(1);
 };
+#define LO_MAP_LOCK(m) std::lock_guard<std::recursive_mutex> lo_map_guard_(const_cast<lo_voxelmap*>(m)->mu)
 
 // Readers see the map as the sequential UpdateVoxelMap leaves it: pending device fits are applied first.
 static const HostVoxelMap& resolved(const lo_voxelmap* m) {
@@ -468,20 +478,31 @@ void lo_voxelmap_destroy(lo_voxelmap* m) { delete m; }
 
 int lo_voxelmap_apply_transform(lo_voxelmap* m, const float T[12]) {
     if (!m || !T) return LO_ERR_ARG;
+    LO_MAP_LOCK(m);
     m->m.apply_transform(T);
     return LO_OK;
 }
 
 int lo_voxelmap_update(lo_voxelmap* m, const float* xyz, size_t n, const double sensor[3], double max_distance, int is_keyframe) {
     if (!m || !sensor || (n > 0 && !xyz)) return LO_ERR_ARG;
+    LO_MAP_LOCK(m);
     m->m.update(xyz, n, sensor, max_distance, is_keyframe != 0);
     return LO_OK;
 }
 
-size_t lo_voxelmap_l0_count(const lo_voxelmap* m) { return m ? resolved(m).l0.size() : 0; }
-size_t lo_voxelmap_l1_count(const lo_voxelmap* m) { return m ? resolved(m).l1.size() : 0; }
+size_t lo_voxelmap_l0_count(const lo_voxelmap* m) {
+    if (!m) return 0;
+    LO_MAP_LOCK(m);
+    return resolved(m).l0.size();
+}
+size_t lo_voxelmap_l1_count(const lo_voxelmap* m) {
+    if (!m) return 0;
+    LO_MAP_LOCK(m);
+    return resolved(m).l1.size();
+}
 size_t lo_voxelmap_surfel_count(const lo_voxelmap* m) {
     if (!m) return 0;
+    LO_MAP_LOCK(m);
     const HostVoxelMap& h = resolved(m);
     size_t c = 0;
     for (size_t i = 0; i < h.l1.size(); ++i) c += h.l1.val_at(i).has_surfel ? 1 : 0;
@@ -490,6 +511,7 @@ size_t lo_voxelmap_surfel_count(const lo_voxelmap* m) {
 
 int lo_voxelmap_set_device_fit(lo_voxelmap* m, int enable) {
     if (!m) return LO_ERR_ARG;
+    LO_MAP_LOCK(m);
     m->m.resolve();
     m->m.defer_fit = enable != 0;
     return LO_OK;
@@ -497,6 +519,7 @@ int lo_voxelmap_set_device_fit(lo_voxelmap* m, int enable) {
 
 size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* normals, float* centroids, float* planarity, size_t cap) {
     if (!m) return 0;
+    LO_MAP_LOCK(m);
     const HostVoxelMap& h = resolved(m);
     size_t c = 0;
     for (size_t i = 0; i < h.l1.size() && c < cap; ++i) {
@@ -516,6 +539,7 @@ size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* norma
 
 size_t lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap) {
     if (!m || !xyz) return 0;
+    LO_MAP_LOCK(m);
     const HostVoxelMap& h = resolved(m);
     size_t c = 0;
     for (; c < h.l0.size() && c < cap; ++c) std::memcpy(xyz + 3 * c, h.l0.val_at(c).c, sizeof(float) * 3);
@@ -527,12 +551,13 @@ int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
     if (patched) *patched = -1;
     lo_config cfg;
     if (lo_get_config(ctx, &cfg) != LO_OK) return LO_ERR_ARG;
+    LO_MAP_LOCK(m);
     HostVoxelMap& H = const_cast<lo_voxelmap*>(m)->m;
     if (cfg.use_surfel_correspondence) {
         uint64_t src = 0, epoch = 0, pos = 0;
         lo::ctx_map_source(ctx, &src, &epoch, &pos);
         if (H.fit_ctx) H.resolve();                     // fits already handed to a context: collect them first
-        if (src == reinterpret_cast<uint64_t>(m) && epoch == H.epoch && pos <= H.journal.size()) {
+        if (src == m->id && epoch == H.epoch && pos <= H.journal.size()) {
             // the changed L1 keys, once each; keys with a pending fit job are patched by k_surfel_fit after these
             lo::OrderedMap<lo::Key3, lo::NoValue, lo::HashKey3> jobs;
             for (const lo::Key3& k : H.job_key) jobs.upsert(k, nullptr);
@@ -565,7 +590,7 @@ int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
                 if (rc == LO_OK) { H.fit_ctx = ctx; H.fit_id = id; }
             }
             if (rc == LO_OK) {
-                lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());
+                lo::ctx_set_map_source(ctx, m->id, H.epoch, H.journal.size());
                 if (patched) *patched = static_cast<int>(cnt + H.job_key.size());
                 return LO_OK;
             }
@@ -575,12 +600,13 @@ int lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patched) {
     H.resolve();                                         // a full upload needs the fitted surfels on the host
     const int rc = lo_map_set_from_voxelmap(ctx, m);
     if (rc == LO_OK && cfg.use_surfel_correspondence)
-        lo::ctx_set_map_source(ctx, reinterpret_cast<uint64_t>(m), H.epoch, H.journal.size());
+        lo::ctx_set_map_source(ctx, m->id, H.epoch, H.journal.size());
     return rc;
 }
 
 int lo_map_set_from_voxelmap(lo_ctx* ctx, const lo_voxelmap* m) {
     if (!ctx || !m) return LO_ERR_ARG;
+    LO_MAP_LOCK(m);
     const size_t s = lo_voxelmap_surfel_count(m);
     std::vector<int32_t> k(3 * std::max<size_t>(s, 1));
     std::vector<float> n(3 * std::max<size_t>(s, 1)), c(3 * std::max<size_t>(s, 1));

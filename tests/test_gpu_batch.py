@@ -152,6 +152,12 @@ def test_batch_argument_checks():
                 b.optimize(None, [big], [np.eye(3, 4, dtype=np.float32)])   # exceeds max_points
             res = b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
             assert not res[0].success          # empty map: no correspondences
+            a.set_exact(True)                  # no batched exact mode: refused, not silently run on the fast path
+            with pytest.raises(RuntimeError):
+                b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
+            with pytest.raises(RuntimeError):
+                BatchOptimizer([a])
+            a.set_exact(False)
         finally:
             b.close()
     finally:

@@ -157,3 +157,79 @@ def test_device_fit_matches_host_fit():
     finally:
         A.close()
         B.close()
+
+
+def test_sync_of_a_new_map_on_the_same_context_uploads_it():
+    """A context that mirrored map M1 and then syncs a NEW map M2 (possibly at M1's recycled address, with the same
+    epoch and a journal at least as long) must upload M2, not patch M1's table: maps are named by a process-unique
+    id, not by their address."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=30)
+    A, B = _ctx(), _ctx()
+    try:
+        v1 = VoxelMap(0.5, 3, 0.1, True)
+        for k in range(0, 9, 2):
+            v1.update(synth.transform(seq.poses[k], voxel_filter(seq.scan(k), 0.5, 8)), seq.poses[k][:3, 3], 60.0, True)
+            _sync(A, v1)
+        v1.close()
+        v2 = VoxelMap(0.5, 3, 0.1, True)
+        for k in range(20, 29, 2):          # a different place: M1's surfels must not survive in A's table
+            v2.update(synth.transform(seq.poses[k], voxel_filter(seq.scan(k), 0.5, 8)), seq.poses[k][:3, 3], 60.0, True)
+        assert _sync(A, v2) == -1
+        _full(B, v2)
+        assert A.surfel_count() == B.surfel_count() == v2.surfel_count()
+        for f in (1, 25):
+            scan = voxel_filter(seq.scan(f), 0.5, 8)
+            _same_lookups(A, B, scan, [seq.poses[f][:3].astype(np.float32).reshape(12)])
+        v2.close()
+    finally:
+        A.close()
+        B.close()
+
+
+def test_patch_duplicate_keys_last_record_wins():
+    """lo_map_patch_surfels with a key given twice (insert then erase, two payloads): the last record decides, as on
+    the host side, and the resident count agrees with the table."""
+    from lidar_odometry_amd import lib
+    A = _ctx()
+    try:
+        keys0 = np.array([[0, 0, 0], [5, 0, 0]], np.int32)
+        n0 = np.tile(np.array([0, 0, 1], np.float32), (2, 1))
+        c0 = np.array([[0.7, 0.7, 0.7], [7.9, 0.7, 0.7]], np.float32)
+        A.set_surfels(keys0, n0, c0)
+        fp = C.POINTER(C.c_float)
+        keys = np.array([[1, 0, 0], [1, 0, 0], [0, 0, 0], [0, 0, 0], [5, 0, 0], [5, 0, 0]], np.int32)
+        nrm = np.tile(np.array([0, 0, 1], np.float32), (6, 1))
+        nrm[3] = [1, 0, 0]
+        cen = np.array([[2.2, .7, .7], [2.2, .7, .7], [.7, .7, .7], [.7, .7, .9], [7.9, .7, .7], [7.9, .7, .7]], np.float32)
+        present = np.array([1, 0, 0, 1, 1, 0], np.uint8)    # key 1: inserted then erased; key 0: erased then re-set
+        rc = lib().lo_map_patch_surfels(A.ctx, keys.ctypes.data_as(C.POINTER(C.c_int32)), nrm.ctypes.data_as(fp),
+                                        cen.ctypes.data_as(fp), present.ctypes.data_as(C.POINTER(C.c_uint8)), 6)
+        assert rc == 0
+        assert A.surfel_count() == 1                       # key 0 only
+        I = np.eye(3, 4, dtype=np.float32).reshape(12)
+        pts = np.array([[0.7, 0.7, 0.7], [2.2, 0.7, 0.7], [7.9, 0.7, 0.7]], np.float32)
+        n, v, r = A.find_correspondences(pts, I)
+        assert n == 1 and v.tolist() == [True, False, False]
+        assert r[0] == 0.0                                 # key 0's LAST payload: normal x, centroid x = 0.7
+    finally:
+        A.close()
+
+
+def test_device_fit_count_before_the_map_is_read():
+    """With device fits pending, the context's surfel count already excludes the fits that failed planarity (no
+    reader of the host map has run yet)."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=22)
+    va, vb = VoxelMap(0.5, 3, 0.1, True), VoxelMap(0.5, 3, 0.1, True)
+    va.set_device_fit(True)
+    A = _ctx()
+    try:
+        for k in range(0, 21, 2):
+            w = synth.transform(seq.poses[k], voxel_filter(seq.scan(k), 0.5, 8))
+            va.update(w, seq.poses[k][:3, 3], 60.0, True)
+            vb.update(w, seq.poses[k][:3, 3], 60.0, True)
+            _sync(A, va)
+            assert A.surfel_count() == vb.surfel_count()     # before va is read
+    finally:
+        A.close()
