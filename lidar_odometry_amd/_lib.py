@@ -42,6 +42,10 @@ EXPORTED_SYMBOLS = (
     "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
     # include/lo_io.h
     "lo_load_kitti_bin", "lo_load_ply", "lo_kitti_pose_line", "lo_save_trajectory_kitti",
+    # include/lo_pgo.h
+    "lo_pgo_create", "lo_pgo_destroy", "lo_pgo_add_first_keyframe", "lo_pgo_add_keyframe_with_odom",
+    "lo_pgo_add_loop_and_optimize", "lo_pgo_get_optimized_pose", "lo_pgo_get_all_optimized_poses",
+    "lo_pgo_has_keyframe", "lo_pgo_keyframe_count", "lo_pgo_loop_closure_count", "lo_pgo_clear",
 )
 
 
@@ -149,6 +153,24 @@ def lib():
     L.lo_kitti_pose_line.argtypes = [fp, C.c_char_p, C.c_size_t]
     L.lo_save_trajectory_kitti.restype = C.c_int
     L.lo_save_trajectory_kitti.argtypes = [C.c_char_p, fp, C.c_size_t]
+    L.lo_pgo_create.restype = vp
+    L.lo_pgo_create.argtypes = []
+    L.lo_pgo_destroy.restype = None
+    L.lo_pgo_destroy.argtypes = [vp]
+    L.lo_pgo_add_first_keyframe.argtypes = [vp, C.c_int, fp]
+    L.lo_pgo_add_keyframe_with_odom.argtypes = [vp, C.c_int, C.c_int, fp, fp, C.c_double, C.c_double]
+    L.lo_pgo_add_loop_and_optimize.argtypes = [vp, C.c_int, C.c_int, fp, C.c_double, C.c_double,
+                                               C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double)]
+    L.lo_pgo_get_optimized_pose.argtypes = [vp, C.c_int, fp]
+    L.lo_pgo_get_all_optimized_poses.restype = C.c_size_t
+    L.lo_pgo_get_all_optimized_poses.argtypes = [vp, C.POINTER(C.c_int), fp, C.c_size_t]
+    L.lo_pgo_has_keyframe.argtypes = [vp, C.c_int]
+    L.lo_pgo_keyframe_count.restype = C.c_size_t
+    L.lo_pgo_keyframe_count.argtypes = [vp]
+    L.lo_pgo_loop_closure_count.restype = C.c_size_t
+    L.lo_pgo_loop_closure_count.argtypes = [vp]
+    L.lo_pgo_clear.restype = None
+    L.lo_pgo_clear.argtypes = [vp]
     L.lo_get_config.restype = C.c_int
     L.lo_pko_kernel_from_name.restype = C.c_int
     L.lo_pko_kernel_from_name.argtypes = [C.c_char_p]
