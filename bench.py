@@ -553,6 +553,13 @@ def run_e2e(args, world, rank, local):
     frames = n_ep * n_frames
     dt_pg, poses_pg, _, _, _ = epoch(True, raws)              # the same loop on pageable numpy scans (one staging copy)
     assert all(np.array_equal(a, b) for a, b in zip(poses_pg, poses)), "pinned and pageable inputs disagree"
+    # A/B: the keyframe update on the host map + patch sync (LO_HOST_MAP=1) -- the same containers, so the same poses
+    os.environ["LO_HOST_MAP"] = "1"
+    try:
+        dt_hm, poses_hm, kf_hm, _, map_hm = epoch(True)
+    finally:
+        del os.environ["LO_HOST_MAP"]
+    assert all(np.array_equal(a, b) for a, b in zip(poses_hm, poses)), "device and host maps disagree"
     err = [float(np.linalg.norm(poses[k][:, 3] - seq.poses[k][:3, 3])) for k in range(n_frames)]
     result = {
         "metric": METRIC + " (end to end: raw scan -> pose incl. keyframe map update)",
@@ -561,12 +568,16 @@ def run_e2e(args, world, rank, local):
         "dtype": "f32 (pose, J, H) + f64 (residuals, PKO)",
         "data": "synthetic raw HDL-64 sequence from rest (60 frames), raw scans in pinned host memory (lo_host_alloc)",
         "config": {"workload": "Estimator::process_frame loop (no loop closure / PGO), config/kitti.yaml, device filter + ICP, "
-                               "host VoxelMap update at keyframes", "raw_points_per_frame_avg": float(np.mean([len(r) for r in raws])),
+                               "device-resident VoxelMap update at keyframes (lo_devmap)",
+                   "raw_points_per_frame_avg": float(np.mean([len(r) for r in raws])),
                    "keyframes_per_frame": kfs / frames, "parallelism": "single GPU per sequence"},
         "breakdown_ms_per_frame": {"device_filter_icp": dev / frames, "keyframe_map_update_host": mp / frames,
                                    "other_host": tot / frames * 1e3 - dev / frames - mp / frames},
         "translation_error_vs_gt_m_max": max(err),
         "pageable_input_frames_per_s": n_frames / dt_pg,
+        "host_map_ab": {"frames_per_s": n_frames / dt_hm, "keyframe_map_update_host_ms_per_frame": map_hm / n_frames,
+                        "poses_bitwise_equal": True,
+                        "what": "same loop with the host VoxelMap + patch sync at keyframes (LO_HOST_MAP=1)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle

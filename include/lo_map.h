@@ -60,6 +60,35 @@ int          lo_map_sync_voxelmap(lo_ctx* ctx, const lo_voxelmap* m, int* patche
 /* FastVoxelFilter::filter(input, output, stride): returns the number of output points (<= n). */
 size_t       lo_voxel_filter(const float* in_xyz, size_t n, float voxel_size, int stride, float* out_xyz);
 
+/* ---- device-resident map ----
+ * The same UpdateVoxelMap / AddPoint / radius prune / planarity erase / ApplyTransformAndRehash as lo_voxelmap_*,
+ * kept in HBM next to an ICP context (surfel mode) whose surfel table it maintains in place: every update is ten
+ * kernel launches on the context's stream and no host work, and the containers (L0 / L1 order, children order,
+ * centroids, surfels) equal the host map's bit for bit.  Capacities are fixed at creation (max_l0 L0 voxels,
+ * max_l0 / 2 L1 voxels, max_points per update); an overflow or a key beyond +-2^20 sets an error bit reported by
+ * lo_devmap_counts.  hierarchy_factor 1 or 3.  Destroy the map before its context. */
+typedef struct lo_devmap lo_devmap;
+lo_devmap*  lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor, float planarity_threshold,
+                             size_t max_l0, size_t max_points, int* err);
+void        lo_devmap_destroy(lo_devmap* m);
+const char* lo_devmap_last_error(const lo_devmap* m);
+/* UpdateVoxelMap(cloud, sensor, max_distance, is_keyframe): world_xyz on the host (on_device = 0, copied) or a device
+ * pointer (on_device = 1, read by the kernels, valid until they ran) */
+int         lo_devmap_update(lo_devmap* m, const float* world_xyz, size_t n, int on_device, const double sensor[3],
+                             double max_distance, int is_keyframe);
+/* the context's last device-filtered scan moved to the world frame by T (util::transform_point_cloud) and inserted,
+ * sensor = T's translation: create_keyframe's update (Estimator.cpp:370-530) without the scan leaving the device */
+int         lo_devmap_update_from_scan(lo_devmap* m, const float T[12], double max_distance);
+/* ApplyTransformAndRehash(T) (VoxelMap.cpp:264-302) + RecomputeAllSurfels (:304-366) */
+int         lo_devmap_apply_transform(lo_devmap* m, const float T[12]);
+/* out = {L0 voxels, L1 voxels, surfels, error bits}; syncs the stream.  LO_ERR_CAPACITY when error bits are set. */
+int         lo_devmap_counts(lo_devmap* m, size_t out[4]);
+/* the containers in their order (tests / GetPointCloud): L0 keys, centroids, point counts; L1 keys, surfel flag,
+ * normal, centroid, planarity, child count and children keys (27 per voxel) */
+size_t      lo_devmap_get_l0(lo_devmap* m, int32_t* keys, float* xyz, int32_t* point_counts, size_t cap);
+size_t      lo_devmap_get_l1(lo_devmap* m, int32_t* keys, uint8_t* has_surfel, float* normals, float* centroids,
+                             float* planarity, int32_t* child_counts, int32_t* children, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,8 +8,11 @@
  *   estimate_motion_dual_frame (:271-320) -> lo_icp_optimize_raw on the device map; failure keeps the guess
  *   velocity = prev^-1 * pose (:177)
  *   should_create_keyframe (:349-368)      -> |dt| > keyframe_distance or |Log(R_kf^-1 R)| > keyframe_rotation
- *   create_keyframe (:370-530)             -> host VoxelMap::UpdateVoxelMap(world cloud, position, 1.2 * max_range)
- *                                             (lo_map.h) + device map upload (and RebuildKdTree in KDTree mode)
+ *   create_keyframe (:370-530)             -> VoxelMap::UpdateVoxelMap(world cloud, position, 1.2 * max_range):
+ *                                             surfel mode: the device-resident map (lo_devmap_update_from_scan,
+ *                                             lo_map.h), which patches the context's table in place -- ten kernel
+ *                                             launches, no host sync (LO_HOST_MAP=1: the host map + patch sync);
+ *                                             KDTree mode: the host map + RebuildKdTree upload
  */
 #ifndef LO_ODOMETRY_H
 #define LO_ODOMETRY_H
@@ -39,7 +42,7 @@ typedef struct {
     int    n_filtered;             /* feature cloud size */
     int    n_corr;
     double device_ms;              /* preprocessing + ICP on the device (HIP events) */
-    double map_ms;                 /* keyframe map update + upload (host wall time), 0 otherwise */
+    double map_ms;                 /* keyframe map update (host wall time: enqueue only with the device map), 0 otherwise */
 } lo_odom_frame;
 
 typedef struct lo_odometry lo_odometry;

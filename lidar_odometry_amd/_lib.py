@@ -36,7 +36,8 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
-    "lo_voxelmap_set_device_fit",
+    "lo_voxelmap_set_device_fit", "lo_devmap_create", "lo_devmap_destroy", "lo_devmap_last_error", "lo_devmap_update",
+    "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_get_l0", "lo_devmap_get_l1",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
     "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
@@ -153,6 +154,20 @@ def lib():
     L.lo_kitti_pose_line.argtypes = [fp, C.c_char_p, C.c_size_t]
     L.lo_save_trajectory_kitti.restype = C.c_int
     L.lo_save_trajectory_kitti.argtypes = [C.c_char_p, fp, C.c_size_t]
+    L.lo_devmap_create.restype = vp
+    L.lo_devmap_create.argtypes = [vp, C.c_float, C.c_int, C.c_float, C.c_size_t, C.c_size_t, C.POINTER(C.c_int)]
+    L.lo_devmap_destroy.restype = None
+    L.lo_devmap_destroy.argtypes = [vp]
+    L.lo_devmap_last_error.restype = C.c_char_p
+    L.lo_devmap_last_error.argtypes = [vp]
+    L.lo_devmap_update.argtypes = [vp, vp, C.c_size_t, C.c_int, dp, C.c_double, C.c_int]
+    L.lo_devmap_update_from_scan.argtypes = [vp, fp, C.c_double]
+    L.lo_devmap_apply_transform.argtypes = [vp, fp]
+    L.lo_devmap_counts.argtypes = [vp, C.POINTER(C.c_size_t)]
+    L.lo_devmap_get_l0.restype = C.c_size_t
+    L.lo_devmap_get_l0.argtypes = [vp, ip, fp, ip, C.c_size_t]
+    L.lo_devmap_get_l1.restype = C.c_size_t
+    L.lo_devmap_get_l1.argtypes = [vp, ip, u8p, fp, fp, fp, ip, ip, C.c_size_t]
     L.lo_pgo_create.restype = vp
     L.lo_pgo_create.argtypes = []
     L.lo_pgo_destroy.restype = None

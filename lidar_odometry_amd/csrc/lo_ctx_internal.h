@@ -25,4 +25,12 @@ struct FitResult {
 int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t n_jobs, const float* cs, size_t n_cs,
                     float thr, uint64_t* ticket);
 int ctx_fit_results(lo_ctx* c, uint64_t ticket, FitResult* out, size_t n_jobs);
+
+// Device map (lo_devmap): the context's surfel table with at least min_slots slots, emptied (asynchronously, on the
+// context stream) unless it is still the generation the map reserved last time; *gen changes whenever the table was
+// emptied, so the map refills it.  Any other upload to the context bumps the generation.
+int ctx_reserve_table(lo_ctx* c, size_t min_slots, void** tab, uint32_t* log2cap, uint64_t* gen);
+// The device-filtered scan of the last lo_icp_optimize_raw / lo_voxel_filter_gpu: device points and the device
+// count (stream-ordered; no sync).
+int ctx_filtered_device(lo_ctx* c, const float** d_pts, const int** d_n);
 }  // namespace lo

@@ -128,6 +128,7 @@ struct lo_ctx {
     hipEvent_t ev_patch = nullptr;
     uint64_t map_src = 0, map_epoch = 0, map_pos = 0;
     uint64_t tab_gen = 0;           // bumped by every full upload (a pending fit's results no longer apply to it)
+    uint64_t devmap_gen = 0;        // the generation a device map (lo_devmap) reserved and maintains
     // deferred surfel fits of a synced host map (lo::ctx_fit_surfels): pinned in / out staging, device copies
     void* h_fit_in = nullptr;
     void* d_fit_in = nullptr;
@@ -573,6 +574,47 @@ void ctx_map_source(const lo_ctx* c, uint64_t* src, uint64_t* epoch, uint64_t* p
 }
 void ctx_set_map_source(lo_ctx* c, uint64_t src, uint64_t epoch, uint64_t pos) {
     c->map_src = src; c->map_epoch = epoch; c->map_pos = pos;
+}
+
+int ctx_reserve_table(lo_ctx* c, size_t min_slots, void** tab, uint32_t* log2cap, uint64_t* gen) {
+    if (!c || !tab || !log2cap || !gen) return LO_ERR_ARG;
+    size_t cap = 2;
+    uint32_t l2 = 1;
+    while (cap < min_slots) { cap <<= 1; ++l2; }
+    if (c->devmap_gen != c->tab_gen || c->devmap_gen == 0 || (size_t(1) << c->log2cap) < cap) {
+        LO_HIP(c, hipSetDevice(c->device));
+        if (cap > c->tab_cap) {
+            LO_HIP(c, hipStreamSynchronize(c->stream));
+            LO_HIP(c, hipFree(c->d_tab));
+            c->d_tab = nullptr;
+            LO_HIP(c, hipMalloc(&c->d_tab, cap * sizeof(Slot)));
+            c->tab_cap = cap;
+        } else {
+            cap = std::max(cap, size_t(1) << c->log2cap);   // keep the larger table
+            l2 = 1;
+            while ((size_t(1) << l2) < cap) ++l2;
+        }
+        LO_HIP(c, hipMemsetAsync(c->d_tab, 0xff, cap * sizeof(Slot), c->stream));
+        c->log2cap = l2;
+        c->resident.clear();
+        c->n_surfels = 0;
+        c->n_tomb = 0;
+        c->map_src = 0;
+        ++c->tab_gen;
+        c->devmap_gen = c->tab_gen;
+    }
+    *tab = c->d_tab;
+    *log2cap = c->log2cap;
+    *gen = c->tab_gen;
+    return LO_OK;
+}
+
+int ctx_filtered_device(lo_ctx* c, const float** d_pts, const int** d_n) {
+    if (!c || !d_pts || !d_n) return LO_ERR_ARG;
+    if (!c->last_dev_count || !c->vf.n_out) { c->err = "no device-filtered scan"; return LO_ERR_STATE; }
+    *d_pts = c->d_pts;
+    *d_n = c->vf.n_out;
+    return LO_OK;
 }
 
 static int grow_pinned_pair(lo_ctx* c, void** h, void** d, size_t* cap, size_t bytes) {

@@ -1,9 +1,12 @@
 // lo_odometry.cpp — Estimator::process_frame without loop closure / PGO (see include/lo_odometry.h), host C++
 // driving the device path: each frame is one lo_icp_optimize_raw call (device voxel filter + GN loop); the
-// pose bookkeeping uses the reference's SE3f algebra (lo_math.h); keyframes update the host VoxelMap
-// (bit-identical UpdateVoxelMap restatement) and re-upload the device map.
+// pose bookkeeping uses the reference's SE3f algebra (lo_math.h); keyframes update the voxel map: in surfel mode the
+// device-resident map (lo_devmap: the filtered scan never leaves the device, the context's table is patched in
+// place, no host sync), in KDTree mode the host VoxelMap (bit-identical UpdateVoxelMap restatement) + re-upload.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -19,6 +22,7 @@ struct lo_odometry {
     lo_odom_config cfg{};
     lo_ctx* icp = nullptr;
     lo_voxelmap* map = nullptr;
+    lo_devmap* dmap = nullptr;            // surfel mode (LO_HOST_MAP=1: the host map + patch sync instead)
     std::string err;
     bool initialized = false;
     SE3f initial, prev, velocity, last_kf;
@@ -29,6 +33,19 @@ struct lo_odometry {
 static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info) {
     // create_keyframe (:370-530): world feature cloud -> UpdateVoxelMap(cloud, position, 1.2 max_range) -> device
     const auto t0 = std::chrono::steady_clock::now();
+    if (o->dmap) {
+        float T[12];
+        lo::se3_to12(pose, T);
+        const int rc = lo_devmap_update_from_scan(o->dmap, T, o->cfg.max_range * 1.2);
+        if (rc != LO_OK) { o->err = lo_devmap_last_error(o->dmap); return rc; }
+        o->last_kf = pose;
+        ++o->keyframes;
+        if (info) {
+            info->keyframe = 1;
+            info->map_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        return LO_OK;
+    }
     const long long n = lo_filtered_points(o->icp, nullptr, 0);
     if (n < 0) { o->err = lo_last_error(o->icp); return static_cast<int>(n); }
     o->feat.resize(3 * static_cast<size_t>(std::max<long long>(n, 1)));
@@ -72,12 +89,20 @@ lo_odometry* lo_odom_create(const lo_odom_config* cfg, int device, int* err) {
                                 cfg->icp.use_surfel_correspondence ? 1 : 0);   // SetComputeSurfels (Estimator.cpp:79)
     if (!o->map) { lo_destroy(o->icp); delete o; if (err) *err = LO_ERR_ARG; return nullptr; }
     if (cfg->icp.use_surfel_correspondence) lo_voxelmap_set_device_fit(o->map, 1);   // refits run in the sync's patch
+    const char* hm = std::getenv("LO_HOST_MAP");
+    if (cfg->icp.use_surfel_correspondence && !(hm && std::atoi(hm))) {
+        int e = LO_OK;
+        o->dmap = lo_devmap_create(o->icp, cfg->icp.voxel_size, cfg->icp.hierarchy_factor, cfg->planarity_threshold,
+                                   size_t(1) << 21, static_cast<size_t>(std::max(cfg->icp.max_points, 16)), &e);
+        if (!o->dmap) { lo_voxelmap_destroy(o->map); lo_destroy(o->icp); delete o; if (err) *err = e; return nullptr; }
+    }
     if (err) *err = LO_OK;
     return o;
 }
 
 void lo_odom_destroy(lo_odometry* o) {
     if (!o) return;
+    lo_devmap_destroy(o->dmap);
     lo_voxelmap_destroy(o->map);
     lo_destroy(o->icp);
     delete o;
@@ -171,6 +196,14 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
 }
 
 size_t lo_odom_keyframe_count(const lo_odometry* o) { return o ? o->keyframes : 0; }
-size_t lo_odom_map_surfels(const lo_odometry* o) { return o ? lo_voxelmap_surfel_count(o->map) : 0; }
+size_t lo_odom_map_surfels(const lo_odometry* o) {
+    if (!o) return 0;
+    if (o->dmap) {
+        size_t c[4] = {0, 0, 0, 0};
+        lo_devmap_counts(o->dmap, c);
+        return c[2];
+    }
+    return lo_voxelmap_surfel_count(o->map);
+}
 
 }  // extern "C"
