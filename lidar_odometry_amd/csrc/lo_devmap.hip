@@ -44,7 +44,7 @@ constexpr int kKids = 27;               // children per L1 voxel at factor 3
 constexpr int kOrch = 1024;             // threads of the single-workgroup phases
 constexpr int kPar = 256;               // threads of the parallel phases
 constexpr int kPruneBlocks = 1024;      // workgroups of the prune mark / compaction
-constexpr int kSimLds = 4096;           // erase batches up to this size replay in LDS (3 arrays per map level)
+constexpr int kSimLds = 3840;           // erase batches up to this size replay in LDS (4 arrays per map level)
 constexpr int kU = 4;                   // items per thread issued together in the single-workgroup phases
 constexpr uint64_t kEmpty = ~0ull;
 constexpr uint64_t kTomb = ~0ull - 1;
@@ -115,6 +115,8 @@ struct DM {
     Slot* tab;
     uint32_t tabl;
     unsigned long long* st;              // diagnostic phase clocks (LO_DM_STAMPS=1), else null
+    float* prm;                          // this update's parameters: sensor xyz, radius^2, pose (from scan) [16]
+    int* prm_n;                          // [0] point count, [1] 1 = points from the context's filtered scan
 };
 // diagnostic: cycles of the phase that just ended, summed over updates (read by nothing but the destroy report)
 #define DM_ST(k)                                                                                    \
@@ -338,6 +340,43 @@ __device__ void erase_sim(int n, const int* list, int q, int* tc, int* tp, int* 
     }
 }
 
+// The same replay with every array in LDS (explicit LDS pointers: ds_* instructions, so a step's reads never wait
+// for an earlier step's memory store the way flat accesses would).  The holes' contents are kept per erase step: hs[k]
+// for the step that first erased position list[k] < m; a tail element moved into a hole records -(k + 1) as its
+// position.  The caller copies hs out to hole[].
+typedef __attribute__((address_space(3))) int lds_int;
+__device__ void erase_sim_lds(int n, const lds_int* ls, int q, lds_int* tc, lds_int* tp, lds_int* hs) {
+    const int m = n - q;
+    int s = n;
+    for (int k0 = 0; k0 < q; k0 += 8) {
+        int ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ev[u] = k0 + u < q ? ls[k0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + u;
+            if (k >= q) break;
+            const int e = ev[u];
+            const int L = s - 1;
+            const int x = tc[L - m];
+            int slot = -1, p = 0;
+            if (e < m) slot = k;
+            else {
+                const int v = tp[e - m];
+                if (v >= 0) p = v; else slot = -v - 1;
+            }
+            if (slot >= 0) {                               // a hole (L >= m, so never the last position)
+                hs[slot] = x;
+                tp[x - m] = -(slot + 1);
+            } else if (p != L) {
+                tc[p - m] = x;
+                tp[x - m] = p;
+            }
+            s = L;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------- container moves
 __device__ void l0_move(const DM& M, int src, int dst) {
     M.k0[dst] = M.k0[src];
@@ -357,8 +396,10 @@ __device__ void l1_move(const DM& M, int src, int dst) {
 // Both levels' erase batches (L0 list0 / q0 over n0 elements, L1 list1 / q1 over n1): replay (two lanes of
 // different waves at once), then apply: erased keys leave the index (tombstone), the survivors that fill holes move
 // and their index entries follow.  Block-wide; updates the counters.
-__device__ void erase_batches(const DM& M, const int* list0, int q0, const int* list1, int q1, int* s_sim) {
+__device__ void erase_batches(const DM& M, const int* list0, int q0, const int* list1, int q1, int* s_sim, int tag) {
     const int n0 = M.cnt[C_N0], n1 = M.cnt[C_N1];
+    if (M.st && threadIdx.x == 0) { atomicAdd(&M.st[48 + 2 * tag], static_cast<unsigned long long>(q0));
+                                    atomicAdd(&M.st[49 + 2 * tag], static_cast<unsigned long long>(q1)); }
     __shared__ int s_bad;
     if (threadIdx.x == 0) s_bad = 0;
     __syncthreads();
@@ -370,21 +411,33 @@ __device__ void erase_batches(const DM& M, const int* list0, int q0, const int* 
         __syncthreads();
         return;
     }
-    // the replay state and the lists in LDS (a lane's dependent steps then wait on LDS, not on memory)
+    // the replay state and the lists in LDS (a lane's dependent steps then wait on LDS, not on memory); batches
+    // beyond kSimLds replay in global scratch
     const bool lds0 = q0 <= kSimLds, lds1 = q1 <= kSimLds;
-    int* tc0 = lds0 ? s_sim : M.simg;
-    int* tp0 = lds0 ? s_sim + kSimLds : M.simg + M.C0;
-    int* tc1 = lds1 ? s_sim + 2 * kSimLds : M.simg + 2 * M.C0;
-    int* tp1 = lds1 ? s_sim + 3 * kSimLds : M.simg + 3 * M.C0;
-    int* ls0 = lds0 ? s_sim + 4 * kSimLds : const_cast<int*>(list0);
-    int* ls1 = lds1 ? s_sim + 5 * kSimLds : const_cast<int*>(list1);
-    for (int t = threadIdx.x; t < q0; t += kOrch) { tc0[t] = n0 - q0 + t; tp0[t] = n0 - q0 + t; if (lds0) ls0[t] = list0[t]; }
-    for (int t = threadIdx.x; t < q1; t += kOrch) { tc1[t] = n1 - q1 + t; tp1[t] = n1 - q1 + t; if (lds1) ls1[t] = list1[t]; }
+    lds_int* L0s = (lds_int*)(s_sim);                                 // ls, tc, tp, hs per level (addrspacecast)
+    lds_int* L1s = L0s + 4 * kSimLds;
+    for (int t = threadIdx.x; t < q0; t += kOrch) {
+        if (lds0) { L0s[t] = list0[t]; L0s[kSimLds + t] = n0 - q0 + t; L0s[2 * kSimLds + t] = n0 - q0 + t; }
+        else { M.simg[t] = n0 - q0 + t; M.simg[M.C0 + t] = n0 - q0 + t; }
+    }
+    for (int t = threadIdx.x; t < q1; t += kOrch) {
+        if (lds1) { L1s[t] = list1[t]; L1s[kSimLds + t] = n1 - q1 + t; L1s[2 * kSimLds + t] = n1 - q1 + t; }
+        else { M.simg[2 * M.C0 + t] = n1 - q1 + t; M.simg[3 * M.C0 + t] = n1 - q1 + t; }
+    }
     __syncthreads();
-    if (threadIdx.x == 0 && q0 > 0) erase_sim(n0, ls0, q0, tc0, tp0, M.hole0);
-    if (threadIdx.x == 64 && q1 > 0) erase_sim(n1, ls1, q1, tc1, tp1, M.hole1);
+    if (threadIdx.x == 0 && q0 > 0) {
+        if (lds0) erase_sim_lds(n0, L0s, q0, L0s + kSimLds, L0s + 2 * kSimLds, L0s + 3 * kSimLds);
+        else erase_sim(n0, list0, q0, M.simg, M.simg + M.C0, M.hole0);
+    }
+    if (threadIdx.x == 64 && q1 > 0) {
+        if (lds1) erase_sim_lds(n1, L1s, q1, L1s + kSimLds, L1s + 2 * kSimLds, L1s + 3 * kSimLds);
+        else erase_sim(n1, list1, q1, M.simg + 2 * M.C0, M.simg + 3 * M.C0, M.hole1);
+    }
     __syncthreads();
     const int m0 = n0 - q0, m1 = n1 - q1;
+    if (lds0) for (int k = threadIdx.x; k < q0; k += kOrch) { if (L0s[k] < m0) M.hole0[L0s[k]] = L0s[3 * kSimLds + k]; }
+    if (lds1) for (int k = threadIdx.x; k < q1; k += kOrch) { if (L1s[k] < m1) M.hole1[L1s[k]] = L1s[3 * kSimLds + k]; }
+    __syncthreads();
     // tombstones first (the erased keys), then the moves: a moved key's index entry is found by key, and its new
     // position is an erased element's -- the two sets of keys are disjoint
     for (int k = threadIdx.x; k < q0; k += kOrch) {
@@ -426,13 +479,22 @@ __device__ void erase_batches(const DM& M, const int* list0, int q0, const int* 
 
 // ---------------------------------------------------------------------------------------------- kernels
 // world points from a device scan: util::transform_point_cloud's order (lo_math.h transform_points)
-__global__ __launch_bounds__(kPar) void k_dm_world(DM M, const float* in, const int* dn, DmPose T, float* out) {
-    const int n = min(*dn, M.NP);
+__global__ __launch_bounds__(kPar) void k_dm_world(DM M, const float* in, const int* dn, float* out) {
+    if (M.prm_n[1] != 1) return;                         // host-given points: already in place
+    const int n = point_count(M, 0, dn);
+    if (blockIdx.x == 0 && threadIdx.x == 0) M.prm_n[0] = n;
+    float T[12];
+    for (int k = 0; k < 12; ++k) T[k] = M.prm[4 + k];
     for (int i = blockIdx.x * kPar + threadIdx.x; i < n; i += gridDim.x * kPar) {
         const float x = in[3 * i], y = in[3 * i + 1], z = in[3 * i + 2];
         for (int r = 0; r < 3; ++r)
-            out[3 * i + r] = ((T.v[4 * r] * x + T.v[4 * r + 1] * y) + T.v[4 * r + 2] * z) + T.v[4 * r + 3] * 1.0f;
+            out[3 * i + r] = ((T[4 * r] * x + T[4 * r + 1] * y) + T[4 * r + 2] * z) + T[4 * r + 3] * 1.0f;
     }
+}
+struct DmParams { float v[16]; int n, from_scan; };
+__global__ void k_dm_setprm(DM M, DmParams P) {
+    if (threadIdx.x < 16) M.prm[threadIdx.x] = P.v[threadIdx.x];
+    if (threadIdx.x == 0) { M.prm_n[0] = P.n; M.prm_n[1] = P.from_scan; }
 }
 
 // prune mark (:146-157): dist^2 = (c - s).squaredNorm() > radius^2 in fp32; per-workgroup counts
@@ -443,8 +505,9 @@ __device__ __forceinline__ void prune_range(int n0, int b, int* lo, int* hi) {
 }
 // (an empty device-filtered cloud prunes nothing: UpdateVoxelMap returns first, :135-137)
 __device__ __forceinline__ int prune_n0(const DM& M, const int* dn) { return (dn && *dn <= 0) ? 0 : M.cnt[C_N0]; }
-__global__ __launch_bounds__(kPar) void k_dm_prune_mark(DM M, float sx, float sy, float sz, float rsq, const int* dn) {
+__global__ __launch_bounds__(kPar) void k_dm_prune_mark(DM M, const int* dn) {
     __shared__ int s_c;
+    const float sx = M.prm[0], sy = M.prm[1], sz = M.prm[2], rsq = M.prm[3];
     if (blockIdx.x == 0 && threadIdx.x == 0) M.cnt[C_REBUILD] = 0;        // the previous update's rebuild ran
     if (threadIdx.x == 0) s_c = 0;
     __syncthreads();
@@ -497,7 +560,7 @@ __global__ __launch_bounds__(kPar) void k_dm_prune_compact(DM M, const int* dn) 
 __global__ __launch_bounds__(kOrch) void k_dm_unregister(DM M) {
     unsigned long long st_t0 = M.st ? __builtin_amdgcn_s_memtime() : 0ull;
     __shared__ int s_w[64];
-    __shared__ int s_sim[6 * kSimLds];
+    __shared__ int s_sim[8 * kSimLds];
     const int q = M.cnt[C_Q];
     if (threadIdx.x == 0) M.cnt[C_NCHG] = 0;
     for (int j = threadIdx.x; j < q; j += kOrch) {
@@ -551,7 +614,7 @@ __global__ __launch_bounds__(kOrch) void k_dm_unregister(DM M) {
     for (int t = threadIdx.x; t < q1; t += kOrch) M.E1[t] = M.emptied[M.E1[t]];
     __syncthreads();
     DM_ST(32);
-    erase_batches(M, M.D, q, M.E1, q1, s_sim);
+    erase_batches(M, M.D, q, M.E1, q1, s_sim, 0);
     DM_ST(33);
 }
 
@@ -860,7 +923,7 @@ __global__ __launch_bounds__(kPar) void k_dm_a_done(DM M, int n_host, const int*
 }
 
 // the touched voxels' surfel decisions and refits (:183-261), all in parallel: each reads only its own children
-__device__ void dm_touched_one(const DM& M, int t) {
+__device__ void dm_touched_one(const DM& M, int t, float* cs) {
     M.fail[t] = 0;
     const int lp = idx_find(M.i1k, M.i1v, M.h1l, M.T[t]);
     M.tlp[t] = lp;
@@ -868,7 +931,6 @@ __device__ void dm_touched_one(const DM& M, int t) {
     const int cnt = M.nk[lp];
     if (cnt < 5) { M.has[lp] = 0; return; }
     if (M.has[lp] && M.last[lp] == cnt) return;
-    float cs[3 * kKids];
     int m = 0;
     for (int q0 = 0; q0 < cnt; q0 += 9) {                 // the children's lookups nine at a time
         uint64_t ck[9];
@@ -897,8 +959,10 @@ __device__ void dm_touched_one(const DM& M, int t) {
     M.last[lp] = cnt;
 }
 __global__ __launch_bounds__(64) void k_dm_touched(DM M) {       // 64-lane workgroups: the fits spread over CUs
+    __shared__ float s_cs[64 * 3 * kKids];                           // each lane's child centroids (not scratch)
     const int nt = M.cnt[C_NT];
-    for (int t = blockIdx.x * 64 + threadIdx.x; t < nt; t += gridDim.x * 64) dm_touched_one(M, t);
+    for (int t = blockIdx.x * 64 + threadIdx.x; t < nt; t += gridDim.x * 64)
+        dm_touched_one(M, t, s_cs + threadIdx.x * 3 * kKids);
 }
 
 // planarity failures in touched order: the voxel's children (child order), then the voxel; then the table patch of
@@ -906,7 +970,7 @@ __global__ __launch_bounds__(64) void k_dm_touched(DM M) {       // 64-lane work
 __global__ __launch_bounds__(kOrch) void k_dm_finish(DM M) {
     unsigned long long st_t0 = M.st ? __builtin_amdgcn_s_memtime() : 0ull;
     __shared__ int s_w[64];
-    __shared__ int s_sim[6 * kSimLds];
+    __shared__ int s_sim[8 * kSimLds];
     const int nt = M.cnt[C_NT];
     const int nf = block_compact(nt, M.F, s_w, [&](int t) { return M.fail[t] != 0; });
     DM_ST(20);
@@ -956,31 +1020,23 @@ __global__ __launch_bounds__(kOrch) void k_dm_finish(DM M) {
     }
     __syncthreads();
     DM_ST(22);
-    erase_batches(M, M.L0e, q0, M.E1, nf, s_sim);
+    erase_batches(M, M.L0e, q0, M.E1, nf, s_sim, 1);
     DM_ST(23);
-    // the ICP table: every changed key's final state (unregistered parents, touched voxels; erased ones are absent)
-    const int nc = M.cnt[C_NCHG];
-    for (int b = 0; b < nc + nt; b += kU * kOrch) {
-        int k[kU], lp[kU], hs[kU];
-        uint64_t key[kU];
-        bool act[kU];
-        FOR_U {
-            k[u] = b + u * kOrch + threadIdx.x;
-            act[u] = k[u] < nc + nt;
-            key[u] = act[u] ? (k[u] < nc ? M.chg[k[u]] : M.T[k[u] - nc]) : 0;
-        }
-        idx_find_n<kU>(M.i1k, M.i1v, M.h1l, key, act, lp);
-        FOR_U hs[u] = (act[u] && lp[u] >= 0) ? M.has[lp[u]] : 0;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (!act[u]) continue;
-            const bool present = hs[u] != 0;
-            tab_set(M.tab, M.tabl, key[u], present, present ? M.nrm + 3 * lp[u] : nullptr,
-                    present ? M.cen + 3 * lp[u] : nullptr, &M.cnt[C_TTOMB]);
-        }
-    }
     DM_ST(24);
-    __syncthreads();
+}
+
+// the ICP table: every changed key's final state (unregistered parents, touched voxels; erased ones are absent)
+__global__ __launch_bounds__(kPar) void k_dm_table(DM M) {
+    const int nc = M.cnt[C_NCHG], nt = M.cnt[C_NT];
+    for (int k = blockIdx.x * kPar + threadIdx.x; k < nc + nt; k += gridDim.x * kPar) {
+        const uint64_t key = k < nc ? M.chg[k] : M.T[k - nc];
+        const int lp = idx_find(M.i1k, M.i1v, M.h1l, key);
+        const bool present = lp >= 0 && M.has[lp];
+        tab_set(M.tab, M.tabl, key, present, present ? M.nrm + 3 * lp : nullptr, present ? M.cen + 3 * lp : nullptr,
+                &M.cnt[C_TTOMB]);
+    }
+}
+__global__ void k_dm_table_check(DM M) {
     if (threadIdx.x == 0 && 4 * M.cnt[C_TTOMB] > (1 << M.tabl)) M.cnt[C_REBUILD] |= R_TAB;
 }
 
@@ -1197,6 +1253,11 @@ struct lo_devmap {
     float* at_nc = nullptr;
     int* at_nn = nullptr;
     uint64_t tab_gen = 0;
+    hipGraphExec_t gexec = nullptr;      // the captured update pipeline and what it was captured with
+    Slot* g_tab = nullptr;
+    uint32_t g_tabl = 0;
+    const float* g_scan = nullptr;
+    const int* g_scan_n = nullptr;
     std::string err;
     int* h_cnt = nullptr;                // pinned copy of the counters
     size_t updates = 0;
@@ -1299,6 +1360,7 @@ lo_devmap* lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor,
     A(M.T, NP, 0); A(M.tlp, NP, 0); A(M.fail, NP, 0); A(M.F, std::max(NP, C1), 0); A(M.Foff, NP, 0);
     A(M.L0e, NP * kKids, 0);
     A(m->d_in, 3 * NP, 0);
+    A(M.prm, 16, 0); A(M.prm_n, 4, 0);
     A(m->at_c, 3 * C0, 0); A(m->at_k, C0, 0); A(m->at_nk, C0, 0); A(m->at_nc, 3 * C0, 0); A(m->at_nn, C0, 0);
 #undef A
     if (const char* e = std::getenv("LO_DM_STAMPS"); e && std::atoi(e) && rc == LO_OK) rc = dm_alloc(m, &M.st, 64, 0);
@@ -1324,6 +1386,7 @@ void lo_devmap_destroy(lo_devmap* m) {
             std::fprintf(stderr, "\n");
         }
     }
+    if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
     for (void* p : m->bufs) (void)hipFree(p);
     if (m->h_cnt) (void)hipHostFree(m->h_cnt);
     delete m;
@@ -1331,38 +1394,87 @@ void lo_devmap_destroy(lo_devmap* m) {
 
 const char* lo_devmap_last_error(const lo_devmap* m) { return m ? m->err.c_str() : "null map"; }
 
-static int dm_update(lo_devmap* m, const float* d_pts, int n, const int* dn, const double sensor[3], double max_distance) {
+// One update = the parameter kernel + a captured graph of the twenty pipeline launches (kernel arguments fixed: the
+// map's buffers, its point buffer, the device count; recaptured when the context's table moved).
+static int dm_capture(lo_devmap* m, const int* d_scan_n, const float* d_scan) {
     DM& M = m->M;
-    int rc = dm_bind_table(m);
-    if (rc != LO_OK) return rc;
-    const float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
-    const float rsq = static_cast<float>(max_distance * max_distance);
-    ++m->updates;
-    hipLaunchKernelGGL(k_dm_prune_mark, dim3(kPruneBlocks), dim3(kPar), 0, m->stream, M, sp[0], sp[1], sp[2], rsq, dn);
-    hipLaunchKernelGGL(k_dm_prune_compact, dim3(kPruneBlocks), dim3(kPar), 0, m->stream, M, dn);
-    hipLaunchKernelGGL(k_dm_unregister, dim3(1), dim3(kOrch), 0, m->stream, M);
-    const int nmax = dn ? M.NP : n;                      // grid-stride launches sized for the largest count
-    const dim3 grid(std::max(1, std::min(1024, (nmax + kPar - 1) / kPar)));
-    hipLaunchKernelGGL(k_dm_keys, grid, dim3(kPar), 0, m->stream, M, d_pts, n, dn);
+    if (m->gexec) { (void)hipGraphExecDestroy(m->gexec); m->gexec = nullptr; }
+    hipGraph_t g = nullptr;
+    DM_HIP(m, hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+    const int* dn = M.prm_n;
+    const dim3 grid(std::max(1, std::min(1024, (M.NP + kPar - 1) / kPar)));
+    const dim3 tgrid(std::max(1, std::min(1024, (M.NP + 63) / 64)));
     const dim3 chunks(kChunk), par(kPar);
-    hipLaunchKernelGGL(k_dm_a_count, chunks, par, 0, m->stream, M, n, dn);
+    hipLaunchKernelGGL(k_dm_world, grid, par, 0, m->stream, M, d_scan, d_scan_n, m->d_in);
+    hipLaunchKernelGGL(k_dm_prune_mark, dim3(kPruneBlocks), par, 0, m->stream, M, dn);
+    hipLaunchKernelGGL(k_dm_prune_compact, dim3(kPruneBlocks), par, 0, m->stream, M, dn);
+    hipLaunchKernelGGL(k_dm_unregister, dim3(1), dim3(kOrch), 0, m->stream, M);
+    hipLaunchKernelGGL(k_dm_keys, grid, par, 0, m->stream, M, m->d_in, 0, dn);
+    hipLaunchKernelGGL(k_dm_a_count, chunks, par, 0, m->stream, M, 0, dn);
     hipLaunchKernelGGL(k_dm_scan3, dim3(1), dim3(kOrch), 0, m->stream, M, 1);
-    hipLaunchKernelGGL(k_dm_a_rank, chunks, par, 0, m->stream, M, n, dn);
-    hipLaunchKernelGGL(k_dm_a_fill, grid, par, 0, m->stream, M, n, dn);
-    hipLaunchKernelGGL(k_dm_a_mean, grid, par, 0, m->stream, M, d_pts, n, dn);
+    hipLaunchKernelGGL(k_dm_a_rank, chunks, par, 0, m->stream, M, 0, dn);
+    hipLaunchKernelGGL(k_dm_a_fill, grid, par, 0, m->stream, M, 0, dn);
+    hipLaunchKernelGGL(k_dm_a_mean, grid, par, 0, m->stream, M, m->d_in, 0, dn);
     hipLaunchKernelGGL(k_dm_r_group, grid, par, 0, m->stream, M);
     hipLaunchKernelGGL(k_dm_r_count, chunks, par, 0, m->stream, M);
     hipLaunchKernelGGL(k_dm_scan3, dim3(1), dim3(kOrch), 0, m->stream, M, 2);
     hipLaunchKernelGGL(k_dm_r_rank, chunks, par, 0, m->stream, M);
     hipLaunchKernelGGL(k_dm_r_fill, grid, par, 0, m->stream, M);
     hipLaunchKernelGGL(k_dm_r_append, grid, par, 0, m->stream, M);
-    hipLaunchKernelGGL(k_dm_a_done, grid, par, 0, m->stream, M, n, dn);
-    const dim3 tgrid(std::max(1, std::min(1024, (nmax + 63) / 64)));
+    hipLaunchKernelGGL(k_dm_a_done, grid, par, 0, m->stream, M, 0, dn);
     hipLaunchKernelGGL(k_dm_touched, tgrid, dim3(64), 0, m->stream, M);
     hipLaunchKernelGGL(k_dm_finish, dim3(1), dim3(kOrch), 0, m->stream, M);
-    hipLaunchKernelGGL(k_dm_rebuild_clear, dim3(1024), dim3(kPar), 0, m->stream, M);
-    hipLaunchKernelGGL(k_dm_rebuild_fill, dim3(1024), dim3(kPar), 0, m->stream, M);
+    hipLaunchKernelGGL(k_dm_table, grid, par, 0, m->stream, M);
+    hipLaunchKernelGGL(k_dm_table_check, dim3(1), dim3(64), 0, m->stream, M);
+    hipLaunchKernelGGL(k_dm_rebuild_clear, dim3(1024), par, 0, m->stream, M);
+    hipLaunchKernelGGL(k_dm_rebuild_fill, dim3(1024), par, 0, m->stream, M);
+    const hipError_t le = hipGetLastError();
+    const hipError_t ce = hipStreamEndCapture(m->stream, &g);
+    if (le != hipSuccess || ce != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        m->err = std::string("graph capture: ") + hipGetErrorString(le != hipSuccess ? le : ce);
+        return LO_ERR_HIP;
+    }
+    const hipError_t ie = hipGraphInstantiate(&m->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) { m->gexec = nullptr; m->err = std::string("graph instantiate: ") + hipGetErrorString(ie); return LO_ERR_HIP; }
+    m->g_tab = M.tab;
+    m->g_tabl = M.tabl;
+    m->g_scan = d_scan;
+    m->g_scan_n = d_scan_n;
+    return LO_OK;
+}
+
+static int dm_update(lo_devmap* m, int n_host, bool from_scan, const float T[12], const double sensor[3],
+                     double max_distance) {
+    DM& M = m->M;
+    int rc = dm_bind_table(m);
+    if (rc != LO_OK) return rc;
+    const float* d_scan = nullptr;
+    const int* d_scan_n = nullptr;
+    if (from_scan) {
+        rc = ctx_filtered_device(m->ctx, &d_scan, &d_scan_n);
+        if (rc != LO_OK) { m->err = lo_last_error(m->ctx); return rc; }
+    } else {
+        d_scan = m->g_scan;                               // unused by the graph in this mode: keep it
+        d_scan_n = m->g_scan_n ? m->g_scan_n : M.prm_n;
+    }
+    if (!m->gexec || m->g_tab != M.tab || m->g_tabl != M.tabl || (from_scan && (m->g_scan != d_scan || m->g_scan_n != d_scan_n))) {
+        rc = dm_capture(m, d_scan_n, d_scan);
+        if (rc != LO_OK) return rc;
+    }
+    DmParams P{};
+    P.v[0] = static_cast<float>(sensor[0]);
+    P.v[1] = static_cast<float>(sensor[1]);
+    P.v[2] = static_cast<float>(sensor[2]);
+    P.v[3] = static_cast<float>(max_distance * max_distance);
+    if (T) std::memcpy(P.v + 4, T, 12 * sizeof(float));
+    P.n = n_host;
+    P.from_scan = from_scan ? 1 : 0;
+    ++m->updates;
+    hipLaunchKernelGGL(k_dm_setprm, dim3(1), dim3(64), 0, m->stream, M, P);
     DM_HIP(m, hipGetLastError());
+    DM_HIP(m, hipGraphLaunch(m->gexec, m->stream));
     return LO_OK;
 }
 
@@ -1372,28 +1484,17 @@ int lo_devmap_update(lo_devmap* m, const float* world_xyz, size_t n, int on_devi
     if (n == 0 || !is_keyframe) return LO_OK;           // UpdateVoxelMap returns before pruning (:135-142)
     if (n > static_cast<size_t>(m->M.NP)) { m->err = "more points than max_points"; return LO_ERR_CAPACITY; }
     DM_HIP(m, hipSetDevice(m->device));
-    const float* d = world_xyz;
-    if (!on_device) {
-        DM_HIP(m, hipMemcpyAsync(m->d_in, world_xyz, n * 3 * sizeof(float), hipMemcpyHostToDevice, m->stream));
-        d = m->d_in;
-    }
-    return dm_update(m, d, static_cast<int>(n), nullptr, sensor, max_distance);
+    DM_HIP(m, hipMemcpyAsync(m->d_in, world_xyz, n * 3 * sizeof(float),
+                             on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, m->stream));
+    return dm_update(m, static_cast<int>(n), false, nullptr, sensor, max_distance);
 }
 
 int lo_devmap_update_from_scan(lo_devmap* m, const float T[12], double max_distance) {
     if (!m || !T) return LO_ERR_ARG;
-    const float* d_scan = nullptr;
-    const int* d_n = nullptr;
-    int rc = ctx_filtered_device(m->ctx, &d_scan, &d_n);
-    if (rc != LO_OK) { m->err = lo_last_error(m->ctx); return rc; }
     DM_HIP(m, hipSetDevice(m->device));
-    DmPose P;
-    std::memcpy(P.v, T, sizeof(P.v));
-    const dim3 grid(std::max(1, std::min(1024, (m->M.NP + kPar - 1) / kPar)));
-    hipLaunchKernelGGL(k_dm_world, grid, dim3(kPar), 0, m->stream, m->M, d_scan, d_n, P, m->d_in);
     const double sensor[3] = {T[3], T[7], T[11]};        // Vector3f -> Vector3d
-    // an empty scan returns before the prune (UpdateVoxelMap :135-137): k_dm_prune_mark reads the count too
-    return dm_update(m, m->d_in, 0, d_n, sensor, max_distance);
+    // an empty scan returns before the prune (UpdateVoxelMap :135-137): the kernels read the device count
+    return dm_update(m, 0, true, T, sensor, max_distance);
 }
 
 int lo_devmap_apply_transform(lo_devmap* m, const float T[12]) {
