@@ -8,6 +8,7 @@ cd "$(dirname "$0")/.." || exit 2
 all=(
   "tests:900:python -m pytest tests -m gpu -x -q -p no:cacheprovider"
   "bench_kitti:600:python bench.py > gpurun_out/bench_kitti.json"
+  "pko_phases:300:python scripts/pko_phases.py > gpurun_out/pko_phases.txt"
   "bench_1m:900:python bench.py --config patch1m --steps 40 --warmup 4 --cpu-budget 10 > gpurun_out/bench_patch1m.json"
   "bench_1m_rand:600:python bench.py --config patch1m --order random --steps 40 --warmup 4 --no-cpu-baseline > gpurun_out/bench_patch1m_random.json"
   "bench_raw:600:python bench.py --config kitti_raw --cpu-budget 10 > gpurun_out/bench_kitti_raw.json"
