@@ -140,6 +140,8 @@ int lo_icp_optimize(lo_ctx* ctx, const float* pts_xyz, size_t n, const float T_i
  * read (and the stream synchronised) by lo_icp_result(). */
 int lo_icp_optimize_async(lo_ctx* ctx, const float* d_pts, size_t n, const float T_init[12]);
 int lo_icp_result(lo_ctx* ctx, float T_out[12], lo_iter_log* logs, lo_stats* stats);
+/* stats->gpu_ms: the device time of a synchronous call (HIP events around its launches); -1 after an async call,
+ * which records no events (each marker packet costs several us of device time between two kernels). */
 int lo_sync(lo_ctx* ctx);
 void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
 /* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again (a fresh
@@ -151,6 +153,15 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * so the per-iteration logs equal the oracle restatement's bit for bit.  Slower (a sequential sum and two fp32 SVDs per
  * GN iteration); scans of at most 16384 points (LO_ERR_CAPACITY beyond). */
 int lo_set_exact(lo_ctx* ctx, int enable);
+/* Scan pipeline (default on; LO_PIPE=0 in the environment turns it off at lo_create).  The reference's optimize
+ * runs GN iterations until convergence (IterativeClosestPointOptimizer.cpp:281-449); the device loop enqueues all
+ * max_iterations and a converged scan's later launches leave early.  With the pipeline, iterations >= main_iterations
+ * (default 2) of a small surfel scan with PKO go to a second stream of the context, and the context stream waits on
+ * the device only until the scan's result is final: the early-exit launches of a converged scan drain beside the
+ * next scan instead of in front of it.  Results are identical with the pipeline on or off; everything enqueued on
+ * the context stream after an optimize sees its final result; lo_sync drains both streams.  main_iterations 0 keeps
+ * the current split. */
+int lo_set_pipeline(lo_ctx* ctx, int enable, int main_iterations);
 /* In-step timing: with enable, each optimize brackets its FIRST correspondence launch (k_correspond, or the KDTree
  * k_knn + k_knn_brute + k_plane) with HIP events on the context stream (up to 1024 scans; enabling resets them).
  * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */

@@ -139,7 +139,26 @@ struct KParams {
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     unsigned long long* em_stat;  // nullable (stage timing on): DevState::em_stat, the lead PKO workgroup's EM timing
     DevState* st;
+    uint32_t* fin;            // nullable (scan pipeline, lo_set_pipeline): the context's "last final scan" word
+    uint32_t seq;             //   and this scan's sequence number, published there once its result is final
+    int tail;                 // 1: a tail-stream launch -- it leaves once scan seq is final (fin_reached; the DevState may
+                              //   then already be the next scan's) and reads the caller's points only after that test
 };
+
+// Scan pipeline: the thread that wrote a scan's final DevState (pose, logs, status) writes it back to memory (agent
+// release: every XCD and the copy engines read the fresh bytes) and then publishes the scan's sequence number with
+// an sc1 store; k_wait_final on the context stream polls that word (MI355X_MICROARCH.md "inter-workgroup
+// visibility": release, then the explicit vmcnt wait, then the relaxed agent-scope flag store).
+// A tail-stream launch's own early-exit test (sc1 load: fresh across XCDs; the scans become final in order).
+__device__ __forceinline__ bool fin_reached(const KParams& P) {
+    return static_cast<int32_t>(__hip_atomic_load(P.fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - P.seq) >= 0;
+}
+__device__ __forceinline__ void publish_final(const KParams& P) {
+    if (!P.fin) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(P.fin, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // The per-iteration buffers a PKO pass works on (own_bufs: the context's own), passed beside the kernel-argument
 // KParams.

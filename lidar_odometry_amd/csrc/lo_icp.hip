@@ -39,6 +39,8 @@ __global__ void k_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
+__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st);
+__global__ void k_wait_seq(const uint32_t* word, uint32_t seq, DevState* st);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
 __global__ void k_knn_reset(KParams P);
@@ -170,6 +172,18 @@ struct lo_ctx {
     float T_init[12];
     size_t last_n = 0;
     bool pending = false;
+    // scan pipeline (lo_set_pipeline; on by default): GN iterations >= pipe_main of a small PKO scan go to a tail
+    // stream, and the context stream waits (k_wait_final) only until the scan's result is final -- a converged
+    // scan's early-exit launches drain beside the next scan instead of in front of it.  The tail starts when the
+    // main part is done (k_wait_seq polls the word k_wait_final sets); no HIP events on the hot path (every marker
+    // packet costs ~5-7 us of device time between two kernels).
+    bool pipe = true;
+    int pipe_main = 2;
+    hipStream_t s_tail = nullptr;
+    uint32_t pipe_seq = 0;
+    uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done
+    bool sync_call = false;         // the optimize in flight is a synchronous call: HIP events time it (gpu_ms)
+    bool last_timed = false;
 };
 
 #define LO_HIP(ctx, call)                                                                  \
@@ -197,11 +211,11 @@ static void launch_pko(lo_ctx* c, const KParams& P, int it) {
 // solves the selected one.
 static bool spec_ok(const KParams& P) { return P.use_pko && P.acc_part && P.nb_acc <= kFuseMaxBlocks; }
 
-static void launch_pko_spec(lo_ctx* c, const KParams& P, int it) {
+static void launch_pko_spec(lo_ctx* c, const KParams& P, int it, hipStream_t s = nullptr) {
     const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     const int G = pko_grid(c->cfg);
     const int W = (P.nb_acc + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
-    hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, c->stream, P, it, G);
+    hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
 }
 
 // One GN iteration after the correspondence stage: PKO with the speculative normal equations + k_solve_pick
@@ -230,6 +244,23 @@ static int ensure_acc_part(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_cand_cnt, cand * sizeof(unsigned)));
     LO_HIP(c, hipMemset(c->d_cand_cnt, 0, cand * sizeof(unsigned)));
     return LO_OK;
+}
+
+// Scan pipeline (first pipelined scan): the tail stream and the two flag words.
+static int pipe_alloc(lo_ctx* c) {
+    if (c->d_fin) return LO_OK;
+    LO_HIP(c, hipStreamCreateWithFlags(&c->s_tail, hipStreamNonBlocking));
+    LO_HIP(c, hipMalloc(&c->d_fin, 2 * sizeof(uint32_t)));
+    LO_HIP(c, hipMemset(c->d_fin, 0, 2 * sizeof(uint32_t)));
+    LO_HIP(c, hipDeviceSynchronize());              // zeroed before either stream's first poll
+    return LO_OK;
+}
+
+// Both streams of the context drained (lo_sync, lo_set_stream, lo_destroy).
+static hipError_t sync_all(lo_ctx* c) {
+    hipError_t e = c->stream ? hipStreamSynchronize(c->stream) : hipSuccess;
+    if (e == hipSuccess && c->s_tail) e = hipStreamSynchronize(c->s_tail);
+    return e;
 }
 
 static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
@@ -460,6 +491,8 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     c->cfg = *cfg;
     c->device = device;
     if (const char* pe = std::getenv("LO_PRESOLVE")) c->presolve = std::atoi(pe) != 0;   // A/B runs
+    if (const char* pp = std::getenv("LO_PIPE")) c->pipe = std::atoi(pp) != 0;
+    if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
@@ -482,7 +515,9 @@ void lo_destroy(lo_ctx* c) {
         g_live.erase(c);
     }
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)sync_all(c);
+    if (c->d_fin) (void)hipFree(c->d_fin);
+    if (c->s_tail) (void)hipStreamDestroy(c->s_tail);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part, c->d_acc_part,
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
@@ -987,7 +1022,10 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
     // reset the GN state (pose by kernel argument: no host staging buffer, scans can queue back to back)
     Pose12 T0;
     std::memcpy(T0.v, T_init, sizeof(float) * 12);
-    LO_HIP(c, hipEventRecord(c->ev0, c->stream));
+    // HIP events only for synchronous calls (gpu_ms): a marker packet costs ~5-7 us of device time per scan
+    const bool timed = c->sync_call;
+    c->last_timed = timed;
+    if (timed) LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     if (n == 0) {
         hipLaunchKernelGGL(k_init, dim3(1), dim3(64), 0, c->stream, c->d_st, T0, 1.0, g.robust_loss_delta);
     } else {
@@ -1010,7 +1048,33 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             if (rc3 != LO_OK) return rc3;
             for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
             LO_HIP(c, hipGetLastError());
-            LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+            if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+            c->pending = true;
+            return LO_OK;
+        }
+        if (fused && P.cand_rec && !c->kd && c->pipe && g.max_iterations > c->pipe_main) {
+            // scan pipeline: iterations < pipe_main on the context stream, the rest on the tail stream behind a
+            // device-side wait for the main part; the context stream then waits only for the final result
+            const int rc2 = pipe_alloc(c);
+            if (rc2 != LO_OK) return rc2;
+            const uint32_t seq = ++c->pipe_seq;
+            P.fin = P0.fin = c->d_fin;
+            P.seq = P0.seq = seq;
+            KParams Pt = P;                               // tail launches: leave once scan seq is final (the
+            Pt.tail = 1;                                  // DevState may already be the next scan's)
+            launch_correspond_first(c, P0, false);
+            hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin + 1, seq, c->d_st);
+            for (int it = 0; it < g.max_iterations; ++it) {
+                const bool tail = it >= c->pipe_main;
+                const hipStream_t s = tail ? c->s_tail : c->stream;
+                const KParams& Pi = tail ? Pt : P;
+                launch_pko_spec(c, Pi, it, s);
+                if (it + 1 < g.max_iterations) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, s, Pi, it);
+                else hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, s, Pi, it);
+            }
+            hipLaunchKernelGGL(k_wait_final, dim3(1), dim3(kWave), 0, c->stream, c->d_fin, seq, c->d_st);
+            LO_HIP(c, hipGetLastError());
+            if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
             c->pending = true;
             return LO_OK;
         }
@@ -1039,7 +1103,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         }
         LO_HIP(c, hipGetLastError());
     }
-    LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+    if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
     c->pending = true;
     return LO_OK;
 }
@@ -1062,6 +1126,7 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     c->pending = false;
     const DevState* hs = c->h_st;
     int status = c->last_n == 0 ? LO_INSUFFICIENT : hs->status;
+    if (status == LO_ERR_HIP) c->err = "scan pipeline: the wait for the scan's final result timed out";
     const int iters = hs->iter;
     if (T_out) {
         if (status == LO_OK) std::memcpy(T_out, hs->pose, sizeof(float) * 12);
@@ -1075,8 +1140,8 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
         st->converged = status == LO_OK ? 1 : 0;
         st->initial_cost = iters > 0 ? hs->logs[0].cost : 0.0;
         st->final_cost = iters > 0 ? hs->logs[iters - 1].cost : 0.0;
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.0f;
+        float ms = -1.0f;                                  // -1: an async call (not timed)
+        if (c->last_timed && hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) ms = -1.0f;
         st->gpu_ms = ms;
     }
     return status;
@@ -1084,7 +1149,7 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
 
 int lo_sync(lo_ctx* c) {
     if (!c) return LO_ERR_ARG;
-    LO_HIP(c, hipStreamSynchronize(c->stream));
+    LO_HIP(c, sync_all(c));
     return LO_OK;
 }
 
@@ -1095,7 +1160,9 @@ int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12
     LO_HIP(c, hipSetDevice(c->device));
     if (n > 0) LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     c->last_dev_count = false;
+    c->sync_call = true;
     int rc = enqueue_optimize(c, c->d_pts, n, T_init);
+    c->sync_call = false;
     if (rc != LO_OK) return rc;
     return lo_icp_result(c, T_out, logs, st);
 }
@@ -1272,7 +1339,9 @@ int lo_icp_optimize_raw(lo_ctx* c, const float* raw, size_t n_raw, int stride, f
         if (rc != LO_OK) return rc;
         src = c->d_raw;
     }
+    c->sync_call = true;
     rc = lo_icp_optimize_raw_async(c, src, n_raw, stride, voxel_size, T_init);
+    c->sync_call = false;
     if (rc != LO_OK) return rc;
     return lo_icp_result(c, T_out, logs, st);
 }
@@ -1476,7 +1545,7 @@ int lo_stage_time(lo_ctx* c, double* avg_us, int* count) {
 int lo_pko_em_stats(lo_ctx* c, unsigned long long out[3], int reset) {
     if (!c || !out) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
-    LO_HIP(c, hipStreamSynchronize(c->stream));
+    LO_HIP(c, sync_all(c));
     LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(c->d_st) + offsetof(DevState, em_stat),
                         3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (reset)
@@ -1490,10 +1559,17 @@ int lo_set_exact(lo_ctx* c, int enable) {
     return LO_OK;
 }
 
+int lo_set_pipeline(lo_ctx* c, int enable, int main_iterations) {
+    if (!c || main_iterations < 0) return LO_ERR_ARG;
+    c->pipe = enable != 0;
+    if (main_iterations > 0) c->pipe_main = main_iterations;
+    return LO_OK;
+}
+
 int lo_set_stream(lo_ctx* c, void* stream) {
     if (!c) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
-    LO_HIP(c, hipStreamSynchronize(c->stream));
+    LO_HIP(c, sync_all(c));
     if (c->own_stream) { LO_HIP(c, hipStreamDestroy(c->stream)); c->own_stream = false; }
     if (stream) c->stream = static_cast<hipStream_t>(stream);
     else { LO_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
@@ -1546,8 +1622,9 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
 
 int lo_debug_counters(lo_ctx* c, unsigned long long out[16]) {
     if (!c || !out) return LO_ERR_ARG;
-    LO_HIP(c, hipStreamSynchronize(c->stream));
-    LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(c->d_st) + offsetof(DevState, dbg), 16 * sizeof(unsigned long long),
+    LO_HIP(c, sync_all(c));
+    const DevState* st = c->d_st;
+    LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(st) + offsetof(DevState, dbg), 16 * sizeof(unsigned long long),
                         hipMemcpyDeviceToHost));
     return LO_OK;
 }

@@ -246,11 +246,13 @@ template <bool CORR>
 __device__ __forceinline__ void pick_body(const KParams& P, int it) {
     DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    const int done = st->done;                    // loaded with the points and the JS grid (one round trip)
+    const int done = st->done || (P.tail && fin_reached(P));   // loaded with the points and the JS grid
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
-    if (CORR && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
+    // tail-stream launches (scan pipeline) read the caller's points only once the scan is known to go on: they
+    // may run after the caller has already taken the final result and reused or freed that buffer
+    if (CORR && !P.tail && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
     __shared__ float s_rec[kCandWords];
     __shared__ int s_skip;
     __shared__ double s_alpha;
@@ -281,8 +283,10 @@ __device__ __forceinline__ void pick_body(const KParams& P, int it) {
         st->alpha = s_alpha;
         st->iter = it + 1;
         if (conv) st->done = 1;
+        if (conv || it + 1 >= P.max_iters) publish_final(P);   // the scan's result is final (scan pipeline)
     }
     if (!CORR || conv) return;                    // converged: the later launches of the scan see DevState::done
+    if (P.tail && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
@@ -467,6 +471,31 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
         st->inliers = 0;
         st->kd_tie = 0;
     }
+}
+
+// Scan pipeline (lo_set_pipeline).  k_wait_final runs on the context stream after the scan's main part: it tells
+// the tail stream that the main part is done (fin[1] = seq: the launches before it have ended, so their stores are
+// visible to the tail's next kernels), then holds the context stream until scan `seq`'s result is final (fin[0] >=
+// seq: publish_final by the pick that converged or ran the last iteration, or the PKO that found too few
+// correspondences).  k_wait_seq heads the scan's tail on the tail stream and waits for fin[1].  One lane polls with
+// sc1 loads (fresh across XCDs; the word is the only thing read).  Both waits are bounded (2 s of the 100 MHz
+// constant clock): on timeout the scan reports LO_ERR_HIP instead of a queue hanging.
+__device__ __forceinline__ bool wait_word(const uint32_t* w, uint32_t seq) {
+    const unsigned long long t0 = wall_clock64();
+    while (static_cast<int32_t>(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+        if (wall_clock64() - t0 > 200000000ull) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st) {
+    if (threadIdx.x != 0) return;
+    __hip_atomic_store(fin + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!wait_word(fin, seq)) st->status = LO_ERR_HIP;
+}
+__global__ void k_wait_seq(const uint32_t* word, uint32_t seq, DevState* st) {
+    if (threadIdx.x != 0) return;
+    if (!wait_word(word, seq)) st->status = LO_ERR_HIP;
 }
 
 // Copy the current pose + status into a caller buffer (16 floats: pose[12], status, iterations, n_corr, 0).

@@ -1005,7 +1005,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     DevState* st = B.st;
     // the done flag, the single-wave prefix's loads and the prefetch below go out in one round trip; the flag is
     // tested once they are in flight (a converged scan leaves without writing anything)
-    const int done0 = st->done;
+    const int done0 = st->done || (P.tail && fin_reached(P));   // tail launch: scan already final
     PrefixLoads pl;
     const bool wave_prefix = !P.direct_res && P.nb <= 64;
     if (wave_prefix && threadIdx.x < 64) prefix_loads(P, B, it, pl);
@@ -1028,7 +1028,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? L.wm : nullptr;
     pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, L.wm, &pl);   // pl is set where it is read (nb <= 64)
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
-        if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; }
+        if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; publish_final(P); }
         return;
     }
     if constexpr (NW == 4 && !ONE_WAVE) {

@@ -142,6 +142,13 @@ class IterativeClosestPointOptimizer:
         if rc != 0:
             raise RuntimeError(f"lo_set_exact failed ({rc})")
 
+    def set_pipeline(self, enable: bool = True, main_iterations: int = 0):
+        """Scan pipeline (default on): GN iterations >= main_iterations run on the context's tail stream and the context
+        stream waits only for the scan's final result; results are identical either way (lo_set_pipeline)."""
+        rc = self._L.lo_set_pipeline(self.ctx, int(bool(enable)), int(main_iterations))
+        if rc != 0:
+            raise RuntimeError(f"lo_set_pipeline failed ({rc})")
+
     def close(self):
         h = getattr(self, "_ctx", None)
         if h:

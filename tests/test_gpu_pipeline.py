@@ -1,0 +1,166 @@
+"""GPU tests of the scan pipeline (lo_set_pipeline): a scan's GN iterations from `main_iterations` on run on the
+context's tail stream (behind a device-side wait for the main part, k_wait_seq), and the context stream waits on the
+device (k_wait_final) only until the scan's result is final, so a converged scan's early-exit launches drain beside
+the next scan (they test the context's "last final scan" word, not the DevState the next scan already owns).
+
+Bar: bit-identical to the pipeline switched off -- pose, every iteration's log, status, iteration count, n_corr --
+for scans that converge in 1-4 iterations, scans that run out of iterations, too few correspondences and empty
+clouds; for scans queued back to back (lo_icp_optimize_async, records exported per scan); for every split of the
+iterations over the two streams; and for map changes between pipelined scans (the change must see the final
+result of the scan before it and be seen by the scan after it).
+Reference loop: IterativeClosestPointOptimizer.cpp:281-449 (optimize runs until convergence / max_iterations).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    cs = []
+    for f in (11, 13, 17, 21, 25):
+        m, pts, Ti, _ = _data.kitti_case(f)
+        cs.append((m, pts, Ti))
+    m, pts, Ti, _ = _data.kitti_case(19, seed=5, sigma_t=0.3, sigma_r=0.03)        # large perturbation: more iterations
+    cs.append((m, pts, Ti))
+    m, pts, Ti, _ = _data.kitti_case(11)
+    cs.append((m, pts + np.float32(5000.0), Ti))                                   # too few correspondences
+    cs.append((m, pts[:0], Ti))                                                    # empty cloud
+    return cs
+
+
+def _ctx(m, max_iterations=None):
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    cfg = ICPConfig()
+    if max_iterations is not None:
+        cfg.max_iterations = max_iterations
+    o = IterativeClosestPointOptimizer(config=cfg, max_points=1 << 16)
+    k, n, c = _data.surfels(m)
+    o.set_surfels(k, n, c)
+    return o
+
+
+def _run(o, pts, Ti):
+    ok, To = o.optimize(None, pts, Ti)
+    st = o.get_last_stats()
+    logs = [(np.asarray(L["pose"], np.float32).tobytes(), float(L["alpha"]), float(L["cost"]), int(L["n_corr"]))
+            for L in st.iterations]
+    return ok, np.asarray(To, np.float32).reshape(12).tobytes(), st.num_iterations, st.num_correspondences, logs
+
+
+@pytest.mark.parametrize("main", [1, 2, 3])
+def test_pipeline_sync_bitwise(main):
+    cs = _cases()
+    o = _ctx(cs[0][0])
+    try:
+        ref = []
+        o.set_pipeline(False)
+        for _, pts, Ti in cs:
+            ref.append(_run(o, pts, Ti))
+        o.set_pipeline(True, main)
+        for rep in range(2):                                   # every case after every other
+            for j, (_, pts, Ti) in enumerate(cs):
+                got = _run(o, pts, Ti)
+                assert got == ref[j], f"case {j} (main {main}, rep {rep})"
+        iters = sorted({r[2] for r in ref})
+        assert max(iters) >= 3, iters                          # some scan really ran iterations on the tail stream
+    finally:
+        o.close()
+
+
+def test_pipeline_more_iterations():
+    """max_iterations 6 (forced non-convergence would need a looser map; the large perturbation runs > 2)."""
+    cs = _cases()
+    o = _ctx(cs[0][0], max_iterations=6)
+    try:
+        o.set_pipeline(False)
+        ref = [_run(o, pts, Ti) for _, pts, Ti in cs]
+        o.set_pipeline(True, 2)
+        got = [_run(o, pts, Ti) for _, pts, Ti in cs]
+        assert got == ref
+    finally:
+        o.close()
+
+
+def _queued(o, d_scans, inits, order):
+    """Every scan of `order` enqueued back to back; each one's 16-float record exported on the context stream."""
+    import torch
+    L = o._L
+    recs = torch.zeros(len(order), 16, dtype=torch.float32, device="cuda:0")
+    for k, i in enumerate(order):
+        T = np.ascontiguousarray(inits[i], np.float32)
+        rc = L.lo_icp_optimize_async(o.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0],
+                                     T.ctypes.data_as(C.POINTER(C.c_float)))
+        assert rc == 0, rc
+        assert L.lo_icp_export_pose(o.ctx, C.c_void_p(recs[k].data_ptr())) == 0
+    assert L.lo_sync(o.ctx) == 0
+    return recs.cpu().numpy()
+
+
+def test_pipeline_async_queue_bitwise():
+    import torch
+    cs = _cases()
+    o = _ctx(cs[0][0])
+    try:
+        d_scans = [torch.from_numpy(np.ascontiguousarray(p, np.float32).reshape(-1, 3)).to("cuda:0") if len(p)
+                   else torch.zeros(1, 3, dtype=torch.float32, device="cuda:0") for _, p, _ in cs]
+        inits = [Ti for _, _, Ti in cs]
+        rng = np.random.default_rng(3)
+        order = [int(x) for x in rng.integers(0, len(cs) - 1, size=40)]   # no empty cloud here (n = 0 -> k_init)
+        o.set_pipeline(False)
+        ref = _queued(o, d_scans, inits, order)
+        o.set_pipeline(True, 2)
+        got = _queued(o, d_scans, inits, order)
+        np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+        # the records equal the synchronous results
+        o.set_pipeline(False)
+        for k in (0, 7, 19, 39):
+            i = order[k]
+            ok, To = o.optimize(None, cs[i][1], cs[i][2])
+            if ok:
+                np.testing.assert_array_equal(got[k, :12], np.asarray(To, np.float32).reshape(12))
+            assert int(got[k, 13]) == o.get_last_stats().num_iterations
+    finally:
+        o.close()
+
+
+def test_pipeline_map_change_between_scans():
+    """A surfel upload between two pipelined scans: the upload waits for the first scan's final result and the second
+    scan sees the new map -- both equal to the unpipelined sequence."""
+    cs = _cases()
+    m2, pts2, Ti2, _ = _data.kitti_case(27, last_kf=30)
+    o = _ctx(cs[0][0])
+    try:
+        def seq():
+            k, n, c = _data.surfels(cs[0][0])
+            o.set_surfels(k, n, c)
+            a = _run(o, cs[5][1], cs[5][2])                    # the many-iteration scan first
+            k2, n2, c2 = _data.surfels(m2)
+            o.set_surfels(k2, n2, c2)
+            b = _run(o, pts2, Ti2)
+            o.set_surfels(k, n, c)
+            d = _run(o, cs[1][1], cs[1][2])
+            return a, b, d
+        o.set_pipeline(False)
+        ref = seq()
+        o.set_pipeline(True, 1)
+        assert seq() == ref
+        o.set_pipeline(True, 2)
+        assert seq() == ref
+    finally:
+        o.close()
+
+
+def test_pipeline_args():
+    cs = _cases()
+    o = _ctx(cs[0][0])
+    try:
+        assert o._L.lo_set_pipeline(o.ctx, 1, -1) != 0
+        assert o._L.lo_set_pipeline(None, 1, 2) != 0
+        o.set_pipeline(True, 0)                                # keeps the split
+    finally:
+        o.close()
