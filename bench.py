@@ -1014,6 +1014,26 @@ def main():
     per_scan = {k: v * gi for k, v in kern_us.items() if not (spec and k == "k_accumulate")}
     dom = max(per_scan, key=per_scan.get)
 
+    # the scan pipeline (lo_set_pipeline, on by default and in `value`): the same steps with it switched off, so the
+    # line shows what the tail stream buys (results are bit-identical either way: tests/test_gpu_pipeline.py)
+    pipeline = {"main_iterations": int(os.environ.get("LO_PIPE_MAIN", "2")),
+                "enabled": os.environ.get("LO_PIPE", "1") != "0",
+                "note": "GN iterations >= main_iterations of a small PKO scan run on the context's tail stream; the "
+                        "context stream is held on the device (k_wait_final) only until the scan's result is final"}
+    if world == 1 and pipeline["enabled"] and rec_log is None:
+        n_po = min(args.steps, 1000)
+        L.lo_set_pipeline(icp.ctx, 0, 0)
+        for k in range(10):
+            step(k)
+        torch.cuda.synchronize(dev)
+        t5 = time.perf_counter()
+        for k in range(n_po):
+            step(k)
+        torch.cuda.synchronize(dev)
+        pipeline["value_pipeline_off"] = n_po / (time.perf_counter() - t5)
+        pipeline["steps_pipeline_off"] = n_po
+        L.lo_set_pipeline(icp.ctx, 1, 0)
+
     # PCIe-inclusive rate (never `value`): lo_icp_optimize on HOST buffers = H2D points, the same device
     # GN loop, D2H pose + per-iteration logs and a stream sync per scan
     n_pc = min(200, max(20, args.steps // 5))
@@ -1210,7 +1230,8 @@ def main():
                    "map_l0_points": wl["vm"].l0_count(), "correspondence": "kdtree 5-NN" if kd else "L1 surfel",
                    "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),
                    "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step, side stream)" if world > 1
-                   else "single GPU, one HIP stream"},
+                   else "single GPU: context stream + tail stream (scan pipeline)"},
+        "pipeline": pipeline,
         "gn_iters_per_sec": total_iters / el,
         "per_rank": None if world == 1 else {"scans_per_s": [args.steps / e for e in per_rank], "timed_s": per_rank,
                                              "backend": args.dist_backend, "gather_check": gather_check},

@@ -141,14 +141,37 @@ struct KParams {
     DevState* st;
     uint32_t* fin;            // nullable (scan pipeline, lo_set_pipeline): the context's "last final scan" word
     uint32_t seq;             //   and this scan's sequence number, published there once its result is final
+    int hold;                 // 1: the main part's last pick (signal_main: fin[1] = seq once its correspondences are out;
+                              //   fin[2] counts its blocks in)
     int tail;                 // 1: a tail-stream launch -- it leaves once scan seq is final (fin_reached; the DevState may
                               //   then already be the next scan's) and reads the caller's points only after that test
 };
 
 // Scan pipeline: the thread that wrote a scan's final DevState (pose, logs, status) writes it back to memory (agent
 // release: every XCD and the copy engines read the fresh bytes) and then publishes the scan's sequence number with
-// an sc1 store; k_wait_final on the context stream polls that word (MI355X_MICROARCH.md "inter-workgroup
+// an sc1 store; k_wait_final (and k_wait_seq) poll that word (MI355X_MICROARCH.md "inter-workgroup
 // visibility": release, then the explicit vmcnt wait, then the relaxed agent-scope flag store).
+// Scan pipeline: poll a flag word until it reaches seq (one lane, sc1 loads: fresh across XCDs; the word is the only
+// thing read), bounded by 2 s of the 100 MHz constant clock -- false on timeout, so no wait can hang a queue.
+__device__ __forceinline__ bool wait_word(const uint32_t* w, uint32_t seq) {
+    const unsigned long long t0 = wall_clock64();
+    while (static_cast<int32_t>(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+        if (wall_clock64() - t0 > 200000000ull) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+// ... until either of two words reaches seq
+__device__ __forceinline__ bool wait_word2(const uint32_t* a, const uint32_t* b, uint32_t seq) {
+    const unsigned long long t0 = wall_clock64();
+    while (static_cast<int32_t>(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0 &&
+           static_cast<int32_t>(__hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+        if (wall_clock64() - t0 > 200000000ull) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
 // A tail-stream launch's own early-exit test (sc1 load: fresh across XCDs; the scans become final in order).
 __device__ __forceinline__ bool fin_reached(const KParams& P) {
     return static_cast<int32_t>(__hip_atomic_load(P.fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - P.seq) >= 0;

@@ -39,8 +39,8 @@ __global__ void k_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
-__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st);
-__global__ void k_wait_seq(const uint32_t* word, uint32_t seq, DevState* st);
+__global__ void k_wait_seq(const uint32_t* fin, uint32_t seq, DevState* st);
+__global__ void k_wait_final(const uint32_t* fin, uint32_t seq, DevState* st);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
 __global__ void k_knn_reset(KParams P);
@@ -173,15 +173,16 @@ struct lo_ctx {
     size_t last_n = 0;
     bool pending = false;
     // scan pipeline (lo_set_pipeline; on by default): GN iterations >= pipe_main of a small PKO scan go to a tail
-    // stream, and the context stream waits (k_wait_final) only until the scan's result is final -- a converged
-    // scan's early-exit launches drain beside the next scan instead of in front of it.  The tail starts when the
-    // main part is done (k_wait_seq polls the word k_wait_final sets); no HIP events on the hot path (every marker
-    // packet costs ~5-7 us of device time between two kernels).
+    // stream, and the context stream is held (k_wait_final) only until the scan's result is final -- a converged
+    // scan's early-exit launches drain beside the next scan instead of in front of it.  The tail starts when the main
+    // part is done (k_wait_seq polls the word the main part's last pick sets); no HIP events on the hot path (every
+    // marker packet costs ~5-7 us of device time between two kernels).
     bool pipe = true;
     int pipe_main = 2;
     hipStream_t s_tail = nullptr;
     uint32_t pipe_seq = 0;
-    uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done
+    uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done,
+                                    // [2] signal_main's block count
     bool sync_call = false;         // the optimize in flight is a synchronous call: HIP events time it (gpu_ms)
     bool last_timed = false;
 };
@@ -250,8 +251,8 @@ static int ensure_acc_part(lo_ctx* c) {
 static int pipe_alloc(lo_ctx* c) {
     if (c->d_fin) return LO_OK;
     LO_HIP(c, hipStreamCreateWithFlags(&c->s_tail, hipStreamNonBlocking));
-    LO_HIP(c, hipMalloc(&c->d_fin, 2 * sizeof(uint32_t)));
-    LO_HIP(c, hipMemset(c->d_fin, 0, 2 * sizeof(uint32_t)));
+    LO_HIP(c, hipMalloc(&c->d_fin, 3 * sizeof(uint32_t)));
+    LO_HIP(c, hipMemset(c->d_fin, 0, 3 * sizeof(uint32_t)));
     LO_HIP(c, hipDeviceSynchronize());              // zeroed before either stream's first poll
     return LO_OK;
 }
@@ -1054,7 +1055,8 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         }
         if (fused && P.cand_rec && !c->kd && c->pipe && g.max_iterations > c->pipe_main) {
             // scan pipeline: iterations < pipe_main on the context stream, the rest on the tail stream behind a
-            // device-side wait for the main part; the context stream then waits only for the final result
+            // device-side wait for the main part; k_wait_final then holds the context stream until the scan's result
+            // is final
             const int rc2 = pipe_alloc(c);
             if (rc2 != LO_OK) return rc2;
             const uint32_t seq = ++c->pipe_seq;
@@ -1062,12 +1064,17 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             P.seq = P0.seq = seq;
             KParams Pt = P;                               // tail launches: leave once scan seq is final (the
             Pt.tail = 1;                                  // DevState may already be the next scan's)
+            KParams Ph = P;                               // the main part's last pick signals the tail (signal_main)
+            Ph.hold = 1;
+            // host submission order main -> tail -> k_wait_final: every device-side wait depends only on work
+            // submitted before it (deadlock-free even if the two streams share a hardware queue)
             launch_correspond_first(c, P0, false);
-            hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin + 1, seq, c->d_st);
             for (int it = 0; it < g.max_iterations; ++it) {
                 const bool tail = it >= c->pipe_main;
+                if (it == c->pipe_main)
+                    hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin, seq, c->d_st);
                 const hipStream_t s = tail ? c->s_tail : c->stream;
-                const KParams& Pi = tail ? Pt : P;
+                const KParams& Pi = tail ? Pt : (it + 1 == c->pipe_main ? Ph : P);
                 launch_pko_spec(c, Pi, it, s);
                 if (it + 1 < g.max_iterations) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, s, Pi, it);
                 else hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, s, Pi, it);

@@ -242,6 +242,26 @@ __global__ __launch_bounds__(kBlock) void k_solve_correspond(KParams P, int it) 
 // the GN state, and with CORR every block then searches its 256 points at the new pose for iteration it + 1 -- the
 // fp64 solve is no longer between the EM's end and the next correspondence search.  Same record = same bits as
 // k_solve_pick / k_solve_correspond.
+// Scan pipeline, the main part's last pick (P.hold) when the scan goes on: every block writes its correspondences
+// back (agent release after its waves' stores have drained) and counts itself in; the last block tells the tail
+// stream that the main part is done (fin[1] = seq).  k_wait_seq heads the tail and the tail's next kernel starts with
+// an acquire.  Nothing here waits: a wait may only depend on work submitted before it, or two streams that share a
+// hardware queue would deadlock.
+__device__ __forceinline__ void signal_main(const KParams& P) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = __hip_atomic_fetch_add(P.fin + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0 || !s_last) return;
+    __hip_atomic_store(P.fin + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(P.fin + 1, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool CORR>
 __device__ __forceinline__ void pick_body(const KParams& P, int it) {
     DevState* st = P.st;
@@ -291,6 +311,7 @@ __device__ __forceinline__ void pick_body(const KParams& P, int it) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
     correspond_tail(P, T, px, py, pz, i, n, 0, blk);
+    if (P.hold) signal_main(P);
 }
 __global__ __launch_bounds__(kBlock) void k_pick_correspond(KParams P, int it) { pick_body<true>(P, it); }
 __global__ __launch_bounds__(kBlock) void k_pick(KParams P, int it) { pick_body<false>(P, it); }
@@ -473,29 +494,19 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
     }
 }
 
-// Scan pipeline (lo_set_pipeline).  k_wait_final runs on the context stream after the scan's main part: it tells
-// the tail stream that the main part is done (fin[1] = seq: the launches before it have ended, so their stores are
-// visible to the tail's next kernels), then holds the context stream until scan `seq`'s result is final (fin[0] >=
-// seq: publish_final by the pick that converged or ran the last iteration, or the PKO that found too few
-// correspondences).  k_wait_seq heads the scan's tail on the tail stream and waits for fin[1].  One lane polls with
-// sc1 loads (fresh across XCDs; the word is the only thing read).  Both waits are bounded (2 s of the 100 MHz
-// constant clock): on timeout the scan reports LO_ERR_HIP instead of a queue hanging.
-__device__ __forceinline__ bool wait_word(const uint32_t* w, uint32_t seq) {
-    const unsigned long long t0 = wall_clock64();
-    while (static_cast<int32_t>(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
-        if (wall_clock64() - t0 > 200000000ull) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-}
-__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st) {
+// Scan pipeline (lo_set_pipeline), both bounded by wait_word (on timeout the scan reports LO_ERR_HIP):
+//   k_wait_seq   heads a scan's tail on the tail stream: the main part is done (fin[1] >= seq, signal_main) or the
+//                scan is already final (fin[0] >= seq: its tail launches only leave early);
+//   k_wait_final follows the tail on the context stream: holds it until the scan's result is final (fin[0] >= seq).
+// Host submission order is main part, tail, k_wait_final: every wait depends only on work submitted before it, so
+// the two streams may share one hardware queue (they then simply run in order).
+__global__ void k_wait_seq(const uint32_t* fin, uint32_t seq, DevState* st) {
     if (threadIdx.x != 0) return;
-    __hip_atomic_store(fin + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!wait_word2(fin, fin + 1, seq)) st->status = LO_ERR_HIP;
+}
+__global__ void k_wait_final(const uint32_t* fin, uint32_t seq, DevState* st) {
+    if (threadIdx.x != 0) return;
     if (!wait_word(fin, seq)) st->status = LO_ERR_HIP;
-}
-__global__ void k_wait_seq(const uint32_t* word, uint32_t seq, DevState* st) {
-    if (threadIdx.x != 0) return;
-    if (!wait_word(word, seq)) st->status = LO_ERR_HIP;
 }
 
 // Copy the current pose + status into a caller buffer (16 floats: pose[12], status, iterations, n_corr, 0).

@@ -1,6 +1,6 @@
 """GPU tests of the scan pipeline (lo_set_pipeline): a scan's GN iterations from `main_iterations` on run on the
 context's tail stream (behind a device-side wait for the main part, k_wait_seq), and the context stream waits on the
-device (k_wait_final) only until the scan's result is final, so a converged scan's early-exit launches drain beside
+device (k_wait_final, submitted after the tail) only until the scan's result is final, so a converged scan's early-exit launches drain beside
 the next scan (they test the context's "last final scan" word, not the DevState the next scan already owns).
 
 Bar: bit-identical to the pipeline switched off -- pose, every iteration's log, status, iteration count, n_corr --
