@@ -598,20 +598,9 @@ __device__ __forceinline__ void correspond_tail(const KParams& P, const float (&
 // ---------------------------------------------------------------------------------------------------
 // One correspondence's weighted normal-equation terms added to acc (:345-410): residual, J, Huber weight,
 // fp32 products fl(fl(w J_i) J_j) as the reference forms them.
-__device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot, const float (&T)[12], double scale,
-                                          float dl, int i, float (&acc)[kNE]) {
-    const int s = slot[i];
-    if (s < 0) return;
-    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
-    const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
-    double r;
-    if (P.kd_res) {
-        r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
-    } else {
-        float wx, wy, wz;
-        transform_pt(T, px, py, pz, wx, wy, wz);
-        r = residual_f64(sl, wx, wy, wz);
-    }
+// acc_terms: the terms of one correspondence from its loaded point / surfel and fp64 residual r.
+__device__ __forceinline__ void acc_terms(const KParams& P, const float (&T)[12], double scale, float dl, double r,
+                                          float px, float py, float pz, const Slot& sl, float (&acc)[kNE]) {
     const float nres = static_cast<float>(r / std_max(scale, 1e-6));          // :374
     // p_world = R p + t (Matrix3f * Vector3f, :368), residual n.(p_w - q) in fp32 (:371)
     const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
@@ -647,6 +636,22 @@ __device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot,
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[21 + j] += wr * J[j];
     acc[27] += wr * res;
+}
+__device__ __forceinline__ void acc_point(const KParams& P, const int32_t* slot, const float (&T)[12], double scale,
+                                          float dl, int i, float (&acc)[kNE]) {
+    const int s = slot[i];
+    if (s < 0) return;
+    const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+    const Slot sl = P.tab[s];             // KDTree path: P.tab = per-point planes, s = i
+    double r;
+    if (P.kd_res) {
+        r = P.kd_res[i];                  // the stored fp64 distance (residuals[i], :374)
+    } else {
+        float wx, wy, wz;
+        transform_pt(T, px, py, pz, wx, wy, wz);
+        r = residual_f64(sl, wx, wy, wz);
+    }
+    acc_terms(P, T, scale, dl, r, px, py, pz, sl, acc);
 }
 __device__ __forceinline__ void acc_point(const KParams& P, const float (&T)[12], double scale, float dl, int i,
                                           float (&acc)[kNE]) {

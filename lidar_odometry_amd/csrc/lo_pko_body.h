@@ -539,6 +539,50 @@ __device__ void acc_blocks(const KParams& P, const int32_t* slot, const float (&
     __shared__ float s_acc[kWavesPerBlock][kNE];
     const int tid = threadIdx.x, wid = tid >> 6;
     const int n = scan_n(P);
+    if (!P.kd_res) {
+        // surfel path, software-pipelined: block vb + 2's slot index and block vb + 1's point and surfel are loaded
+        // while block vb is accumulated (the slot -> surfel chain otherwise costs two round trips per block); the
+        // terms (acc_terms) and the reductions are exactly the per-block ones below, so the partials are the same bits
+        auto slot_of = [&](int vb) { const int i = vb * kBlock + tid; return (vb < vb1 && i < n) ? slot[i] : -1; };
+        int s1 = slot_of(vb0), s2 = slot_of(vb0 + 1);
+        float px = 0.0f, py = 0.0f, pz = 0.0f;
+        Slot sl{};
+        if (s1 >= 0) {
+            const int i = vb0 * kBlock + tid;
+            px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2];
+            sl = P.tab[s1];
+        }
+        for (int vb = vb0; vb < vb1; ++vb) {
+            const int s0 = s1;
+            const float cx = px, cy = py, cz = pz;
+            const Slot cs = sl;
+            s1 = s2;
+            s2 = slot_of(vb + 2);
+            if (s1 >= 0) {
+                const int i = (vb + 1) * kBlock + tid;
+                px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2];
+                sl = P.tab[s1];
+            }
+            float acc[kNE];
+#pragma unroll
+            for (int k = 0; k < kNE; ++k) acc[k] = 0.0f;
+            if (s0 >= 0) {
+                float wx, wy, wz;
+                transform_pt(T, cx, cy, cz, wx, wy, wz);
+                acc_terms(P, T, scale, dl, residual_f64(cs, wx, wy, wz), cx, cy, cz, cs, acc);
+            }
+            wave_totals_f32<kNE>(acc, s_acc[wid]);
+            __syncthreads();
+            if (tid < kNE) {
+                double v = 0.0;
+#pragma unroll
+                for (int w = 0; w < kWavesPerBlock; ++w) v += static_cast<double>(s_acc[w][tid]);
+                Mem<SC1>::st(dst + static_cast<size_t>(vb) * kNE + tid, v);
+            }
+            __syncthreads();
+        }
+        return;
+    }
     for (int vb = vb0; vb < vb1; ++vb) {
         float acc[kNE];
 #pragma unroll
@@ -567,6 +611,9 @@ __device__ __forceinline__ float cand_delta(const KParams& P, int c) {
 // arrival reads them past L1 and re-zeroes the counter for the next launch.  The record [kCandWords] is read by
 // k_pick_correspond / k_pick after the launch, so the selected solve leaves the iteration's critical path.
 __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
+#ifdef LO_PKO_STAMPS
+    const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
+#endif
     const int nb = P.nb_acc;
     const int W = (nb + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
     const int c = wgi / W, part = wgi - c * W;
@@ -615,6 +662,13 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
     }
     __syncthreads();
     if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
+#ifdef LO_PKO_STAMPS
+    if (tid == 0) {                          // diagnostic: the slowest candidate workgroup's cycles (dbg[15])
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memtime() - c_t0);
+        if (c == 0) P.st->dbg[7] = __builtin_amdgcn_s_memtime() - c_t0;
+    }
+#endif
 }
 
 // Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts

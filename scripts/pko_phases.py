@@ -40,5 +40,7 @@ for f in (11, 13, 17, 21, 25, 31):
           + f" | per EM iter {dt[4] / max(out[8], 1):.0f} cyc"
           + f" | JS: post-EM barrier {out[12] - t[5]} gpdf {out[10] - out[12]} terms {out[11] - out[10]}"
           + f" sum {t[6] - out[11]}"
-          + f" | sample: events {out[13] - t[1]} residual {out[14] - out[13]} barrier {t[2] - out[14]}", flush=True)
+          + f" | sample: events {out[13] - t[1]} residual {out[14] - out[13]} barrier {t[2] - out[14]}"
+          + f" | candidate wg: first {out[7]} slowest {out[15]} cyc", flush=True)
+    lib().lo_debug_reset(icp.ctx) if hasattr(lib(), "lo_debug_reset") else None
 print("mean share: " + " ".join(f"{nm}={v / tot.sum():.2f}" for nm, v in zip(names, tot)))
