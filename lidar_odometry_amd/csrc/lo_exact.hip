@@ -93,6 +93,53 @@ __device__ inline void so3_exp_exact(const float w[3], float R[3][3]) {
 // (IterativeClosestPointOptimizer.cpp:304-316).  One workgroup: the residuals of the accepted points (+inf for the
 // rest) in dynamic LDS, bitonic sort, then one lane accumulates as std::accumulate does ----
 constexpr int kExactScaleThreads = 1024;
+
+// acc += v_0 + v_1 + ... + v_{cnt-1}, one rounding per element in index order (v_k = x_k, or (x_k - m)^2 with SQ), as
+// one wave-uniform chain: each 16-lane row holds 16 consecutive elements in a register and v_fmac_f64_dpp with a
+// row_newbcast source adds element 16c + N as acc = fma(v, 1.0, acc), which rounds exactly as acc + v -- no LDS
+// round trip between the adds (one lane reading LDS per element was ~25x slower).  Wave 0 only; elements past cnt
+// are never broadcast (the row guard) and never read.
+template <int N>
+__device__ __forceinline__ void bcast_add(double& acc, double v, double one) {
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(v), "v"(one), "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void bcast_add_row(double& acc, double v, double one, int left) {
+    if constexpr (N < 16) {
+        if (N < left) {
+            bcast_add<N>(acc, v, one);
+            bcast_add_row<N + 1>(acc, v, one, left);
+        }
+    }
+}
+template <bool SQ>
+__device__ __forceinline__ void seq_sum_rows(const double* s_x, int cnt, double m, double& acc) {
+    constexpr int kW = 4;                                  // rows of 16 elements per window
+    const int n16 = threadIdx.x & 15;
+    const double one = 1.0;
+    double cur[kW], nxt[kW];
+#pragma unroll
+    for (int w = 0; w < kW; ++w) cur[w] = (16 * w + n16 < cnt) ? s_x[16 * w + n16] : 0.0;
+    for (int base = 0; base < cnt; base += 16 * kW) {
+#pragma unroll
+        for (int w = 0; w < kW; ++w) {
+            const int i = base + 16 * (kW + w) + n16;
+            nxt[w] = (i < cnt) ? s_x[i] : 0.0;
+        }
+        double v[kW];
+#pragma unroll
+        for (int w = 0; w < kW; ++w) {
+            if constexpr (SQ) { const double d = cur[w] - m; v[w] = d * d; } else { v[w] = cur[w]; }
+        }
+        // the DPP sources above were written by VALU ops: two wait states before the first broadcast read
+        asm volatile("s_nop 1" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+#pragma unroll
+        for (int w = 0; w < kW; ++w) bcast_add_row<0>(acc, v[w], one, cnt - (base + 16 * w));
+#pragma unroll
+        for (int w = 0; w < kW; ++w) cur[w] = nxt[w];
+    }
+}
 __global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, int n2) {
     DevState* st = P.st;
     if (st->done) return;
@@ -129,16 +176,24 @@ __global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, i
             __syncthreads();
         }
     }
-    if (tid != 0) return;
-    int cnt = 0;
-    double sum = 0.0;
-    while (cnt < n && s_r[cnt] != __builtin_inf()) sum += s_r[cnt++];
+    // cnt = the first +inf (the unaccepted points sort last), found in parallel
+    __shared__ int s_cnt;
+    if (tid == 0) s_cnt = n;
+    __syncthreads();
+    for (int i = tid; i < n; i += kExactScaleThreads)
+        if (s_r[i] == __builtin_inf() && (i == 0 || s_r[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
+    __syncthreads();
+    if (tid >= kWave) return;
+    const int cnt = s_cnt;
     if (cnt == 0) return;                                  // too few correspondences: the PKO launch reports it
+    // std::accumulate in sorted order, then the variance loop, each one sequential chain run by wave 0
+    double sum = 0.0;
+    seq_sum_rows<false>(s_r, cnt, 0.0, sum);
     const double mean = sum / cnt;
     double var = 0.0;
-    for (int i = 0; i < cnt; ++i) var += (s_r[i] - mean) * (s_r[i] - mean);
+    seq_sum_rows<true>(s_r, cnt, mean, var);
     var /= cnt;
-    st->scale = sqrt(var) / 6.0;
+    if (tid == 0) st->scale = sqrt(var) / 6.0;
 }
 
 // ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =
@@ -213,25 +268,55 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
 
 // ---- the running fp32 sums over the correspondences in scan order (one lane per H / g / cost entry), then the
 // reference's solve and right-update, convergence test and the iteration's log ----
-__global__ __launch_bounds__(kWave) void k_exact_solve(KParams P, int it) {
+// The 43 sums run in point order, one lane each (wave 0), over the term rows staged through LDS: the other waves
+// copy chunk c + 1 (contiguous in the row-major term buffer, so coalesced) while wave 0 sums chunk c, so the
+// sequential adds wait on LDS rather than on a global round trip per row (one lane loading its column from global
+// memory, 8 rows in flight, took ~140 us at KITTI size).
+constexpr int kExactSolveThreads = 512;
+constexpr int kExactRows = 160;                                // rows per chunk; 2 chunks x 27.5 KB of LDS
+constexpr int kExactChunk = kExactRows * kExactTerms;
+constexpr int kExactPer = (kExactChunk + kExactSolveThreads - kWave - 1) / (kExactSolveThreads - kWave);
+__global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, int it) {
     DevState* st = P.st;
     if (st->done) return;
     __shared__ float tot[kExactTerms];
-    const int lane = threadIdx.x, n = scan_n(P);
-    if (lane < kExactTerms) {
-        const float* col = P.ex_terms + lane;
-        float s = 0.0f;
-        int i = 0;
-        for (; i + 8 <= n; i += 8) {                         // 8 loads in flight, the adds in point order
-            float v[8];
+    __shared__ float buf[2][kExactChunk];
+    const int tid = threadIdx.x, lane = tid, n = scan_n(P);
+    const int n_chunks = (n + kExactRows - 1) / kExactRows;
+    const size_t total = static_cast<size_t>(n) * kExactTerms;
+    for (int k = tid; k < kExactChunk && k < static_cast<int>(total); k += kExactSolveThreads) buf[0][k] = P.ex_terms[k];
+    __syncthreads();
+    float s = 0.0f;
+    for (int c = 0; c < n_chunks; ++c) {
+        if (tid >= kWave) {                                    // copy chunk c + 1 into the other buffer
+            const size_t base = static_cast<size_t>(c + 1) * kExactChunk;
+            float v[kExactPer];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = col[static_cast<size_t>(i + u) * kExactTerms];
+            for (int u = 0; u < kExactPer; ++u) {
+                const int k = (tid - kWave) + u * (kExactSolveThreads - kWave);
+                v[u] = (k < kExactChunk && base + k < total) ? P.ex_terms[base + k] : 0.0f;
+            }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s += v[u];
+            for (int u = 0; u < kExactPer; ++u) {
+                const int k = (tid - kWave) + u * (kExactSolveThreads - kWave);
+                if (k < kExactChunk) buf[(c + 1) & 1][k] = v[u];
+            }
+        } else if (lane < kExactTerms) {                       // the adds, in point order
+            const float* rows = buf[c & 1] + lane;
+            const int m = min(kExactRows, n - c * kExactRows);
+            int r = 0;
+            for (; r + 16 <= m; r += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = rows[(r + u) * kExactTerms];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s += v[u];
+            }
+            for (; r < m; ++r) s += rows[r * kExactTerms];
         }
-        for (; i < n; ++i) s += col[static_cast<size_t>(i) * kExactTerms];
-        tot[lane] = s;
+        __syncthreads();
     }
+    if (lane < kExactTerms) tot[lane] = s;
     __syncthreads();
     if (lane != 0) return;
     float Hf[36], mg[6], delta[6];

@@ -1013,7 +1013,7 @@ static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P
     if (it == 0) hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
-    hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(kWave), 0, c->stream, P, it);
+    hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
 }
 
 static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12], const int* n_dev = nullptr) {
@@ -1133,7 +1133,15 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     c->pending = false;
     const DevState* hs = c->h_st;
     int status = c->last_n == 0 ? LO_INSUFFICIENT : hs->status;
-    if (status == LO_ERR_HIP) c->err = "scan pipeline: the wait for the scan's final result timed out";
+    if (status == LO_ERR_HIP && c->pipe) {
+        // the two streams did not run concurrently (e.g. rocprofv3 counter collection serialises dispatches): this
+        // scan reports the error, and the context falls back to the single-stream GN loop from the next scan on
+        c->err = "scan pipeline: the wait for the scan's final result timed out (pipeline now off for this context)";
+        c->pipe = false;
+        if (c->s_tail) (void)hipStreamSynchronize(c->s_tail);
+        std::fprintf(stderr, "liblo_icp: scan pipeline wait timed out (streams serialised?); pipeline disabled for "
+                             "this context (LO_PIPE=0 selects that up front)\n");
+    }
     const int iters = hs->iter;
     if (T_out) {
         if (status == LO_OK) std::memcpy(T_out, hs->pose, sizeof(float) * 12);

@@ -21,8 +21,8 @@ all=(
   "stats_e2e:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_e2e -o run --output-format csv -- python bench.py --config kitti_e2e --steps 240 --no-cpu-baseline --pmc off"
   "stats_loop:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_loop -o run --output-format csv -- python bench.py --config kitti_loop --steps 100 --warmup 12 --no-cpu-baseline --pmc off"
   "stats_1m:600:rocprofv3 --kernel-trace --stats -d gpurun_out/stats_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
-  "pmcf_kitti:600:rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
-  "pmcw_kitti:600:rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
+  "pmcf_kitti:600:LO_PIPE=0 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
+  "pmcw_kitti:600:LO_PIPE=0 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_kitti -o run --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --pmc off"
   "pmcf_1m:600:rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
   "pmcw_1m:600:rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_1m -o run --output-format csv -- python bench.py --config patch1m --steps 20 --warmup 2 --no-cpu-baseline --pmc off"
 )
