@@ -151,7 +151,8 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * in scan order, the iteration-0 scale from the sorted residuals, the fp32 LDLT and SO3 re-projection through
  * JacobiSVD -- the reference's own operation order (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99),
  * so the per-iteration logs equal the oracle restatement's bit for bit.  Slower (a sequential sum and two fp32 SVDs per
- * GN iteration); scans of at most 16384 points (LO_ERR_CAPACITY beyond). */
+ * GN iteration); up to 16384 points the iteration-0 residuals are sorted in one workgroup's LDS, larger scans (up to
+ * max_points) sort them with hipCUB's radix sort in device memory. */
 int lo_set_exact(lo_ctx* ctx, int enable);
 /* Scan pipeline (default on; LO_PIPE=0 in the environment turns it off at lo_create).  The reference's optimize
  * runs GN iterations until convergence (IterativeClosestPointOptimizer.cpp:281-449); the device loop enqueues all

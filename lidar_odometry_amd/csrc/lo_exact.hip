@@ -196,6 +196,75 @@ __global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, i
     if (tid == 0) st->scale = sqrt(var) / 6.0;
 }
 
+// ---- iteration 0 for scans beyond the one-workgroup sort (kExactMaxPoints < n): k_exact_resid writes every point's
+// residual (+inf without a correspondence) to global memory, the context sorts them ascending (hipCUB radix sort:
+// the same order as std::sort for the non-NaN values; -0 / +0 ties do not change any sum), and k_exact_scale_g
+// finds the first +inf and runs the two sequential sums over the sorted residuals, staged through LDS by the
+// copy waves as in k_exact_solve ----
+__global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) {
+    DevState* st = P.st;
+    const int i = blockIdx.x * kBlock + threadIdx.x, n = scan_n(P);
+    if (i >= P.n) return;
+    double v = __builtin_inf();                                // also past a device-counted scan's end (sorted last)
+    const int s = i < n ? P.slot[i] : -1;
+    if (s >= 0 && P.kd_res) {
+        v = P.kd_res[i];
+    } else if (s >= 0) {
+        float T[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+        float wx, wy, wz;
+        transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], wx, wy, wz);
+        v = residual_f64(P.tab[s], wx, wy, wz);
+    }
+    out[i] = v;
+}
+
+constexpr int kScaleGThreads = 1024;
+constexpr int kScaleGChunk = 4096;                             // doubles per staged chunk (2 x 32 KB of LDS)
+template <bool SQ>
+__device__ __forceinline__ void staged_seq_sum(const double* __restrict__ x, int cnt, double m, double& acc,
+                                               double (*buf)[kScaleGChunk]) {
+    const int tid = threadIdx.x;
+    const int n_chunks = (cnt + kScaleGChunk - 1) / kScaleGChunk;
+    for (int k = tid; k < kScaleGChunk && k < cnt; k += kScaleGThreads) buf[0][k] = x[k];
+    __syncthreads();
+    for (int c = 0; c < n_chunks; ++c) {
+        if (tid >= kWave) {                                    // copy chunk c + 1
+            const int base = (c + 1) * kScaleGChunk;
+            for (int k = tid - kWave; k < kScaleGChunk && base + k < cnt; k += kScaleGThreads - kWave)
+                buf[(c + 1) & 1][k] = x[base + k];
+        } else {
+            seq_sum_rows<SQ>(buf[c & 1], min(kScaleGChunk, cnt - c * kScaleGChunk), m, acc);
+        }
+        __syncthreads();
+    }
+}
+__global__ __launch_bounds__(kScaleGThreads) void k_exact_scale_g(KParams P, const double* __restrict__ sorted) {
+    DevState* st = P.st;
+    if (st->done) return;
+    __shared__ double buf[2][kScaleGChunk];
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x, n = scan_n(P);
+    if (tid == 0) s_cnt = n;
+    __syncthreads();
+    for (int i = tid; i < n; i += kScaleGThreads)
+        if (sorted[i] == __builtin_inf() && (i == 0 || sorted[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
+    __syncthreads();
+    const int cnt = s_cnt;
+    if (cnt == 0) return;                                      // too few correspondences: the PKO launch reports it
+    double sum = 0.0;
+    staged_seq_sum<false>(sorted, cnt, 0.0, sum, buf);
+    // wave 0 holds the sum; the mean goes to every wave through LDS (the other waves keep copying)
+    __shared__ double s_mean;
+    if (tid == 0) s_mean = sum / cnt;
+    __syncthreads();
+    const double mean = s_mean;
+    double var = 0.0;
+    staged_seq_sum<true>(sorted, cnt, mean, var, buf);
+    if (tid == 0) st->scale = sqrt(var / cnt) / 6.0;
+}
+
 // ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =
 // J[col] * (w J[row]) (all 36), g[j] = (w r) J[j], cost = (w r) r; zeros for points without a correspondence
 // (adding +0 to the running sums leaves them unchanged) ----

@@ -4,6 +4,7 @@
 // and the DevState that carries the Gauss-Newton loop.  lo_icp_optimize enqueues the whole loop
 // (4 kernels x max_iterations) with no host synchronisation in between; the kernels read
 // DevState::done and fall through once the scan has converged or failed.
+#include <hipcub/hipcub.hpp>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -63,6 +64,8 @@ struct FitOut;
 __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
                              FitOut* out);
 __global__ void k_exact_scale(KParams P, int n2);
+__global__ void k_exact_resid(KParams P, double* out);
+__global__ void k_exact_scale_g(KParams P, const double* sorted);
 __global__ void k_exact_terms(KParams P);
 __global__ void k_exact_solve(KParams P, int it);
 }  // namespace lo
@@ -109,6 +112,11 @@ struct lo_ctx {
     bool presolve = true;           //   candidates solve inside the PKO launch (LO_PRESOLVE=0: k_solve_* instead)
     bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
     float* d_ex_terms = nullptr;
+    size_t ex_cap = 0;              //   rows of d_ex_terms
+    double* d_ex_res = nullptr;     //   scans beyond kExactMaxPoints: residuals, sorted residuals, hipCUB scratch
+    double* d_ex_sorted = nullptr;
+    void* d_ex_sort_tmp = nullptr;
+    size_t ex_res_cap = 0, ex_sort_tmp_bytes = 0;
     double* d_js = nullptr;
     double* d_res = nullptr;        // parity entry points (per-point residual / direct residual input)
     size_t res_cap = 0;
@@ -524,6 +532,7 @@ void lo_destroy(lo_ctx* c) {
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_ex_terms, c->d_res_pko,
+                    c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp,
                     c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
@@ -982,7 +991,7 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
 }
 
 static constexpr int kStageEvents = 1024;
-static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: sort / term buffer capacity
+static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: one-workgroup sort in LDS up to here
 
 // A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
 // (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
@@ -994,23 +1003,54 @@ static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
 }
 
 // Reference-exact mode (lo_exact.hip): device buffers on first use, then per GN iteration the correspondence stage,
-// (iteration 0) the sorted-order scale, the PKO, the per-point terms and the sequential sums + fp32 solve.
+// (iteration 0) the sorted-order scale, the PKO, the per-point terms and the sequential sums + fp32 solve.  Scans of
+// at most kExactMaxPoints sort in one workgroup's LDS (*n2 = the power of two it sorts); larger scans (*n2 = 0)
+// write their residuals out, sort them with hipCUB's radix sort and sum from global memory (k_exact_scale_g).
 static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
-    if (n > static_cast<size_t>(kExactMaxPoints)) { c->err = "exact mode: at most 16384 points"; return LO_ERR_CAPACITY; }
-    if (!c->d_ex_terms) {
-        LO_HIP(c, hipMalloc(&c->d_ex_terms, static_cast<size_t>(kExactMaxPoints) * 43 * sizeof(float)));
+    if (!c->d_ex_terms || c->ex_cap < std::max(n, static_cast<size_t>(kExactMaxPoints))) {
+        if (c->d_ex_terms) LO_HIP(c, hipFree(c->d_ex_terms));
+        c->d_ex_terms = nullptr;
+        c->ex_cap = std::max(n, static_cast<size_t>(kExactMaxPoints));
+        LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * 43 * sizeof(float)));
         LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kExactMaxPoints * 8));
     }
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
+    if (n > static_cast<size_t>(kExactMaxPoints)) {
+        if (c->ex_res_cap < n) {
+            if (c->d_ex_res) LO_HIP(c, hipFree(c->d_ex_res));
+            if (c->d_ex_sorted) LO_HIP(c, hipFree(c->d_ex_sorted));
+            if (c->d_ex_sort_tmp) LO_HIP(c, hipFree(c->d_ex_sort_tmp));
+            c->d_ex_res = c->d_ex_sorted = nullptr;
+            c->d_ex_sort_tmp = nullptr;
+            c->ex_res_cap = n;
+            LO_HIP(c, hipMalloc(&c->d_ex_res, n * sizeof(double)));
+            LO_HIP(c, hipMalloc(&c->d_ex_sorted, n * sizeof(double)));
+            size_t tmp = 0;
+            LO_HIP(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, c->d_ex_res, c->d_ex_sorted, static_cast<int>(n)));
+            c->ex_sort_tmp_bytes = tmp;
+            LO_HIP(c, hipMalloc(&c->d_ex_sort_tmp, tmp));
+        }
+        *n2 = 0;
+        return LO_OK;
+    }
     *n2 = 1;
     while (*n2 < static_cast<int>(n)) *n2 <<= 1;
     return LO_OK;
 }
 static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P0, int it, int n2, bool kd) {
     launch_correspond(c, it == 0 ? P0 : P, 0, kd);
-    if (it == 0) hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
+    if (it == 0 && n2 > 0) {
+        hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
+    } else if (it == 0) {
+        const int n = P.n;                                   // the bound (a device-filtered scan counts on the device)
+        hipLaunchKernelGGL(k_exact_resid, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, P, c->d_ex_res);
+        size_t tmp = c->ex_sort_tmp_bytes;
+        (void)hipcub::DeviceRadixSort::SortKeys(c->d_ex_sort_tmp, tmp, c->d_ex_res, c->d_ex_sorted, n, 0,
+                                                static_cast<int>(sizeof(double) * 8), c->stream);
+        hipLaunchKernelGGL(k_exact_scale_g, dim3(1), dim3(1024), 0, c->stream, P, c->d_ex_sorted);
+    }
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
     hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads

@@ -120,5 +120,16 @@ def test_exact_insufficient_and_capacity(exact):
     exact.set_surfels(k, n, c)
     ok, To = exact.optimize(None, pts + np.float32(5000.0), Ti)
     assert not ok
-    with pytest.raises(RuntimeError):
-        exact.optimize(None, np.zeros((20000, 3), np.float32), Ti)
+    # beyond the one-workgroup sort (16384 points) the scan takes the hipCUB-sort path instead of failing
+    _bitwise(exact, m, np.zeros((20000, 3), np.float32), Ti)
+
+
+@pytest.mark.parametrize("n_points", [40_000])
+def test_exact_large_scan_bitwise(exact, n_points):
+    """C5-style planar-patch scan beyond kExactMaxPoints: residuals sorted by hipCUB's radix sort, the sorted-order
+    mean / variance and the 43 term sums staged through LDS -- still every iteration bit-identical to the oracle."""
+    m, pts, Ti, _ = _data.patch_case(n_points=n_points)
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    st = _bitwise(exact, m, pts, Ti)
+    assert st.num_iterations >= 1
