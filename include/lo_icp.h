@@ -35,6 +35,7 @@ extern "C" {
 #define LO_ERR_HIP        -2
 #define LO_ERR_CAPACITY   -3
 #define LO_ERR_STATE      -4
+#define LO_ERR_PIPELINE   -5   /* device-side status only: a scan-pipeline wait timed out (lo_pipeline_status) */
 
 #define LO_MAX_ITERS      64
 
@@ -163,6 +164,11 @@ int lo_set_exact(lo_ctx* ctx, int enable);
  * the context stream after an optimize sees its final result; lo_sync drains both streams.  main_iterations 0 keeps
  * the current split. */
 int lo_set_pipeline(lo_ctx* ctx, int enable, int main_iterations);
+/* Scan-pipeline state: out[0] enabled, out[1] main iterations, out[2] timeouts (a device-side wait gave up -- the two
+ * streams were not run concurrently -- and the pipeline was switched off), out[3] synchronous scans re-run on one
+ * stream after a timeout.  A scan whose wait timed out reports LO_ERR_PIPELINE in its device status (the exported
+ * record of an async scan); lo_icp_result re-runs it on one stream instead of returning that status. */
+int lo_pipeline_status(lo_ctx* ctx, int out[4]);
 /* In-step timing: with enable, each optimize brackets its FIRST correspondence launch (k_correspond, or the KDTree
  * k_knn + k_knn_brute + k_plane) with HIP events on the context stream (up to 1024 scans; enabling resets them).
  * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */
@@ -276,6 +282,11 @@ int lo_build_normal_equations(lo_ctx* ctx, const float* pts_xyz, size_t n, const
 /* PKO sampling: first min(gmm_sample_size, n) entries of std::shuffle(iota(n), mt19937(42))
  * as the device tables reproduce them (AdaptiveMEstimator.cpp:319-328). Host-side. */
 int lo_pko_sample_indices(lo_ctx* ctx, size_t n, int32_t* out);
+/* Parity entry point of the reference-exact scale (IterativeClosestPointOptimizer.cpp:304-316: std::sort, then
+ * std::accumulate): s = 0; s += x[i] in index order (after an ascending sort when sort != 0), one fp64 rounding per
+ * addition, for n <= 16384 non-negative doubles -- computed by the device kernel the exact mode uses (lo_seqsum.h).
+ * stats (nullable): segment heads (-1: the plain chain ran), fallback segments, fallback terms, device cycles. */
+int lo_seq_sum_f64(lo_ctx* ctx, const double* x, size_t n, int sort, double* out_sum, long long stats[4]);
 /* Diagnostic: 16 device counters (phase timestamps of the -DLO_PKO_STAMPS build; zeros otherwise). */
 int lo_debug_counters(lo_ctx* ctx, unsigned long long out[16]);
 /* Context-free host variant (no GPU needed): sample_size = gmm_sample_size. */

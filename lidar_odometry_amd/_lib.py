@@ -20,6 +20,7 @@ LO_ERR_ARG = -1
 LO_ERR_HIP = -2
 LO_ERR_CAPACITY = -3
 LO_ERR_STATE = -4
+LO_ERR_PIPELINE = -5
 LO_MAX_ITERS = 64
 
 # Every symbol include/lo_icp.h declares (checked by tests/test_abi.py).
@@ -28,8 +29,8 @@ EXPORTED_SYMBOLS = (
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
-    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
-    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters",
+    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
+    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters", "lo_seq_sum_f64",
     "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
     "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
     # include/lo_map.h
@@ -212,6 +213,9 @@ def lib():
     L.lo_pko_sample_indices.argtypes = [vp, C.c_size_t, ip]
     L.lo_pko_sample_indices_host.argtypes = [C.c_size_t, C.c_int, ip]
     L.lo_debug_counters.argtypes = [vp, C.POINTER(C.c_ulonglong)]
+    L.lo_pipeline_status.argtypes = [vp, C.POINTER(C.c_int)]
+    L.lo_seq_sum_f64.argtypes = [vp, C.POINTER(C.c_double), C.c_size_t, C.c_int, C.POINTER(C.c_double),
+                                 C.POINTER(C.c_longlong)]
     L.lo_batch_create.restype = vp
     L.lo_batch_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(C.c_int)]
     L.lo_batch_destroy.restype = None

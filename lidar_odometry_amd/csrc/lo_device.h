@@ -38,6 +38,13 @@ constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP ro
 constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
 constexpr int kCandWords = 48;      // a candidate's solved GN step: pose[12] | cost | H[21] | g[6] | delta[6] | conv | pad
 constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv = 46;
+// reference-exact candidates (lo_pko_body.h acc_candidate_exact): staged factor rows in the PKO launch's dynamic LDS
+constexpr int kXcPPL = 2;                                  // points per producer lane per chunk
+constexpr int kXcRegions = 3 * kXcPPL;                     // 64-point regions per chunk (3 producer waves)
+constexpr int kXcChunk = kXcRegions * kWave;              // 384 points
+constexpr int kXcStride = 15;                              // floats per staged row: 14 factors + 1 (odd: no bank conflicts)
+constexpr int kXcBuf = kXcChunk * kXcStride;
+constexpr size_t kXcLdsBytes = (2 * kXcBuf + 2 * kXcRegions + 43 + kCandWords) * sizeof(float);
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;
@@ -136,10 +143,13 @@ struct KParams {
                               //   k_solve_correspond), read back by the PKO sample instead of recomputing it
     float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
+    int exact_cand;           // 1: the PKO launch's candidates form the reference's sequential fp32 sums and solve
+                              //   (reference-exact mode, acc_candidate_exact; one workgroup per candidate)
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
     unsigned long long* em_stat;  // nullable (stage timing on): DevState::em_stat, the lead PKO workgroup's EM timing
     DevState* st;
     uint32_t* fin;            // nullable (scan pipeline, lo_set_pipeline): the context's "last final scan" word
+                              //   (fin[1] main part done, fin[2] signal_main's block count, fin[3] pipeline broken)
     uint32_t seq;             //   and this scan's sequence number, published there once its result is final
     int hold;                 // 1: the main part's last pick (signal_main: fin[1] = seq once its correspondences are out;
                               //   fin[2] counts its blocks in)
@@ -152,21 +162,25 @@ struct KParams {
 // an sc1 store; k_wait_final (and k_wait_seq) poll that word (MI355X_MICROARCH.md "inter-workgroup
 // visibility": release, then the explicit vmcnt wait, then the relaxed agent-scope flag store).
 // Scan pipeline: poll a flag word until it reaches seq (one lane, sc1 loads: fresh across XCDs; the word is the only
-// thing read), bounded by 2 s of the 100 MHz constant clock -- false on timeout, so no wait can hang a queue.
-__device__ __forceinline__ bool wait_word(const uint32_t* w, uint32_t seq) {
+// thing read), bounded by `bound` ticks of the 100 MHz constant clock -- false on timeout, so no wait can hang a queue.
+// A wait also gives up at once when the pipeline is broken (fin[3] != 0: an earlier wait timed out).
+__device__ __forceinline__ bool wait_word(const uint32_t* w, uint32_t seq, const uint32_t* broken, unsigned long long bound) {
     const unsigned long long t0 = wall_clock64();
     while (static_cast<int32_t>(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
-        if (wall_clock64() - t0 > 200000000ull) return false;
+        if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+        if (wall_clock64() - t0 > bound) return false;
         __builtin_amdgcn_s_sleep(1);
     }
     return true;
 }
 // ... until either of two words reaches seq
-__device__ __forceinline__ bool wait_word2(const uint32_t* a, const uint32_t* b, uint32_t seq) {
+__device__ __forceinline__ bool wait_word2(const uint32_t* a, const uint32_t* b, uint32_t seq, const uint32_t* broken,
+                                           unsigned long long bound) {
     const unsigned long long t0 = wall_clock64();
     while (static_cast<int32_t>(__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0 &&
            static_cast<int32_t>(__hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
-        if (wall_clock64() - t0 > 200000000ull) return false;
+        if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+        if (wall_clock64() - t0 > bound) return false;
         __builtin_amdgcn_s_sleep(1);
     }
     return true;
@@ -176,6 +190,12 @@ __device__ __forceinline__ bool wait_word2(const uint32_t* a, const uint32_t* b,
 __device__ __forceinline__ bool fin_reached(const KParams& P) {
     return static_cast<int32_t>(__hip_atomic_load(P.fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - P.seq) >= 0;
 }
+// ... and the sticky "pipeline broken" word: once a wait has timed out, the two streams are no longer ordered against
+// each other, so no tail launch may touch the context's buffers (they may already belong to a later scan).
+__device__ __forceinline__ bool pipe_broken(const KParams& P) {
+    return __hip_atomic_load(P.fin + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+__device__ __forceinline__ bool tail_gone(const KParams& P) { return P.tail && (fin_reached(P) || pipe_broken(P)); }
 __device__ __forceinline__ void publish_final(const KParams& P) {
     if (!P.fin) return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -13,185 +13,79 @@
 
 #include "lo_device.h"
 #include "lo_math.h"
+#include "lo_seqsum.h"
+#include "lo_exact.h"
 
 namespace lo {
 
-constexpr int kExactTerms = 43;        // H (36, full: the reference's H is not symmetrised), g (6), cost
-
-// ---- the reference's fp32 solve and pose update (restated exactly as the oracle states them) ----
-// LDLT<Matrix<float,6,6>> (Eigen ldlt_inplace<Lower>::unblocked with diagonal pivoting + LDLT::_solve_impl)
-__device__ inline void ldlt6_solve_f32(const float (&Hin)[36], const float (&b)[6], float (&x)[6]) {
-    float m[6][6];
-    for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) m[r][c] = Hin[r * 6 + c];
-    int transp[6];
-    float temp[6];
-    bool zero_all = false;
-    for (int k = 0; k < 6; ++k) {
-        int big = k;
-        float bv = fabsf(m[k][k]);
-        for (int i = k + 1; i < 6; ++i) if (fabsf(m[i][i]) > bv) { bv = fabsf(m[i][i]); big = i; }
-        transp[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; ++j) { const float t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
-            for (int i = big + 1; i < 6; ++i) { const float t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
-            { const float t = m[k][k]; m[k][k] = m[big][big]; m[big][big] = t; }
-            for (int i = k + 1; i < big; ++i) { const float t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
-        }
-        if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
-            float acc = 0.0f;
-            for (int j = 0; j < k; ++j) acc += m[k][j] * temp[j];
-            m[k][k] -= acc;
-            for (int i = k + 1; i < 6; ++i) {
-                float a = 0.0f;
-                for (int j = 0; j < k; ++j) a += m[i][j] * temp[j];
-                m[i][k] -= a;
-            }
-        }
-        const float akk = m[k][k];
-        const bool valid = fabsf(akk) > 0.0f;
-        if (k == 0 && !valid) { zero_all = true; break; }
-        if (k < 5 && valid) for (int i = k + 1; i < 6; ++i) m[i][k] /= akk;
-    }
-    if (zero_all) { for (int i = 0; i < 6; ++i) x[i] = 0.0f; return; }
-    float d[6];
-    for (int i = 0; i < 6; ++i) d[i] = b[i];
-    for (int k = 0; k < 6; ++k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
-    for (int i = 0; i < 6; ++i) { float a = 0.0f; for (int j = 0; j < i; ++j) a += m[i][j] * d[j]; d[i] -= a; }
-    for (int i = 0; i < 6; ++i) d[i] = (fabsf(m[i][i]) > FLT_MIN) ? d[i] / m[i][i] : 0.0f;
-    for (int i = 5; i >= 0; --i) { float a = 0.0f; for (int j = i + 1; j < 6; ++j) a += m[j][i] * d[j]; d[i] -= a; }
-    for (int k = 5; k >= 0; --k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
-    for (int i = 0; i < 6; ++i) x[i] = d[i];
-}
-
-__device__ inline float norm3e(const float* v) { return sqrtf(dot3e(v[0], v[1], v[2], v[0], v[1], v[2])); }
-
-// SO3::Exp (MathUtils.cpp:23-39, kEps 1e-6f) with the SO3(Matrix3f) re-projection of its result; sin / cos are
-// evaluated in fp64 and rounded (the correctly rounded fp32 value; glibc's sinf agrees with it for 99.6 % of the
-// floats in [1e-7, 0.8], cosf for 99.99 %)
-__device__ inline void so3_exp_exact(const float w[3], float R[3][3]) {
-    const float theta = norm3e(w);
-    float M[3][3];
-    if (theta < 1e-6f) {
-        const float H[3][3] = {{0.0f, -w[2], w[1]}, {w[2], 0.0f, -w[0]}, {-w[1], w[0], 0.0f}};
-        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) M[r][c] = (r == c ? 1.0f : 0.0f) + H[r][c];
-    } else {
-        const float ti = 1.0f / theta;
-        const float k[3] = {w[0] * ti, w[1] * ti, w[2] * ti};
-        const float K[3][3] = {{0.0f, -k[2], k[1]}, {k[2], 0.0f, -k[0]}, {-k[1], k[0], 0.0f}};
-        const float s = static_cast<float>(sin(static_cast<double>(theta)));
-        const float omc = 1.0f - static_cast<float>(cos(static_cast<double>(theta)));
-        float sK[3][3], KK[3][3];
-        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) sK[r][c] = omc * K[r][c];
-        mul33e(sK, K, KK);
-        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) M[r][c] = ((r == c ? 1.0f : 0.0f) + s * K[r][c]) + KK[r][c];
-    }
-    so3_project_svd(M, R);
-}
+// Diagnostic build only (-DLO_EXACT_STAMPS, `make diag`): thread 0 of the scale kernel stores s_memtime at its phase
+// boundaries into DevState::dbg (lo_debug_counters); the product kernel executes no stamp.
+#ifdef LO_EXACT_STAMPS
+#define LO_XSTAMP(st, i) do { if (threadIdx.x == 0) (st)->dbg[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define LO_XSTAMP(st, i) do { } while (0)
+#endif
 
 // ---- iteration 0: scale = sqrt(var) / 6 of the residuals sorted ascending, mean and variance summed in that order
-// (IterativeClosestPointOptimizer.cpp:304-316).  One workgroup: the residuals of the accepted points (+inf for the
-// rest) in dynamic LDS, bitonic sort, then one lane accumulates as std::accumulate does ----
-constexpr int kExactScaleThreads = 1024;
+// (IterativeClosestPointOptimizer.cpp:304-316).  One workgroup: the accepted residuals (+inf for the rest) sorted in
+// registers / LDS (bitonic, lo_seqsum.h), then both sequential sums reproduced by mono_seq_sum (integer prefix sums
+// between binade changes, a short walk over the segment heads) -- the same bits as std::accumulate's chain ----
 
-// acc += v_0 + v_1 + ... + v_{cnt-1}, one rounding per element in index order (v_k = x_k, or (x_k - m)^2 with SQ), as
-// one wave-uniform chain: each 16-lane row holds 16 consecutive elements in a register and v_fmac_f64_dpp with a
-// row_newbcast source adds element 16c + N as acc = fma(v, 1.0, acc), which rounds exactly as acc + v -- no LDS
-// round trip between the adds (one lane reading LDS per element was ~25x slower).  Wave 0 only; elements past cnt
-// are never broadcast (the row guard) and never read.
-template <int N>
-__device__ __forceinline__ void bcast_add(double& acc, double v, double one) {
-    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-                 : "+v"(acc) : "v"(v), "v"(one), "i"(N));
-}
-template <int N>
-__device__ __forceinline__ void bcast_add_row(double& acc, double v, double one, int left) {
-    if constexpr (N < 16) {
-        if (N < left) {
-            bcast_add<N>(acc, v, one);
-            bcast_add_row<N + 1>(acc, v, one, left);
-        }
-    }
-}
-template <bool SQ>
-__device__ __forceinline__ void seq_sum_rows(const double* s_x, int cnt, double m, double& acc) {
-    constexpr int kW = 4;                                  // rows of 16 elements per window
-    const int n16 = threadIdx.x & 15;
-    const double one = 1.0;
-    double cur[kW], nxt[kW];
-#pragma unroll
-    for (int w = 0; w < kW; ++w) cur[w] = (16 * w + n16 < cnt) ? s_x[16 * w + n16] : 0.0;
-    for (int base = 0; base < cnt; base += 16 * kW) {
-#pragma unroll
-        for (int w = 0; w < kW; ++w) {
-            const int i = base + 16 * (kW + w) + n16;
-            nxt[w] = (i < cnt) ? s_x[i] : 0.0;
-        }
-        double v[kW];
-#pragma unroll
-        for (int w = 0; w < kW; ++w) {
-            if constexpr (SQ) { const double d = cur[w] - m; v[w] = d * d; } else { v[w] = cur[w]; }
-        }
-        // the DPP sources above were written by VALU ops: two wait states before the first broadcast read
-        asm volatile("s_nop 1" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-#pragma unroll
-        for (int w = 0; w < kW; ++w) bcast_add_row<0>(acc, v[w], one, cnt - (base + 16 * w));
-#pragma unroll
-        for (int w = 0; w < kW; ++w) cur[w] = nxt[w];
-    }
-}
-__global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, int n2) {
+template <int PT>
+__global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P) {
     DevState* st = P.st;
     if (st->done) return;
-    extern __shared__ double s_r[];
-    const int tid = threadIdx.x, n = scan_n(P);
-    float T[12];
+    extern __shared__ double s_x[];                          // kSeqThreads * PT doubles
+    __shared__ SeqScratch S;
+    LO_XSTAMP(st, 0);
+    const int tid = threadIdx.x, n = scan_n(P), base = tid * PT;
+    double v[PT];
+    int nacc = 0;
+    bool nan = false;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
-    for (int i = tid; i < n2; i += kExactScaleThreads) {
-        double v = __builtin_inf();
-        if (i < n) {
-            const int s = P.slot[i];
-            if (s >= 0 && P.kd_res) {
-                v = P.kd_res[i];                           // KDTree variant: the plane distance it accepted
-            } else if (s >= 0) {
-                float wx, wy, wz;
-                transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], wx, wy, wz);
-                v = residual_f64(P.tab[s], wx, wy, wz);
-            }
+    for (int a = 0; a < PT; ++a) {
+        const int i = base + a;
+        double r = __builtin_inf();
+        if (i < n && P.slot[i] >= 0) {
+            r = P.kd_res ? P.kd_res[i] : P.res_out[i];       // the stored fp64 residual (k_correspond / k_plane)
+            ++nacc;
+            nan = nan || isnan(r);
         }
-        s_r[i] = v;
+        v[a] = r;
     }
-    __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < n2; i += kExactScaleThreads) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const double a = s_r[i], b = s_r[l];
-                    const bool up = (i & k) == 0;
-                    if (up ? (a > b) : (a < b)) { s_r[i] = b; s_r[l] = a; }
-                }
-            }
-            __syncthreads();
+    int cnt;
+    (void)block_excl_scan<int>(nacc, S.wi, cnt);
+    const bool any_nan = __syncthreads_or(nan ? 1 : 0) != 0;
+    if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
+    if (any_nan) {
+        // a NaN residual makes the mean, the variance and the scale NaN in any summation order
+        if (tid == 0) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) if (P.slot[i] >= 0) s = s + (P.kd_res ? P.kd_res[i] : P.res_out[i]);
+            st->scale = sqrt(s) / 6.0;
         }
+        return;
     }
-    // cnt = the first +inf (the unaccepted points sort last), found in parallel
-    __shared__ int s_cnt;
-    if (tid == 0) s_cnt = n;
+    LO_XSTAMP(st, 1);
+    bitonic_sort_block<PT>(v, s_x);
+#pragma unroll
+    for (int a = 0; a < PT; ++a) s_x[base + a] = v[a];
     __syncthreads();
-    for (int i = tid; i < n; i += kExactScaleThreads)
-        if (s_r[i] == __builtin_inf() && (i == 0 || s_r[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
-    __syncthreads();
-    if (tid >= kWave) return;
-    const int cnt = s_cnt;
-    if (cnt == 0) return;                                  // too few correspondences: the PKO launch reports it
-    // std::accumulate in sorted order, then the variance loop, each one sequential chain run by wave 0
-    double sum = 0.0;
-    seq_sum_rows<false>(s_r, cnt, 0.0, sum);
+    LO_XSTAMP(st, 2);
+    double sum;
+    if (!mono_seq_sum<PT>(v, cnt, s_x, S, 0.0, kExpNone, false, 0.0, sum, nullptr)) sum = chain_seq_sum(s_x, cnt, 0.0, S);
+    LO_XSTAMP(st, 3);
     const double mean = sum / cnt;
-    double var = 0.0;
-    seq_sum_rows<true>(s_r, cnt, mean, var);
+    double w[PT];
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        w[a] = (base + a < cnt) ? (v[a] - mean) * (v[a] - mean) : 0.0;
+        s_x[base + a] = w[a];
+    }
+    __syncthreads();
+    double var;
+    if (!mono_seq_sum<PT>(w, cnt, s_x, S, 0.0, kExpNone, false, 0.0, var, nullptr)) var = chain_seq_sum(s_x, cnt, 0.0, S);
+    LO_XSTAMP(st, 4);
     var /= cnt;
     if (tid == 0) st->scale = sqrt(var) / 6.0;
 }
@@ -199,8 +93,8 @@ __global__ __launch_bounds__(kExactScaleThreads) void k_exact_scale(KParams P, i
 // ---- iteration 0 for scans beyond the one-workgroup sort (kExactMaxPoints < n): k_exact_resid writes every point's
 // residual (+inf without a correspondence) to global memory, the context sorts them ascending (hipCUB radix sort:
 // the same order as std::sort for the non-NaN values; -0 / +0 ties do not change any sum), and k_exact_scale_g
-// finds the first +inf and runs the two sequential sums over the sorted residuals, staged through LDS by the
-// copy waves as in k_exact_solve ----
+// runs both sequential sums over the sorted residuals chunk by chunk (mono_seq_sum with the prediction and the running
+// sum carried from chunk to chunk; every chunk starts a segment) ----
 __global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) {
     DevState* st = P.st;
     const int i = blockIdx.x * kBlock + threadIdx.x, n = scan_n(P);
@@ -220,49 +114,135 @@ __global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) 
     out[i] = v;
 }
 
-constexpr int kScaleGThreads = 1024;
-constexpr int kScaleGChunk = 4096;                             // doubles per staged chunk (2 x 32 KB of LDS)
+constexpr int kScaleGPT = 8;
+constexpr int kScaleGChunk = kSeqThreads * kScaleGPT;          // terms per chunk (64 KB of LDS)
 template <bool SQ>
-__device__ __forceinline__ void staged_seq_sum(const double* __restrict__ x, int cnt, double m, double& acc,
-                                               double (*buf)[kScaleGChunk]) {
-    const int tid = threadIdx.x;
-    const int n_chunks = (cnt + kScaleGChunk - 1) / kScaleGChunk;
-    for (int k = tid; k < kScaleGChunk && k < cnt; k += kScaleGThreads) buf[0][k] = x[k];
-    __syncthreads();
-    for (int c = 0; c < n_chunks; ++c) {
-        if (tid >= kWave) {                                    // copy chunk c + 1
-            const int base = (c + 1) * kScaleGChunk;
-            for (int k = tid - kWave; k < kScaleGChunk && base + k < cnt; k += kScaleGThreads - kWave)
-                buf[(c + 1) & 1][k] = x[base + k];
-        } else {
-            seq_sum_rows<SQ>(buf[c & 1], min(kScaleGChunk, cnt - c * kScaleGChunk), m, acc);
+__device__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double m, double* s_x, SeqScratch& S) {
+    const int tid = threadIdx.x, base = tid * kScaleGPT;
+    double s = 0.0, Tc = 0.0;
+    int ec = kExpNone;
+    for (int c0 = 0; c0 < cnt; c0 += kScaleGChunk) {
+        const int mc = min(kScaleGChunk, cnt - c0);
+        for (int k = tid; k < kScaleGChunk; k += kSeqThreads) {
+            double v = 0.0;
+            if (k < mc) {
+                v = x[c0 + k];
+                if constexpr (SQ) v = (v - m) * (v - m);
+            }
+            s_x[k] = v;
         }
         __syncthreads();
+        double xv[kScaleGPT];
+#pragma unroll
+        for (int a = 0; a < kScaleGPT; ++a) xv[a] = s_x[base + a];
+        double Tn;
+        if (mono_seq_sum<kScaleGPT>(xv, mc, s_x, S, Tc, ec, true, s, s, &Tn)) {
+            Tc = Tn;
+            ec = S.e_carry;
+        } else {
+            s = chain_seq_sum(s_x, mc, s, S);
+            Tc = s;
+            ec = binade64(s);
+        }
+        __syncthreads();                                       // s_x / S reuse by the next chunk
     }
+    return s;
 }
-__global__ __launch_bounds__(kScaleGThreads) void k_exact_scale_g(KParams P, const double* __restrict__ sorted) {
+__global__ __launch_bounds__(kSeqThreads) void k_exact_scale_g(KParams P, const double* __restrict__ sorted) {
     DevState* st = P.st;
     if (st->done) return;
-    __shared__ double buf[2][kScaleGChunk];
+    __shared__ double s_x[kScaleGChunk];
+    __shared__ SeqScratch S;
     __shared__ int s_cnt;
     const int tid = threadIdx.x, n = scan_n(P);
     if (tid == 0) s_cnt = n;
     __syncthreads();
-    for (int i = tid; i < n; i += kScaleGThreads)
-        if (sorted[i] == __builtin_inf() && (i == 0 || sorted[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
-    __syncthreads();
+    int nan = 0;
+    for (int i = tid; i < n; i += kSeqThreads) {
+        const double v = sorted[i];
+        if (v == __builtin_inf() && (i == 0 || sorted[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
+        nan |= isnan(v) ? 1 : 0;
+    }
+    const bool any_nan = __syncthreads_or(nan) != 0;
     const int cnt = s_cnt;
     if (cnt == 0) return;                                      // too few correspondences: the PKO launch reports it
-    double sum = 0.0;
-    staged_seq_sum<false>(sorted, cnt, 0.0, sum, buf);
-    // wave 0 holds the sum; the mean goes to every wave through LDS (the other waves keep copying)
-    __shared__ double s_mean;
-    if (tid == 0) s_mean = sum / cnt;
-    __syncthreads();
-    const double mean = s_mean;
-    double var = 0.0;
-    staged_seq_sum<true>(sorted, cnt, mean, var, buf);
+    if (any_nan) {
+        if (tid == 0) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) if (sorted[i] != __builtin_inf()) s = s + sorted[i];
+            st->scale = sqrt(s) / 6.0;
+        }
+        return;
+    }
+    const double sum = chunked_seq_sum<false>(sorted, cnt, 0.0, s_x, S);
+    const double var = chunked_seq_sum<true>(sorted, cnt, sum / cnt, s_x, S);
     if (tid == 0) st->scale = sqrt(var / cnt) / 6.0;
+}
+
+// Parity / diagnostic entry (lo_seq_sum_f64): the sequential sum of n <= kExactMaxPoints non-negative doubles in
+// index order (sorted ascending first with SORT), by the same sort and mono_seq_sum as k_exact_scale.  out[0] = the
+// sum; stats = heads, fallback segments, fallback terms, s_memtime cycles of the sort + sum.
+template <int PT>
+__global__ __launch_bounds__(kSeqThreads) void k_seq_sum_diag(const double* __restrict__ x, int n, int sort, double* out,
+                                                             long long* stats) {
+    extern __shared__ double s_x[];
+    __shared__ SeqScratch S;
+    const int tid = threadIdx.x, base = tid * PT;
+    double v[PT];
+#pragma unroll
+    for (int a = 0; a < PT; ++a) v[a] = (base + a < n) ? x[base + a] : (sort ? __builtin_inf() : 0.0);
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if (sort) bitonic_sort_block<PT>(v, s_x);
+#pragma unroll
+    for (int a = 0; a < PT; ++a) s_x[base + a] = v[a];
+    __syncthreads();
+    double sum;
+    long long heads = -1;                                    // -1: more than kSeqHeadCap heads (the plain chain ran)
+    if (tid == 0) S.fb_seg = S.fb_terms = 0;
+    if (mono_seq_sum<PT>(v, n, s_x, S, 0.0, kExpNone, false, 0.0, sum, nullptr)) heads = S.nheads;
+    else sum = chain_seq_sum(s_x, n, 0.0, S);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (tid == 0) {
+        out[0] = sum;
+        stats[0] = heads;
+        stats[1] = S.fb_seg;
+        stats[2] = S.fb_terms;
+        stats[3] = static_cast<long long>(t1 - t0);
+    }
+}
+template <int PT>
+static void launch_seq_diag_pt(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_seq_sum_diag<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kSeqThreads * PT * 8);
+    hipLaunchKernelGGL(k_seq_sum_diag<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, x, n,
+                       sort, out, stats);
+}
+void launch_seq_sum_diag(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s) {
+    if (n <= kSeqThreads) launch_seq_diag_pt<1>(x, n, sort, out, stats, s);
+    else if (n <= 2 * kSeqThreads) launch_seq_diag_pt<2>(x, n, sort, out, stats, s);
+    else if (n <= 4 * kSeqThreads) launch_seq_diag_pt<4>(x, n, sort, out, stats, s);
+    else if (n <= 8 * kSeqThreads) launch_seq_diag_pt<8>(x, n, sort, out, stats, s);
+    else launch_seq_diag_pt<16>(x, n, sort, out, stats, s);
+}
+
+// Host side: the scale launch for a scan of at most kExactMaxPoints points (PT = its padded size / kSeqThreads).
+template <int PT>
+static void launch_scale_pt(const KParams& P, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale<PT>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kSeqThreads * PT * 8);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_exact_scale<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, P);
+}
+void launch_exact_scale(const KParams& P, int n, hipStream_t s) {
+    if (n <= kSeqThreads) launch_scale_pt<1>(P, s);
+    else if (n <= 2 * kSeqThreads) launch_scale_pt<2>(P, s);
+    else if (n <= 4 * kSeqThreads) launch_scale_pt<4>(P, s);
+    else if (n <= 8 * kSeqThreads) launch_scale_pt<8>(P, s);
+    else launch_scale_pt<16>(P, s);
 }
 
 // ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =
@@ -304,35 +284,13 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
         transform_pt(T, px, py, pz, wx, wy, wz);
         r64 = residual_f64(sl, wx, wy, wz);
     }
-    const float nres = static_cast<float>(r64 / std_max(scale, 1e-6));
-    const float qx = dot3f(T[0], T[1], T[2], px, py, pz) + T[3];
-    const float qy = dot3f(T[4], T[5], T[6], px, py, pz) + T[7];
-    const float qz = dot3f(T[8], T[9], T[10], px, py, pz) + T[11];
-    const float n0 = sl.n[0], n1 = sl.n[1], n2 = sl.n[2];
-    const float res = dot3f(n0, n1, n2, qx - sl.c[0], qy - sl.c[1], qz - sl.c[2]);
-    float J[6];
-    J[0] = dot3f(n0, n1, n2, T[0], T[4], T[8]);
-    J[1] = dot3f(n0, n1, n2, T[1], T[5], T[9]);
-    J[2] = dot3f(n0, n1, n2, T[2], T[6], T[10]);
-    const float a0 = dot3f(-n0, -n1, -n2, T[0], T[4], T[8]);
-    const float a1 = dot3f(-n0, -n1, -n2, T[1], T[5], T[9]);
-    const float a2 = dot3f(-n0, -n1, -n2, T[2], T[6], T[10]);
-    J[3] = dot3f(a0, a1, a2, 0.0f, pz, -py);
-    J[4] = dot3f(a0, a1, a2, -pz, 0.0f, px);
-    J[5] = dot3f(a0, a1, a2, py, -px, 0.0f);
-    float w = 1.0f;
-    if (P.robust) {
-        const float an = fabsf(nres);
-        if (P.cauchy_loss) { const float ratio = an / dl; w = 1.0f / (1.0f + ratio * ratio); }
-        else if (an > dl) w = dl / an;
+    float f[14];
+    exact_point_factors(P, T, scale, dl, r64, px, py, pz, sl, f);
+    for (int k = 0; k < kExactTerms; ++k) {
+        int fa, fb;
+        exact_term_factors(k, fa, fb);
+        out[k] = f[fa] * f[fb];
     }
-    float wJ[6];
-    for (int j = 0; j < 6; ++j) wJ[j] = w * J[j];
-    for (int row = 0; row < 6; ++row)
-        for (int col = 0; col < 6; ++col) out[row * 6 + col] = J[col] * wJ[row];
-    const float wr = w * res;
-    for (int j = 0; j < 6; ++j) out[36 + j] = wr * J[j];
-    out[42] = wr * res;
 }
 
 // ---- the running fp32 sums over the correspondences in scan order (one lane per H / g / cost entry), then the
@@ -388,28 +346,9 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
     if (lane < kExactTerms) tot[lane] = s;
     __syncthreads();
     if (lane != 0) return;
-    float Hf[36], mg[6], delta[6];
-    for (int k = 0; k < 36; ++k) Hf[k] = tot[k];
-    for (int j = 0; j < 6; ++j) mg[j] = -tot[36 + j];
-    ldlt6_solve_f32(Hf, mg, delta);                            // :418
-    const float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
-    float Rd[3][3];
-    if (norm3e(dw) < 1e-10f) {                                 // :427-431
-        const float I[3][3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
-        so3_project_svd(I, Rd);
-    } else {
-        so3_exp_exact(dw, Rd);
-    }
-    float R[3][3], t[3], M[3][3], Rn[3][3];
-    for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) R[r][c] = st->pose[r * 4 + c]; t[r] = st->pose[r * 4 + 3]; }
-    mul33e(R, Rd, M);                                           // SE3::operator* (MathUtils.h:144-147)
-    so3_project_svd(M, Rn);
-    float pn[12];
-    for (int r = 0; r < 3; ++r) {
-        for (int c = 0; c < 3; ++c) pn[r * 4 + c] = Rn[r][c];
-        pn[r * 4 + 3] = t[r] + dot3e(R[r][0], R[r][1], R[r][2], dt[0], dt[1], dt[2]);
-    }
-    const bool conv = norm3e(dt) < P.tol_t && norm3e(dw) < P.tol_r;   // :443-448
+    float tf[kExactTerms], pn[12], delta[6];
+    for (int k = 0; k < kExactTerms; ++k) tf[k] = tot[k];
+    const bool conv = exact_solve_step(tf, st->pose, P.tol_t, P.tol_r, pn, delta);
     for (int q = 0; q < 12; ++q) st->pose[q] = pn[q];
     if (it < LO_MAX_ITERS) {
         lo_iter_log& L = st->logs[it];

@@ -29,6 +29,7 @@
 namespace lo {
 __global__ void k_correspond(KParams P, int with_stats);
 template <int NW> __global__ void k_pko_t(KParams P, int it, int G);
+__global__ void k_pko_tx(KParams P, int it, int G);
 __global__ void k_pko_finish(KParams P);
 __global__ void k_accumulate(KParams P, int it, int fuse);
 __global__ void k_solve(KParams P, int it, int ne_only);
@@ -40,8 +41,8 @@ __global__ void k_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
 __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha);
 __global__ void k_export_pose(const DevState* st, float* out);
-__global__ void k_wait_seq(const uint32_t* fin, uint32_t seq, DevState* st);
-__global__ void k_wait_final(const uint32_t* fin, uint32_t seq, DevState* st);
+__global__ void k_wait_seq(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound);
+__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
 __global__ void k_knn_reset(KParams P);
@@ -63,7 +64,8 @@ struct FitJob {
 struct FitOut;
 __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
                              FitOut* out);
-__global__ void k_exact_scale(KParams P, int n2);
+void launch_exact_scale(const KParams& P, int n, hipStream_t s);
+void launch_seq_sum_diag(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s);
 __global__ void k_exact_resid(KParams P, double* out);
 __global__ void k_exact_scale_g(KParams P, const double* sorted);
 __global__ void k_exact_terms(KParams P);
@@ -190,7 +192,14 @@ struct lo_ctx {
     hipStream_t s_tail = nullptr;
     uint32_t pipe_seq = 0;
     uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done,
-                                    // [2] signal_main's block count
+                                    // [2] signal_main's block count, [3] broken (a wait timed out; sticky)
+    uint32_t* h_broken = nullptr;   // pinned, device-mapped: the seq of the scan whose wait timed out (0: none)
+    uint32_t* d_hbroken = nullptr;
+    unsigned long long pipe_bound = 200000000ull;   // wait bound in 100 MHz ticks (2 s; LO_PIPE_WAIT_MS)
+    unsigned pipe_timeouts = 0;     // times a wait timed out and the pipeline was switched off (lo_pipeline_status)
+    unsigned pipe_reruns = 0;       // synchronous scans re-run on one stream after such a timeout
+    const float* last_pts = nullptr;   // the scan in flight (a re-run after a pipeline timeout)
+    const int* last_ndev = nullptr;
     bool sync_call = false;         // the optimize in flight is a synchronous call: HIP events time it (gpu_ms)
     bool last_timed = false;
 };
@@ -221,10 +230,15 @@ static void launch_pko(lo_ctx* c, const KParams& P, int it) {
 static bool spec_ok(const KParams& P) { return P.use_pko && P.acc_part && P.nb_acc <= kFuseMaxBlocks; }
 
 static void launch_pko_spec(lo_ctx* c, const KParams& P, int it, hipStream_t s = nullptr) {
-    const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
+    size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     const int G = pko_grid(c->cfg);
-    const int W = (P.nb_acc + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
-    hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
+    int W = (P.nb_acc + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
+    if (P.exact_cand) {                                  // one workgroup per exact candidate, factor rows in LDS
+        W = 1;
+        pre_bytes = std::max(pre_bytes, kXcLdsBytes);
+    }
+    if (P.exact_cand) hipLaunchKernelGGL(k_pko_tx, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
+    else hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
 }
 
 // One GN iteration after the correspondence stage: PKO with the speculative normal equations + k_solve_pick
@@ -252,6 +266,9 @@ static int ensure_acc_part(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_cand_rec, cand * kCandWords * sizeof(float)));
     LO_HIP(c, hipMalloc(&c->d_cand_cnt, cand * sizeof(unsigned)));
     LO_HIP(c, hipMemset(c->d_cand_cnt, 0, cand * sizeof(unsigned)));
+    // the exact candidates' staging sits in the PKO launch's dynamic LDS (beyond the 64 KB default with the static part)
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(kXcLdsBytes + 16384)));
     return LO_OK;
 }
 
@@ -259,11 +276,16 @@ static int ensure_acc_part(lo_ctx* c) {
 static int pipe_alloc(lo_ctx* c) {
     if (c->d_fin) return LO_OK;
     LO_HIP(c, hipStreamCreateWithFlags(&c->s_tail, hipStreamNonBlocking));
-    LO_HIP(c, hipMalloc(&c->d_fin, 3 * sizeof(uint32_t)));
-    LO_HIP(c, hipMemset(c->d_fin, 0, 3 * sizeof(uint32_t)));
+    LO_HIP(c, hipMalloc(&c->d_fin, 4 * sizeof(uint32_t)));
+    LO_HIP(c, hipMemset(c->d_fin, 0, 4 * sizeof(uint32_t)));
+    LO_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_broken), sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    *c->h_broken = 0;
+    LO_HIP(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_hbroken), c->h_broken, 0));
     LO_HIP(c, hipDeviceSynchronize());              // zeroed before either stream's first poll
     return LO_OK;
 }
+
 
 // Both streams of the context drained (lo_sync, lo_set_stream, lo_destroy).
 static hipError_t sync_all(lo_ctx* c) {
@@ -271,6 +293,22 @@ static hipError_t sync_all(lo_ctx* c) {
     if (e == hipSuccess && c->s_tail) e = hipStreamSynchronize(c->s_tail);
     return e;
 }
+
+// A pipeline wait timed out (the dispatcher ran the two streams out of submission order): drain both streams, switch
+// the pipeline off for this context, clear the flag words.  Scans enqueued before this point report LO_ERR_PIPELINE
+// (their tails left without touching anything); a synchronous call re-runs its scan on one stream (lo_icp_result).
+static int pipe_recover(lo_ctx* c) {
+    LO_HIP(c, sync_all(c));
+    c->pipe = false;
+    ++c->pipe_timeouts;
+    c->err = "scan pipeline: a device-side wait timed out (the two streams were not run concurrently, e.g. rocprofv3 "
+             "counter collection); pipeline switched off for this context";
+    LO_HIP(c, hipMemset(c->d_fin, 0, 4 * sizeof(uint32_t)));
+    LO_HIP(c, hipStreamSynchronize(nullptr));
+    __atomic_store_n(c->h_broken, 0u, __ATOMIC_RELEASE);
+    return LO_OK;
+}
+static bool pipe_flagged(const lo_ctx* c) { return c->h_broken && __atomic_load_n(c->h_broken, __ATOMIC_ACQUIRE) != 0u; }
 
 static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
     P.tab = c->d_kd_plane;
@@ -471,7 +509,7 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
     // k_pko_t's dynamic block-prefix LDS reaches 64 KB at the 4M-point maximum
-    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(kMaxBlocks * sizeof(int))));
     c->kd = g.use_surfel_correspondence == 0;
     if (c->kd) {
@@ -500,8 +538,14 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     c->cfg = *cfg;
     c->device = device;
     if (const char* pe = std::getenv("LO_PRESOLVE")) c->presolve = std::atoi(pe) != 0;   // A/B runs
+    // rocprofv3 counter collection serialises dispatches across queues, which the pipeline's device-side waits cannot
+    // survive (k_wait_final): the pipeline starts off under it unless LO_PIPE says otherwise
+    if (const char* cc = std::getenv("ROCPROF_COUNTER_COLLECTION")) {
+        if (*cc && std::strcmp(cc, "0") != 0 && std::strcmp(cc, "False") != 0 && std::strcmp(cc, "false") != 0) c->pipe = false;
+    }
     if (const char* pp = std::getenv("LO_PIPE")) c->pipe = std::atoi(pp) != 0;
     if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
+    if (const char* pw = std::getenv("LO_PIPE_WAIT_MS")) c->pipe_bound = 100000ull * std::max(1, std::atoi(pw));
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
@@ -526,6 +570,7 @@ void lo_destroy(lo_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)sync_all(c);
     if (c->d_fin) (void)hipFree(c->d_fin);
+    if (c->h_broken) (void)hipHostFree(c->h_broken);
     if (c->s_tail) (void)hipStreamDestroy(c->s_tail);
     void* bufs[] = {c->d_pts, c->d_slot, c->d_wmask, c->d_blk_cnt, c->d_blk_sum, c->d_blk_m2, c->d_blk_part, c->d_acc_part,
                     c->d_js, c->d_res, c->d_u8, c->d_st, c->d_tab, c->d_alphas, c->d_Z, c->d_tabs_i,
@@ -1004,7 +1049,7 @@ static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
 
 // Reference-exact mode (lo_exact.hip): device buffers on first use, then per GN iteration the correspondence stage,
 // (iteration 0) the sorted-order scale, the PKO, the per-point terms and the sequential sums + fp32 solve.  Scans of
-// at most kExactMaxPoints sort in one workgroup's LDS (*n2 = the power of two it sorts); larger scans (*n2 = 0)
+// at most kExactMaxPoints sort in one workgroup (*n2 = n: registers + LDS, lo_seqsum.h); larger scans (*n2 = 0)
 // write their residuals out, sort them with hipCUB's radix sort and sum from global memory (k_exact_scale_g).
 static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     if (!c->d_ex_terms || c->ex_cap < std::max(n, static_cast<size_t>(kExactMaxPoints))) {
@@ -1012,8 +1057,6 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
         c->d_ex_terms = nullptr;
         c->ex_cap = std::max(n, static_cast<size_t>(kExactMaxPoints));
         LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * 43 * sizeof(float)));
-        LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kExactMaxPoints * 8));
     }
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
@@ -1035,22 +1078,25 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
         *n2 = 0;
         return LO_OK;
     }
-    *n2 = 1;
-    while (*n2 < static_cast<int>(n)) *n2 <<= 1;
+    *n2 = static_cast<int>(n);
     return LO_OK;
+}
+// the iteration-0 scale of reference-exact mode (between the scan's first correspondence launch and its first PKO)
+static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStream_t s) {
+    if (n2 > 0) {
+        launch_exact_scale(P, n2, s);
+        return;
+    }
+    const int n = P.n;                                       // the bound (a device-filtered scan counts on the device)
+    hipLaunchKernelGGL(k_exact_resid, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, P, c->d_ex_res);
+    size_t tmp = c->ex_sort_tmp_bytes;
+    (void)hipcub::DeviceRadixSort::SortKeys(c->d_ex_sort_tmp, tmp, c->d_ex_res, c->d_ex_sorted, n, 0,
+                                            static_cast<int>(sizeof(double) * 8), s);
+    hipLaunchKernelGGL(k_exact_scale_g, dim3(1), dim3(1024), 0, s, P, c->d_ex_sorted);
 }
 static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P0, int it, int n2, bool kd) {
     launch_correspond(c, it == 0 ? P0 : P, 0, kd);
-    if (it == 0 && n2 > 0) {
-        hipLaunchKernelGGL(k_exact_scale, dim3(1), dim3(1024), static_cast<size_t>(n2) * 8, c->stream, P, n2);
-    } else if (it == 0) {
-        const int n = P.n;                                   // the bound (a device-filtered scan counts on the device)
-        hipLaunchKernelGGL(k_exact_resid, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, P, c->d_ex_res);
-        size_t tmp = c->ex_sort_tmp_bytes;
-        (void)hipcub::DeviceRadixSort::SortKeys(c->d_ex_sort_tmp, tmp, c->d_ex_res, c->d_ex_sorted, n, 0,
-                                                static_cast<int>(sizeof(double) * 8), c->stream);
-        hipLaunchKernelGGL(k_exact_scale_g, dim3(1), dim3(1024), 0, c->stream, P, c->d_ex_sorted);
-    }
+    if (it == 0) launch_exact_scale_any(c, P, n2, c->stream);
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
     hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
@@ -1060,6 +1106,8 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
     const lo_config& g = c->cfg;
     std::memcpy(c->T_init, T_init, sizeof(float) * 12);
     c->last_n = n;
+    c->last_pts = d_pts;
+    c->last_ndev = n_dev;
     // reset the GN state (pose by kernel argument: no host staging buffer, scans can queue back to back)
     Pose12 T0;
     std::memcpy(T0.v, T_init, sizeof(float) * 12);
@@ -1081,17 +1129,28 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
         // small scan with PKO: the solve of iteration it runs fused with the correspondence search of it + 1
         // (k_solve_correspond; KDTree: k_solve_knn, then k_knn_brute + k_plane), the last solve alone (k_solve_pick)
         const bool fused = spec_ok(P) && g.max_iterations <= LO_MAX_ITERS;
+        int n2 = 0;
         if (c->exact) {
-            // reference-exact GN loop (lo_exact.hip): correspondences, (iteration 0) sorted-order scale, PKO,
-            // per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
-            int n2 = 1;
             const int rc3 = exact_prepare(c, P, n, &n2);
             if (rc3 != LO_OK) return rc3;
-            for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
-            LO_HIP(c, hipGetLastError());
-            if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
-            c->pending = true;
-            return LO_OK;
+            P0.ex_terms = P.ex_terms;
+            P0.scale_given = P.scale_given;
+            if (!(fused && P.cand_rec && !c->kd && n2 > 0)) {
+                // reference-exact GN loop without candidates (lo_exact.hip): correspondences, (iteration 0) sorted-order
+                // scale, PKO, per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
+                for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
+                LO_HIP(c, hipGetLastError());
+                if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
+                c->pending = true;
+                return LO_OK;
+            }
+            // small scans with PKO: the same launch sequence as the default mode, with the sorted-order scale after the
+            // first correspondence launch and the PKO launch's candidates forming the reference's sequential sums
+            P.exact_cand = P0.exact_cand = 1;
+        }
+        if (pipe_flagged(c)) {                            // an earlier scan's wait timed out: one stream from now on
+            const int rc4 = pipe_recover(c);
+            if (rc4 != LO_OK) return rc4;
         }
         if (fused && P.cand_rec && !c->kd && c->pipe && g.max_iterations > c->pipe_main) {
             // scan pipeline: iterations < pipe_main on the context stream, the rest on the tail stream behind a
@@ -1109,17 +1168,20 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             // host submission order main -> tail -> k_wait_final: every device-side wait depends only on work
             // submitted before it (deadlock-free even if the two streams share a hardware queue)
             launch_correspond_first(c, P0, false);
+            if (c->exact) launch_exact_scale_any(c, P, n2, c->stream);
             for (int it = 0; it < g.max_iterations; ++it) {
                 const bool tail = it >= c->pipe_main;
                 if (it == c->pipe_main)
-                    hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin, seq, c->d_st);
+                    hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin, seq, c->d_st, c->d_hbroken,
+                                       c->pipe_bound);
                 const hipStream_t s = tail ? c->s_tail : c->stream;
                 const KParams& Pi = tail ? Pt : (it + 1 == c->pipe_main ? Ph : P);
                 launch_pko_spec(c, Pi, it, s);
                 if (it + 1 < g.max_iterations) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, s, Pi, it);
                 else hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, s, Pi, it);
             }
-            hipLaunchKernelGGL(k_wait_final, dim3(1), dim3(kWave), 0, c->stream, c->d_fin, seq, c->d_st);
+            hipLaunchKernelGGL(k_wait_final, dim3(1), dim3(kWave), 0, c->stream, c->d_fin, seq, c->d_st, c->d_hbroken,
+                               c->pipe_bound);
             LO_HIP(c, hipGetLastError());
             if (timed) LO_HIP(c, hipEventRecord(c->ev1, c->stream));
             c->pending = true;
@@ -1132,7 +1194,10 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
                 launch_gn_tail(c, P, it);
                 continue;
             }
-            if (it == 0) launch_correspond_first(c, P0, c->kd);
+            if (it == 0) {
+                launch_correspond_first(c, P0, c->kd);
+                if (c->exact) launch_exact_scale_any(c, P, n2, c->stream);
+            }
             launch_pko_spec(c, P, it);
             if (it + 1 < g.max_iterations && !c->kd) {
                 if (P.cand_rec) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
@@ -1173,14 +1238,22 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     c->pending = false;
     const DevState* hs = c->h_st;
     int status = c->last_n == 0 ? LO_INSUFFICIENT : hs->status;
-    if (status == LO_ERR_HIP && c->pipe) {
-        // the two streams did not run concurrently (e.g. rocprofv3 counter collection serialises dispatches): this
-        // scan reports the error, and the context falls back to the single-stream GN loop from the next scan on
-        c->err = "scan pipeline: the wait for the scan's final result timed out (pipeline now off for this context)";
-        c->pipe = false;
-        if (c->s_tail) (void)hipStreamSynchronize(c->s_tail);
-        std::fprintf(stderr, "liblo_icp: scan pipeline wait timed out (streams serialised?); pipeline disabled for "
-                             "this context (LO_PIPE=0 selects that up front)\n");
+    if (status == LO_ERR_PIPELINE) {
+        // this scan's pipeline wait timed out: pipeline off, then the same scan again on one stream (its points are
+        // still the caller's until this call returns)
+        int rc = pipe_recover(c);
+        if (rc != LO_OK) return rc;
+        float T0[12];
+        std::memcpy(T0, c->T_init, sizeof(T0));
+        const bool timed = c->sync_call;
+        rc = enqueue_optimize(c, c->last_pts, c->last_n, T0, c->last_ndev);
+        c->sync_call = timed;
+        if (rc != LO_OK) return rc;
+        LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
+        LO_HIP(c, hipStreamSynchronize(c->stream));
+        c->pending = false;
+        ++c->pipe_reruns;
+        status = hs->status;
     }
     const int iters = hs->iter;
     if (T_out) {
@@ -1614,6 +1687,15 @@ int lo_set_exact(lo_ctx* c, int enable) {
     return LO_OK;
 }
 
+int lo_pipeline_status(lo_ctx* c, int out[4]) {
+    if (!c || !out) return LO_ERR_ARG;
+    out[0] = c->pipe ? 1 : 0;
+    out[1] = c->pipe_main;
+    out[2] = static_cast<int>(c->pipe_timeouts);
+    out[3] = static_cast<int>(c->pipe_reruns);
+    return LO_OK;
+}
+
 int lo_set_pipeline(lo_ctx* c, int enable, int main_iterations) {
     if (!c || main_iterations < 0) return LO_ERR_ARG;
     c->pipe = enable != 0;
@@ -1672,6 +1754,24 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     float ms = 0.0f;
     LO_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     *avg_ms = ms / reps;
+    return LO_OK;
+}
+
+int lo_seq_sum_f64(lo_ctx* c, const double* x, size_t n, int sort, double* out_sum, long long stats[4]) {
+    if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(kExactMaxPoints)) return LO_ERR_ARG;
+    LO_HIP(c, hipSetDevice(c->device));
+    double* d = nullptr;
+    LO_HIP(c, hipMalloc(&d, (n + 1) * sizeof(double) + 4 * sizeof(long long)));
+    long long* d_st = reinterpret_cast<long long*>(d + n + 1);
+    if (n > 0) LO_HIP(c, hipMemcpy(d, x, n * sizeof(double), hipMemcpyHostToDevice));
+    launch_seq_sum_diag(d, static_cast<int>(n), sort, d + n, d_st, c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    long long st[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(out_sum, d + n, sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) { c->err = std::string("lo_seq_sum_f64: ") + hipGetErrorString(e); return LO_ERR_HIP; }
+    if (stats) for (int k = 0; k < 4; ++k) stats[k] = st[k];
     return LO_OK;
 }
 

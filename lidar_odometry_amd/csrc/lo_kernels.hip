@@ -266,7 +266,7 @@ template <bool CORR>
 __device__ __forceinline__ void pick_body(const KParams& P, int it) {
     DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    const int done = st->done || (P.tail && fin_reached(P));   // loaded with the points and the JS grid
+    const int done = st->done || tail_gone(P);   // loaded with the points and the JS grid
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -494,19 +494,30 @@ __global__ void k_init(DevState* st, Pose12 T, double scale, double alpha) {
     }
 }
 
-// Scan pipeline (lo_set_pipeline), both bounded by wait_word (on timeout the scan reports LO_ERR_HIP):
+// Scan pipeline (lo_set_pipeline), both bounded by wait_word:
 //   k_wait_seq   heads a scan's tail on the tail stream: the main part is done (fin[1] >= seq, signal_main) or the
 //                scan is already final (fin[0] >= seq: its tail launches only leave early);
 //   k_wait_final follows the tail on the context stream: holds it until the scan's result is final (fin[0] >= seq).
 // Host submission order is main part, tail, k_wait_final: every wait depends only on work submitted before it, so
-// the two streams may share one hardware queue (they then simply run in order).
-__global__ void k_wait_seq(const uint32_t* fin, uint32_t seq, DevState* st) {
-    if (threadIdx.x != 0) return;
-    if (!wait_word2(fin, fin + 1, seq)) st->status = LO_ERR_HIP;
+// the two streams may share one hardware queue (they then simply run in order).  What breaks the device-side waits is a
+// dispatcher that serialises the two queues OUT of submission order (rocprofv3 counter collection runs one dispatch
+// at a time and can take the context stream's k_wait_final before the tail stream's launches: the wait then waits for
+// work that cannot start until it ends).  A wait that times out -- or finds the pipeline already broken -- marks the
+// scan LO_ERR_PIPELINE and sets the sticky broken word on the device (fin[3]: every later tail launch leaves without
+// touching the context's buffers, every later wait gives up at once) and in pinned host memory (hbroken: the host turns
+// the pipeline off at its next enqueue and re-runs a synchronous call's scan on one stream).
+__device__ __forceinline__ void pipe_fail(uint32_t* fin, uint32_t* hbroken, uint32_t seq, DevState* st) {
+    st->status = LO_ERR_PIPELINE;
+    __hip_atomic_store(fin + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (hbroken) __hip_atomic_store(hbroken, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ void k_wait_final(const uint32_t* fin, uint32_t seq, DevState* st) {
+__global__ void k_wait_seq(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound) {
     if (threadIdx.x != 0) return;
-    if (!wait_word(fin, seq)) st->status = LO_ERR_HIP;
+    if (!wait_word2(fin, fin + 1, seq, fin + 3, bound)) pipe_fail(fin, hbroken, seq, st);
+}
+__global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound) {
+    if (threadIdx.x != 0) return;
+    if (!wait_word(fin, seq, fin + 3, bound)) pipe_fail(fin, hbroken, seq, st);
 }
 
 // Copy the current pose + status into a caller buffer (16 floats: pose[12], status, iterations, n_corr, 0).

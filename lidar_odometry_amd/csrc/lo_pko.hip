@@ -8,6 +8,10 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_pko_t(KParams P, int it, int G) {
     pko_body<NW, false>(P, own_bufs(P), it, blockIdx.x, G);
 }
+// Reference-exact mode (lo_set_exact): the same launch with acc_candidate_exact as the candidates.
+__global__ __launch_bounds__(256) void k_pko_tx(KParams P, int it, int G) {
+    pko_body<4, false, true>(P, own_bufs(P), it, blockIdx.x, G);
+}
 
 // Batched launch: blockIdx.y = job, gridDim.x workgroups per job split its alpha grid.  <4, false>: the
 // single-scan workgroup (few jobs); <1, true>: one wave per job that fits the GMM alone (many jobs: the

@@ -23,6 +23,7 @@
 #include "lo_device.h"
 #include "lo_math.h"
 #include "lo_solve.h"
+#include "lo_exact.h"
 
 #include <cfloat>
 
@@ -671,6 +672,117 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 #endif
 }
 
+// Reference-exact candidates (lo_set_exact, scans with nb_acc <= kFuseMaxBlocks): candidate c's GN step exactly as the
+// reference forms it -- the 43 running fp32 sums of build_ne in correspondence (scan) order (:345-410), Eigen's fp32
+// LDLT and the re-projected update (:417-448; lo_exact.h) -- in ONE workgroup while the EM runs, written as the same
+// 48-word record acc_candidate writes, so k_pick_correspond / k_pick take it unchanged.  Waves 1-3 form each accepted
+// point's 14 factors (J, w J, w r, r; exact_point_factors) for a chunk of 384 points and stage them in LDS,
+// compacted per 64-point region in point order; wave 0's lane k adds term k = fa[k] * fb[k] of every staged row to
+// its running sum, one rounding per addition, one chunk behind the producers (double-buffered, one barrier per
+// chunk).  The producers' loads run a chunk ahead (slot indices two).  LDS: the dynamic buffer (after the prefix).
+
+__device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
+    if (c > P.NA) return;
+    float* s_f = dyn;                                      // [2][kXcBuf]
+    int* s_cnt = reinterpret_cast<int*>(dyn + 2 * kXcBuf); // [2][kXcRegions]
+    float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
+    float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n = scan_n(P);
+    const int nch = (n + kXcChunk - 1) / kXcChunk;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+    const float dl = cand_delta(P, c);
+    __syncthreads();                                       // the prefix's use of the dynamic buffer is over
+    // producer state: this lane's kXcPPL points of the current chunk (loaded) and of the next (slots only)
+    int sl_cur[kXcPPL], sl_nxt[kXcPPL];
+    float px[kXcPPL], py[kXcPPL], pz[kXcPPL];
+    Slot sv[kXcPPL];
+    double rv[kXcPPL];
+    auto pidx = [&](int ch, int q) { return ch * kXcChunk + ((wid - 1) * kXcPPL + q) * kWave + lane; };
+    auto slot_at = [&](int ch, int q) { const int i = pidx(ch, q); return (ch < nch && i < n) ? P.slot[i] : -1; };
+    auto load_pt = [&](int ch, int q, int s) {
+        if (s >= 0) {
+            const int i = pidx(ch, q);
+            px[q] = P.pts[3 * i]; py[q] = P.pts[3 * i + 1]; pz[q] = P.pts[3 * i + 2];
+            sv[q] = P.tab[s];
+            rv[q] = P.kd_res ? P.kd_res[i] : P.res_out[i];     // the stored fp64 residual (same bits as recomputing)
+        }
+    };
+    if (wid > 0) {
+#pragma unroll
+        for (int q = 0; q < kXcPPL; ++q) { sl_cur[q] = slot_at(0, q); sl_nxt[q] = slot_at(1, q); }
+#pragma unroll
+        for (int q = 0; q < kXcPPL; ++q) load_pt(0, q, sl_cur[q]);
+    }
+    // consumer state: lane k's term factors and running sum
+    int fa = 0, fb = 0;
+    exact_term_factors(lane < kExactTerms ? lane : 0, fa, fb);
+    float sum = 0.0f;
+    for (int ch = 0; ch <= nch; ++ch) {
+        if (wid > 0 && ch < nch) {
+            float* buf = s_f + (ch & 1) * kXcBuf;
+#pragma unroll
+            for (int q = 0; q < kXcPPL; ++q) {
+                const bool valid = sl_cur[q] >= 0;
+                const uint64_t m = __ballot(valid);
+                const int r = (wid - 1) * kXcPPL + q;
+                if (valid) {
+                    float f[14];
+                    exact_point_factors(P, T, scale, dl, rv[q], px[q], py[q], pz[q], sv[q], f);
+                    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                    float* row = buf + (r * kWave + rank) * kXcStride;
+#pragma unroll
+                    for (int k = 0; k < 14; ++k) row[k] = f[k];
+                }
+                if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = __popcll(m);
+            }
+            // the next chunk's points / surfels / residuals, and the slots of the one after
+#pragma unroll
+            for (int q = 0; q < kXcPPL; ++q) { sl_cur[q] = sl_nxt[q]; sl_nxt[q] = slot_at(ch + 2, q); }
+#pragma unroll
+            for (int q = 0; q < kXcPPL; ++q) load_pt(ch + 1, q, sl_cur[q]);
+        } else if (wid == 0 && ch > 0) {
+            const int b = (ch - 1) & 1;
+            const float* buf = s_f + b * kXcBuf;
+            for (int r = 0; r < kXcRegions; ++r) {
+                const int cnt = s_cnt[b * kXcRegions + r];
+                const float* rows = buf + r * kWave * kXcStride;
+                int i = 0;
+                for (; i + 8 <= cnt; i += 8) {
+                    float t[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = rows[(i + u) * kXcStride + fa] * rows[(i + u) * kXcStride + fb];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sum += t[u];
+                }
+                for (; i < cnt; ++i) sum += rows[i * kXcStride + fa] * rows[i * kXcStride + fb];
+            }
+        }
+        __syncthreads();
+    }
+    if (wid == 0 && lane < kExactTerms) s_tot[lane] = sum;
+    __syncthreads();
+    if (tid == 0) {
+        float tot[kExactTerms], pn[12], delta[6];
+#pragma unroll
+        for (int k = 0; k < kExactTerms; ++k) tot[k] = s_tot[k];
+        const bool conv = exact_solve_step(tot, T, P.tol_t, P.tol_r, pn, delta);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) s_rec[q] = pn[q];
+        s_rec[kCandCost] = tot[42];
+        int k = 0;
+        for (int r = 0; r < 6; ++r) for (int cc = r; cc < 6; ++cc) s_rec[kCandH + k++] = tot[r * 6 + cc];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) { s_rec[kCandG + j] = tot[36 + j]; s_rec[kCandD + j] = delta[j]; }
+        s_rec[kCandConv] = conv ? 1.0f : 0.0f;
+        s_rec[kCandConv + 1] = 0.0f;
+    }
+    __syncthreads();
+    if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
+}
+
 // Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts
 // (s_pre, nb ints of LDS) and the normalisation scale -- iteration 0: std/6 of the accepted residuals from the
 // per-block (count, sum, M2) by a Chan merge about the global mean (IterativeClosestPointOptimizer.cpp:304-316);
@@ -1052,14 +1164,15 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
 }
 
 // wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
-// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate).
+// single-scan launch, workgroups wg >= G are speculative normal-equation candidates (acc_candidate; XC: the
+// reference-exact acc_candidate_exact, a separate instantiation so the default kernel's code is not touched).
 // ONE_WAVE (batched launches of many scans): the GMM is fitted by wave 0 alone (gmm_fit_1w).
-template <int NW, bool ONE_WAVE>
+template <int NW, bool ONE_WAVE, bool XC = false>
 __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, int it, int wg, int G) {
     DevState* st = B.st;
     // the done flag, the single-wave prefix's loads and the prefetch below go out in one round trip; the flag is
     // tested once they are in flight (a converged scan leaves without writing anything)
-    const int done0 = st->done || (P.tail && fin_reached(P));   // tail launch: scan already final
+    const int done0 = st->done || tail_gone(P);   // tail launch: scan already final (or the pipeline broken)
     PrefixLoads pl;
     const bool wave_prefix = !P.direct_res && P.nb <= 64;
     if (wave_prefix && threadIdx.x < 64) prefix_loads(P, B, it, pl);
@@ -1081,13 +1194,24 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     double s_scale;
     const uint64_t* s_wmask = P.nb <= 64 && !P.direct_res ? L.wm : nullptr;
     pko_prefix<NW>(P, B, it, lead, s_pre, nc, s_scale, L.wm, &pl);   // pl is set where it is read (nb <= 64)
+    if (P.tail) {
+        // A tail launch tests the scan's state once more before acting on what the prefix read: another workgroup of
+        // this launch may have published the scan final (too few correspondences) after this one passed done0, and
+        // the context stream may already run the next scan on the same buffers.  fin is published before the next
+        // scan can start, so a workgroup that still sees it unpublished here read this scan's data.
+        __shared__ int s_gone;
+        if (tid == 0) s_gone = tail_gone(P) ? 1 : 0;
+        __syncthreads();
+        if (s_gone) return;
+    }
     if (!P.direct_res && nc < P.min_corr) {                     // :298-302
         if (lead && tid == 0) { st->status = LO_INSUFFICIENT; st->done = 1; st->n_corr = nc; publish_final(P); }
         return;
     }
     if constexpr (NW == 4 && !ONE_WAVE) {
         if (wg >= G) {                                          // after the scale: the candidates need it
-            acc_candidate(P, s_scale, wg - G);
+            if constexpr (XC) acc_candidate_exact(P, s_scale, wg - G, reinterpret_cast<float*>(s_pre));
+            else acc_candidate(P, s_scale, wg - G);
             return;
         }
     }

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Diagnostic: phase clocks of the reference-exact iteration-0 scale kernel (liblo_icp_diagx.so, -DLO_EXACT_STAMPS).
+
+    LO_ICP_LIB=lidar_odometry_amd/liblo_icp_diagx.so python scripts/exact_stamps.py [--config kitti]
+
+Prints s_memtime deltas: load + count | sort | mean sum | variance sum, per scan of the bench workload.
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="kitti")
+    a = ap.parse_args()
+    import bench
+    from lidar_odometry_amd import lib
+    from lidar_odometry_amd.icp import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
+    wl = bench.WORKLOADS[a.config](0)
+    icp = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
+                                         device=0, max_points=max(len(s) for s in wl["scans"]))
+    L = lib()
+    assert L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle) == 0
+    icp.set_exact(True)
+    rows = []
+    for i in range(len(wl["scans"])):
+        icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
+        d = (C.c_ulonglong * 16)()
+        assert L.lo_debug_counters(icp.ctx, d) == 0
+        rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3]])
+    r = np.array(rows, dtype=np.float64)
+    print("cycles (s_memtime) per phase, mean over", len(rows), "scans: load/count %.0f  sort %.0f  mean-sum %.0f  "
+          "var-sum %.0f" % tuple(r.mean(0)), flush=True)
+    icp.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -164,3 +164,83 @@ def test_pipeline_args():
         o.set_pipeline(True, 0)                                # keeps the split
     finally:
         o.close()
+
+
+def test_pipeline_tail_insufficient_queued():
+    """A scan that drops below min_correspondence_points at an iteration on the tail stream (main = 1): the tail
+    launch's lead workgroup publishes the scan final while its siblings may still be in the PKO prefix, and the next
+    scan starts on the same buffers.  Queued back to back among other scans, every record equals the pipeline-off run
+    (the tail workgroups re-test the scan's state after the prefix, lo_pko_body.h)."""
+    import torch
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    cs = _cases()[:6]
+    o = _ctx(cs[0][0])
+    try:
+        o.set_pipeline(False)
+        ncs = []
+        for _, pts, Ti in cs:
+            o.optimize(None, pts, Ti)
+            ncs.append([int(L["n_corr"]) for L in o.get_last_stats().iterations])
+    finally:
+        o.close()
+    # min_corr = iteration 0's count of a scan whose count falls at iteration 1: that scan fails on the tail
+    pick = [j for j, n in enumerate(ncs) if len(n) >= 2 and n[1] < n[0]]
+    assert pick, ncs
+    j0 = pick[0]
+    cfg = ICPConfig(min_correspondence_points=ncs[j0][0])
+    o = IterativeClosestPointOptimizer(config=cfg, max_points=1 << 16)
+    try:
+        k, n, c = _data.surfels(cs[0][0])
+        o.set_surfels(k, n, c)
+        d_scans = [torch.from_numpy(np.ascontiguousarray(p, np.float32).reshape(-1, 3)).to("cuda:0") for _, p, _ in cs]
+        inits = [Ti for _, _, Ti in cs]
+        order = [j0 if k % 2 == 0 else k % len(cs) for k in range(40)]
+        o.set_pipeline(False)
+        ref = _queued(o, d_scans, inits, order)
+        assert int(ref[0, 12]) == 1 and int(ref[0, 13]) == 1          # LO_INSUFFICIENT after one iteration
+        o.set_pipeline(True, 1)
+        for rep in range(3):
+            got = _queued(o, d_scans, inits, order)
+            np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32), err_msg=f"rep {rep}")
+    finally:
+        o.close()
+
+
+def test_pipeline_timeout_under_counter_collection():
+    """The failure the device-side waits had: under `rocprofv3 --pmc` dispatches are serialised across queues, and a
+    wait can run before the work it waits for.  Forced on (LO_PIPE=1) with a 20 ms bound, a timed-out wait marks its
+    scan LO_ERR_PIPELINE and breaks the pipeline for good: queued records are either bit-identical to the pipeline-off
+    run or flagged (never silently wrong), synchronous calls re-run the scan on one stream (bit-identical), and
+    lo_pipeline_status reports it.  Without LO_PIPE the context starts with the pipeline off under counter collection."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    import sys
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        pytest.skip("rocprofv3 not installed")
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_pipe_child.py")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for force in ("1", ""):
+        env = dict(os.environ, LO_PIPE_WAIT_MS="20", TMPDIR="/tmp")
+        env.pop("LO_PIPE", None)
+        if force:
+            env["LO_PIPE"] = force
+        outdir = os.path.join("/tmp", f"lo_pipe_pmc_{os.getpid()}_{force or 'auto'}")
+        r = subprocess.run(["timeout", "-k", "10", "100", prof, "--pmc", "FETCH_SIZE", "-d", outdir, "-o", "run",
+                            "--output-format", "csv", "--", sys.executable, child], cwd=root, env=env,
+                           capture_output=True, text=True)
+        shutil.rmtree(outdir, ignore_errors=True)
+        assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        outs[force] = json.loads(line)
+    forced, auto = outs["1"], outs[""]
+    assert forced["sync_bitwise"] and forced["queued_bitwise_or_flagged"], forced
+    assert forced["status_start"][0] == 1
+    if forced["queued_flagged"] or forced["status_end"][2]:
+        assert forced["status_end"][2] >= 1, forced                    # the timeout is reported
+    assert auto["status_start"][0] == 0, auto                          # counter collection: pipeline off up front
+    assert auto["sync_bitwise"] and auto["queued_bitwise_or_flagged"] and auto["queued_flagged"] == 0, auto
+    print("forced:", forced, "auto:", auto)
