@@ -206,10 +206,26 @@ def parity_vs_oracle(gpu, cpu) -> dict:
             "alpha_every_iteration_equal": same_alpha_all}
 
 
-def cpu_baseline(wl, budget_s: float, gpu=None, gpu_exact=None):
+def parity_bitwise(gpu, ref) -> int:
+    """Scans whose every iteration's pose, alpha and n_corr, the final pose and the status equal the oracle's bits."""
+    return sum(int(g["ok"] == c["ok"] and np.array_equal(np.asarray(g["T"], np.float32).view(np.uint32),
+                                                        np.asarray(c["T"], np.float32).view(np.uint32))
+                   and len(g["logs"]) == len(c["logs"])
+                   and all(np.array_equal(np.asarray(a["pose"], np.float32).view(np.uint32),
+                                          np.asarray(b["pose"], np.float32).view(np.uint32)) and
+                           a["alpha"] == b["alpha"] and a["n_corr"] == b["n_corr"] for a, b in zip(g["logs"], c["logs"])))
+               for g, c in zip(gpu, ref))
+
+
+MODE_NOTE = {"exact": "lo_set_exact: the reference's fp32 operation order (sequential sums in correspondence order, "
+                      "sorted-order iteration-0 scale, fp32 LDLT, JacobiSVD-projected SO3)",
+             "default": "fp64 tree sums, Chan-merged iteration-0 scale, fp64 LDLT + polar SO3"}
+
+
+def cpu_baseline(wl, budget_s: float, gpu_by_mode=None, value_mode="exact"):
     """The oracle port timed on this host (1 thread, bounded sample); its first pass over the distinct scans is also
-    the parity reference for the GPU results of the same scans (gpu: default mode, gpu_exact: reference-exact mode,
-    compared bit for bit)."""
+    the parity reference for the GPU results of the same scans, per arithmetic mode (gpu_by_mode: {mode: results});
+    `parity` is the mode reported as value, `parity_other` the other one."""
     import oracle
     m = oracle.VoxelMap(wl["voxel"], 3, 0.1, True)
     for w, s in wl["keyframes"]:
@@ -233,21 +249,14 @@ def cpu_baseline(wl, budget_s: float, gpu=None, gpu_exact=None):
            "gn_iters_per_sec": n_iters / el,
            "sample": f"{n_scans} optimize() calls over {len(scans)} distinct scans in {el:.1f} s "
                      f"(oracle/liblo_oracle.so, single thread, g++ -O3, same synthetic inputs)"}
-    if gpu is not None:
-        out["parity"] = parity_vs_oracle(gpu, ref)
-        out["parity"]["mode"] = "default (fp64 tree sums, fp64 LDLT + polar SO3)"
-    if gpu_exact is not None:
-        bitwise = sum(int(g["ok"] == c["ok"] and np.array_equal(np.asarray(g["T"], np.float32).view(np.uint32),
-                                                                   np.asarray(c["T"], np.float32).view(np.uint32))
-                          and len(g["logs"]) == len(c["logs"])
-                          and all(np.array_equal(a["pose"].view(np.uint32), b["pose"].view(np.uint32)) and
-                                  a["alpha"] == b["alpha"] and a["n_corr"] == b["n_corr"]
-                                  for a, b in zip(g["logs"], c["logs"])))
-                      for g, c in zip(gpu_exact, ref))
-        out["parity_exact"] = {"scans": len(ref), "bitwise_equal": bitwise,
-                               "mode": "lo_set_exact: the reference's fp32 operation order (sequential sums, fp32 "
-                                       "LDLT, JacobiSVD SO3); every iteration's pose, alpha and n_corr compared bit "
-                                       "for bit"}
+    for mode, gpu in (gpu_by_mode or {}).items():
+        if gpu is None:
+            continue
+        p = parity_vs_oracle(gpu, ref)
+        p["bitwise_equal"] = parity_bitwise(gpu, ref)
+        p["mode"] = mode
+        p["mode_note"] = MODE_NOTE[mode]
+        out["parity" if mode == value_mode else "parity_other"] = p
     return out
 
 
@@ -526,7 +535,7 @@ def run_e2e(args, world, rank, local):
         pinned.append(a)
 
     def epoch(timed, scans=pinned):
-        od = LidarOdometry(device=local, initial_pose=seq.poses[0])
+        od = LidarOdometry(device=local, initial_pose=seq.poses[0], exact=args.mode == "exact")
         dt, poses, kf, dev_ms, map_ms = 0.0, [], 0, 0.0, 0.0
         try:
             for r in scans:
@@ -570,7 +579,8 @@ def run_e2e(args, world, rank, local):
         "config": {"workload": "Estimator::process_frame loop (no loop closure / PGO), config/kitti.yaml, device filter + ICP, "
                                "device-resident VoxelMap update at keyframes (lo_devmap)",
                    "raw_points_per_frame_avg": float(np.mean([len(r) for r in raws])),
-                   "keyframes_per_frame": kfs / frames, "parallelism": "single GPU per sequence"},
+                   "keyframes_per_frame": kfs / frames, "parallelism": "single GPU per sequence",
+                   "mode": args.mode, "mode_note": MODE_NOTE[args.mode]},
         "breakdown_ms_per_frame": {"device_filter_icp": dev / frames, "keyframe_map_update_host": mp / frames,
                                    "other_host": tot / frames * 1e3 - dev / frames - mp / frames},
         "translation_error_vs_gt_m_max": max(err),
@@ -583,10 +593,21 @@ def run_e2e(args, world, rank, local):
         import oracle
         t = time.perf_counter()
         n_cpu = 0
-        while time.perf_counter() - t < args.cpu_budget:
-            oracle.odometry(raws, initial=seq.poses[0])
+        ref_poses = None
+        while time.perf_counter() - t < args.cpu_budget or ref_poses is None:
+            rp, _ = oracle.odometry(raws, initial=seq.poses[0])
+            if ref_poses is None:
+                ref_poses = rp
             n_cpu += n_frames
         el = time.perf_counter() - t
+        gp = np.stack([np.asarray(P, np.float32)[:3, :4].reshape(12) for P in poses])
+        dtr = float(np.abs(gp.reshape(-1, 3, 4)[:, :, 3] - np.asarray(ref_poses).reshape(-1, 3, 4)[:, :, 3]).max())
+        result["parity"] = {"frames": n_frames, "mode": args.mode,
+                            "poses_bitwise_equal": int(sum(np.array_equal(a.view(np.uint32),
+                                                                          np.asarray(b, np.float32).view(np.uint32))
+                                                           for a, b in zip(gp, ref_poses))),
+                            "max_abs_dt_m": dtr,
+                            "vs": "oracle.odometry on the same raw scans (the CPU restatement of the frame loop)"}
         result["cpu_baseline"] = {"value": n_cpu / el, "unit": "frames/s", "cores": 1, "kind": "port",
                                   "sample": f"{n_cpu} frames ({n_cpu // n_frames} passes over the {n_frames}-frame sequence) "
                                             f"in {el:.1f} s, oracle.odometry (same loop on the CPU restatement)"}
@@ -612,6 +633,7 @@ def run_loop(args, world, rank, local):
         pairs.append((cur, pose12(synth.perturb(seq.poses[fb], rng, 0.3, 0.03)), mat, pose12(seq.poses[fa])))
     torch.cuda.set_device(local)
     icp = IterativeClosestPointOptimizer(device=local, max_points=max(len(p[0]) for p in pairs))
+    icp.set_exact(args.mode == "exact")
     try:
         for k in range(max(args.warmup, len(pairs))):
             icp.optimize_loop(*pairs[k % len(pairs)])
@@ -633,7 +655,7 @@ def run_loop(args, world, rank, local):
         "config": {"workload": "IterativeClosestPointOptimizer::optimize_loop between keyframes 3-4 frames apart, "
                                "config/kitti.yaml", "points_per_cloud_avg": float(np.mean([len(p[0]) for p in pairs])),
                    "gn_iters_per_solve": n_it / args.steps, "success_fraction": n_ok / args.steps,
-                   "parallelism": "single GPU"},
+                   "parallelism": "single GPU", "mode": args.mode, "mode_note": MODE_NOTE[args.mode]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         t = time.perf_counter()
@@ -773,6 +795,11 @@ def main():
                     help="extra measurement with --config kitti: this many distinct 1M-point scans (C5), one context "
                          "each, rotated so each launch reads its scan from HBM; 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="exact", choices=["exact", "default"],
+                    help="arithmetic order of the timed GN step: exact = the reference's own fp32 order (lo_set_exact: "
+                         "sequential sums, fp32 LDLT, JacobiSVD SO3; bit-identical to the oracle), default = fp64 tree "
+                         "sums + fp64 solve (within ~1e-7 per step, but a near-tie in the PKO's JS argmin can flip "
+                         "alpha); the other mode is timed beside it as other_mode")
     ap.add_argument("--order", default="azimuth", choices=["azimuth", "random"], help="patch1m scan point order")
     ap.add_argument("--sequences", type=int, default=8,
                     help="extra measurement: independent sequences sharing this GPU, one context + HIP stream each "
@@ -842,6 +869,8 @@ def main():
     icp = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not kd), AdaptiveMEstimatorConfig(),
                                          MapGeometry(voxel_size=wl["voxel"]), device=local, max_points=max_pts)
     L = lib()
+    icp.set_exact(args.mode == "exact")
+    other = "default" if args.mode == "exact" else "exact"
     # one stream shared by the ICP context and torch (pose-record copies, the gather's events): a dedicated stream,
     # because handle 0 (torch's legacy default stream) means "the context's own non-blocking stream" to
     # lo_set_stream, which the default stream does not order against
@@ -1043,41 +1072,29 @@ def main():
         icp.optimize(None, wl["scans"][i], inits[i])
     pcie_rate = n_pc / (time.perf_counter() - t1)
 
-    # reference-exact arithmetic (lo_set_exact: sequential fp32 sums in the reference's order, fp32 LDLT, JacobiSVD
-    # SO3): the same steps timed, and every scan's result kept for the bit-for-bit comparison with the oracle
-    exact, gpu_exact = None, None
-    if world == 1 and max_pts <= 16384:
-        icp.set_exact(True)
-        gpu_exact = []
-        for i in range(len(d_scans)):
-            ok, To = icp.optimize(None, wl["scans"][i], inits[i])
-            st = icp.get_last_stats()
-            gpu_exact.append({"ok": bool(ok), "T": np.asarray(To, np.float32).reshape(12).copy(), "logs": st.iterations})
-        L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
-        n_ex = min(args.steps, 300)
-
-        def exact_step(k):
-            i = k % len(d_scans)
-            if raw:
-                rc = L.lo_icp_optimize_raw_async(icp.ctx, C.c_void_p(d_raw[i].data_ptr()), d_raw[i].shape[0], 8,
-                                                 C.c_float(0.5), fptr(inits[i]))
-            else:
-                rc = L.lo_icp_optimize_async(icp.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0],
-                                             fptr(inits[i]))
-            assert rc == 0, rc
-        for k in range(10):
-            exact_step(k)
-        torch.cuda.synchronize(dev)
-        t4 = time.perf_counter()
-        for k in range(n_ex):
-            exact_step(k)
-        torch.cuda.synchronize(dev)
-        el4 = time.perf_counter() - t4
-        icp.set_exact(False)
-        exact = {"value": n_ex / el4, "unit": "scans/s", "steps": n_ex,
-                 "gn_iters_per_sec": sum(iters[k % len(iters)] for k in range(n_ex)) / el4,
-                 "note": "lo_set_exact: the reference's own fp32 operation order, bit-identical to the oracle "
-                         "(cpu_baseline.parity_exact); timed like value, never value"}
+    # the other arithmetic mode (exact <-> default): the same steps timed, and every scan's result kept for the parity
+    # comparison with the oracle (cpu_baseline.parity_other)
+    icp.set_exact(other == "exact")
+    gpu_other = []
+    for i in range(len(d_scans)):
+        ok, To = icp.optimize(None, wl["scans"][i], inits[i])
+        st = icp.get_last_stats()
+        gpu_other.append({"ok": bool(ok), "T": np.asarray(To, np.float32).reshape(12).copy(), "logs": st.iterations})
+    L.lo_set_stream(icp.ctx, C.c_void_p(stream.cuda_stream))
+    n_ot = min(args.steps, 300)
+    for k in range(10):
+        step(k)
+    torch.cuda.synchronize(dev)
+    t4 = time.perf_counter()
+    for k in range(n_ot):
+        step(k)
+    torch.cuda.synchronize(dev)
+    el4 = time.perf_counter() - t4
+    icp.set_exact(args.mode == "exact")
+    other_mode = {"mode": other, "value": n_ot / el4, "unit": "scans/s", "steps": n_ot,
+                  "gn_iters_per_sec": sum(len(gpu_other[k % len(gpu_other)]["logs"]) for k in range(n_ot)) / el4,
+                  "mode_note": MODE_NOTE[other],
+                  "note": "the other arithmetic mode, timed like value (never value); parity in cpu_baseline.parity_other"}
 
     # independent sequences sharing the GPU (serving many sensors / logs): B contexts, one HIP stream each,
     # scans enqueued round-robin without host syncs; aggregate scans/s.  Never `value`.
@@ -1087,6 +1104,8 @@ def main():
         ctxs = [icp] + [IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not kd), AdaptiveMEstimatorConfig(),
                                                        MapGeometry(voxel_size=wl["voxel"]), device=local, max_points=max_pts)
                         for _ in range(B - 1)]
+        for o in ctxs[1:]:
+            o.set_exact(args.mode == "exact")
         L.lo_set_stream(icp.ctx, None)                  # back to the context's own stream
         for o in ctxs[1:]:
             assert L.lo_map_set_from_voxelmap(o.ctx, wl["vm"].handle) == 0
@@ -1112,7 +1131,7 @@ def main():
         for o in ctxs:
             L.lo_sync(o.ctx)
         el2 = time.perf_counter() - t2
-        multi = {"sequences": B, "value": B * K2 / el2, "unit": "scans/s", "steps_per_sequence": K2,
+        multi = {"sequences": B, "value": B * K2 / el2, "unit": "scans/s", "steps_per_sequence": K2, "mode": args.mode,
                  "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
                  "note": "independent scan streams, one context + HIP stream each; aggregate throughput, not value"}
         for o in ctxs[1:]:
@@ -1125,7 +1144,7 @@ def main():
     if sizes:
         from lidar_odometry_amd import BatchOptimizer
         from lidar_odometry_amd._lib import LoBatchRec
-        batched = {"unit": "scans/s", "runs": [],
+        batched = {"unit": "scans/s", "runs": [], "mode": "default",
                    "note": "B independent sequences on one GPU (one context each: own map copy, scan, GN state), "
                            "advanced in lockstep by lo_batch_optimize_async; aggregate throughput, not value"}
         pool = []
@@ -1229,8 +1248,10 @@ def main():
                    "distinct_scans": len(wl["scans"]), "map_surfels": wl["vm"].surfel_count(),
                    "map_l0_points": wl["vm"].l0_count(), "correspondence": "kdtree 5-NN" if kd else "L1 surfel",
                    "max_iterations": 4, "gn_iters_per_scan_avg": float(np.mean(iters)),
-                   "parallelism": f"scan-parallel x{world} (RCCL pose all-gather per step, side stream)" if world > 1
-                   else "single GPU: context stream + tail stream (scan pipeline)"},
+                   "parallelism": (f"scan-parallel x{world} (pose all-gather per step over "
+                                   f"{'gloo, host memory' if gloo else 'RCCL, side stream'})") if world > 1
+                   else "single GPU: context stream + tail stream (scan pipeline)",
+                   "mode": args.mode, "mode_note": MODE_NOTE[args.mode]},
         "pipeline": pipeline,
         "gn_iters_per_sec": total_iters / el,
         "per_rank": None if world == 1 else {"scans_per_s": [args.steps / e for e in per_rank], "timed_s": per_rank,
@@ -1260,10 +1281,10 @@ def main():
                      "in_cache_note": "working set (points + slot writes + one 32-B table sector per point) within the "
                                       "256 MB Infinity Cache: the fraction measures cache, not HBM, bandwidth"},
         "roofline_dominant": pko_roofline(em_live),
-        "exact_mode": exact,
+        "other_mode": other_mode,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget, gpu_res, gpu_exact)
+        result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget, {args.mode: gpu_res, other: gpu_other}, args.mode)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and args.config == "kitti" and args.c5 > 0:
         result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5)

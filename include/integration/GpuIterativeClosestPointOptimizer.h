@@ -16,7 +16,8 @@
  *   - const OptimizationStats& get_last_stats() (:203-215), filled as the reference fills it;
  *   - update_config / get_config (:220-225).
  * The map the kernels read is a device copy of the VoxelMap's L1 surfels (VoxelMap::GetSurfelAtPoint's table,
- * VoxelMap.cpp:368-386).  sync_map() rebuilds it from the map's PUBLIC interface only; call it after every mutation
+ * VoxelMap.cpp:368-386).  sync_map() reads it from the map's PUBLIC interface only and sends the device only the
+ * surfels that changed since the previous sync (lo_map_sync_surfels); call it after every mutation
  * (Estimator.cpp:457 UpdateVoxelMap, :877 / :1181 ApplyTransformAndRehash).  In the KDTree configuration
  * (use_surfel_correspondence = false) it uploads VoxelMap::GetPointCloud() instead (RebuildKdTree's input, :461).
  *
@@ -135,31 +136,36 @@ public:
             nrm.insert(nrm.end(), {nv.x(), nv.y(), nv.z()});
             ctr.insert(ctr.end(), {c.x(), c.y(), c.z()});
         }
-        check(lo_map_set_surfels(m_ctx, keys.data(), nrm.data(), ctr.data(), keys.size() / 3), "lo_map_set_surfels");
+        // only the voxels UpdateVoxelMap changed since the last sync reach the device (VoxelMap.cpp:187-261: new and
+        // refitted surfels, surfels that lost planarity or were pruned); the first sync uploads the whole table
+        int patched = 0;
+        check(lo_map_sync_surfels(m_ctx, keys.data(), nrm.data(), ctr.data(), keys.size() / 3, &patched),
+              "lo_map_sync_surfels");
+        m_last_sync_patched = patched;
     }
+    int last_sync_patched() const { return m_last_sync_patched; }   // records sent by the last sync_map (-1: full)
 
     const OptimizationStats& get_last_stats() const { return m_last_stats; }
-    void update_config(const ICPConfig& config) {            // :220; a new context with the new parameters
+    void update_config(const ICPConfig& config) {            // :220: only the parameters change; the device map stays
+        lo_config c = make_config(config);
+        check(lo_update_config(m_ctx, &c), "lo_update_config");
         m_config = config;
-        lo_destroy(m_ctx);
-        m_ctx = nullptr;
-        create_context();
     }
     const ICPConfig& get_config() const { return m_config; }
     lo_ctx* context() const { return m_ctx; }                // e.g. lo_set_exact(context(), 1)
 
 private:
-    void create_context() {
+    lo_config make_config(const ICPConfig& cfg) const {
         lo_config c;
         lo_config_default_kitti(&c);
-        c.max_iterations = m_config.max_iterations;
-        c.translation_tolerance = m_config.translation_tolerance;
-        c.rotation_tolerance = m_config.rotation_tolerance;
-        c.max_correspondence_distance = m_config.max_correspondence_distance;
-        c.min_correspondence_points = m_config.min_correspondence_points;
-        c.use_robust_loss = m_config.use_robust_loss ? 1 : 0;
-        c.robust_loss_delta = m_config.robust_loss_delta;
-        c.use_surfel_correspondence = m_config.use_surfel_correspondence ? 1 : 0;
+        c.max_iterations = cfg.max_iterations;
+        c.translation_tolerance = cfg.translation_tolerance;
+        c.rotation_tolerance = cfg.rotation_tolerance;
+        c.max_correspondence_distance = cfg.max_correspondence_distance;
+        c.min_correspondence_points = cfg.min_correspondence_points;
+        c.use_robust_loss = cfg.use_robust_loss ? 1 : 0;
+        c.robust_loss_delta = cfg.robust_loss_delta;
+        c.use_surfel_correspondence = cfg.use_surfel_correspondence ? 1 : 0;
         // outlier_rejection_ratio, use_kdtree, max_kdtree_neighbors: not read by optimize
         c.use_adaptive_m_estimator = 0;                      // no estimator: robust_loss_delta, Huber (:70-73, :320)
         c.loss_cauchy = 0;
@@ -179,6 +185,10 @@ private:
         c.voxel_size = m_voxel_size;
         c.hierarchy_factor = m_hierarchy_factor;
         c.max_points = m_max_points;
+        return c;
+    }
+    void create_context() {
+        lo_config c = make_config(m_config);
         int err = 0;
         m_ctx = lo_create(&c, m_device, &err);   // rejects what the device kernels cannot take (gmm_components > 3, ...)
         if (!m_ctx) throw std::runtime_error("lo_create failed with code " + std::to_string(err));
@@ -239,6 +249,7 @@ private:
     int m_device;
     int m_max_points;
     OptimizationStats m_last_stats;
+    int m_last_sync_patched = 0;
     lo_ctx* m_ctx = nullptr;
 };
 

@@ -121,6 +121,14 @@ int lo_map_set_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normal
  * map with lo_map_set_surfels instead. */
 int lo_map_patch_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids,
                          const uint8_t* present, size_t m);
+/* The reference-side sync after UpdateVoxelMap (Estimator.cpp:457) for a caller that keeps the reference's own VoxelMap:
+ * the map's whole current surfel set (GetL1Surfels, VoxelMap.cpp:405-418, filed under L1 keys) is diffed on the host
+ * against the set this context last received through this call, and only the difference -- new or refitted surfels,
+ * surfels that left (VoxelMap.cpp:187-261) -- is patched into the device table in place (lo_map_patch_surfels), so
+ * the device work is O(changed voxels).  The first call, a table changed by anything else since, or a table too full
+ * for the patch upload everything (lo_map_set_surfels).  patched (nullable): records sent, -1 after a full upload. */
+int lo_map_sync_surfels(lo_ctx* ctx, const int32_t* keys_xyz, const float* normals, const float* centroids, size_t m,
+                        int* patched);
 size_t lo_map_surfel_count(const lo_ctx* ctx);
 
 /* KDTree variant (use_surfel_correspondence = 0): the map point cloud the reference's kd-tree indexes,
@@ -164,6 +172,10 @@ int lo_set_exact(lo_ctx* ctx, int enable);
  * the context stream after an optimize sees its final result; lo_sync drains both streams.  main_iterations 0 keeps
  * the current split. */
 int lo_set_pipeline(lo_ctx* ctx, int enable, int main_iterations);
+/* IterativeClosestPointOptimizer::update_config (IterativeClosestPointOptimizer.h:220): new parameters, same context --
+ * the device map, buffers and stream stay.  voxel_size, hierarchy_factor, max_points and use_surfel_correspondence
+ * are fixed at lo_create (LO_ERR_STATE); new PKO parameters rebuild the PKO tables. */
+int lo_update_config(lo_ctx* ctx, const lo_config* cfg);
 /* Scan-pipeline state: out[0] enabled, out[1] main iterations, out[2] timeouts (a device-side wait gave up -- the two
  * streams were not run concurrently -- and the pipeline was switched off), out[3] synchronous scans re-run on one
  * stream after a timeout.  A scan whose wait timed out reports LO_ERR_PIPELINE in its device status (the exported
@@ -287,6 +299,11 @@ int lo_pko_sample_indices(lo_ctx* ctx, size_t n, int32_t* out);
  * addition, for n <= 16384 non-negative doubles -- computed by the device kernel the exact mode uses (lo_seqsum.h).
  * stats (nullable): segment heads (-1: the plain chain ran), fallback segments, fallback terms, device cycles. */
 int lo_seq_sum_f64(lo_ctx* ctx, const double* x, size_t n, int sort, double* out_sum, long long stats[4]);
+/* Parity entry point of the large-scan exact normal equations (IterativeClosestPointOptimizer.cpp:359-415: running fp32
+ * sums in correspondence order): s = 0.0f; s += x[i] in index order, one fp32 rounding per addition, terms of any sign,
+ * computed by the device kernel the exact mode uses for scans beyond 16384 points (lo_seqsum.h signed_seq_sum).
+ * stats (nullable): segment heads, segments summed term by term, chunks on the plain chain, device cycles. */
+int lo_seq_sum_f32(lo_ctx* ctx, const float* x, size_t n, float* out_sum, long long stats[4]);
 /* Diagnostic: 16 device counters (phase timestamps of the -DLO_PKO_STAMPS build; zeros otherwise). */
 int lo_debug_counters(lo_ctx* ctx, unsigned long long out[16]);
 /* Context-free host variant (no GPU needed): sample_size = gmm_sample_size. */

@@ -135,15 +135,9 @@ __device__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double 
         double xv[kScaleGPT];
 #pragma unroll
         for (int a = 0; a < kScaleGPT; ++a) xv[a] = s_x[base + a];
-        double Tn;
-        if (mono_seq_sum<kScaleGPT>(xv, mc, s_x, S, Tc, ec, true, s, s, &Tn)) {
-            Tc = Tn;
-            ec = S.e_carry;
-        } else {
-            s = chain_seq_sum(s_x, mc, s, S);
-            Tc = s;
-            ec = binade64(s);
-        }
+        if (mono_seq_sum<kScaleGPT>(xv, mc, s_x, S, Tc, ec, true, s, s, nullptr)) ec = S.e_carry;
+        else { s = chain_seq_sum(s_x, mc, s, S); ec = binade64(s); }
+        Tc = s;                                                // the exact running sum predicts the next chunk best
         __syncthreads();                                       // s_x / S reuse by the next chunk
     }
     return s;
@@ -263,10 +257,13 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
     __syncthreads();
     const int i = blockIdx.x * kBlock + tid;
     if (i >= scan_n(P)) return;
-    float* out = P.ex_terms + static_cast<size_t>(i) * kExactTerms;
+    // row-major [point][43], or term-major [43][ex_ld] (coalesced columns for k_exact_sum43)
+    const size_t o0 = P.ex_ld ? static_cast<size_t>(i) : static_cast<size_t>(i) * kExactTerms;
+    const size_t os = P.ex_ld ? static_cast<size_t>(P.ex_ld) : 1;
+    float* out = P.ex_terms + o0;
     const int s = P.slot[i];
     if (s < 0) {
-        for (int k = 0; k < kExactTerms; ++k) out[k] = 0.0f;
+        for (int k = 0; k < kExactTerms; ++k) out[k * os] = 0.0f;
         return;
     }
     float T[12];
@@ -289,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
     for (int k = 0; k < kExactTerms; ++k) {
         int fa, fb;
         exact_term_factors(k, fa, fb);
-        out[k] = f[fa] * f[fb];
+        out[k * os] = f[fa] * f[fb];
     }
 }
 
@@ -349,6 +346,99 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
     float tf[kExactTerms], pn[12], delta[6];
     for (int k = 0; k < kExactTerms; ++k) tf[k] = tot[k];
     const bool conv = exact_solve_step(tf, st->pose, P.tol_t, P.tol_r, pn, delta);
+    for (int q = 0; q < 12; ++q) st->pose[q] = pn[q];
+    if (it < LO_MAX_ITERS) {
+        lo_iter_log& L = st->logs[it];
+        for (int q = 0; q < 12; ++q) L.pose[q] = pn[q];
+        L.n_corr = st->n_corr;
+        L.scale = st->scale;
+        L.alpha = st->alpha;
+        L.cost = tot[42];
+        int k = 0;
+        for (int r = 0; r < 6; ++r) for (int c = r; c < 6; ++c) L.H[k++] = tot[r * 6 + c];
+        for (int j = 0; j < 6; ++j) { L.g[j] = tot[36 + j]; L.delta[j] = delta[j]; }
+    }
+    st->iter = it + 1;
+    if (conv) st->done = 1;
+}
+
+// ---- large scans (n > kExactMaxPoints): the 43 running sums of build_ne in point order, one workgroup per term
+// column of the term-major buffer, each reproduced by signed_seq_sum (lo_seqsum.h: integer prefix sums between the
+// running sum's predicted binade / sign changes) chunk by chunk; k_exact_finish then solves as k_exact_solve does ----
+constexpr int kSumPT = 8;
+constexpr int kSumChunk = kSeqThreads * kSumPT;
+// col[0, n) summed in fp32 in index order, as the reference's running sums do; stats (nullable): heads, segments
+// summed term by term, chunks that fell back to the plain chain.
+__device__ float column_seq_sum(const float* __restrict__ col, int n, float* s_x, SeqScratchS& S, int* stats) {
+    const int tid = threadIdx.x, base = tid * kSumPT;
+    float s = 0.0f;
+    int ec = kExpNone, gc = 0, nh = 0, fb = 0, chains = 0;
+    for (int c0 = 0; c0 < n; c0 += kSumChunk) {
+        const int mc = min(kSumChunk, n - c0);
+        for (int t = tid; t < kSumChunk; t += kSeqThreads) s_x[t] = t < mc ? col[c0 + t] : 0.0f;
+        __syncthreads();
+        float xv[kSumPT];
+#pragma unroll
+        for (int a = 0; a < kSumPT; ++a) xv[a] = s_x[base + a];
+        double Tn;
+        int en, gn;
+        if (signed_seq_sum<kSumPT>(xv, mc, s_x, S, static_cast<double>(s), ec, gc, s, s, Tn, en, gn)) {
+            nh += S.nheads;
+            fb += S.fb_seg;
+        } else {
+            if (tid < kWave) {                                 // more heads than the list holds: the plain chain
+                for (int j = 0; j < mc; ++j) s = s + s_x[j];
+                if (tid == 0) S.result = s;
+            }
+            __syncthreads();
+            s = S.result;
+            en = binade_abs(static_cast<double>(s));
+            gn = s > 0.0f ? 1 : (s < 0.0f ? -1 : 0);
+            ++chains;
+        }
+        ec = en;
+        gc = gn;
+        __syncthreads();                                       // s_x / S reuse by the next chunk
+    }
+    if (stats && tid == 0) { stats[0] = nh; stats[1] = fb; stats[2] = chains; }
+    return s;
+}
+__global__ __launch_bounds__(kSeqThreads) void k_exact_sum43(KParams P) {
+    DevState* st = P.st;
+    if (st->done) return;
+    __shared__ float s_x[kSumChunk];
+    __shared__ SeqScratchS S;
+    const float s = column_seq_sum(P.ex_terms + static_cast<size_t>(blockIdx.x) * P.ex_ld, scan_n(P), s_x, S, nullptr);
+    if (threadIdx.x == 0) P.ex_tot[blockIdx.x] = s;
+}
+// Parity / diagnostic entry (lo_seq_sum_f32): one column through the same reproduction.
+__global__ __launch_bounds__(kSeqThreads) void k_seq_sum_f32_diag(const float* __restrict__ x, int n, float* out,
+                                                                  long long* stats) {
+    __shared__ float s_x[kSumChunk];
+    __shared__ SeqScratchS S;
+    __shared__ int st3[3];
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const float s = column_seq_sum(x, n, s_x, S, st3);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = s;
+        stats[0] = st3[0];
+        stats[1] = st3[1];
+        stats[2] = st3[2];
+        stats[3] = static_cast<long long>(t1 - t0);
+    }
+}
+void launch_seq_sum_f32_diag(const float* x, int n, float* out, long long* stats, hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_sum_f32_diag, dim3(1), dim3(kSeqThreads), 0, s, x, n, out, stats);
+}
+
+__global__ void k_exact_finish(KParams P, int it) {
+    DevState* st = P.st;
+    if (st->done || threadIdx.x != 0) return;
+    float tot[kExactTerms], pn[12], delta[6];
+    for (int k = 0; k < kExactTerms; ++k) tot[k] = P.ex_tot[k];
+    const bool conv = exact_solve_step(tot, st->pose, P.tol_t, P.tol_r, pn, delta);
     for (int q = 0; q < 12; ++q) st->pose[q] = pn[q];
     if (it < LO_MAX_ITERS) {
         lo_iter_log& L = st->logs[it];

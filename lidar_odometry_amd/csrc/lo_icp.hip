@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,10 +67,13 @@ __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float t
                              FitOut* out);
 void launch_exact_scale(const KParams& P, int n, hipStream_t s);
 void launch_seq_sum_diag(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s);
+void launch_seq_sum_f32_diag(const float* x, int n, float* out, long long* stats, hipStream_t s);
 __global__ void k_exact_resid(KParams P, double* out);
 __global__ void k_exact_scale_g(KParams P, const double* sorted);
 __global__ void k_exact_terms(KParams P);
 __global__ void k_exact_solve(KParams P, int it);
+__global__ void k_exact_sum43(KParams P);
+__global__ void k_exact_finish(KParams P, int it);
 }  // namespace lo
 
 using namespace lo;
@@ -115,6 +119,7 @@ struct lo_ctx {
     bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
     float* d_ex_terms = nullptr;
     size_t ex_cap = 0;              //   rows of d_ex_terms
+    float* d_ex_tot = nullptr;      //   large scans: the 43 sums (k_exact_sum43 -> k_exact_finish)
     double* d_ex_res = nullptr;     //   scans beyond kExactMaxPoints: residuals, sorted residuals, hipCUB scratch
     double* d_ex_sorted = nullptr;
     void* d_ex_sort_tmp = nullptr;
@@ -140,6 +145,11 @@ struct lo_ctx {
     hipEvent_t ev_patch = nullptr;
     uint64_t map_src = 0, map_epoch = 0, map_pos = 0;
     uint64_t tab_gen = 0;           // bumped by every full upload (a pending fit's results no longer apply to it)
+    uint64_t tab_edit = 0;          // bumped by every change of the table (uploads, patches, fits, a device map's claim)
+    // lo_map_sync_surfels: the surfel set last synced through it (key -> normal, centroid), valid while the table has
+    // not been changed by anything else since (mirror_edit == tab_edit)
+    std::unordered_map<uint64_t, std::array<float, 6>> smirror;
+    uint64_t mirror_edit = ~0ull;
     uint64_t devmap_gen = 0;        // the generation a device map (lo_devmap) reserved and maintains
     // deferred surfel fits of a synced host map (lo::ctx_fit_surfels): pinned in / out staging, device copies
     void* h_fit_in = nullptr;
@@ -464,6 +474,34 @@ static int kd_alloc(lo_ctx* c) {
     return LO_OK;
 }
 
+// PKO tables (alpha grid, Z(alpha), the shuffle tables, the k-means draws), host-built for the context's config
+static int upload_pko_tables(lo_ctx* c) {
+    const lo_config& g = c->cfg;
+    for (void* p : {static_cast<void*>(c->d_alphas), static_cast<void*>(c->d_Z), static_cast<void*>(c->d_tabs_i)})
+        if (p) LO_HIP(c, hipFree(p));
+    c->d_alphas = nullptr;
+    c->d_Z = nullptr;
+    c->d_tabs_i = nullptr;
+    build_pko_tables(c->tables, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
+                     g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel);
+    const PkoTables& t = c->tables;
+    LO_HIP(c, hipMalloc(&c->d_alphas, t.alphas.size() * sizeof(double)));
+    LO_HIP(c, hipMalloc(&c->d_Z, t.Z.size() * sizeof(double)));
+    LO_HIP(c, hipMemcpy(c->d_alphas, t.alphas.data(), t.alphas.size() * sizeof(double), hipMemcpyHostToDevice));
+    LO_HIP(c, hipMemcpy(c->d_Z, t.Z.data(), t.Z.size() * sizeof(double), hipMemcpyHostToDevice));
+    std::vector<int32_t> all;
+    auto append = [&](const std::vector<int32_t>& v, size_t& off) { off = all.size(); all.insert(all.end(), v.begin(), v.end()); all.push_back(0); };
+    append(t.small_off, c->off_small_off);
+    append(t.small_perm, c->off_small_perm);
+    append(t.base, c->off_base);
+    append(t.ev_off, c->off_ev_off);
+    append(t.ev_steps, c->off_ev_steps);
+    append(t.km_draws, c->off_km);
+    LO_HIP(c, hipMalloc(&c->d_tabs_i, all.size() * sizeof(int32_t)));
+    LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return LO_OK;
+}
+
 static int ctx_alloc(lo_ctx* c) {
     const lo_config& g = c->cfg;
     LO_HIP(c, hipSetDevice(c->device));
@@ -488,28 +526,12 @@ static int ctx_alloc(lo_ctx* c) {
     c->log2cap = 1;
     LO_HIP(c, hipMalloc(&c->d_tab, c->tab_cap * sizeof(Slot)));
     LO_HIP(c, hipMemset(c->d_tab, 0xff, c->tab_cap * sizeof(Slot)));
-    // PKO tables
-    build_pko_tables(c->tables, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
-                     g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel);
-    const PkoTables& t = c->tables;
-    LO_HIP(c, hipMalloc(&c->d_alphas, t.alphas.size() * sizeof(double)));
-    LO_HIP(c, hipMalloc(&c->d_Z, t.Z.size() * sizeof(double)));
-    LO_HIP(c, hipMemcpy(c->d_alphas, t.alphas.data(), t.alphas.size() * sizeof(double), hipMemcpyHostToDevice));
-    LO_HIP(c, hipMemcpy(c->d_Z, t.Z.data(), t.Z.size() * sizeof(double), hipMemcpyHostToDevice));
-    std::vector<int32_t> all;
-    auto append = [&](const std::vector<int32_t>& v, size_t& off) { off = all.size(); all.insert(all.end(), v.begin(), v.end()); all.push_back(0); };
-    append(t.small_off, c->off_small_off);
-    append(t.small_perm, c->off_small_perm);
-    append(t.base, c->off_base);
-    append(t.ev_off, c->off_ev_off);
-    append(t.ev_steps, c->off_ev_steps);
-    append(t.km_draws, c->off_km);
-    LO_HIP(c, hipMalloc(&c->d_tabs_i, all.size() * sizeof(int32_t)));
-    LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    const int rc_t = upload_pko_tables(c);
+    if (rc_t != LO_OK) return rc_t;
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
     // k_pko_t's dynamic block-prefix LDS reaches 64 KB at the 4M-point maximum
-    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(kMaxBlocks * sizeof(int))));
     c->kd = g.use_surfel_correspondence == 0;
     if (c->kd) {
@@ -577,7 +599,7 @@ void lo_destroy(lo_ctx* c) {
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_ex_terms, c->d_res_pko,
-                    c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp,
+                    c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp, c->d_ex_tot,
                     c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
@@ -646,6 +668,7 @@ int lo_map_set_surfels(lo_ctx* c, const int32_t* keys, const float* normals, con
     c->n_tomb = 0;
     c->map_src = 0;                                      // no longer mirrors a synced host map
     ++c->tab_gen;
+    ++c->tab_edit;
     return LO_OK;
 }
 
@@ -693,6 +716,7 @@ int ctx_reserve_table(lo_ctx* c, size_t min_slots, void** tab, uint32_t* log2cap
         ++c->tab_gen;
         c->devmap_gen = c->tab_gen;
     }
+    ++c->tab_edit;                                       // the device map patches the table from now on
     *tab = c->d_tab;
     *log2cap = c->log2cap;
     *gen = c->tab_gen;
@@ -789,6 +813,7 @@ int ctx_fit_surfels(lo_ctx* c, const int32_t* keys, const int32_t* offs, size_t 
         c->fit_ticket = ++g_ticket;
     }
     c->fit_gen = c->tab_gen;
+    ++c->tab_edit;
     c->fit_keys.swap(pk);
     c->fit_reconciled = false;
     c->fit_thr = thr;
@@ -881,11 +906,120 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     c->n_tomb += ers;
     c->n_surfels = c->resident.size();
     if (n_rec == 0) return LO_OK;
+    ++c->tab_edit;
     LO_HIP(c, hipMemcpyAsync(c->d_patch, c->h_patch, n_rec * sizeof(MapPatchRec), hipMemcpyHostToDevice, c->stream));
     LO_HIP(c, hipEventRecord(c->ev_patch, c->stream));
     hipLaunchKernelGGL(k_map_patch, dim3((n_rec + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, c->d_tab,
                        c->log2cap, static_cast<const MapPatchRec*>(c->d_patch), n_rec);
     LO_HIP(c, hipGetLastError());
+    return LO_OK;
+}
+
+// The reference-side sync: the map's whole current surfel set, diffed on the host against the set this
+// context last received through this call; only the difference goes to the device (lo_map_patch_surfels: upserts of
+// new / refitted surfels, erases of the ones that left).  The first call, a table changed by anything else since, or a
+// full table uploads everything (lo_map_set_surfels).  *patched = records sent, -1 after a full upload.
+int lo_map_sync_surfels(lo_ctx* c, const int32_t* keys, const float* normals, const float* centroids, size_t m,
+                        int* patched) {
+    if (!c) return LO_ERR_ARG;
+    if (m > 0 && (!keys || !normals || !centroids)) { c->err = "null surfel arrays"; return LO_ERR_ARG; }
+    if (c->kd) { c->err = "KDTree-mode context (lo_map_set_points)"; return LO_ERR_STATE; }
+    std::unordered_map<uint64_t, size_t> in;
+    in.reserve(2 * m);
+    for (size_t i = 0; i < m; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            const int32_t v = keys[3 * i + a];
+            if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
+        }
+        in[pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2])] = i;   // a repeated key: the last record
+    }
+    auto payload = [&](size_t i) {
+        return std::array<float, 6>{normals[3 * i], normals[3 * i + 1], normals[3 * i + 2], centroids[3 * i],
+                                    centroids[3 * i + 1], centroids[3 * i + 2]};
+    };
+    auto full = [&]() -> int {
+        const int rc = lo_map_set_surfels(c, keys, normals, centroids, m);
+        if (rc != LO_OK) return rc;
+        c->smirror.clear();
+        c->smirror.reserve(2 * in.size());
+        for (const auto& kv : in) c->smirror[kv.first] = payload(kv.second);
+        c->mirror_edit = c->tab_edit;
+        if (patched) *patched = -1;
+        return LO_OK;
+    };
+    if (c->mirror_edit != c->tab_edit) return full();
+    std::vector<int32_t> pk;
+    std::vector<float> pn, pc;
+    std::vector<uint8_t> pres;
+    for (const auto& kv : in) {
+        const std::array<float, 6> p = payload(kv.second);
+        auto it = c->smirror.find(kv.first);
+        if (it != c->smirror.end() && std::memcmp(it->second.data(), p.data(), sizeof(p)) == 0) continue;   // unchanged
+        const size_t i = kv.second;
+        pk.insert(pk.end(), {keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]});
+        pn.insert(pn.end(), {p[0], p[1], p[2]});
+        pc.insert(pc.end(), {p[3], p[4], p[5]});
+        pres.push_back(1);
+    }
+    for (const auto& kv : c->smirror) {
+        if (in.count(kv.first)) continue;                 // still a surfel
+        const uint64_t k = kv.first;
+        pk.insert(pk.end(), {static_cast<int32_t>(k & 0x1FFFFF) - (1 << 20), static_cast<int32_t>((k >> 21) & 0x1FFFFF) - (1 << 20),
+                             static_cast<int32_t>((k >> 42) & 0x1FFFFF) - (1 << 20)});
+        pn.insert(pn.end(), {0.0f, 0.0f, 0.0f});
+        pc.insert(pc.end(), {0.0f, 0.0f, 0.0f});
+        pres.push_back(0);
+    }
+    const size_t np = pres.size();
+    if (np == 0) { if (patched) *patched = 0; return LO_OK; }
+    const int rc = lo_map_patch_surfels(c, pk.data(), pn.data(), pc.data(), pres.data(), np);
+    if (rc == LO_ERR_CAPACITY) return full();            // tombstones / growth: rebuild the table
+    if (rc != LO_OK) return rc;
+    for (size_t r = 0; r < np; ++r) {
+        const uint64_t k = pack_key_host(pk[3 * r], pk[3 * r + 1], pk[3 * r + 2]);
+        if (pres[r]) c->smirror[k] = {pn[3 * r], pn[3 * r + 1], pn[3 * r + 2], pc[3 * r], pc[3 * r + 1], pc[3 * r + 2]};
+        else c->smirror.erase(k);
+    }
+    c->mirror_edit = c->tab_edit;
+    if (patched) *patched = static_cast<int>(np);
+    return LO_OK;
+}
+
+// IterativeClosestPointOptimizer::update_config (IterativeClosestPointOptimizer.h:220) replaces the parameters and
+// nothing else: the device map, the scan buffers and the stream stay.  The layout fields (voxel geometry, max_points,
+// correspondence mode) size or key those and cannot change here.  New PKO parameters rebuild the PKO tables.
+int lo_update_config(lo_ctx* c, const lo_config* cfg) {
+    if (!c) return LO_ERR_ARG;
+    std::string e;
+    int rc = validate_config(cfg, e);
+    if (rc != LO_OK) { c->err = e; return rc; }
+    const lo_config& o = c->cfg;
+    if (cfg->voxel_size != o.voxel_size || cfg->hierarchy_factor != o.hierarchy_factor || cfg->max_points != o.max_points ||
+        cfg->use_surfel_correspondence != o.use_surfel_correspondence) {
+        c->err = "update_config: voxel_size / hierarchy_factor / max_points / use_surfel_correspondence are fixed at lo_create";
+        return LO_ERR_STATE;
+    }
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, sync_all(c));
+    const bool pko_changed = cfg->gmm_sample_size != o.gmm_sample_size || cfg->gmm_components != o.gmm_components ||
+                             cfg->min_scale_factor != o.min_scale_factor || cfg->max_scale_factor != o.max_scale_factor ||
+                             cfg->num_alpha_segments != o.num_alpha_segments ||
+                             cfg->truncated_threshold != o.truncated_threshold || cfg->pko_kernel != o.pko_kernel;
+    const bool na_changed = cfg->num_alpha_segments != o.num_alpha_segments;
+    c->cfg = *cfg;
+    if (pko_changed) {
+        rc = upload_pko_tables(c);
+        if (rc != LO_OK) return rc;
+    }
+    if (na_changed || (cfg->use_adaptive_m_estimator && !c->d_acc_part)) {
+        // the candidate buffers are sized by the alpha grid: re-made on the next optimize
+        if (c->d_acc_part) LO_HIP(c, hipFree(c->d_acc_part));
+        if (c->d_cand_rec) LO_HIP(c, hipFree(c->d_cand_rec));
+        if (c->d_cand_cnt) LO_HIP(c, hipFree(c->d_cand_cnt));
+        c->d_acc_part = nullptr;
+        c->d_cand_rec = nullptr;
+        c->d_cand_cnt = nullptr;
+    }
     return LO_OK;
 }
 
@@ -1061,6 +1195,9 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
     if (n > static_cast<size_t>(kExactMaxPoints)) {
+        if (!c->d_ex_tot) LO_HIP(c, hipMalloc(&c->d_ex_tot, 64 * sizeof(float)));
+        P.ex_ld = static_cast<int>(n);                     // term-major: one coalesced column per sum
+        P.ex_tot = c->d_ex_tot;
         if (c->ex_res_cap < n) {
             if (c->d_ex_res) LO_HIP(c, hipFree(c->d_ex_res));
             if (c->d_ex_sorted) LO_HIP(c, hipFree(c->d_ex_sorted));
@@ -1099,7 +1236,12 @@ static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P
     if (it == 0) launch_exact_scale_any(c, P, n2, c->stream);
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
-    hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
+    if (P.ex_ld) {                                           // large scan: 43 parallel sequential-sum reproductions
+        hipLaunchKernelGGL(k_exact_sum43, dim3(43), dim3(1024), 0, c->stream, P);
+        hipLaunchKernelGGL(k_exact_finish, dim3(1), dim3(64), 0, c->stream, P, it);
+    } else {
+        hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
+    }
 }
 
 static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float T_init[12], const int* n_dev = nullptr) {
@@ -1771,6 +1913,24 @@ int lo_seq_sum_f64(lo_ctx* c, const double* x, size_t n, int sort, double* out_s
     if (e == hipSuccess) e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) { c->err = std::string("lo_seq_sum_f64: ") + hipGetErrorString(e); return LO_ERR_HIP; }
+    if (stats) for (int k = 0; k < 4; ++k) stats[k] = st[k];
+    return LO_OK;
+}
+
+int lo_seq_sum_f32(lo_ctx* c, const float* x, size_t n, float* out_sum, long long stats[4]) {
+    if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(INT32_MAX)) return LO_ERR_ARG;
+    LO_HIP(c, hipSetDevice(c->device));
+    float* d = nullptr;
+    LO_HIP(c, hipMalloc(&d, (n + 2) * sizeof(float) + 4 * sizeof(long long)));
+    long long* d_st = reinterpret_cast<long long*>(reinterpret_cast<char*>(d) + ((n + 2) * sizeof(float) + 7) / 8 * 8);
+    if (n > 0) LO_HIP(c, hipMemcpy(d, x, n * sizeof(float), hipMemcpyHostToDevice));
+    launch_seq_sum_f32_diag(d, static_cast<int>(n), d + n, d_st, c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    long long st[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(out_sum, d + n, sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) { c->err = std::string("lo_seq_sum_f32: ") + hipGetErrorString(e); return LO_ERR_HIP; }
     if (stats) for (int k = 0; k < 4; ++k) stats[k] = st[k];
     return LO_OK;
 }

@@ -23,6 +23,8 @@
 // chain.  Prototype + randomized check against the sequential loop: tests/test_seqsum.py (CPU) and
 // tests/test_gpu_exact.py (bit-identical scales through the whole GN step).
 #pragma once
+#include <climits>
+
 #include "lo_device.h"
 
 namespace lo {
@@ -125,7 +127,7 @@ __device__ bool mono_seq_sum(const double (&x)[PT], int cnt, const double* s_x, 
         const int j = base + a;
         bool head = false;
         long long qa = 0;
-        if (j < cnt && x[a] != 0.0) {
+        if (j < cnt && (x[a] != 0.0 || (head0 && j == 0))) {   // a chunk's first term heads it even when zero
             const int E = e[a];
             if (E < -1000 || E != ep || (head0 && j == 0)) {
                 head = true;
@@ -313,6 +315,195 @@ __device__ void bitonic_sort_block(double (&v)[PT], double* s_x) {
         if (j >= 2) bitonic_reg<PT, 2>(v, base, k);
         if (j >= 1) bitonic_reg<PT, 1>(v, base, k);
     }
+}
+
+}  // namespace lo
+
+namespace lo {
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Signed fp32 sequential sums (the reference's build_ne accumulates H, g and the cost as running fp32 sums,
+// IterativeClosestPointOptimizer.cpp:359-415).  The same idea as mono_seq_sum, for terms of either sign: while the
+// running sum s keeps its sign and binade [2^E, 2^(E+1)) in magnitude, fl(s + x) = s + u rint(x / u) with u = 2^(E-23).
+// A segment's partial sums are no longer monotone, so its check bounds the smallest and the largest integer prefix over
+// the segment (segment minima / maxima by LDS atomics), and a segment also ends where the predicted sign changes.
+// Terms come in chunks (kSeqThreads * PT), each chunk starting a segment; the walk carries s from chunk to chunk.
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int kSHeadCap = 2048;
+
+struct SeqScratchS {
+    double wd[kSeqWaves];
+    long long wl[kSeqWaves];
+    int wi[kSeqWaves];
+    int elast[kSeqThreads];
+    int glast[kSeqThreads];
+    int h_idx[kSHeadCap];
+    int h_e[kSHeadCap];
+    int h_g[kSHeadCap];
+    long long h_p[kSHeadCap];
+    long long h_min[kSHeadCap];
+    long long h_max[kSHeadCap];
+    float result;
+    int e_carry, g_carry;
+    int nheads, fb_seg;
+};
+
+__device__ __forceinline__ int binade_abs(double v) {       // binade of |v| when it is a normal fp32 magnitude
+    const double a = fabs(v);
+    const uint64_t b = __builtin_bit_cast(uint64_t, a);
+    const int f = static_cast<int>((b >> 52) & 0x7FF);
+    const int e = f - 1023;
+    return (a > 0.0 && f != 0x7FF && e >= -120 && e <= 126) ? e : kExpNone;
+}
+
+// s_in + x_0 + ... + x_{cnt-1} in fp32, one rounding per addition in index order; thread t holds terms t*PT.. (zeros past
+// cnt), s_x[0, cnt) the same terms (LDS).  T0 / e0 / g0: the approximate prefix, predicted binade and sign carried in
+// from the previous chunk; term 0 always starts a segment.  Every thread returns the sum and the carries; false (nothing
+// computed) when the chunk has more than kSHeadCap heads.
+template <int PT>
+__device__ bool signed_seq_sum(const float (&x)[PT], int cnt, const float* s_x, SeqScratchS& S, double T0, int e0,
+                               int g0, float s_in, float& s_out, double& T_out, int& e_out, int& g_out) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int base = tid * PT;
+    double tl[PT];
+    double run = 0.0;
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        run += (base + a < cnt) ? static_cast<double>(x[a]) : 0.0;
+        tl[a] = run;
+    }
+    double ttot;
+    const double tex = T0 + block_excl_scan<double>(run, S.wd, ttot);
+    int e[PT], g[PT];
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        const double T = tex + tl[a];
+        e[a] = binade_abs(T);
+        g[a] = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
+    }
+    S.elast[tid] = e[PT - 1];
+    S.glast[tid] = g[PT - 1];
+    __syncthreads();
+    int ep = tid ? S.elast[tid - 1] : e0, gp = tid ? S.glast[tid - 1] : g0;
+    long long q[PT];
+    bool hd[PT];
+    long long ql = 0;
+    int nhl = 0;
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        const int j = base + a;
+        bool head = false;
+        long long qa = 0;
+        if (j < cnt && (x[a] != 0.0f || j == 0)) {             // a chunk's first term heads it even when zero
+            const int E = e[a];
+            if (E == kExpNone || E != ep || g[a] != gp || j == 0) {
+                head = true;
+            } else {
+                const double t = ldexp(static_cast<double>(x[a]), 23 - E);   // exact
+                const double f = floor(t), fr = t - f;
+                if (fr == 0.5) head = true;
+                else qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
+            }
+        }
+        ep = e[a];
+        gp = g[a];
+        hd[a] = head;
+        q[a] = qa;
+        ql += qa;
+        nhl += head ? 1 : 0;
+    }
+    long long ptot;
+    const long long pex = block_excl_scan<long long>(ql, S.wl, ptot);
+    int htot;
+    const int hbase = block_excl_scan<int>(nhl, S.wi, htot);
+    if (htot > kSHeadCap) return false;
+    for (int k = tid; k < htot; k += kSeqThreads) { S.h_min[k] = LLONG_MAX; S.h_max[k] = LLONG_MIN; }
+    long long prun = pex;
+    int hk = hbase;
+    long long P[PT];
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        prun += q[a];
+        P[a] = prun;
+        if (hd[a]) { S.h_idx[hk] = base + a; S.h_e[hk] = e[a]; S.h_g[hk] = g[a]; S.h_p[hk] = prun; ++hk; }
+    }
+    if (tid == kSeqThreads - 1) { S.e_carry = e[PT - 1]; S.g_carry = g[PT - 1]; }
+    if (tid == 0) S.nheads = htot;
+    __syncthreads();
+    // segment minima / maxima of P over the non-head terms (a thread's terms are consecutive: one flush per segment run)
+    {
+        int seg = hbase - 1;
+        long long mn = LLONG_MAX, mx = LLONG_MIN;
+#pragma unroll
+        for (int a = 0; a < PT; ++a) {
+            const int j = base + a;
+            if (j >= cnt) break;
+            if (hd[a]) {
+                if (seg >= 0 && mn != LLONG_MAX) { atomicMin(&S.h_min[seg], mn); atomicMax(&S.h_max[seg], mx); }
+                ++seg;
+                mn = LLONG_MAX;
+                mx = LLONG_MIN;
+                continue;
+            }
+            if (seg < 0) continue;                               // zeros before the first head
+            mn = P[a] < mn ? P[a] : mn;
+            mx = P[a] > mx ? P[a] : mx;
+        }
+        if (seg >= 0 && mn != LLONG_MAX) { atomicMin(&S.h_min[seg], mn); atomicMax(&S.h_max[seg], mx); }
+    }
+    __syncthreads();
+    if (wid == 0) {
+        float s = s_in;
+        int fbs = 0;
+        for (int k0 = 0; k0 < htot; k0 += 64) {
+            const int kk = k0 + lane;
+            int hi = 0, he = 0, hg = 0, hend = cnt;
+            long long hp = 0, pend = ptot, hmn = LLONG_MAX, hmx = LLONG_MIN;
+            float hx = 0.0f;
+            if (kk < htot) {
+                hi = S.h_idx[kk];
+                he = S.h_e[kk];
+                hg = S.h_g[kk];
+                hp = S.h_p[kk];
+                hmn = S.h_min[kk];
+                hmx = S.h_max[kk];
+                hx = s_x[hi];
+                if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
+            }
+            const int m = min(64, htot - k0);
+            for (int l = 0; l < m; ++l) {
+                const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hx), l));
+                if (end > h + 1) {
+                    const int E = __builtin_amdgcn_readlane(he, l), G = __builtin_amdgcn_readlane(hg, l);
+                    const long long p0 = rl64i(hp, l);
+                    const long long lo_q = rl64i(hmn, l) - p0, hi_q = rl64i(hmx, l) - p0, Q = rl64i(pend, l) - p0;
+                    const double d = static_cast<double>(s);
+                    const double u = ldexp(1.0, E - 23);
+                    const double lo = ldexp(1.0, E) + u, top = ldexp(1.0, E + 1) - u;
+                    bool ok = binade_abs(d) == E && E != kExpNone && (G > 0 ? d > 0.0 : d < 0.0) &&
+                              rl64i(hmn, l) != LLONG_MAX;
+                    if (ok) {
+                        const double a0 = d + static_cast<double>(lo_q) * u, a1 = d + static_cast<double>(hi_q) * u;
+                        ok = G > 0 ? (a0 >= lo && a1 <= top) : (-a1 >= lo && -a0 <= top);
+                    }
+                    if (ok) {
+                        s = static_cast<float>(d + static_cast<double>(Q) * u);
+                    } else {
+                        for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                        ++fbs;
+                    }
+                }
+            }
+        }
+        if (lane == 0) { S.result = s; S.fb_seg = fbs; }
+    }
+    __syncthreads();
+    s_out = S.result;
+    T_out = T0 + ttot;
+    e_out = S.e_carry;
+    g_out = S.g_carry;
+    return true;
 }
 
 }  // namespace lo

@@ -182,6 +182,30 @@ class IterativeClosestPointOptimizer:
             raise ValueError("keys/normals/centroids length mismatch")
         self._check(lib().lo_map_set_surfels(self._ctx, k.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(n), _fptr(c), len(k)))
 
+    def sync_surfels(self, keys, normals, centroids) -> int:
+        """The map's whole current surfel set after UpdateVoxelMap; only the difference to the last sync is patched into
+        the device table (lo_map_sync_surfels).  Returns the records sent, -1 after a full upload."""
+        k = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 3)
+        n = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        c = np.ascontiguousarray(centroids, dtype=np.float32).reshape(-1, 3)
+        if not (len(k) == len(n) == len(c)):
+            raise ValueError("keys/normals/centroids length mismatch")
+        patched = C.c_int(0)
+        self._check(lib().lo_map_sync_surfels(self._ctx, k.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(n), _fptr(c),
+                                              len(k), C.byref(patched)))
+        return int(patched.value)
+
+    def update_config(self, config: ICPConfig):
+        """IterativeClosestPointOptimizer::update_config (IterativeClosestPointOptimizer.h:220): new parameters, same
+        context -- the device map stays (lo_update_config)."""
+        cfg = make_config(config, self.adaptive, self.geometry, self._cfg.max_points)
+        self._check(self._L.lo_update_config(self.ctx, C.byref(cfg)))
+        self.config = config
+        self._cfg = cfg
+
+    def get_config(self) -> ICPConfig:
+        return self.config
+
     def set_map_points(self, points):
         """KDTree variant: upload VoxelMap::GetPointCloud (L0 centroids, L0 order) -- RebuildKdTree's input."""
         p = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)

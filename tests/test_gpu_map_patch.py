@@ -233,3 +233,69 @@ def test_device_fit_count_before_the_map_is_read():
             assert A.surfel_count() == vb.surfel_count()     # before va is read
     finally:
         A.close()
+
+
+def test_sync_surfels_sends_only_the_difference():
+    """lo_map_sync_surfels (the reference-side sync of a caller that keeps its own VoxelMap): the whole current surfel
+    set goes in, only the changed voxels reach the device, and every lookup equals a full upload's."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=42)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A, B = _ctx(), _ctx()
+    try:
+        prev = None
+        for k in range(0, 41, 2):
+            T = seq.poses[k]
+            vm.update(synth.transform(T, voxel_filter(seq.scan(k), 0.5, 8)), T[:3, 3], 60.0, True)
+            keys, nrm, ctr, _ = vm.surfels()
+            p = A.sync_surfels(keys, nrm, ctr)
+            B.set_surfels(keys, nrm, ctr)
+            cur = {tuple(kk): (tuple(nn), tuple(cc)) for kk, nn, cc in zip(keys.tolist(), nrm.tolist(), ctr.tolist())}
+            if prev is None:
+                assert p == -1                                  # first sync: full upload
+            else:
+                changed = sum(1 for kk, v in cur.items() if prev.get(kk) != v) + sum(1 for kk in prev if kk not in cur)
+                assert p == -1 or p == changed, (p, changed)
+            assert A.sync_surfels(keys, nrm, ctr) == 0          # nothing changed since
+            assert A.surfel_count() == B.surfel_count() == len(cur)
+            prev = cur
+            if k % 8 == 0:
+                f = k + 1
+                pts = voxel_filter(seq.scan(f), 0.5, 8)
+                _same_lookups(A, B, pts, [seq.poses[f][:3, :].astype(np.float32).reshape(12)])
+        # a table changed by anything else (a plain upload) makes the next sync a full one
+        A.set_surfels(keys[:10], nrm[:10], ctr[:10])
+        assert A.sync_surfels(keys, nrm, ctr) == -1
+        _same_lookups(A, B, pts, [seq.poses[41][:3, :].astype(np.float32).reshape(12)])
+    finally:
+        A.close()
+        B.close()
+
+
+def test_update_config_keeps_the_device_map():
+    """update_config (IterativeClosestPointOptimizer.h:220) replaces the parameters only: the next optimize runs on the
+    same device map, equal to a fresh context made with the new parameters."""
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
+    from tests import _data
+    m, pts, Ti, _ = _data.kitti_case(15, seed=5, sigma_t=0.3, sigma_r=0.03)
+    k, n, c = _data.surfels(m)
+    A = IterativeClosestPointOptimizer(max_points=1 << 16)
+    B = IterativeClosestPointOptimizer(ICPConfig(max_iterations=2, min_correspondence_points=20), max_points=1 << 16)
+    try:
+        A.set_surfels(k, n, c)
+        B.set_surfels(k, n, c)
+        ok4, _ = A.optimize(None, pts, Ti)
+        assert ok4 and A.get_last_stats().num_iterations >= 3
+        A.update_config(ICPConfig(max_iterations=2, min_correspondence_points=20))
+        okA, TA = A.optimize(None, pts, Ti)
+        okB, TB = B.optimize(None, pts, Ti)
+        assert okA and okB and A.get_last_stats().num_iterations == 2
+        np.testing.assert_array_equal(np.asarray(TA, np.float32).view(np.uint32), np.asarray(TB, np.float32).view(np.uint32))
+        from lidar_odometry_amd import MapGeometry
+        with pytest.raises(RuntimeError):                     # the voxel geometry is fixed at creation
+            cfg = ICPConfig()
+            A.geometry = MapGeometry(voxel_size=0.4)
+            A.update_config(cfg)
+    finally:
+        A.close()
+        B.close()

@@ -68,3 +68,43 @@ def test_seq_sum_is_mostly_parallel(ctx):
     x = np.abs(np.random.default_rng(3).normal(0, 0.05, 3962))
     _, st = _dev_sum(ctx, x, 1)
     assert 0 < st[0] < 200 and st[1] == 0, st
+
+
+def _seq32(x):
+    s = np.float32(0.0)
+    for v in np.asarray(x, np.float32):
+        s = np.float32(s + v)
+    return s
+
+
+def _dev_sum32(o, x):
+    from lidar_odometry_amd import lib
+    x = np.ascontiguousarray(x, np.float32)
+    out = C.c_float(0.0)
+    st = (C.c_longlong * 4)()
+    rc = lib().lo_seq_sum_f32(o.ctx, x.ctypes.data_as(C.POINTER(C.c_float)), len(x), C.byref(out), st)
+    assert rc == 0, rc
+    return np.float32(out.value), list(st)
+
+
+def _cases32():
+    rng = np.random.default_rng(11)
+    yield "random_walk", rng.normal(0, 1, 200_000)
+    yield "drift", rng.normal(0.01, 1, 100_000)
+    yield "positive", np.abs(rng.normal(0, 1, 50_000)) ** 2
+    yield "ties_1/8", np.round(rng.normal(0, 1, 30_000) * 8) / 8            # exact cancellations, halfway ties
+    yield "products", rng.normal(0, 1, 70_000) * rng.normal(0, 1, 70_000) * np.abs(rng.normal(0, 0.1, 70_000))
+    yield "zeros_sparse", np.where(rng.uniform(0, 1, 40_000) < 0.8, 0.0, rng.normal(0, 1, 40_000))
+    yield "leading_zero_chunks", np.concatenate([np.zeros(9000), rng.normal(0, 1, 9000)])
+    yield "tiny_and_huge", np.concatenate([rng.normal(0, 1e-30, 5000), rng.normal(0, 1e20, 100), rng.normal(0, 1, 5000)])
+    yield "single", np.array([-0.5])
+    yield "empty", np.zeros(0)
+
+
+def test_seq_sum_f32_bitwise(ctx):
+    """The large-scan exact path's 43 running fp32 sums (signed terms: g, off-diagonal H) reproduced bit for bit."""
+    for name, x in _cases32():
+        x32 = np.asarray(x, np.float32)
+        ref = _seq32(x32)
+        got, st = _dev_sum32(ctx, x32)
+        assert got.view(np.uint32) == ref.view(np.uint32), (name, got, ref, st)

@@ -96,6 +96,7 @@ def test_struct_fields_exist(adapter, ref):
     icp, pko = ref["optimization/IterativeClosestPointOptimizer.h"], ref["optimization/AdaptiveMEstimator.h"]
     checks = [
         (r"\bm_config", _body(icp, r"struct ICPConfig\s*\{")),
+        (r"\bcfg", _body(icp, r"struct ICPConfig\s*\{")),          # make_config's ICPConfig argument
         (r"\bp", _body(pko, r"struct AdaptiveMEstimatorConfig\s*\{")),
         (r"\bm_last_stats", _body(icp, r"struct OptimizationStats\s*\{")),
     ]
