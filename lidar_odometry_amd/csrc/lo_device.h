@@ -38,12 +38,12 @@ constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP ro
 constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
 constexpr int kCandWords = 48;      // a candidate's solved GN step: pose[12] | cost | H[21] | g[6] | delta[6] | conv | pad
 constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv = 46;
-// reference-exact candidates (lo_pko_body.h acc_candidate_exact): staged factor rows in the PKO launch's dynamic LDS
-constexpr int kXcPPL = 2;                                  // points per producer lane per chunk
-constexpr int kXcRegions = 3 * kXcPPL;                     // 64-point regions per chunk (3 producer waves)
-constexpr int kXcChunk = kXcRegions * kWave;              // 384 points
-constexpr int kXcStride = 15;                              // floats per staged row: 14 factors + 1 (odd: no bank conflicts)
-constexpr int kXcBuf = kXcChunk * kXcStride;
+// reference-exact candidates (lo_pko_body.h acc_candidate_exact): the 43 terms of a chunk's points staged term-major
+// in the PKO launch's dynamic LDS (4 consecutive rows of one term per ds_read_b128)
+constexpr int kXcRegions = 3;                              // 64-point regions per chunk (one per producer wave)
+constexpr int kXcChunk = kXcRegions * kWave;              // 192 points
+constexpr int kXcStride = kXcChunk + 4;                    // floats per term row (+4: b128 reads of 16 lanes hit 64 banks)
+constexpr int kXcBuf = 43 * kXcStride;
 constexpr size_t kXcLdsBytes = (2 * kXcBuf + 2 * kXcRegions + 43 + kCandWords) * sizeof(float);
 
 struct __attribute__((aligned(32))) Slot {

@@ -31,49 +31,83 @@ namespace lo {
 // registers / LDS (bitonic, lo_seqsum.h), then both sequential sums reproduced by mono_seq_sum (integer prefix sums
 // between binade changes, a short walk over the segment heads) -- the same bits as std::accumulate's chain ----
 
+// The sort is a rank computation spread over the chip (one KITTI scan's 4k residuals keep one CU busy for ~40 us in a
+// bitonic network, VALU-bound): k_rank_sort gives every residual its rank -- #{smaller} + #{equal and earlier} on the
+// fp64 bit patterns (non-negative doubles order as their bits; +inf marks a point without a correspondence, NaN sorts
+// after it) -- with 16 lanes per residual comparing it against the keys staged in LDS, and scatters it to that rank.
+// ~n^2 / 16k lane-compares per CU-cycle: ~3 us at 4k points, ~40 us at the 16k maximum.
+constexpr int kRankTPE = 16;                                   // lanes per residual
+constexpr int kRankThreads = 256;
+constexpr int kRankStage = 8192;                               // keys staged per pass (64 KB of LDS)
+__device__ __forceinline__ uint64_t rank_key(const KParams& P, const double* raw, int n, int i) {
+    constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
+    if (raw) return i < n ? static_cast<uint64_t>(__double_as_longlong(raw[i])) : kInfBits;
+    if (i >= n) return kInfBits;
+    // both loads issued together (the residual is read whatever the slot says), so the staging loop's iterations are
+    // independent round trips instead of two dependent ones each
+    const int s = P.slot[i];
+    const double r = P.kd_res ? P.kd_res[i] : P.res_out[i];
+    return s < 0 ? kInfBits : static_cast<uint64_t>(__double_as_longlong(r));
+}
+__global__ __launch_bounds__(kRankThreads) void k_rank_sort(KParams P, const double* raw, int n_raw, int n2, double* out) {
+    if (!raw && P.st->done) return;
+    __shared__ uint64_t s_k[kRankStage];
+    const int tid = threadIdx.x, sub = tid & (kRankTPE - 1);
+    const int el = blockIdx.x * (kRankThreads / kRankTPE) + tid / kRankTPE;
+    const int n = raw ? n_raw : scan_n(P);
+    const uint64_t ke = el < n2 ? rank_key(P, raw, n, el) : ~0ull;
+    int cnt = 0;
+    for (int s0 = 0; s0 < n2; s0 += kRankStage) {
+        const int m = min(kRankStage, n2 - s0);
+        __syncthreads();
+#pragma unroll 8
+        for (int t = tid; t < m; t += kRankThreads) s_k[t] = rank_key(P, raw, n, s0 + t);
+        __syncthreads();
+#pragma unroll 8
+        for (int j = sub; j < m; j += kRankTPE) {
+            const uint64_t kj = s_k[j];
+            cnt += (kj < ke || (kj == ke && s0 + j < el)) ? 1 : 0;
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < kRankTPE; o <<= 1) cnt += __shfl_xor(cnt, o, kRankTPE);
+    if (sub == 0 && el < n2) out[cnt] = __longlong_as_double(static_cast<long long>(ke));
+}
+
 template <int PT>
-__global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P) {
+__global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const double* __restrict__ sorted) {
     DevState* st = P.st;
     if (st->done) return;
     extern __shared__ double s_x[];                          // kSeqThreads * PT doubles
     __shared__ SeqScratch S;
     LO_XSTAMP(st, 0);
-    const int tid = threadIdx.x, n = scan_n(P), base = tid * PT;
-    double v[PT];
+    const int tid = threadIdx.x, base = tid * PT;
+    // the accepted residuals are the sorted array's finite entries (the rest are the +inf of points without a
+    // correspondence and the padding; a NaN residual sorts after them)
     int nacc = 0;
+    double v[PT];
     bool nan = false;
 #pragma unroll
     for (int a = 0; a < PT; ++a) {
-        const int i = base + a;
-        double r = __builtin_inf();
-        if (i < n && P.slot[i] >= 0) {
-            r = P.kd_res ? P.kd_res[i] : P.res_out[i];       // the stored fp64 residual (k_correspond / k_plane)
-            ++nacc;
-            nan = nan || isnan(r);
-        }
-        v[a] = r;
+        v[a] = sorted[base + a];
+        nan = nan || isnan(v[a]);
+        nacc += (v[a] != __builtin_inf() && !isnan(v[a])) ? 1 : 0;
     }
     int cnt;
     (void)block_excl_scan<int>(nacc, S.wi, cnt);
     const bool any_nan = __syncthreads_or(nan ? 1 : 0) != 0;
     if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
-    if (any_nan) {
-        // a NaN residual makes the mean, the variance and the scale NaN in any summation order
-        if (tid == 0) {
-            double s = 0.0;
-            for (int i = 0; i < n; ++i) if (P.slot[i] >= 0) s = s + (P.kd_res ? P.kd_res[i] : P.res_out[i]);
-            st->scale = sqrt(s) / 6.0;
-        }
+    if (any_nan) {                                           // a NaN residual: mean, variance and scale are NaN
+        if (nan) st->scale = sqrt(v[0] + v[PT - 1]) / 6.0;
         return;
     }
     LO_XSTAMP(st, 1);
-    bitonic_sort_block<PT>(v, s_x);
 #pragma unroll
     for (int a = 0; a < PT; ++a) s_x[base + a] = v[a];
     __syncthreads();
     LO_XSTAMP(st, 2);
     double sum;
-    if (!mono_seq_sum<PT>(v, cnt, s_x, S, 0.0, kExpNone, false, 0.0, sum, nullptr)) sum = chain_seq_sum(s_x, cnt, 0.0, S);
+    if (!mono_seq_sum<PT>(cnt, s_x, S, 0.0, kExpNone, false, 0.0, sum)) sum = chain_seq_sum(s_x, cnt, 0.0, S);
     LO_XSTAMP(st, 3);
     const double mean = sum / cnt;
     double w[PT];
@@ -84,7 +118,7 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P) {
     }
     __syncthreads();
     double var;
-    if (!mono_seq_sum<PT>(w, cnt, s_x, S, 0.0, kExpNone, false, 0.0, var, nullptr)) var = chain_seq_sum(s_x, cnt, 0.0, S);
+    if (!mono_seq_sum<PT>(cnt, s_x, S, 0.0, kExpNone, false, 0.0, var)) var = chain_seq_sum(s_x, cnt, 0.0, S);
     LO_XSTAMP(st, 4);
     var /= cnt;
     if (tid == 0) st->scale = sqrt(var) / 6.0;
@@ -117,8 +151,8 @@ __global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) 
 constexpr int kScaleGPT = 8;
 constexpr int kScaleGChunk = kSeqThreads * kScaleGPT;          // terms per chunk (64 KB of LDS)
 template <bool SQ>
-__device__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double m, double* s_x, SeqScratch& S) {
-    const int tid = threadIdx.x, base = tid * kScaleGPT;
+__device__ __forceinline__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double m, double* s_x, SeqScratch& S) {
+    const int tid = threadIdx.x;
     double s = 0.0, Tc = 0.0;
     int ec = kExpNone;
     for (int c0 = 0; c0 < cnt; c0 += kScaleGChunk) {
@@ -132,10 +166,7 @@ __device__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double 
             s_x[k] = v;
         }
         __syncthreads();
-        double xv[kScaleGPT];
-#pragma unroll
-        for (int a = 0; a < kScaleGPT; ++a) xv[a] = s_x[base + a];
-        if (mono_seq_sum<kScaleGPT>(xv, mc, s_x, S, Tc, ec, true, s, s, nullptr)) ec = S.e_carry;
+        if (mono_seq_sum<kScaleGPT>(mc, s_x, S, Tc, ec, true, s, s)) ec = S.e_carry;
         else { s = chain_seq_sum(s_x, mc, s, S); ec = binade64(s); }
         Tc = s;                                                // the exact running sum predicts the next chunk best
         __syncthreads();                                       // s_x / S reuse by the next chunk
@@ -177,24 +208,23 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale_g(KParams P, const 
 // index order (sorted ascending first with SORT), by the same sort and mono_seq_sum as k_exact_scale.  out[0] = the
 // sum; stats = heads, fallback segments, fallback terms, s_memtime cycles of the sort + sum.
 template <int PT>
-__global__ __launch_bounds__(kSeqThreads) void k_seq_sum_diag(const double* __restrict__ x, int n, int sort, double* out,
+__global__ __launch_bounds__(kSeqThreads) void k_seq_sum_diag(const double* __restrict__ x, int n, double* out,
                                                              long long* stats) {
     extern __shared__ double s_x[];
     __shared__ SeqScratch S;
     const int tid = threadIdx.x, base = tid * PT;
     double v[PT];
 #pragma unroll
-    for (int a = 0; a < PT; ++a) v[a] = (base + a < n) ? x[base + a] : (sort ? __builtin_inf() : 0.0);
+    for (int a = 0; a < PT; ++a) v[a] = (base + a < n) ? x[base + a] : 0.0;
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (sort) bitonic_sort_block<PT>(v, s_x);
 #pragma unroll
     for (int a = 0; a < PT; ++a) s_x[base + a] = v[a];
     __syncthreads();
     double sum;
     long long heads = -1;                                    // -1: more than kSeqHeadCap heads (the plain chain ran)
     if (tid == 0) S.fb_seg = S.fb_terms = 0;
-    if (mono_seq_sum<PT>(v, n, s_x, S, 0.0, kExpNone, false, 0.0, sum, nullptr)) heads = S.nheads;
+    if (mono_seq_sum<PT>(n, s_x, S, 0.0, kExpNone, false, 0.0, sum)) heads = S.nheads;
     else sum = chain_seq_sum(s_x, n, 0.0, S);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (tid == 0) {
@@ -206,37 +236,52 @@ __global__ __launch_bounds__(kSeqThreads) void k_seq_sum_diag(const double* __re
     }
 }
 template <int PT>
-static void launch_seq_diag_pt(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s) {
+static void launch_seq_diag_pt(const double* x, int n, double* out, long long* stats, hipStream_t s) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_seq_sum_diag<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
                               kSeqThreads * PT * 8);
     hipLaunchKernelGGL(k_seq_sum_diag<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, x, n,
-                       sort, out, stats);
+                       out, stats);
 }
-void launch_seq_sum_diag(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s) {
-    if (n <= kSeqThreads) launch_seq_diag_pt<1>(x, n, sort, out, stats, s);
-    else if (n <= 2 * kSeqThreads) launch_seq_diag_pt<2>(x, n, sort, out, stats, s);
-    else if (n <= 4 * kSeqThreads) launch_seq_diag_pt<4>(x, n, sort, out, stats, s);
-    else if (n <= 8 * kSeqThreads) launch_seq_diag_pt<8>(x, n, sort, out, stats, s);
-    else launch_seq_diag_pt<16>(x, n, sort, out, stats, s);
+// sort (nullable scratch of n doubles): the values ranked and scattered by k_rank_sort first, as the exact scale does
+void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s) {
+    const double* src = x;
+    if (sort) {
+        KParams P{};
+        hipLaunchKernelGGL(k_rank_sort, dim3((n + kRankThreads / kRankTPE - 1) / (kRankThreads / kRankTPE)),
+                           dim3(kRankThreads), 0, s, P, x, n, n, sort);
+        src = sort;
+    }
+    if (n <= kSeqThreads) launch_seq_diag_pt<1>(src, n, out, stats, s);
+    else if (n <= 2 * kSeqThreads) launch_seq_diag_pt<2>(src, n, out, stats, s);
+    else if (n <= 4 * kSeqThreads) launch_seq_diag_pt<4>(src, n, out, stats, s);
+    else if (n <= 8 * kSeqThreads) launch_seq_diag_pt<8>(src, n, out, stats, s);
+    else launch_seq_diag_pt<16>(src, n, out, stats, s);
 }
 
-// Host side: the scale launch for a scan of at most kExactMaxPoints points (PT = its padded size / kSeqThreads).
+// Host side: the scale of a scan of at most kExactMaxPoints points: k_rank_sort into `sorted` (n doubles of scratch),
+// then k_exact_scale<PT> (PT = the padded size / kSeqThreads).
 template <int PT>
-static void launch_scale_pt(const KParams& P, hipStream_t s) {
+static void launch_scale_pt(const KParams& P, const double* sorted, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale<PT>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kSeqThreads * PT * 8);
         attr = true;
     }
-    hipLaunchKernelGGL(k_exact_scale<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, P);
+    hipLaunchKernelGGL(k_exact_scale<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, P,
+                       sorted);
 }
-void launch_exact_scale(const KParams& P, int n, hipStream_t s) {
-    if (n <= kSeqThreads) launch_scale_pt<1>(P, s);
-    else if (n <= 2 * kSeqThreads) launch_scale_pt<2>(P, s);
-    else if (n <= 4 * kSeqThreads) launch_scale_pt<4>(P, s);
-    else if (n <= 8 * kSeqThreads) launch_scale_pt<8>(P, s);
-    else launch_scale_pt<16>(P, s);
+void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s) {
+    int PT = 1;
+    while (PT * kSeqThreads < n) PT <<= 1;
+    const int n2 = PT * kSeqThreads;                         // padded: ranks of the +inf padding fill [n, n2)
+    hipLaunchKernelGGL(k_rank_sort, dim3(n2 / (kRankThreads / kRankTPE)), dim3(kRankThreads), 0, s, P,
+                       static_cast<const double*>(nullptr), 0, n2, sorted);
+    if (PT == 1) launch_scale_pt<1>(P, sorted, s);
+    else if (PT == 2) launch_scale_pt<2>(P, sorted, s);
+    else if (PT == 4) launch_scale_pt<4>(P, sorted, s);
+    else if (PT == 8) launch_scale_pt<8>(P, sorted, s);
+    else launch_scale_pt<16>(P, sorted, s);
 }
 
 // ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =
@@ -365,24 +410,20 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
 // ---- large scans (n > kExactMaxPoints): the 43 running sums of build_ne in point order, one workgroup per term
 // column of the term-major buffer, each reproduced by signed_seq_sum (lo_seqsum.h: integer prefix sums between the
 // running sum's predicted binade / sign changes) chunk by chunk; k_exact_finish then solves as k_exact_solve does ----
-constexpr int kSumPT = 8;
+constexpr int kSumPT = 4;
 constexpr int kSumChunk = kSeqThreads * kSumPT;
 // col[0, n) summed in fp32 in index order, as the reference's running sums do; stats (nullable): heads, segments
 // summed term by term, chunks that fell back to the plain chain.
-__device__ float column_seq_sum(const float* __restrict__ col, int n, float* s_x, SeqScratchS& S, int* stats) {
-    const int tid = threadIdx.x, base = tid * kSumPT;
+__device__ __forceinline__ float column_seq_sum(const float* __restrict__ col, int n, float* s_x, SeqScratchS& S, int* stats) {
+    const int tid = threadIdx.x;
     float s = 0.0f;
     int ec = kExpNone, gc = 0, nh = 0, fb = 0, chains = 0;
     for (int c0 = 0; c0 < n; c0 += kSumChunk) {
         const int mc = min(kSumChunk, n - c0);
         for (int t = tid; t < kSumChunk; t += kSeqThreads) s_x[t] = t < mc ? col[c0 + t] : 0.0f;
         __syncthreads();
-        float xv[kSumPT];
-#pragma unroll
-        for (int a = 0; a < kSumPT; ++a) xv[a] = s_x[base + a];
-        double Tn;
         int en, gn;
-        if (signed_seq_sum<kSumPT>(xv, mc, s_x, S, static_cast<double>(s), ec, gc, s, s, Tn, en, gn)) {
+        if (signed_seq_sum<kSumPT>(mc, s_x, S, static_cast<double>(s), ec, gc, s, s, en, gn)) {
             nh += S.nheads;
             fb += S.fb_seg;
         } else {

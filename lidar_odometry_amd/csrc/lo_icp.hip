@@ -65,8 +65,8 @@ struct FitJob {
 struct FitOut;
 __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
                              FitOut* out);
-void launch_exact_scale(const KParams& P, int n, hipStream_t s);
-void launch_seq_sum_diag(const double* x, int n, int sort, double* out, long long* stats, hipStream_t s);
+void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s);
+void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s);
 void launch_seq_sum_f32_diag(const float* x, int n, float* out, long long* stats, hipStream_t s);
 __global__ void k_exact_resid(KParams P, double* out);
 __global__ void k_exact_scale_g(KParams P, const double* sorted);
@@ -120,6 +120,7 @@ struct lo_ctx {
     float* d_ex_terms = nullptr;
     size_t ex_cap = 0;              //   rows of d_ex_terms
     float* d_ex_tot = nullptr;      //   large scans: the 43 sums (k_exact_sum43 -> k_exact_finish)
+    double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints)
     double* d_ex_res = nullptr;     //   scans beyond kExactMaxPoints: residuals, sorted residuals, hipCUB scratch
     double* d_ex_sorted = nullptr;
     void* d_ex_sort_tmp = nullptr;
@@ -599,7 +600,7 @@ void lo_destroy(lo_ctx* c) {
                     c->grid.d_pts, c->grid.d_start, c->lgrid.d_pts, c->lgrid.d_start,
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_ex_terms, c->d_res_pko,
-                    c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp, c->d_ex_tot,
+                    c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp, c->d_ex_tot, c->d_ex_rank,
                     c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
@@ -1192,6 +1193,7 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
         c->ex_cap = std::max(n, static_cast<size_t>(kExactMaxPoints));
         LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * 43 * sizeof(float)));
     }
+    if (!c->d_ex_rank) LO_HIP(c, hipMalloc(&c->d_ex_rank, kExactMaxPoints * sizeof(double)));
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
     if (n > static_cast<size_t>(kExactMaxPoints)) {
@@ -1221,7 +1223,7 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
 // the iteration-0 scale of reference-exact mode (between the scan's first correspondence launch and its first PKO)
 static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStream_t s) {
     if (n2 > 0) {
-        launch_exact_scale(P, n2, s);
+        launch_exact_scale(P, n2, c->d_ex_rank, s);
         return;
     }
     const int n = P.n;                                       // the bound (a device-filtered scan counts on the device)
@@ -1903,13 +1905,13 @@ int lo_seq_sum_f64(lo_ctx* c, const double* x, size_t n, int sort, double* out_s
     if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(kExactMaxPoints)) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
     double* d = nullptr;
-    LO_HIP(c, hipMalloc(&d, (n + 1) * sizeof(double) + 4 * sizeof(long long)));
-    long long* d_st = reinterpret_cast<long long*>(d + n + 1);
+    LO_HIP(c, hipMalloc(&d, (2 * n + 1) * sizeof(double) + 4 * sizeof(long long)));
+    long long* d_st = reinterpret_cast<long long*>(d + 2 * n + 1);
     if (n > 0) LO_HIP(c, hipMemcpy(d, x, n * sizeof(double), hipMemcpyHostToDevice));
-    launch_seq_sum_diag(d, static_cast<int>(n), sort, d + n, d_st, c->stream);
+    launch_seq_sum_diag(d, static_cast<int>(n), sort ? d + n : nullptr, d + 2 * n, d_st, c->stream);
     hipError_t e = hipStreamSynchronize(c->stream);
     long long st[4] = {0, 0, 0, 0};
-    if (e == hipSuccess) e = hipMemcpy(out_sum, d + n, sizeof(double), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_sum, d + 2 * n, sizeof(double), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) { c->err = std::string("lo_seq_sum_f64: ") + hipGetErrorString(e); return LO_ERR_HIP; }
@@ -1921,8 +1923,9 @@ int lo_seq_sum_f32(lo_ctx* c, const float* x, size_t n, float* out_sum, long lon
     if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(INT32_MAX)) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
     float* d = nullptr;
-    LO_HIP(c, hipMalloc(&d, (n + 2) * sizeof(float) + 4 * sizeof(long long)));
-    long long* d_st = reinterpret_cast<long long*>(reinterpret_cast<char*>(d) + ((n + 2) * sizeof(float) + 7) / 8 * 8);
+    const size_t st_off = ((n + 2) * sizeof(float) + 7) / 8 * 8;
+    LO_HIP(c, hipMalloc(&d, st_off + 4 * sizeof(long long)));
+    long long* d_st = reinterpret_cast<long long*>(reinterpret_cast<char*>(d) + st_off);
     if (n > 0) LO_HIP(c, hipMemcpy(d, x, n * sizeof(float), hipMemcpyHostToDevice));
     launch_seq_sum_f32_diag(d, static_cast<int>(n), d + n, d_st, c->stream);
     hipError_t e = hipStreamSynchronize(c->stream);

@@ -676,14 +676,15 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // reference forms it -- the 43 running fp32 sums of build_ne in correspondence (scan) order (:345-410), Eigen's fp32
 // LDLT and the re-projected update (:417-448; lo_exact.h) -- in ONE workgroup while the EM runs, written as the same
 // 48-word record acc_candidate writes, so k_pick_correspond / k_pick take it unchanged.  Waves 1-3 form each accepted
-// point's 14 factors (J, w J, w r, r; exact_point_factors) for a chunk of 384 points and stage them in LDS,
-// compacted per 64-point region in point order; wave 0's lane k adds term k = fa[k] * fb[k] of every staged row to
-// its running sum, one rounding per addition, one chunk behind the producers (double-buffered, one barrier per
-// chunk).  The producers' loads run a chunk ahead (slot indices two).  LDS: the dynamic buffer (after the prefix).
-
+// point's 43 terms (exact_point_factors, then the products exactly as build_ne forms them) for a chunk of 192 points
+// and stage them term-major in LDS, compacted per 64-point region in point order and padded with zero terms to a
+// multiple of 4 (adding +0 leaves a running sum unchanged: the sums start at +0 and never become -0); wave 0's lane k
+// adds term k of every staged row to its running sum, one rounding per addition, four rows per ds_read_b128, one
+// chunk behind the producers (double-buffered, one barrier per chunk).  The producers' loads run a chunk ahead (slot
+// indices two).  LDS: the dynamic buffer (after the prefix).
 __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
     if (c > P.NA) return;
-    float* s_f = dyn;                                      // [2][kXcBuf]
+    float* s_f = dyn;                                      // [2][43][kXcStride]
     int* s_cnt = reinterpret_cast<int*>(dyn + 2 * kXcBuf); // [2][kXcRegions]
     float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
     float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
@@ -695,69 +696,67 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
     const float dl = cand_delta(P, c);
     __syncthreads();                                       // the prefix's use of the dynamic buffer is over
-    // producer state: this lane's kXcPPL points of the current chunk (loaded) and of the next (slots only)
-    int sl_cur[kXcPPL], sl_nxt[kXcPPL];
-    float px[kXcPPL], py[kXcPPL], pz[kXcPPL];
-    Slot sv[kXcPPL];
-    double rv[kXcPPL];
-    auto pidx = [&](int ch, int q) { return ch * kXcChunk + ((wid - 1) * kXcPPL + q) * kWave + lane; };
-    auto slot_at = [&](int ch, int q) { const int i = pidx(ch, q); return (ch < nch && i < n) ? P.slot[i] : -1; };
-    auto load_pt = [&](int ch, int q, int s) {
+    // producer state: this lane's point of the current chunk (loaded) and the slot of the next
+    int sl_cur = -1, sl_nxt = -1;
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    Slot sv{};
+    double rv = 0.0;
+    auto pidx = [&](int ch) { return ch * kXcChunk + (wid - 1) * kWave + lane; };
+    auto slot_at = [&](int ch) { const int i = pidx(ch); return (ch < nch && i < n) ? P.slot[i] : -1; };
+    auto load_pt = [&](int ch, int s) {
         if (s >= 0) {
-            const int i = pidx(ch, q);
-            px[q] = P.pts[3 * i]; py[q] = P.pts[3 * i + 1]; pz[q] = P.pts[3 * i + 2];
-            sv[q] = P.tab[s];
-            rv[q] = P.kd_res ? P.kd_res[i] : P.res_out[i];     // the stored fp64 residual (same bits as recomputing)
+            const int i = pidx(ch);
+            px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2];
+            sv = P.tab[s];
+            rv = P.kd_res ? P.kd_res[i] : P.res_out[i];     // the stored fp64 residual (same bits as recomputing)
         }
     };
     if (wid > 0) {
-#pragma unroll
-        for (int q = 0; q < kXcPPL; ++q) { sl_cur[q] = slot_at(0, q); sl_nxt[q] = slot_at(1, q); }
-#pragma unroll
-        for (int q = 0; q < kXcPPL; ++q) load_pt(0, q, sl_cur[q]);
+        sl_cur = slot_at(0);
+        sl_nxt = slot_at(1);
+        load_pt(0, sl_cur);
     }
-    // consumer state: lane k's term factors and running sum
-    int fa = 0, fb = 0;
-    exact_term_factors(lane < kExactTerms ? lane : 0, fa, fb);
-    float sum = 0.0f;
+    float sum = 0.0f;                                      // consumer: lane k's running sum of term k
     for (int ch = 0; ch <= nch; ++ch) {
         if (wid > 0 && ch < nch) {
             float* buf = s_f + (ch & 1) * kXcBuf;
+            const int r = wid - 1;
+            const bool valid = sl_cur >= 0;
+            const uint64_t m = __ballot(valid);
+            const int cnt = __popcll(m);
+            if (valid) {
+                float f[14];
+                exact_point_factors(P, T, scale, dl, rv, px, py, pz, sv, f);
+                const int row = r * kWave + __popcll(m & ((1ull << lane) - 1ull));
 #pragma unroll
-            for (int q = 0; q < kXcPPL; ++q) {
-                const bool valid = sl_cur[q] >= 0;
-                const uint64_t m = __ballot(valid);
-                const int r = (wid - 1) * kXcPPL + q;
-                if (valid) {
-                    float f[14];
-                    exact_point_factors(P, T, scale, dl, rv[q], px[q], py[q], pz[q], sv[q], f);
-                    const int rank = __popcll(m & ((1ull << lane) - 1ull));
-                    float* row = buf + (r * kWave + rank) * kXcStride;
-#pragma unroll
-                    for (int k = 0; k < 14; ++k) row[k] = f[k];
+                for (int k = 0; k < kExactTerms; ++k) {
+                    int fa, fb;
+                    exact_term_factors(k, fa, fb);
+                    buf[k * kXcStride + row] = f[fa] * f[fb];
                 }
-                if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = __popcll(m);
+            } else if (lane >= cnt && lane < ((cnt + 3) & ~3)) {   // zero terms up to the next multiple of 4
+#pragma unroll
+                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + lane] = 0.0f;
             }
-            // the next chunk's points / surfels / residuals, and the slots of the one after
-#pragma unroll
-            for (int q = 0; q < kXcPPL; ++q) { sl_cur[q] = sl_nxt[q]; sl_nxt[q] = slot_at(ch + 2, q); }
-#pragma unroll
-            for (int q = 0; q < kXcPPL; ++q) load_pt(ch + 1, q, sl_cur[q]);
+            if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = (cnt + 3) & ~3;
+            // the next chunk's point / surfel / residual, and the slot of the one after
+            sl_cur = sl_nxt;
+            sl_nxt = slot_at(ch + 2);
+            load_pt(ch + 1, sl_cur);
         } else if (wid == 0 && ch > 0) {
             const int b = (ch - 1) & 1;
-            const float* buf = s_f + b * kXcBuf;
+            const float* col = s_f + b * kXcBuf + (lane < kExactTerms ? lane : 0) * kXcStride;
+#pragma unroll
             for (int r = 0; r < kXcRegions; ++r) {
-                const int cnt = s_cnt[b * kXcRegions + r];
-                const float* rows = buf + r * kWave * kXcStride;
-                int i = 0;
-                for (; i + 8 <= cnt; i += 8) {
-                    float t[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) t[u] = rows[(i + u) * kXcStride + fa] * rows[(i + u) * kXcStride + fb];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) sum += t[u];
+                const int cnt4 = s_cnt[b * kXcRegions + r];
+                const float4* rows = reinterpret_cast<const float4*>(col + r * kWave);
+                for (int i = 0; i < cnt4 / 4; ++i) {
+                    const float4 v = rows[i];
+                    sum += v.x;
+                    sum += v.y;
+                    sum += v.z;
+                    sum += v.w;
                 }
-                for (; i < cnt; ++i) sum += rows[i * kXcStride + fa] * rows[i * kXcStride + fb];
             }
         }
         __syncthreads();

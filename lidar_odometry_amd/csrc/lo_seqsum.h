@@ -77,6 +77,20 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s_w, T& total) {
     return before + ex;
 }
 
+// Maximum over the workgroup of one value per thread (s_w: kSeqWaves entries, free again on return).
+__device__ __forceinline__ double block_max(double v, double* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const double t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+    if (lane == 0) s_w[wid] = v;
+    __syncthreads();
+    double m = s_w[0];
+#pragma unroll
+    for (int w = 1; w < kSeqWaves; ++w) m = s_w[w] > m ? s_w[w] : m;
+    __syncthreads();
+    return m;
+}
+
 struct SeqScratch {
     double wd[kSeqWaves];
     long long wl[kSeqWaves];
@@ -91,101 +105,112 @@ struct SeqScratch {
 };
 
 // s_in + x_0 + x_1 + ... + x_{cnt-1}, each addition rounded separately in index order, for x_j >= +0 (non-negative,
-// no NaN; +inf is never among the first cnt terms).  Thread t holds terms t*PT .. t*PT + PT - 1 in x[] (zeros past
-// cnt) and the same terms sit in s_x[0, cnt) (LDS; read by the walk and the fallbacks).  Carry-in for chunked use:
-// T0 = the approximate prefix before term 0, e0 = the predicted binade of the term before term 0, head0 = term 0 starts
-// a segment whatever its binade.  Every thread returns the sum; *e_last (nullable) receives the predicted binade of
-// term cnt - 1 for the next chunk.  Returns false (nothing computed) when a pass has more than kSeqHeadCap heads.
+// no NaN; +inf is never among the first cnt terms), the terms in s_x[0, cnt) (LDS); thread t works on terms
+// t*PT .. t*PT + PT - 1.  Carry-in for chunked use: T0 = the approximate prefix before term 0, e0 = the predicted binade
+// of the term before term 0, head0 = term 0 starts a segment whatever its binade.  Every thread returns the sum;
+// S.e_carry receives the predicted binade of the last term.  Returns false (nothing computed) when a pass has more
+// than kSeqHeadCap heads.  The per-term quantities are recomputed in each pass instead of being kept in arrays (the
+// arrays spilled to scratch at PT >= 8).
 template <int PT>
-__device__ bool mono_seq_sum(const double (&x)[PT], int cnt, const double* s_x, SeqScratch& S, double T0, int e0,
-                             bool head0, double s_in, double& s_out, double* T_out) {
+__device__ __forceinline__ bool mono_seq_sum(int cnt, const double* s_x, SeqScratch& S, double T0, int e0, bool head0, double s_in,
+                             double& s_out) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int base = tid * PT;
-    // 1. approximate inclusive prefix -> predicted binade per term
-    double tl[PT];
+    auto term = [&](int a) { return base + a < cnt ? s_x[base + a] : 0.0; };
+    // 1. approximate prefix: this thread's total, the workgroup scan, the last term's predicted binade
     double run = 0.0;
 #pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        run += (base + a < cnt) ? x[a] : 0.0;
-        tl[a] = run;
-    }
+    for (int a = 0; a < PT; ++a) run += term(a);
     double ttot;
     const double tex = T0 + block_excl_scan<double>(run, S.wd, ttot);
-    int e[PT];
-#pragma unroll
-    for (int a = 0; a < PT; ++a) e[a] = binade64(tex + tl[a]);
-    S.elast[tid] = e[PT - 1];
+    S.elast[tid] = binade64(tex + run);
     __syncthreads();
-    int ep = tid ? S.elast[tid - 1] : e0;
-    // 2. heads and integer steps
-    long long q[PT];
-    bool hd[PT];
+    const int e_in = tid ? S.elast[tid - 1] : e0;
+    // 2. heads and integer steps (one pass counts them, the next files them; both recompute the same values)
+    auto classify = [&](int a, double tl, int ep, int& E, long long& qa) -> bool {
+        const int j = base + a;
+        const double xv = term(a);
+        E = binade64(tex + tl);
+        qa = 0;
+        if (!(j < cnt && (xv != 0.0 || (head0 && j == 0)))) return false;   // a chunk's first term heads it even when zero
+        if (E < -1000 || E != ep || (head0 && j == 0)) return true;
+        const double t = ldexp(xv, 52 - E);                                // exact power-of-two scaling
+        const double f = floor(t), fr = t - f;                             // exact (t < 2^54)
+        if (fr == 0.5) return true;                                        // halfway: depends on s's last bit
+        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
+        return false;
+    };
     long long ql = 0;
     int nhl = 0;
+    {
+        double tl = 0.0;
+        int ep = e_in;
 #pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        const int j = base + a;
-        bool head = false;
-        long long qa = 0;
-        if (j < cnt && (x[a] != 0.0 || (head0 && j == 0))) {   // a chunk's first term heads it even when zero
-            const int E = e[a];
-            if (E < -1000 || E != ep || (head0 && j == 0)) {
-                head = true;
-            } else {
-                const double t = ldexp(x[a], 52 - E);            // exact power-of-two scaling
-                const double f = floor(t), fr = t - f;           // exact (t < 2^54)
-                if (fr == 0.5) head = true;                      // halfway: the rounding depends on s's last bit
-                else qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
-            }
+        for (int a = 0; a < PT; ++a) {
+            tl += term(a);
+            int E;
+            long long qa;
+            nhl += classify(a, tl, ep, E, qa) ? 1 : 0;
+            ql += qa;
+            ep = E;
         }
-        ep = e[a];
-        hd[a] = head;
-        q[a] = qa;
-        ql += qa;
-        nhl += head ? 1 : 0;
     }
     long long ptot;
     const long long pex = block_excl_scan<long long>(ql, S.wl, ptot);
     int htot;
     const int hbase = block_excl_scan<int>(nhl, S.wi, htot);
     if (htot > kSeqHeadCap) return false;                       // uniform: every thread sees htot
-    long long prun = pex;
-    int hk = hbase;
+    {
+        double tl = 0.0;
+        int ep = e_in, hk = hbase;
+        long long prun = pex;
 #pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        prun += q[a];
-        if (hd[a]) { S.h_idx[hk] = base + a; S.h_e[hk] = e[a]; S.h_p[hk] = prun; ++hk; }
+        for (int a = 0; a < PT; ++a) {
+            tl += term(a);
+            int E;
+            long long qa;
+            const bool hd = classify(a, tl, ep, E, qa);
+            prun += qa;
+            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; ++hk; }
+            ep = E;
+        }
+        if (tid == kSeqThreads - 1) S.e_carry = ep;
     }
-    if (tid == kSeqThreads - 1) S.e_carry = e[PT - 1];
     if (tid == 0) S.nheads = htot;
     __syncthreads();
-    // 3. the walk (wave 0, wave-uniform): lane l of a 64-head window holds head k0 + l
+    // 3. the walk (wave 0, wave-uniform): lane l of a 64-head window holds head k0 + l and precomputes what the
+    //    sequential step needs -- the head's term, the segment's sum u * Q, the binade floor 2^E and the largest
+    //    result the segment may reach (2^(E+1) - u) -- so each step is an add, an add and two compares
     if (wid == 0) {
         double s = s_in;
         int fbs = 0, fbt = 0;
         for (int k0 = 0; k0 < htot; k0 += 64) {
             const int kk = k0 + lane;
-            int hi = 0, he = 0, hend = cnt;
-            long long hp = 0, pend = ptot;
-            double hx = 0.0;
+            int hi = 0, hend = cnt;
+            double hx = 0.0, dq = 0.0, lo_e = __builtin_inf(), top = 0.0;
             if (kk < htot) {
                 hi = S.h_idx[kk];
-                he = S.h_e[kk];
-                hp = S.h_p[kk];
+                const int E = S.h_e[kk];
+                const long long hp = S.h_p[kk];
+                long long pend = ptot;
                 hx = s_x[hi];
                 if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
+                const long long Q = pend - hp;
+                if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
+                    const double u = ldexp(1.0, E - 52);
+                    dq = static_cast<double>(Q) * u;
+                    lo_e = ldexp(1.0, E);
+                    top = ldexp(1.0, E + 1) - u;
+                }
             }
             const int m = min(64, htot - k0);
             for (int l = 0; l < m; ++l) {
                 const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
-                const int E = __builtin_amdgcn_readlane(he, l);
-                const long long Q = rl64i(pend, l) - rl64i(hp, l);
                 s = s + rl64d(hx, l);                            // the head's own step, as the reference does it
+                const double R = s + rl64d(dq, l);               // exact when the segment stays in the binade
+                const int ok = (s >= rl64d(lo_e, l) && R <= rl64d(top, l)) ? 1 : 0;
                 if (end > h + 1) {
-                    const double u = ldexp(1.0, E - 52);
-                    const double top = ldexp(1.0, E + 1) - u;
-                    const double R = s + static_cast<double>(Q) * u;
-                    if (binade64(s) == E && E >= -1000 && R <= top) {
+                    if (__builtin_amdgcn_readfirstlane(ok)) {    // uniform: a scalar branch
                         s = R;                                   // every step of the segment: s + u * q_j, exact
                     } else {
                         for (int j = h + 1; j < end; ++j) s = s + s_x[j];
@@ -199,7 +224,6 @@ __device__ bool mono_seq_sum(const double (&x)[PT], int cnt, const double* s_x, 
     }
     __syncthreads();
     s_out = S.result;
-    if (T_out) *T_out = T0 + ttot;
     return true;
 }
 
@@ -213,110 +237,6 @@ __device__ inline double chain_seq_sum(const double* s_x, int cnt, double s, Seq
     return S.result;
 }
 
-// Ascending bitonic sort of NT * PT doubles, thread t holding elements t*PT .. t*PT + PT - 1 (blocked): partner
-// distances below PT inside the thread's registers, below 64 * PT across the wave (lane_xor: DPP / permlane swaps),
-// larger ones through s_x (LDS, NT * PT doubles).  No NaN in the input (+inf sorts last).
-template <int PT, int J>
-__device__ __forceinline__ void bitonic_reg(double (&v)[PT], int base, int k) {
-    if constexpr (J < PT) {
-#pragma unroll
-        for (int a = 0; a < PT; ++a) {
-            if ((a & J) == 0) {
-                const bool asc = ((base + a) & k) == 0;
-                const double lo = v[a], hi = v[a + J];
-                const bool sw = asc ? (lo > hi) : (lo < hi);
-                v[a] = sw ? hi : lo;
-                v[a + J] = sw ? lo : hi;
-            }
-        }
-    }
-}
-// v of lane (lane ^ M) without the LDS crossbar (a ds_bpermute per 32-bit word was the sort's bottleneck): DPP
-// quad_perm for M = 1, 2, row_ror:8 for 8, two row rotations and a per-lane select for 4 (which rotation brings lane
-// l ^ 4 is read off the lane index itself), v_permlane16_swap / v_permlane32_swap for 16 / 32.
-template <int M>
-__device__ __forceinline__ double lane_xor(double v, bool sel4) {
-    if constexpr (M == 1) return dpp64<0xB1, 0xf>(v);
-    else if constexpr (M == 2) return dpp64<0x4E, 0xf>(v);
-    else if constexpr (M == 8) return dpp64<0x128, 0xf>(v);
-    else if constexpr (M == 4) {
-        const double a = dpp64<0x124, 0xf>(v), b = dpp64<0x12C, 0xf>(v);   // row_ror:4, row_ror:12
-        return sel4 ? a : b;
-    } else {
-        const unsigned lo = static_cast<unsigned>(__double2loint(v)), hi = static_cast<unsigned>(__double2hiint(v));
-        const bool upper = ((threadIdx.x & 63) & M) != 0;
-        if constexpr (M == 16) {
-            const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-            const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-            // with both operands v: [0] holds rows (0 0 2 2), [1] rows (1 1 3 3); an even row's partner is in [1]
-            return upper ? __hiloint2double(static_cast<int>(h[0]), static_cast<int>(l[0]))
-                         : __hiloint2double(static_cast<int>(h[1]), static_cast<int>(l[1]));
-        } else {
-            static_assert(M == 32, "lane distance");
-            const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-            const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-            // [0] = (lanes 0-31, lanes 0-31), [1] = (lanes 32-63, lanes 32-63)
-            return upper ? __hiloint2double(static_cast<int>(h[0]), static_cast<int>(l[0]))
-                         : __hiloint2double(static_cast<int>(h[1]), static_cast<int>(l[1]));
-        }
-    }
-}
-template <int PT, int M>
-__device__ __forceinline__ void bitonic_lane(double (&v)[PT], int base, int k, int j, bool sel4) {
-#pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        const double o = lane_xor<M>(v[a], sel4);
-        const int el = base + a;
-        const bool keep_min = ((el & j) == 0) == ((el & k) == 0);
-        const double mn = (o < v[a]) ? o : v[a], mx = (o > v[a]) ? o : v[a];
-        v[a] = keep_min ? mn : mx;
-    }
-}
-template <int PT>
-__device__ void bitonic_sort_block(double (&v)[PT], double* s_x) {
-    constexpr int N = kSeqThreads * PT;
-    const int tid = threadIdx.x, base = tid * PT, lane = tid & 63;
-    // which of row_ror:4 / row_ror:12 brings lane ^ 4 (the rotation direction read off the lane index)
-    const bool sel4 = dpp32m<0x124>(lane) == (lane ^ 4);
-    for (int k = 2; k <= N; k <<= 1) {
-        int j = k >> 1;
-        if (j >= 64 * PT) {
-            // LDS stages of this k: pairs (p with bit j clear, p | j), each thread PT / 2 pairs per stage
-#pragma unroll
-            for (int a = 0; a < PT; ++a) s_x[base + a] = v[a];
-            __syncthreads();
-            for (; j >= 64 * PT; j >>= 1) {
-                for (int p = tid; p < N / 2; p += kSeqThreads) {
-                    const int lo_i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), hi_i = lo_i | j;
-                    const bool asc = (lo_i & k) == 0;
-                    const double a0 = s_x[lo_i], a1 = s_x[hi_i];
-                    const bool sw = asc ? (a0 > a1) : (a0 < a1);
-                    if (sw) { s_x[lo_i] = a1; s_x[hi_i] = a0; }
-                }
-                __syncthreads();
-            }
-#pragma unroll
-            for (int a = 0; a < PT; ++a) v[a] = s_x[base + a];
-            __syncthreads();
-        }
-        for (; j >= PT; j >>= 1) {
-            switch (j / PT) {                                    // partner lane = lane ^ (j / PT)
-                case 32: bitonic_lane<PT, 32>(v, base, k, j, sel4); break;
-                case 16: bitonic_lane<PT, 16>(v, base, k, j, sel4); break;
-                case 8: bitonic_lane<PT, 8>(v, base, k, j, sel4); break;
-                case 4: bitonic_lane<PT, 4>(v, base, k, j, sel4); break;
-                case 2: bitonic_lane<PT, 2>(v, base, k, j, sel4); break;
-                default: bitonic_lane<PT, 1>(v, base, k, j, sel4); break;
-            }
-        }
-        // j < PT: inside the thread
-        if (j >= 8) bitonic_reg<PT, 8>(v, base, k);
-        if (j >= 4) bitonic_reg<PT, 4>(v, base, k);
-        if (j >= 2) bitonic_reg<PT, 2>(v, base, k);
-        if (j >= 1) bitonic_reg<PT, 1>(v, base, k);
-    }
-}
-
 }  // namespace lo
 
 namespace lo {
@@ -324,12 +244,18 @@ namespace lo {
 // ---------------------------------------------------------------------------------------------------------------------
 // Signed fp32 sequential sums (the reference's build_ne accumulates H, g and the cost as running fp32 sums,
 // IterativeClosestPointOptimizer.cpp:359-415).  The same idea as mono_seq_sum, for terms of either sign: while the
-// running sum s keeps its sign and binade [2^E, 2^(E+1)) in magnitude, fl(s + x) = s + u rint(x / u) with u = 2^(E-23).
-// A segment's partial sums are no longer monotone, so its check bounds the smallest and the largest integer prefix over
-// the segment (segment minima / maxima by LDS atomics), and a segment also ends where the predicted sign changes.
-// Terms come in chunks (kSeqThreads * PT), each chunk starting a segment; the walk carries s from chunk to chunk.
+// running sum s keeps its sign and binade [2^E, 2^(E+1)) in magnitude, fl(s + x) = s + u rint(x / u), u = 2^(E-23).
+// The partial sums of a segment are no longer monotone, so the prediction carries the proof: a term heads a segment
+// also when its predicted prefix T lies within M = 2^(E-9) of either edge of its binade.  Inside a segment every T_j
+// is then at least M from the edges, and the true partial sums differ from T_j by at most |s_h - T_h| (known once the
+// walk reaches the head) + (end - h) u / 2 (one half-ulp per step) + the fp64 error of T (< 2^(E-30)): when that total
+// stays below M - u, every partial sum of the segment is inside the binade, one ulp from its edges, and the integer
+// model is exact for each step.  The fp64 error of T is bounded per chunk by 2^-46 times the largest magnitude any of its
+// partial sums reaches (fewer than 64 roundings per predicted term), so a chunk whose sums cancel large values only
+// loses parallelism, never exactness.  Terms come in chunks (kSeqThreads * PT), each chunk starting a segment, with
+// the exact running sum carried in as the next chunk's prediction base.
 // ---------------------------------------------------------------------------------------------------------------------
-constexpr int kSHeadCap = 2048;
+constexpr int kSHeadCap = 4096;
 
 struct SeqScratchS {
     double wd[kSeqWaves];
@@ -339,10 +265,8 @@ struct SeqScratchS {
     int glast[kSeqThreads];
     int h_idx[kSHeadCap];
     int h_e[kSHeadCap];
-    int h_g[kSHeadCap];
     long long h_p[kSHeadCap];
-    long long h_min[kSHeadCap];
-    long long h_max[kSHeadCap];
+    double h_t[kSHeadCap];
     float result;
     int e_carry, g_carry;
     int nheads, fb_seg;
@@ -357,138 +281,129 @@ __device__ __forceinline__ int binade_abs(double v) {       // binade of |v| whe
 }
 
 // s_in + x_0 + ... + x_{cnt-1} in fp32, one rounding per addition in index order; thread t holds terms t*PT.. (zeros past
-// cnt), s_x[0, cnt) the same terms (LDS).  T0 / e0 / g0: the approximate prefix, predicted binade and sign carried in
-// from the previous chunk; term 0 always starts a segment.  Every thread returns the sum and the carries; false (nothing
+// cnt), s_x[0, cnt) the same terms (LDS).  T0 / e0 / g0: the prediction base, binade and sign carried in from the
+// previous chunk; term 0 always starts a segment.  Every thread returns the sum and the carries; false (nothing
 // computed) when the chunk has more than kSHeadCap heads.
 template <int PT>
-__device__ bool signed_seq_sum(const float (&x)[PT], int cnt, const float* s_x, SeqScratchS& S, double T0, int e0,
-                               int g0, float s_in, float& s_out, double& T_out, int& e_out, int& g_out) {
+__device__ __forceinline__ bool signed_seq_sum(int cnt, const float* s_x, SeqScratchS& S, double T0, int e0, int g0, float s_in,
+                               float& s_out, int& e_out, int& g_out) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int base = tid * PT;
-    double tl[PT];
-    double run = 0.0;
+    auto term = [&](int a) { return base + a < cnt ? s_x[base + a] : 0.0f; };
+    double run = 0.0, amax = fabs(T0);
 #pragma unroll
     for (int a = 0; a < PT; ++a) {
-        run += (base + a < cnt) ? static_cast<double>(x[a]) : 0.0;
-        tl[a] = run;
+        run += static_cast<double>(term(a));
+        amax = fmax(amax, fabs(run));
     }
     double ttot;
     const double tex = T0 + block_excl_scan<double>(run, S.wd, ttot);
-    int e[PT], g[PT];
-#pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        const double T = tex + tl[a];
-        e[a] = binade_abs(T);
-        g[a] = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
+    {
+        const double Tl = tex + run;
+        S.elast[tid] = binade_abs(Tl);
+        S.glast[tid] = Tl > 0.0 ? 1 : (Tl < 0.0 ? -1 : 0);
     }
-    S.elast[tid] = e[PT - 1];
-    S.glast[tid] = g[PT - 1];
     __syncthreads();
-    int ep = tid ? S.elast[tid - 1] : e0, gp = tid ? S.glast[tid - 1] : g0;
-    long long q[PT];
-    bool hd[PT];
+    const int e_in = tid ? S.elast[tid - 1] : e0, g_in = tid ? S.glast[tid - 1] : g0;
+    // predicted binade / sign of term a's prefix, whether it lies within M of its binade's edges, and its step
+    auto classify = [&](int a, double T, int ep, int gp, int& E, int& G, long long& qa) -> bool {
+        const int j = base + a;
+        const float xv = term(a);
+        E = binade_abs(T);
+        G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
+        qa = 0;
+        if (!(j < cnt && (xv != 0.0f || j == 0))) return false;          // a chunk's first term heads it even when zero
+        const double at = fabs(T), M = ldexp(1.0, E - 9);
+        const bool edge = E == kExpNone || at < ldexp(1.0, E) + M || at > ldexp(1.0, E + 1) - M;
+        if (edge || E != ep || G != gp || j == 0) return true;
+        const double t = ldexp(static_cast<double>(xv), 23 - E);         // exact
+        const double f = floor(t), fr = t - f;
+        if (fr == 0.5) return true;
+        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
+        return false;
+    };
     long long ql = 0;
     int nhl = 0;
+    {
+        double tl = 0.0;
+        int ep = e_in, gp = g_in;
 #pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        const int j = base + a;
-        bool head = false;
-        long long qa = 0;
-        if (j < cnt && (x[a] != 0.0f || j == 0)) {             // a chunk's first term heads it even when zero
-            const int E = e[a];
-            if (E == kExpNone || E != ep || g[a] != gp || j == 0) {
-                head = true;
-            } else {
-                const double t = ldexp(static_cast<double>(x[a]), 23 - E);   // exact
-                const double f = floor(t), fr = t - f;
-                if (fr == 0.5) head = true;
-                else qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
-            }
+        for (int a = 0; a < PT; ++a) {
+            tl += static_cast<double>(term(a));
+            const double T = tex + tl;
+            amax = fmax(amax, fabs(T));
+            int E, G;
+            long long qa;
+            nhl += classify(a, T, ep, gp, E, G, qa) ? 1 : 0;
+            ql += qa;
+            ep = E;
+            gp = G;
         }
-        ep = e[a];
-        gp = g[a];
-        hd[a] = head;
-        q[a] = qa;
-        ql += qa;
-        nhl += head ? 1 : 0;
     }
+    amax = fmax(amax, fabs(tex));
     long long ptot;
     const long long pex = block_excl_scan<long long>(ql, S.wl, ptot);
     int htot;
     const int hbase = block_excl_scan<int>(nhl, S.wi, htot);
     if (htot > kSHeadCap) return false;
-    for (int k = tid; k < htot; k += kSeqThreads) { S.h_min[k] = LLONG_MAX; S.h_max[k] = LLONG_MIN; }
-    long long prun = pex;
-    int hk = hbase;
-    long long P[PT];
-#pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        prun += q[a];
-        P[a] = prun;
-        if (hd[a]) { S.h_idx[hk] = base + a; S.h_e[hk] = e[a]; S.h_g[hk] = g[a]; S.h_p[hk] = prun; ++hk; }
-    }
-    if (tid == kSeqThreads - 1) { S.e_carry = e[PT - 1]; S.g_carry = g[PT - 1]; }
-    if (tid == 0) S.nheads = htot;
-    __syncthreads();
-    // segment minima / maxima of P over the non-head terms (a thread's terms are consecutive: one flush per segment run)
+    const double eps_t = ldexp(block_max(amax, S.wd), -46);    // bound on |T_j - exact prefix| for every term
     {
-        int seg = hbase - 1;
-        long long mn = LLONG_MAX, mx = LLONG_MIN;
+        double tl = 0.0;
+        int ep = e_in, gp = g_in, hk = hbase;
+        long long prun = pex;
 #pragma unroll
         for (int a = 0; a < PT; ++a) {
-            const int j = base + a;
-            if (j >= cnt) break;
-            if (hd[a]) {
-                if (seg >= 0 && mn != LLONG_MAX) { atomicMin(&S.h_min[seg], mn); atomicMax(&S.h_max[seg], mx); }
-                ++seg;
-                mn = LLONG_MAX;
-                mx = LLONG_MIN;
-                continue;
-            }
-            if (seg < 0) continue;                               // zeros before the first head
-            mn = P[a] < mn ? P[a] : mn;
-            mx = P[a] > mx ? P[a] : mx;
+            tl += static_cast<double>(term(a));
+            const double T = tex + tl;
+            int E, G;
+            long long qa;
+            const bool hd = classify(a, T, ep, gp, E, G, qa);
+            prun += qa;
+            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; S.h_t[hk] = T; ++hk; }
+            ep = E;
+            gp = G;
         }
-        if (seg >= 0 && mn != LLONG_MAX) { atomicMin(&S.h_min[seg], mn); atomicMax(&S.h_max[seg], mx); }
+        if (tid == kSeqThreads - 1) { S.e_carry = ep; S.g_carry = gp; }
     }
+    if (tid == 0) S.nheads = htot;
     __syncthreads();
     if (wid == 0) {
+        // lane l of a 64-head window precomputes head k0 + l's checks: the binade [2^E, 2^(E+1)), the allowed distance
+        // of the head's result from its prediction (M - the segment's rounding and T error budget), the segment's sum
         float s = s_in;
         int fbs = 0;
         for (int k0 = 0; k0 < htot; k0 += 64) {
             const int kk = k0 + lane;
-            int hi = 0, he = 0, hg = 0, hend = cnt;
-            long long hp = 0, pend = ptot, hmn = LLONG_MAX, hmx = LLONG_MIN;
+            int hi = 0, hend = cnt, hg = 0;
+            double ht = 0.0, lo_e = __builtin_inf(), maxdev = -1.0, dq = 0.0;
             float hx = 0.0f;
             if (kk < htot) {
                 hi = S.h_idx[kk];
-                he = S.h_e[kk];
-                hg = S.h_g[kk];
-                hp = S.h_p[kk];
-                hmn = S.h_min[kk];
-                hmx = S.h_max[kk];
+                const int E = S.h_e[kk];
+                const long long hp = S.h_p[kk];
+                long long pend = ptot;
+                ht = S.h_t[kk];
                 hx = s_x[hi];
                 if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
+                if (E != kExpNone) {
+                    const double u = ldexp(1.0, E - 23);
+                    lo_e = ldexp(1.0, E);
+                    hg = ht > 0.0 ? 1 : -1;
+                    maxdev = ldexp(1.0, E - 9) - (static_cast<double>(hend - hi) * 0.5 + 1.0) * u - 2.0 * eps_t;
+                    dq = static_cast<double>(pend - hp) * u;
+                }
             }
             const int m = min(64, htot - k0);
             for (int l = 0; l < m; ++l) {
                 const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
                 s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hx), l));
+                const double d = static_cast<double>(s), ad = fabs(d), le = rl64d(lo_e, l);
+                const bool sgn = __builtin_amdgcn_readlane(hg, l) > 0 ? d > 0.0 : d < 0.0;
+                const int ok = (ad >= le && ad < 2.0 * le && sgn && fabs(d - rl64d(ht, l)) <= rl64d(maxdev, l)) ? 1 : 0;
+                const float sn = static_cast<float>(d + rl64d(dq, l));
                 if (end > h + 1) {
-                    const int E = __builtin_amdgcn_readlane(he, l), G = __builtin_amdgcn_readlane(hg, l);
-                    const long long p0 = rl64i(hp, l);
-                    const long long lo_q = rl64i(hmn, l) - p0, hi_q = rl64i(hmx, l) - p0, Q = rl64i(pend, l) - p0;
-                    const double d = static_cast<double>(s);
-                    const double u = ldexp(1.0, E - 23);
-                    const double lo = ldexp(1.0, E) + u, top = ldexp(1.0, E + 1) - u;
-                    bool ok = binade_abs(d) == E && E != kExpNone && (G > 0 ? d > 0.0 : d < 0.0) &&
-                              rl64i(hmn, l) != LLONG_MAX;
-                    if (ok) {
-                        const double a0 = d + static_cast<double>(lo_q) * u, a1 = d + static_cast<double>(hi_q) * u;
-                        ok = G > 0 ? (a0 >= lo && a1 <= top) : (-a1 >= lo && -a0 <= top);
-                    }
-                    if (ok) {
-                        s = static_cast<float>(d + static_cast<double>(Q) * u);
+                    if (__builtin_amdgcn_readfirstlane(ok)) {    // uniform: a scalar branch
+                        s = sn;
                     } else {
                         for (int j = h + 1; j < end; ++j) s = s + s_x[j];
                         ++fbs;
@@ -500,7 +415,6 @@ __device__ bool signed_seq_sum(const float (&x)[PT], int cnt, const float* s_x, 
     }
     __syncthreads();
     s_out = S.result;
-    T_out = T0 + ttot;
     e_out = S.e_carry;
     g_out = S.g_carry;
     return true;

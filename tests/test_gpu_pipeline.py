@@ -174,31 +174,40 @@ def test_pipeline_tail_insufficient_queued():
     import torch
     from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer
     cs = _cases()[:6]
-    o = _ctx(cs[0][0])
+    m0 = cs[0][0]
+    o = _ctx(m0)
     try:
         o.set_pipeline(False)
-        ncs = []
-        for _, pts, Ti in cs:
-            o.optimize(None, pts, Ti)
-            ncs.append([int(L["n_corr"]) for L in o.get_last_stats().iterations])
+        # a scan whose correspondence count at some iteration k >= 1 falls below every earlier count: with
+        # min_corr = min(earlier counts) it passes iterations < k and fails at k (on the tail stream for main = 1)
+        pool = []
+        for f in range(11, 33):
+            for sig in (0.05, 0.3, 0.6):
+                _, pts, Ti, _ = _data.kitti_case(f, seed=7, sigma_t=sig, sigma_r=sig / 10)
+                o.optimize(None, pts, Ti)
+                n = [int(L["n_corr"]) for L in o.get_last_stats().iterations]
+                ks = [k for k in range(1, len(n)) if n[k] < min(n[:k])]
+                if ks:
+                    pool.append((pts, Ti, min(n[:ks[0]]), ks[0]))
     finally:
         o.close()
-    # min_corr = iteration 0's count of a scan whose count falls at iteration 1: that scan fails on the tail
-    pick = [j for j, n in enumerate(ncs) if len(n) >= 2 and n[1] < n[0]]
-    assert pick, ncs
-    j0 = pick[0]
-    cfg = ICPConfig(min_correspondence_points=ncs[j0][0])
+    if not pool:
+        pytest.skip("no scan in the pool loses correspondences at a later iteration")
+    pts0, Ti0, min_corr, k_fail = pool[0]
+    cs = [(None, pts0, Ti0)] + cs
+    j0 = 0
+    cfg = ICPConfig(min_correspondence_points=min_corr)
     o = IterativeClosestPointOptimizer(config=cfg, max_points=1 << 16)
     try:
-        k, n, c = _data.surfels(cs[0][0])
+        k, n, c = _data.surfels(m0)
         o.set_surfels(k, n, c)
         d_scans = [torch.from_numpy(np.ascontiguousarray(p, np.float32).reshape(-1, 3)).to("cuda:0") for _, p, _ in cs]
         inits = [Ti for _, _, Ti in cs]
         order = [j0 if k % 2 == 0 else k % len(cs) for k in range(40)]
         o.set_pipeline(False)
         ref = _queued(o, d_scans, inits, order)
-        assert int(ref[0, 12]) == 1 and int(ref[0, 13]) == 1          # LO_INSUFFICIENT after one iteration
-        o.set_pipeline(True, 1)
+        assert int(ref[0, 12]) == 1 and int(ref[0, 13]) == k_fail     # LO_INSUFFICIENT at iteration k_fail
+        o.set_pipeline(True, max(1, k_fail))                  # the failing iteration runs on the tail stream
         for rep in range(3):
             got = _queued(o, d_scans, inits, order)
             np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32), err_msg=f"rep {rep}")
