@@ -176,6 +176,10 @@ int lo_set_pipeline(lo_ctx* ctx, int enable, int main_iterations);
  * the device map, buffers and stream stay.  voxel_size, hierarchy_factor, max_points and use_surfel_correspondence
  * are fixed at lo_create (LO_ERR_STATE); new PKO parameters rebuild the PKO tables. */
 int lo_update_config(lo_ctx* ctx, const lo_config* cfg);
+/* Workgroups of a PKO launch that fit the GMM (each fits it redundantly, then evaluates its share of the alpha grid):
+ * 0 (default, LO_PKO_GROUPS) = one alpha each (the latency-optimal single-stream shape); fewer leave the chip to other
+ * contexts' launches when many sequences share a GPU.  Results are identical for every value. */
+int lo_set_pko_groups(lo_ctx* ctx, int groups);
 /* Scan-pipeline state: out[0] enabled, out[1] main iterations, out[2] timeouts (a device-side wait gave up -- the two
  * streams were not run concurrently -- and the pipeline was switched off), out[3] synchronous scans re-run on one
  * stream after a timeout.  A scan whose wait timed out reports LO_ERR_PIPELINE in its device status (the exported

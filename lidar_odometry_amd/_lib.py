@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
-    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_update_config", "lo_map_sync_surfels", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
+    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_set_pko_groups", "lo_update_config", "lo_map_sync_surfels", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters", "lo_seq_sum_f64", "lo_seq_sum_f32",
     "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
     "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
@@ -214,6 +214,7 @@ def lib():
     L.lo_pko_sample_indices_host.argtypes = [C.c_size_t, C.c_int, ip]
     L.lo_debug_counters.argtypes = [vp, C.POINTER(C.c_ulonglong)]
     L.lo_pipeline_status.argtypes = [vp, C.POINTER(C.c_int)]
+    L.lo_set_pko_groups.argtypes = [vp, C.c_int]
     L.lo_update_config.argtypes = [vp, C.POINTER(LoConfig)]
     L.lo_map_sync_surfels.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_size_t,
                                       C.POINTER(C.c_int)]

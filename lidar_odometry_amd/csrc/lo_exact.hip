@@ -9,6 +9,7 @@
 // so a scan's per-iteration logs equal the oracle's bit for bit (tests/test_gpu_exact.py).  It costs a sequential
 // sum per iteration (~15 us at KITTI size) and two fp32 Jacobi SVDs per solve: a parity mode, not the default.
 // Scans up to kExactMaxPoints (the sort and the term buffer are sized for it).
+#include <algorithm>
 #include <cfloat>
 
 #include "lo_device.h"
@@ -39,36 +40,56 @@ namespace lo {
 constexpr int kRankTPE = 16;                                   // lanes per residual
 constexpr int kRankThreads = 256;
 constexpr int kRankStage = 8192;                               // keys staged per pass (64 KB of LDS)
-__device__ __forceinline__ uint64_t rank_key(const KParams& P, const double* raw, int n, int i) {
+// A residual's sort key: its fp64 bits, +inf for a point without a correspondence or past the scan.  Branch-free with
+// clamped indices, so the staging loop's loads all go out together.
+template <bool RAW>
+__device__ __forceinline__ uint64_t rank_key(const int32_t* __restrict__ slot, const double* __restrict__ res, int n, int i) {
     constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
-    if (raw) return i < n ? static_cast<uint64_t>(__double_as_longlong(raw[i])) : kInfBits;
-    if (i >= n) return kInfBits;
-    // both loads issued together (the residual is read whatever the slot says), so the staging loop's iterations are
-    // independent round trips instead of two dependent ones each
-    const int s = P.slot[i];
-    const double r = P.kd_res ? P.kd_res[i] : P.res_out[i];
-    return s < 0 ? kInfBits : static_cast<uint64_t>(__double_as_longlong(r));
+    const int ic = i < n ? i : 0;
+    const uint64_t r = static_cast<uint64_t>(__double_as_longlong(res[ic]));
+    if constexpr (RAW) return i < n ? r : kInfBits;
+    const int s = slot[ic];
+    return (i < n && s >= 0) ? r : kInfBits;
 }
+template <bool RAW>
 __global__ __launch_bounds__(kRankThreads) void k_rank_sort(KParams P, const double* raw, int n_raw, int n2, double* out) {
-    if (!raw && P.st->done) return;
+    if (!RAW && P.st->done) return;
     __shared__ uint64_t s_k[kRankStage];
+    if (!RAW && blockIdx.x == 0) LO_XSTAMP(P.st, 5);
     const int tid = threadIdx.x, sub = tid & (kRankTPE - 1);
     const int el = blockIdx.x * (kRankThreads / kRankTPE) + tid / kRankTPE;
-    const int n = raw ? n_raw : scan_n(P);
-    const uint64_t ke = el < n2 ? rank_key(P, raw, n, el) : ~0ull;
+    const int n = RAW ? n_raw : scan_n(P);
+    const int32_t* slot = P.slot;
+    const double* res = RAW ? raw : (P.kd_res ? P.kd_res : P.res_out);
+    const uint64_t ke = el < n2 ? rank_key<RAW>(slot, res, n, el) : ~0ull;
     int cnt = 0;
     for (int s0 = 0; s0 < n2; s0 += kRankStage) {
         const int m = min(kRankStage, n2 - s0);
         __syncthreads();
-#pragma unroll 8
-        for (int t = tid; t < m; t += kRankThreads) s_k[t] = rank_key(P, raw, n, s0 + t);
+        for (int t0 = 0; t0 < m; t0 += 8 * kRankThreads) {   // eight keys' loads in flight per thread
+            uint64_t kk[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kk[u] = rank_key<RAW>(slot, res, n, s0 + t0 + u * kRankThreads + tid);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + u * kRankThreads + tid;
+                if (t < m) s_k[t] = kk[u];
+            }
+        }
         __syncthreads();
-#pragma unroll 8
-        for (int j = sub; j < m; j += kRankTPE) {
-            const uint64_t kj = s_k[j];
-            cnt += (kj < ke || (kj == ke && s0 + j < el)) ? 1 : 0;
+        if (!RAW && blockIdx.x == 0) LO_XSTAMP(P.st, 6);
+        for (int j0 = 0; j0 < m; j0 += 8 * kRankTPE) {     // eight LDS reads in flight, then the compares
+            uint64_t kj[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kj[u] = s_k[min(j0 + u * kRankTPE + sub, m - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int j = j0 + u * kRankTPE + sub;
+                cnt += (j < m && (kj[u] < ke || (kj[u] == ke && s0 + j < el))) ? 1 : 0;
+            }
         }
     }
+    if (!RAW && blockIdx.x == 0) LO_XSTAMP(P.st, 7);
 #pragma unroll
     for (int o = 1; o < kRankTPE; o <<= 1) cnt += __shfl_xor(cnt, o, kRankTPE);
     if (sub == 0 && el < n2) out[cnt] = __longlong_as_double(static_cast<long long>(ke));
@@ -247,8 +268,9 @@ void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long
     const double* src = x;
     if (sort) {
         KParams P{};
-        hipLaunchKernelGGL(k_rank_sort, dim3((n + kRankThreads / kRankTPE - 1) / (kRankThreads / kRankTPE)),
-                           dim3(kRankThreads), 0, s, P, x, n, n, sort);
+        if (n > 0)
+            hipLaunchKernelGGL(k_rank_sort<true>, dim3((n + kRankThreads / kRankTPE - 1) / (kRankThreads / kRankTPE)),
+                               dim3(kRankThreads), 0, s, P, x, n, n, sort);
         src = sort;
     }
     if (n <= kSeqThreads) launch_seq_diag_pt<1>(src, n, out, stats, s);
@@ -272,16 +294,24 @@ static void launch_scale_pt(const KParams& P, const double* sorted, hipStream_t 
                        sorted);
 }
 void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s) {
-    int PT = 1;
-    while (PT * kSeqThreads < n) PT <<= 1;
+    int PT = std::max(1, (n + kSeqThreads - 1) / kSeqThreads);
+    PT = PT <= 8 ? PT : (PT <= 10 ? 10 : (PT <= 12 ? 12 : 16));   // the instantiated widths
     const int n2 = PT * kSeqThreads;                         // padded: ranks of the +inf padding fill [n, n2)
-    hipLaunchKernelGGL(k_rank_sort, dim3(n2 / (kRankThreads / kRankTPE)), dim3(kRankThreads), 0, s, P,
+    hipLaunchKernelGGL(k_rank_sort<false>, dim3(n2 / (kRankThreads / kRankTPE)), dim3(kRankThreads), 0, s, P,
                        static_cast<const double*>(nullptr), 0, n2, sorted);
-    if (PT == 1) launch_scale_pt<1>(P, sorted, s);
-    else if (PT == 2) launch_scale_pt<2>(P, sorted, s);
-    else if (PT == 4) launch_scale_pt<4>(P, sorted, s);
-    else if (PT == 8) launch_scale_pt<8>(P, sorted, s);
-    else launch_scale_pt<16>(P, sorted, s);
+    switch (PT) {
+        case 1: launch_scale_pt<1>(P, sorted, s); break;
+        case 2: launch_scale_pt<2>(P, sorted, s); break;
+        case 3: launch_scale_pt<3>(P, sorted, s); break;
+        case 4: launch_scale_pt<4>(P, sorted, s); break;
+        case 5: launch_scale_pt<5>(P, sorted, s); break;
+        case 6: launch_scale_pt<6>(P, sorted, s); break;
+        case 7: launch_scale_pt<7>(P, sorted, s); break;
+        case 8: launch_scale_pt<8>(P, sorted, s); break;
+        case 10: launch_scale_pt<10>(P, sorted, s); break;
+        case 12: launch_scale_pt<12>(P, sorted, s); break;
+        default: launch_scale_pt<16>(P, sorted, s); break;
+    }
 }
 
 // ---- per-correspondence terms of build_ne (:345-410) with this iteration's Huber delta: H[row][col] =

@@ -200,6 +200,7 @@ struct lo_ctx {
     // marker packet costs ~5-7 us of device time between two kernels).
     bool pipe = true;
     int pipe_main = 2;
+    int pko_groups = 0;             // EM workgroups per PKO launch (lo_set_pko_groups / LO_PKO_GROUPS; 0 = one per alpha)
     hipStream_t s_tail = nullptr;
     uint32_t pipe_seq = 0;
     uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done,
@@ -226,12 +227,17 @@ struct lo_ctx {
 
 // PKO workgroups: one alpha of the JS grid per workgroup (each fits the GMM redundantly), capped at kPkoMaxWGs
 static int pko_grid(const lo_config& g) { return std::max(1, std::min(kPkoMaxWGs, g.num_alpha_segments)); }
+// the context's EM workgroup count: pko_groups (lo_set_pko_groups; 0 = one alpha per workgroup, pko_grid)
+static int pko_grid(const lo_ctx* c) {
+    const int full = pko_grid(c->cfg);
+    return c->pko_groups > 0 ? std::min(full, c->pko_groups) : full;
+}
 
 static void launch_pko(lo_ctx* c, const KParams& P, int it) {
     // dynamic LDS for the per-block prefix (nb ints; 64 KB only at the 4M-point maximum)
     const size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     // 4 waves: the EM runs one GMM component per wave (gmm_fit_split), up to 256 samples (4 per lane)
-    const int G = pko_grid(c->cfg);
+    const int G = pko_grid(c);
     hipLaunchKernelGGL(k_pko_t<4>, dim3(G), dim3(256), pre_bytes, c->stream, P, it, G);
 }
 
@@ -242,7 +248,7 @@ static bool spec_ok(const KParams& P) { return P.use_pko && P.acc_part && P.nb_a
 
 static void launch_pko_spec(lo_ctx* c, const KParams& P, int it, hipStream_t s = nullptr) {
     size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
-    const int G = pko_grid(c->cfg);
+    const int G = pko_grid(c);
     int W = (P.nb_acc + kSpecBlocksPerWG - 1) / kSpecBlocksPerWG;
     if (P.exact_cand) {                                  // one workgroup per exact candidate, factor rows in LDS
         W = 1;
@@ -569,6 +575,7 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     if (const char* pp = std::getenv("LO_PIPE")) c->pipe = std::atoi(pp) != 0;
     if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
     if (const char* pw = std::getenv("LO_PIPE_WAIT_MS")) c->pipe_bound = 100000ull * std::max(1, std::atoi(pw));
+    if (const char* pg = std::getenv("LO_PKO_GROUPS")) c->pko_groups = std::max(0, std::atoi(pg));
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
@@ -1828,6 +1835,12 @@ int lo_pko_em_stats(lo_ctx* c, unsigned long long out[3], int reset) {
 int lo_set_exact(lo_ctx* c, int enable) {
     if (!c) return LO_ERR_ARG;
     c->exact = enable != 0;
+    return LO_OK;
+}
+
+int lo_set_pko_groups(lo_ctx* c, int groups) {
+    if (!c || groups < 0) return LO_ERR_ARG;
+    c->pko_groups = groups;
     return LO_OK;
 }
 

@@ -734,9 +734,10 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
                     exact_term_factors(k, fa, fb);
                     buf[k * kXcStride + row] = f[fa] * f[fb];
                 }
-            } else if (lane >= cnt && lane < ((cnt + 3) & ~3)) {   // zero terms up to the next multiple of 4
+            }
+            if (lane < ((cnt + 3) & ~3) - cnt) {                   // zero terms in rows cnt .. the next multiple of 4
 #pragma unroll
-                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + lane] = 0.0f;
+                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + cnt + lane] = 0.0f;
             }
             if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = (cnt + 3) & ~3;
             // the next chunk's point / surfel / residual, and the slot of the one after

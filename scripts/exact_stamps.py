@@ -34,10 +34,10 @@ def main():
         icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
         d = (C.c_ulonglong * 16)()
         assert L.lo_debug_counters(icp.ctx, d) == 0
-        rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3]])
+        rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3], d[6] - d[5], d[7] - d[6]])
     r = np.array(rows, dtype=np.float64)
-    print("cycles (s_memtime) per phase, mean over", len(rows), "scans: load/count %.0f  sort %.0f  mean-sum %.0f  "
-          "var-sum %.0f" % tuple(r.mean(0)), flush=True)
+    print("cycles (s_memtime) per phase, mean over", len(rows), "scans: scale load/count %.0f  store %.0f  mean-sum "
+          "%.0f  var-sum %.0f | rank-sort WG 0: staging %.0f  compares %.0f" % tuple(r.mean(0)), flush=True)
     icp.close()
 
 
