@@ -23,8 +23,10 @@ namespace lo {
 // boundaries into DevState::dbg (lo_debug_counters); the product kernel executes no stamp.
 #ifdef LO_EXACT_STAMPS
 #define LO_XSTAMP(st, i) do { if (threadIdx.x == 0) (st)->dbg[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define LO_XSTAT(st, i, v) do { if (threadIdx.x == 0) (st)->dbg[i] = static_cast<unsigned long long>(v); } while (0)
 #else
 #define LO_XSTAMP(st, i) do { } while (0)
+#define LO_XSTAT(st, i, v) do { } while (0)
 #endif
 
 // ---- iteration 0: scale = sqrt(var) / 6 of the residuals sorted ascending, mean and variance summed in that order
@@ -35,11 +37,11 @@ namespace lo {
 // The sort is a rank computation spread over the chip (one KITTI scan's 4k residuals keep one CU busy for ~40 us in a
 // bitonic network, VALU-bound): k_rank_sort gives every residual its rank -- #{smaller} + #{equal and earlier} on the
 // fp64 bit patterns (non-negative doubles order as their bits; +inf marks a point without a correspondence, NaN sorts
-// after it) -- with 16 lanes per residual comparing it against the keys staged in LDS, and scatters it to that rank.
-// ~n^2 / 16k lane-compares per CU-cycle: ~3 us at 4k points, ~40 us at the 16k maximum.
-constexpr int kRankTPE = 16;                                   // lanes per residual
+// after it) -- with a wave per residual comparing it against the keys staged in LDS, and scatters it to that rank.
+// The compares are latency-bound, so the grid is wide (n/4 workgroups of 32 KB LDS, ~4 waves per SIMD at 4k points).
+constexpr int kRankTPE = 64;                                   // lanes per residual
 constexpr int kRankThreads = 256;
-constexpr int kRankStage = 8192;                               // keys staged per pass (64 KB of LDS)
+constexpr int kRankStage = 4096;                               // keys staged per pass (32 KB of LDS)
 // A residual's sort key: its fp64 bits, +inf for a point without a correspondence or past the scan.  Branch-free with
 // clamped indices, so the staging loop's loads all go out together.
 template <bool RAW>
@@ -130,6 +132,10 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const do
     double sum;
     if (!mono_seq_sum<PT>(cnt, s_x, S, 0.0, kExpNone, false, 0.0, sum)) sum = chain_seq_sum(s_x, cnt, 0.0, S);
     LO_XSTAMP(st, 3);
+    LO_XSTAT(st, 8, S.nheads);
+    LO_XSTAT(st, 9, S.fb_seg);
+    LO_XSTAT(st, 10, S.fb_terms);
+    LO_XSTAT(st, 14, cnt);
     const double mean = sum / cnt;
     double w[PT];
 #pragma unroll
@@ -141,6 +147,9 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const do
     double var;
     if (!mono_seq_sum<PT>(cnt, s_x, S, 0.0, kExpNone, false, 0.0, var)) var = chain_seq_sum(s_x, cnt, 0.0, S);
     LO_XSTAMP(st, 4);
+    LO_XSTAT(st, 11, S.nheads);
+    LO_XSTAT(st, 12, S.fb_seg);
+    LO_XSTAT(st, 13, S.fb_terms);
     var /= cnt;
     if (tid == 0) st->scale = sqrt(var) / 6.0;
 }

@@ -180,14 +180,16 @@ __device__ __forceinline__ bool mono_seq_sum(int cnt, const double* s_x, SeqScra
     __syncthreads();
     // 3. the walk (wave 0, wave-uniform): lane l of a 64-head window holds head k0 + l and precomputes what the
     //    sequential step needs -- the head's term, the segment's sum u * Q, the binade floor 2^E and the largest
-    //    result the segment may reach (2^(E+1) - u) -- so each step is an add, an add and two compares
+    //    result the segment may reach (2^(E+1) - u); a one-term segment, or a lane past the last head, passes any
+    //    check (its dq is 0), a segment without a valid binade fails every check.  Heads go eight at a time as a
+    //    branch-free chain of two adds each; a group in which any check failed is redone head by head from its start
     if (wid == 0) {
         double s = s_in;
         int fbs = 0, fbt = 0;
         for (int k0 = 0; k0 < htot; k0 += 64) {
             const int kk = k0 + lane;
             int hi = 0, hend = cnt;
-            double hx = 0.0, dq = 0.0, lo_e = __builtin_inf(), top = 0.0;
+            double hx = -0.0, dq = -0.0, lo_e = -__builtin_inf(), top = __builtin_inf();   // x + -0 == x, also for x = -0
             if (kk < htot) {
                 hi = S.h_idx[kk];
                 const int E = S.h_e[kk];
@@ -196,26 +198,41 @@ __device__ __forceinline__ bool mono_seq_sum(int cnt, const double* s_x, SeqScra
                 hx = s_x[hi];
                 if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
                 const long long Q = pend - hp;
-                if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
-                    const double u = ldexp(1.0, E - 52);
-                    dq = static_cast<double>(Q) * u;
-                    lo_e = ldexp(1.0, E);
-                    top = ldexp(1.0, E + 1) - u;
+                if (hend > hi + 1) {
+                    lo_e = __builtin_inf();
+                    top = 0.0;
+                    if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
+                        const double u = ldexp(1.0, E - 52);
+                        dq = static_cast<double>(Q) * u;
+                        lo_e = ldexp(1.0, E);
+                        top = ldexp(1.0, E + 1) - u;
+                    }
                 }
             }
             const int m = min(64, htot - k0);
-            for (int l = 0; l < m; ++l) {
-                const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
-                s = s + rl64d(hx, l);                            // the head's own step, as the reference does it
-                const double R = s + rl64d(dq, l);               // exact when the segment stays in the binade
-                const int ok = (s >= rl64d(lo_e, l) && R <= rl64d(top, l)) ? 1 : 0;
-                if (end > h + 1) {
-                    if (__builtin_amdgcn_readfirstlane(ok)) {    // uniform: a scalar branch
-                        s = R;                                   // every step of the segment: s + u * q_j, exact
-                    } else {
-                        for (int j = h + 1; j < end; ++j) s = s + s_x[j];
-                        ++fbs;
-                        fbt += end - h - 1;
+            for (int l0 = 0; l0 < m; l0 += 8) {
+                const double s0 = s;
+                int bad = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {                    // lanes past m are the no-op heads above
+                    const double s1 = s + rl64d(hx, l0 + u);     // the head's own step, as the reference does it
+                    const double R = s1 + rl64d(dq, l0 + u);     // exact when the segment stays in the binade
+                    bad |= (s1 >= rl64d(lo_e, l0 + u) && R <= rl64d(top, l0 + u)) ? 0 : 1;
+                    s = R;
+                }
+                if (__builtin_amdgcn_readfirstlane(bad)) {       // uniform: redo the group head by head
+                    s = s0;
+                    for (int l = l0; l < min(l0 + 8, m); ++l) {
+                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                        s = s + rl64d(hx, l);
+                        const double R = s + rl64d(dq, l);
+                        if (__builtin_amdgcn_readfirstlane((s >= rl64d(lo_e, l) && R <= rl64d(top, l)) ? 1 : 0)) {
+                            s = R;
+                        } else {
+                            for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                            ++fbs;
+                            fbt += end - h - 1;
+                        }
                     }
                 }
             }
@@ -369,14 +386,16 @@ __device__ __forceinline__ bool signed_seq_sum(int cnt, const float* s_x, SeqScr
     __syncthreads();
     if (wid == 0) {
         // lane l of a 64-head window precomputes head k0 + l's checks: the binade [2^E, 2^(E+1)), the allowed distance
-        // of the head's result from its prediction (M - the segment's rounding and T error budget), the segment's sum
+        // of the head's result from its prediction (M - the segment's rounding and T error budget), the segment's sum;
+        // a one-term segment or a lane past the last head passes (dq 0), a segment without a binade fails.  Eight heads
+        // at a time as a branch-free chain; a group with a failed check is redone head by head from its start
         float s = s_in;
         int fbs = 0;
         for (int k0 = 0; k0 < htot; k0 += 64) {
             const int kk = k0 + lane;
-            int hi = 0, hend = cnt, hg = 0;
-            double ht = 0.0, lo_e = __builtin_inf(), maxdev = -1.0, dq = 0.0;
-            float hx = 0.0f;
+            int hi = 0, hend = cnt, hg = 0, pass = 1;
+            double ht = 0.0, lo_e = __builtin_inf(), maxdev = -1.0, dq = -0.0;          // x + -0 == x, also for x = -0
+            float hx = -0.0f;
             if (kk < htot) {
                 hi = S.h_idx[kk];
                 const int E = S.h_e[kk];
@@ -385,7 +404,8 @@ __device__ __forceinline__ bool signed_seq_sum(int cnt, const float* s_x, SeqScr
                 ht = S.h_t[kk];
                 hx = s_x[hi];
                 if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
-                if (E != kExpNone) {
+                pass = hend > hi + 1 ? 0 : 1;
+                if (!pass && E != kExpNone) {
                     const double u = ldexp(1.0, E - 23);
                     lo_e = ldexp(1.0, E);
                     hg = ht > 0.0 ? 1 : -1;
@@ -393,20 +413,36 @@ __device__ __forceinline__ bool signed_seq_sum(int cnt, const float* s_x, SeqScr
                     dq = static_cast<double>(pend - hp) * u;
                 }
             }
-            const int m = min(64, htot - k0);
-            for (int l = 0; l < m; ++l) {
-                const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
-                s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hx), l));
-                const double d = static_cast<double>(s), ad = fabs(d), le = rl64d(lo_e, l);
+            auto check = [&](double d, int l) -> bool {
+                const double ad = fabs(d), le = rl64d(lo_e, l);
                 const bool sgn = __builtin_amdgcn_readlane(hg, l) > 0 ? d > 0.0 : d < 0.0;
-                const int ok = (ad >= le && ad < 2.0 * le && sgn && fabs(d - rl64d(ht, l)) <= rl64d(maxdev, l)) ? 1 : 0;
-                const float sn = static_cast<float>(d + rl64d(dq, l));
-                if (end > h + 1) {
-                    if (__builtin_amdgcn_readfirstlane(ok)) {    // uniform: a scalar branch
-                        s = sn;
-                    } else {
-                        for (int j = h + 1; j < end; ++j) s = s + s_x[j];
-                        ++fbs;
+                return __builtin_amdgcn_readlane(pass, l) != 0 ||
+                       (ad >= le && ad < 2.0 * le && sgn && fabs(d - rl64d(ht, l)) <= rl64d(maxdev, l));
+            };
+            auto rlf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+            const int m = min(64, htot - k0);
+            for (int l0 = 0; l0 < m; l0 += 8) {
+                const float s0 = s;
+                int bad = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s = s + rlf(hx, l0 + u);
+                    const double d = static_cast<double>(s);
+                    bad |= check(d, l0 + u) ? 0 : 1;
+                    s = static_cast<float>(d + rl64d(dq, l0 + u));
+                }
+                if (__builtin_amdgcn_readfirstlane(bad)) {
+                    s = s0;
+                    for (int l = l0; l < min(l0 + 8, m); ++l) {
+                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                        s = s + rlf(hx, l);
+                        const double d = static_cast<double>(s);
+                        if (__builtin_amdgcn_readfirstlane(check(d, l) ? 1 : 0)) {
+                            s = static_cast<float>(d + rl64d(dq, l));
+                        } else {
+                            for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                            ++fbs;
+                        }
                     }
                 }
             }

@@ -29,15 +29,19 @@ def main():
     L = lib()
     assert L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle) == 0
     icp.set_exact(True)
-    rows = []
+    rows, stats = [], []
     for i in range(len(wl["scans"])):
         icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
         d = (C.c_ulonglong * 16)()
         assert L.lo_debug_counters(icp.ctx, d) == 0
         rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3], d[6] - d[5], d[7] - d[6]])
+        stats.append([d[14], d[8], d[9], d[10], d[11], d[12], d[13]])
     r = np.array(rows, dtype=np.float64)
     print("cycles (s_memtime) per phase, mean over", len(rows), "scans: scale load/count %.0f  store %.0f  mean-sum "
           "%.0f  var-sum %.0f | rank-sort WG 0: staging %.0f  compares %.0f" % tuple(r.mean(0)), flush=True)
+    for k, t in enumerate(stats):
+        print("scan %d: %d accepted | mean sum: %d heads, %d segments / %d terms term by term | variance: %d heads, "
+              "%d / %d" % (k, *t), flush=True)
     icp.close()
 
 
