@@ -305,8 +305,9 @@ int lo_pko_sample_indices(lo_ctx* ctx, size_t n, int32_t* out);
 int lo_seq_sum_f64(lo_ctx* ctx, const double* x, size_t n, int sort, double* out_sum, long long stats[4]);
 /* Parity entry point of the large-scan exact normal equations (IterativeClosestPointOptimizer.cpp:359-415: running fp32
  * sums in correspondence order): s = 0.0f; s += x[i] in index order, one fp32 rounding per addition, terms of any sign,
- * computed by the device kernel the exact mode uses for scans beyond 16384 points (lo_seqsum.h signed_seq_sum).
- * stats (nullable): segment heads, segments summed term by term, chunks on the plain chain, device cycles. */
+ * computed by the device kernels the exact mode uses for scans beyond 16384 points (lo_seqsum.h "Long signed fp32
+ * columns": chunk sums, classification, walk).  n <= 4M (the largest scan).  stats (nullable): segment heads, segments
+ * summed term by term, chunks run term by term (more heads than a chunk's record list holds), device microseconds. */
 int lo_seq_sum_f32(lo_ctx* ctx, const float* x, size_t n, float* out_sum, long long stats[4]);
 /* Diagnostic: 16 device counters (phase timestamps of the -DLO_PKO_STAMPS build; zeros otherwise). */
 int lo_debug_counters(lo_ctx* ctx, unsigned long long out[16]);

@@ -142,7 +142,7 @@ struct KParams {
     double* res_out;          // nullable: per-point fp64 residual of the accepted correspondences (k_correspond /
                               //   k_solve_correspond), read back by the PKO sample instead of recomputing it
     float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms
-    int ex_ld;                //   0: row-major [point][43]; > 0: term-major [43][ex_ld] (large scans, k_exact_sum43)
+    int ex_ld;                //   0: row-major [point][43]; > 0: term-major [43][ex_ld] (large scans, launch_mw_sums)
     float* ex_tot;            //   term-major path: the 43 sequential sums
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
     int exact_cand;           // 1: the PKO launch's candidates form the reference's sequential fp32 sums and solve

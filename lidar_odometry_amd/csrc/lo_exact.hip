@@ -156,9 +156,8 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const do
 
 // ---- iteration 0 for scans beyond the one-workgroup sort (kExactMaxPoints < n): k_exact_resid writes every point's
 // residual (+inf without a correspondence) to global memory, the context sorts them ascending (hipCUB radix sort:
-// the same order as std::sort for the non-NaN values; -0 / +0 ties do not change any sum), and k_exact_scale_g
-// runs both sequential sums over the sorted residuals chunk by chunk (mono_seq_sum with the prediction and the running
-// sum carried from chunk to chunk; every chunk starts a segment) ----
+// the same order as std::sort for the non-NaN values; -0 / +0 ties do not change any sum), and launch_mwm_scale runs
+// both sequential sums over the sorted residuals across the chip (lo_seqsum.h MwmBuf, kernels k_mwm_* below) ----
 __global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) {
     DevState* st = P.st;
     const int i = blockIdx.x * kBlock + threadIdx.x, n = scan_n(P);
@@ -176,62 +175,6 @@ __global__ __launch_bounds__(kBlock) void k_exact_resid(KParams P, double* out) 
         v = residual_f64(P.tab[s], wx, wy, wz);
     }
     out[i] = v;
-}
-
-constexpr int kScaleGPT = 8;
-constexpr int kScaleGChunk = kSeqThreads * kScaleGPT;          // terms per chunk (64 KB of LDS)
-template <bool SQ>
-__device__ __forceinline__ double chunked_seq_sum(const double* __restrict__ x, int cnt, double m, double* s_x, SeqScratch& S) {
-    const int tid = threadIdx.x;
-    double s = 0.0, Tc = 0.0;
-    int ec = kExpNone;
-    for (int c0 = 0; c0 < cnt; c0 += kScaleGChunk) {
-        const int mc = min(kScaleGChunk, cnt - c0);
-        for (int k = tid; k < kScaleGChunk; k += kSeqThreads) {
-            double v = 0.0;
-            if (k < mc) {
-                v = x[c0 + k];
-                if constexpr (SQ) v = (v - m) * (v - m);
-            }
-            s_x[k] = v;
-        }
-        __syncthreads();
-        if (mono_seq_sum<kScaleGPT>(mc, s_x, S, Tc, ec, true, s, s)) ec = S.e_carry;
-        else { s = chain_seq_sum(s_x, mc, s, S); ec = binade64(s); }
-        Tc = s;                                                // the exact running sum predicts the next chunk best
-        __syncthreads();                                       // s_x / S reuse by the next chunk
-    }
-    return s;
-}
-__global__ __launch_bounds__(kSeqThreads) void k_exact_scale_g(KParams P, const double* __restrict__ sorted) {
-    DevState* st = P.st;
-    if (st->done) return;
-    __shared__ double s_x[kScaleGChunk];
-    __shared__ SeqScratch S;
-    __shared__ int s_cnt;
-    const int tid = threadIdx.x, n = scan_n(P);
-    if (tid == 0) s_cnt = n;
-    __syncthreads();
-    int nan = 0;
-    for (int i = tid; i < n; i += kSeqThreads) {
-        const double v = sorted[i];
-        if (v == __builtin_inf() && (i == 0 || sorted[i - 1] != __builtin_inf())) atomicMin(&s_cnt, i);
-        nan |= isnan(v) ? 1 : 0;
-    }
-    const bool any_nan = __syncthreads_or(nan) != 0;
-    const int cnt = s_cnt;
-    if (cnt == 0) return;                                      // too few correspondences: the PKO launch reports it
-    if (any_nan) {
-        if (tid == 0) {
-            double s = 0.0;
-            for (int i = 0; i < n; ++i) if (sorted[i] != __builtin_inf()) s = s + sorted[i];
-            st->scale = sqrt(s) / 6.0;
-        }
-        return;
-    }
-    const double sum = chunked_seq_sum<false>(sorted, cnt, 0.0, s_x, S);
-    const double var = chunked_seq_sum<true>(sorted, cnt, sum / cnt, s_x, S);
-    if (tid == 0) st->scale = sqrt(var / cnt) / 6.0;
 }
 
 // Parity / diagnostic entry (lo_seq_sum_f64): the sequential sum of n <= kExactMaxPoints non-negative doubles in
@@ -341,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
     __syncthreads();
     const int i = blockIdx.x * kBlock + tid;
     if (i >= scan_n(P)) return;
-    // row-major [point][43], or term-major [43][ex_ld] (coalesced columns for k_exact_sum43)
+    // row-major [point][43], or term-major [43][ex_ld] (coalesced columns for the column sums, launch_mw_sums)
     const size_t o0 = P.ex_ld ? static_cast<size_t>(i) : static_cast<size_t>(i) * kExactTerms;
     const size_t os = P.ex_ld ? static_cast<size_t>(P.ex_ld) : 1;
     float* out = P.ex_terms + o0;
@@ -446,73 +389,813 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
     if (conv) st->done = 1;
 }
 
-// ---- large scans (n > kExactMaxPoints): the 43 running sums of build_ne in point order, one workgroup per term
-// column of the term-major buffer, each reproduced by signed_seq_sum (lo_seqsum.h: integer prefix sums between the
-// running sum's predicted binade / sign changes) chunk by chunk; k_exact_finish then solves as k_exact_solve does ----
-constexpr int kSumPT = 4;
-constexpr int kSumChunk = kSeqThreads * kSumPT;
-// col[0, n) summed in fp32 in index order, as the reference's running sums do; stats (nullable): heads, segments
-// summed term by term, chunks that fell back to the plain chain.
-__device__ __forceinline__ float column_seq_sum(const float* __restrict__ col, int n, float* s_x, SeqScratchS& S, int* stats) {
-    const int tid = threadIdx.x;
-    float s = 0.0f;
-    int ec = kExpNone, gc = 0, nh = 0, fb = 0, chains = 0;
-    for (int c0 = 0; c0 < n; c0 += kSumChunk) {
-        const int mc = min(kSumChunk, n - c0);
-        for (int t = tid; t < kSumChunk; t += kSeqThreads) s_x[t] = t < mc ? col[c0 + t] : 0.0f;
-        __syncthreads();
-        int en, gn;
-        if (signed_seq_sum<kSumPT>(mc, s_x, S, static_cast<double>(s), ec, gc, s, s, en, gn)) {
-            nh += S.nheads;
-            fb += S.fb_seg;
-        } else {
-            if (tid < kWave) {                                 // more heads than the list holds: the plain chain
-                for (int j = 0; j < mc; ++j) s = s + s_x[j];
-                if (tid == 0) S.result = s;
-            }
-            __syncthreads();
-            s = S.result;
-            en = binade_abs(static_cast<double>(s));
-            gn = s > 0.0f ? 1 : (s < 0.0f ? -1 : 0);
-            ++chains;
-        }
-        ec = en;
-        gc = gn;
-        __syncthreads();                                       // s_x / S reuse by the next chunk
+// ---- long columns across the chip (lo_seqsum.h "Long signed fp32 columns"): chunk sums -> classification -> walk ----
+__device__ __forceinline__ int mw_n(int n_cap, const int* n_dev) { return n_dev ? *n_dev : n_cap; }
+
+__global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__ col0, int ld, int n_cap,
+                                                       const int* n_dev, const DevState* st, MwBuf B) {
+    if (st && st->done) return;
+    __shared__ double s_w[2][4];
+    const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
+    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    double v = 0.0, a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMwChunk / 256; ++k) {                 // 16 terms per thread, coalesced
+        const int j = k * 256 + tid;
+        const double x = j < mc ? static_cast<double>(col[j]) : 0.0;
+        v += x;
+        a += fabs(x);
     }
-    if (stats && tid == 0) { stats[0] = nh; stats[1] = fb; stats[2] = chains; }
-    return s;
-}
-__global__ __launch_bounds__(kSeqThreads) void k_exact_sum43(KParams P) {
-    DevState* st = P.st;
-    if (st->done) return;
-    __shared__ float s_x[kSumChunk];
-    __shared__ SeqScratchS S;
-    const float s = column_seq_sum(P.ex_terms + static_cast<size_t>(blockIdx.x) * P.ex_ld, scan_n(P), s_x, S, nullptr);
-    if (threadIdx.x == 0) P.ex_tot[blockIdx.x] = s;
-}
-// Parity / diagnostic entry (lo_seq_sum_f32): one column through the same reproduction.
-__global__ __launch_bounds__(kSeqThreads) void k_seq_sum_f32_diag(const float* __restrict__ x, int n, float* out,
-                                                                  long long* stats) {
-    __shared__ float s_x[kSumChunk];
-    __shared__ SeqScratchS S;
-    __shared__ int st3[3];
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    const float s = column_seq_sum(x, n, s_x, S, st3);
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { v += __shfl_xor(v, o, 64); a += __shfl_xor(a, o, 64); }
+    if (lane == 0) { s_w[0][wid] = v; s_w[1][wid] = a; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        out[0] = s;
-        stats[0] = st3[0];
-        stats[1] = st3[1];
-        stats[2] = st3[2];
-        stats[3] = static_cast<long long>(t1 - t0);
+    if (tid == 0) {
+        const size_t o = static_cast<size_t>(colI) * B.nchunks + c;
+        B.csum[o] = ((s_w[0][0] + s_w[0][1]) + s_w[0][2]) + s_w[0][3];
+        B.cabs[o] = ((s_w[1][0] + s_w[1][1]) + s_w[1][2]) + s_w[1][3];
     }
-}
-void launch_seq_sum_f32_diag(const float* x, int n, float* out, long long* stats, hipStream_t s) {
-    hipLaunchKernelGGL(k_seq_sum_f32_diag, dim3(1), dim3(kSeqThreads), 0, s, x, n, out, stats);
 }
 
+constexpr int kMwWaves = kMwThreads / kWave;
+struct MwScratch {
+    double wd[kMwWaves];
+    long long wl[kMwWaves];
+    int wi[kMwWaves];
+    int elast[kMwThreads];
+    int glast[kMwThreads];
+    int h_idx[kMwCap];
+    int h_e[kMwCap];
+    long long h_p[kMwCap];
+    double h_t[kMwCap];
+};
+
+// The chunk's prediction base: the chunk sums (+ modelled drift, DRIFT) of the chunks before it, and the magnitude sum
+// through this chunk.  Every thread returns both.
+template <bool DRIFT>
+__device__ __forceinline__ void mw_base(const MwBuf& B, size_t co, int c, double* s_w, double& T0, double& A) {
+    double t0 = 0.0, a0 = 0.0;
+    for (int k = threadIdx.x; k <= c; k += kMwThreads) {
+        if (k < c) t0 += DRIFT ? B.csum[co + k] + B.dcorr[co + k] : B.csum[co + k];
+        a0 += B.cabs[co + k];
+    }
+    (void)block_excl_scan<double, kMwThreads>(t0, s_w, T0);
+    (void)block_excl_scan<double, kMwThreads>(a0, s_w, A);
+}
+
+__global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict__ col0, int ld, int n_cap,
+                                                        const int* n_dev, const DevState* st, MwBuf B) {
+    if (st && st->done) return;
+    __shared__ double s_w[kMwWaves];
+    const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x;
+    const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
+    const size_t co = static_cast<size_t>(colI) * B.nchunks;
+    if (mc <= 0) {
+        if (tid == 0) B.dcorr[co + c] = 0.0;
+        return;
+    }
+    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    double T0, A;
+    mw_base<false>(B, co, c, s_w, T0, A);
+    const int base = tid * kMwPT;
+    float v[kMwPT];
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) v[a] = base + a < mc ? col[base + a] : 0.0f;
+    double run = 0.0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
+    double ttot;
+    const double tex = T0 + block_excl_scan<double, kMwThreads>(run, s_w, ttot);
+    double d = 0.0, tl = 0.0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) {                          // each step's rounding in its predicted binade
+        tl += static_cast<double>(v[a]);
+        const int E = binade_abs(tex + tl);
+        if (E != kExpNone) {
+            const double x = static_cast<double>(v[a]);
+            d += ldexp(rint(ldexp(x, 23 - E)), E - 23) - x;
+        }
+    }
+    double dtot;
+    (void)block_excl_scan<double, kMwThreads>(d, s_w, dtot);
+    if (tid == 0) B.dcorr[co + c] = dtot;
+}
+
+__global__ __launch_bounds__(kMwThreads) void k_mw_classify(const float* __restrict__ col0, int ld, int n_cap,
+                                                             const int* n_dev, const DevState* st, MwBuf B) {
+    if (st && st->done) return;
+    __shared__ MwScratch S;
+    const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x;
+    const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
+    const size_t co = static_cast<size_t>(colI) * B.nchunks;
+    if (mc <= 0) {
+        if (tid == 0) B.nh[co + c] = 0;
+        return;
+    }
+    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    double T0, A;
+    mw_base<true>(B, co, c, S.wd, T0, A);
+    const double eps_t = ldexp(A + fabs(T0), -45);             // bound on the in-chunk prediction error (see above)
+    const int base = tid * kMwPT;
+    float v[kMwPT];
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) v[a] = base + a < mc ? col[base + a] : 0.0f;
+    double run = 0.0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
+    double ttot;
+    const double tex = T0 + block_excl_scan<double, kMwThreads>(run, S.wd, ttot);
+    {
+        const double Tl = tex + run;
+        S.elast[tid] = binade_abs(Tl);
+        S.glast[tid] = Tl > 0.0 ? 1 : (Tl < 0.0 ? -1 : 0);
+    }
+    __syncthreads();
+    const int e_in = tid ? S.elast[tid - 1] : kExpNone, g_in = tid ? S.glast[tid - 1] : 0;
+    // heads: binade / sign changes, edge proximity, halfway ties; term 0 of every chunk heads a segment
+    auto classify = [&](int a, double T, int ep, int gp, int& E, int& G, long long& qa) -> bool {
+        const int j = base + a;
+        const float xv = v[a];
+        E = binade_abs(T);
+        G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
+        qa = 0;
+        if (!(j < mc && (xv != 0.0f || j == 0))) return false;
+        const double at = fabs(T), M = ldexp(1.0, E - 9);
+        const bool edge = E == kExpNone || at < ldexp(1.0, E) + M || at > ldexp(1.0, E + 1) - M;
+        if (edge || E != ep || G != gp || j == 0) return true;
+        const double t = ldexp(static_cast<double>(xv), 23 - E);
+        const double f = floor(t), fr = t - f;
+        if (fr == 0.5) return true;
+        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
+        return false;
+    };
+    long long ql = 0;
+    int nhl = 0;
+    {
+        double tl = 0.0;
+        int ep = e_in, gp = g_in;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) {
+            tl += static_cast<double>(v[a]);
+            int E, G;
+            long long qa;
+            nhl += classify(a, tex + tl, ep, gp, E, G, qa) ? 1 : 0;
+            ql += qa;
+            ep = E;
+            gp = G;
+        }
+    }
+    long long ptot;
+    const long long pex = block_excl_scan<long long, kMwThreads>(ql, S.wl, ptot);
+    int htot;
+    const int hbase = block_excl_scan<int, kMwThreads>(nhl, S.wi, htot);
+    const size_t rb = (co + c) * kMwCap;
+    if (htot > kMwCap) {                                       // uniform: the whole chunk as one term-by-term run
+        if (tid == 0) {
+            B.nh[co + c] = 1;
+            B.idx[rb] = c0;
+            B.end[rb] = c0 + mc;
+            B.x[rb] = col[0];
+            B.dq[rb] = -0.0f;
+            B.flag[rb] = kMwFail;
+            B.dlo[rb] = __builtin_inf();
+            B.dhi[rb] = -__builtin_inf();
+        }
+        return;
+    }
+    {
+        double tl = 0.0;
+        int ep = e_in, gp = g_in, hk = hbase;
+        long long prun = pex;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) {
+            tl += static_cast<double>(v[a]);
+            const double T = tex + tl;
+            int E, G;
+            long long qa;
+            const bool hd = classify(a, T, ep, gp, E, G, qa);
+            prun += qa;
+            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; S.h_t[hk] = T; ++hk; }
+            ep = E;
+            gp = G;
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < htot; k += kMwThreads) {             // one record per head
+        const int hi = S.h_idx[k], E = S.h_e[k];
+        const long long hp = S.h_p[k];
+        const double ht = S.h_t[k];
+        const bool last = k + 1 >= htot;
+        const int hend = last ? mc : S.h_idx[k + 1];
+        const long long pend = last ? ptot : S.h_p[k + 1];
+        int flag = hend > hi + 1 ? 0 : 1;
+        double dlo = __builtin_inf(), dhi = -__builtin_inf();
+        float dq = -0.0f;
+        if (!flag) {
+            flag = kMwFail;
+            if (E != kExpNone) {
+                const double u = ldexp(1.0, E - 23), lo = ldexp(1.0, E);
+                const double dev = ldexp(1.0, E - 9) - (static_cast<double>(hend - hi) * 0.5 + 1.0) * u - 2.0 * eps_t;
+                if (dev >= 0.0) {
+                    // |d - ht| <= dev, rounded inwards; the binade of the head's sign, its top end exclusive
+                    const double slack = ldexp(fabs(ht) + dev, -51);
+                    const double top = 2.0 * lo - ldexp(lo, -52);
+                    dlo = (ht - dev) + slack;
+                    dhi = (ht + dev) - slack;
+                    if (ht > 0.0) { dlo = fmax(dlo, lo); dhi = fmin(dhi, top); }
+                    else { dlo = fmax(dlo, -top); dhi = fmin(dhi, -lo); }
+                    dq = static_cast<float>(static_cast<double>(pend - hp) * u);
+                    flag = 0;
+                }
+            }
+        }
+        const size_t r = rb + k;
+        B.idx[r] = c0 + hi;
+        B.end[r] = c0 + hend;
+        B.x[r] = col[hi];
+        B.dq[r] = dq;
+        B.flag[r] = flag;
+        B.dlo[r] = dlo;
+        B.dhi[r] = dhi;
+    }
+    if (tid == 0) B.nh[co + c] = htot;
+}
+
+// s + col[j0] + ... + col[j1 - 1] term by term (one wave, wave-uniform).  The terms come in through scalar loads, 32 at a
+// time with the next 32 in flight, so the chain is one v_add_f32 per term with an SGPR operand (no readlane hazards).
+__device__ __forceinline__ float walk_terms(const float* __restrict__ col, int j0, int j1, float s) {
+    constexpr int kB = 32;
+    j0 = __builtin_amdgcn_readfirstlane(j0);
+    j1 = __builtin_amdgcn_readfirstlane(j1);
+    const int lane = threadIdx.x & 63;
+    int j = j0;
+    {                                                          // to a 128-byte boundary: one load per lane
+        const int a = min(j1, (j0 + kB - 1) & ~(kB - 1));
+        const float v = lane < a - j0 ? col[j0 + lane] : -0.0f;
+        for (int l = 0; l < a - j0; ++l) s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+        j = a;
+    }
+    if (j + kB <= j1) {
+        float cur[kB], nxt[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) cur[u] = col[j + u];
+        for (; j + 2 * kB <= j1; j += kB) {
+#pragma unroll
+            for (int u = 0; u < kB; ++u) nxt[u] = col[j + kB + u];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) s = s + cur[u];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) s = s + cur[u];
+        j += kB;
+    }
+    {                                                          // the rest (< kB terms): one load per lane
+        const float v = lane < j1 - j ? col[j + lane] : -0.0f;
+        for (int l = 0; l < j1 - j; ++l) s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    }
+    return s;
+}
+
+// Compaction: chunk c's records to their place in the column's walk order (offset = the heads of the chunks before it).
+__global__ __launch_bounds__(256) void k_mw_compact(int n_cap, const int* n_dev, const DevState* st, MwBuf B) {
+    if (st && st->done) return;
+    __shared__ int s_w[4];
+    const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x;
+    const int n = mw_n(n_cap, n_dev), nc = (n + kMwChunk - 1) / kMwChunk;
+    if (c >= nc) return;
+    const size_t co = static_cast<size_t>(colI) * B.nchunks;
+    int before = 0;
+    for (int k = tid; k < c; k += 256) before += B.nh[co + k];
+    int off;
+    (void)block_excl_scan<int, 256>(before, s_w, off);
+    const int h = B.nh[co + c];
+    const size_t src = (co + c) * kMwCap, dst = static_cast<size_t>(colI) * B.cstride + off;
+    for (int k = tid; k < h; k += 256) {
+        B.c_idx[dst + k] = B.idx[src + k];
+        B.c_end[dst + k] = B.end[src + k];
+        B.c_x[dst + k] = B.x[src + k];
+        B.c_dq[dst + k] = B.dq[src + k];
+        B.c_flag[dst + k] = B.flag[src + k];
+        B.c_dlo[dst + k] = B.dlo[src + k];
+        B.c_dhi[dst + k] = B.dhi[src + k];
+    }
+    if (c == nc - 1) {                                         // no-op records after the last head
+        if (tid < kMwPad) {
+            const size_t r = dst + h + tid;
+            B.c_idx[r] = 0; B.c_end[r] = 0; B.c_flag[r] = 1; B.c_x[r] = -0.0f; B.c_dq[r] = -0.0f;
+            B.c_dlo[r] = 0.0; B.c_dhi[r] = 0.0;
+        }
+        if (tid == 0) B.ntot[colI] = off + h;
+    }
+}
+
+// One wave per column: every head in order, a window of 64 heads at a time (the next window's records in flight).
+// The fast path adds the window's heads as a plain fp32 chain -- s += x (the head's own step), s += dq (its segment)
+// -- lane l keeping the sum right after head l's step; the 64 checks then run lane-parallel.  A failed check at head f
+// restarts from its recorded sum (exact: every earlier head passed), sums f's segment term by term and takes the rest
+// of the window head by head.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
+// term-by-term run.
+__global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, int ld, int n_cap, const int* n_dev,
+                                                const DevState* st, MwBuf B, float* out, long long* stats) {
+    if (st && st->done) return;
+    const int lane = threadIdx.x, colI = blockIdx.x;
+    const int n = mw_n(n_cap, n_dev);
+    const float* col = col0 + static_cast<size_t>(colI) * ld;
+    const size_t rb = static_cast<size_t>(colI) * B.cstride;
+    const int total = n > 0 ? B.ntot[colI] : 0;
+    struct Win { int hi, end, flag; float x, dq; double dlo, dhi; };
+    auto load = [&](int k0) {                                  // records past the last head are no-ops (kMwPad)
+        const size_t r = rb + k0 + lane;
+        return Win{B.c_idx[r], B.c_end[r], B.c_flag[r], B.c_x[r], B.c_dq[r], B.c_dlo[r], B.c_dhi[r]};
+    };
+    auto rlf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+    float s = 0.0f;
+    int fbs = 0, chained = 0;
+    // one window: the plain chain, the lane-parallel checks, the slow path from the first failure
+    __shared__ float2 s_xd[64];                                // the window's (x, dq), read back as broadcasts
+    auto process = [&](const Win& cur, int k0) {
+        float rec = 0.0f;
+        s_xd[lane] = make_float2(cur.x, cur.dq);
+        __syncthreads();
+#pragma unroll
+        for (int l = 0; l < 64; ++l) {                          // lanes past the window's end are no-ops
+            const float2 xd = s_xd[l];
+            s = s + xd.x;
+            rec = lane == l ? s : rec;
+            s = s + xd.y;
+        }
+        __syncthreads();
+        const double d = static_cast<double>(rec);
+        const bool ok = cur.flag == 1 || (cur.flag == 0 && d >= cur.dlo && d <= cur.dhi);
+        const unsigned long long badm = __ballot(!ok);
+        if (badm) {                                            // uniform
+            const int f = __builtin_ctzll(badm);
+            s = rlf(rec, f);                                   // exact: every head before f passed
+            {
+                const int h = __builtin_amdgcn_readlane(cur.hi, f), end = __builtin_amdgcn_readlane(cur.end, f);
+                chained += __builtin_amdgcn_readlane(cur.flag, f) == kMwFail && end - h > 1 ? 1 : 0;
+                s = walk_terms(col, h + 1, end, s);
+                ++fbs;
+            }
+            const int m = min(64, total - k0);
+            for (int l = f + 1; l < m; ++l) {                   // the rest of the window head by head
+                const int h = __builtin_amdgcn_readlane(cur.hi, l), end = __builtin_amdgcn_readlane(cur.end, l);
+                s = s + rlf(cur.x, l);
+                const double dl = static_cast<double>(s);
+                const int fl = __builtin_amdgcn_readlane(cur.flag, l);
+                const bool okl = fl == 1 || (fl == 0 && dl >= rl64d(cur.dlo, l) && dl <= rl64d(cur.dhi, l));
+                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) {
+                    s = s + rlf(cur.dq, l);
+                } else {
+                    chained += fl == kMwFail && end - h > 1 ? 1 : 0;
+                    s = walk_terms(col, h + 1, end, s);
+                    ++fbs;
+                }
+            }
+        }
+    };
+    Win cur = load(0);                                         // the next window's records in flight
+    for (int k0 = 0; k0 < total; k0 += 64) {
+        const Win nxt = load(k0 + 64);
+        process(cur, k0);
+        cur = nxt;
+    }
+    if (lane == 0) {
+        out[colI] = s;
+        if (stats) { stats[3 * colI] = total; stats[3 * colI + 1] = fbs; stats[3 * colI + 2] = chained; }
+#ifdef LO_EXACT_STAMPS
+        if (st) {                                              // walk statistics summed over columns and iterations
+            DevState* w = const_cast<DevState*>(st);
+            atomicAdd(&w->dbg[15], static_cast<unsigned long long>(total));
+            atomicAdd(&w->dbg[13], static_cast<unsigned long long>(fbs));
+            atomicAdd(&w->dbg[12], static_cast<unsigned long long>(chained));
+        }
+#endif
+    }
+}
+
+// Host side: the fp32 sequential sums of ncol columns (col0 + k * ld, n terms each; n_dev: a device-side count <= n_cap
+// instead) into out[0, ncol), B sized for n_cap.  stats (nullable): 3 per column.
+void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
+                    float* out, long long* stats, hipStream_t s) {
+    const int nc = (n_cap + kMwChunk - 1) / kMwChunk;
+    if (nc > 0) {
+        hipLaunchKernelGGL(k_mw_chunk_sums, dim3(nc, ncol), dim3(256), 0, s, col0, ld, n_cap, n_dev, st, B);
+        hipLaunchKernelGGL(k_mw_drift, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+        hipLaunchKernelGGL(k_mw_classify, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+        hipLaunchKernelGGL(k_mw_compact, dim3(nc, ncol), dim3(256), 0, s, n_cap, n_dev, st, B);
+    }
+    hipLaunchKernelGGL(k_mw_walk, dim3(ncol), dim3(64), 0, s, col0, ld, n_cap, n_dev, st, B, out, stats);
+}
+// Bytes of an MwBuf for ncol columns of up to n_cap terms, and its layout in one allocation.
+size_t mw_bytes(int ncol, int n_cap) {
+    const size_t nc = static_cast<size_t>(std::max(1, (n_cap + kMwChunk - 1) / kMwChunk));
+    const size_t rec = static_cast<size_t>(ncol) * nc * kMwCap, per = static_cast<size_t>(ncol) * nc;
+    const size_t crec = static_cast<size_t>(ncol) * (nc * kMwCap + kMwPad);
+    return (rec + crec) * (5 * sizeof(int) + 2 * sizeof(double)) + per * (sizeof(int) + 3 * sizeof(double)) +
+           static_cast<size_t>(ncol) * sizeof(int) + 20 * 256;
+}
+MwBuf mw_layout(void* mem, int ncol, int n_cap) {
+    MwBuf B{};
+    const size_t nc = static_cast<size_t>(std::max(1, (n_cap + kMwChunk - 1) / kMwChunk));
+    const size_t rec = static_cast<size_t>(ncol) * nc * kMwCap, per = static_cast<size_t>(ncol) * nc;
+    const size_t crec = static_cast<size_t>(ncol) * (nc * kMwCap + kMwPad);
+    char* p = static_cast<char*>(mem);
+    auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) / 256 * 256; return q; };
+    B.dlo = reinterpret_cast<double*>(take(rec * 8));
+    B.dhi = reinterpret_cast<double*>(take(rec * 8));
+    B.c_dlo = reinterpret_cast<double*>(take(crec * 8));
+    B.c_dhi = reinterpret_cast<double*>(take(crec * 8));
+    B.csum = reinterpret_cast<double*>(take(per * 8));
+    B.cabs = reinterpret_cast<double*>(take(per * 8));
+    B.dcorr = reinterpret_cast<double*>(take(per * 8));
+    B.idx = reinterpret_cast<int*>(take(rec * 4));
+    B.end = reinterpret_cast<int*>(take(rec * 4));
+    B.x = reinterpret_cast<float*>(take(rec * 4));
+    B.dq = reinterpret_cast<float*>(take(rec * 4));
+    B.flag = reinterpret_cast<int*>(take(rec * 4));
+    B.c_idx = reinterpret_cast<int*>(take(crec * 4));
+    B.c_end = reinterpret_cast<int*>(take(crec * 4));
+    B.c_x = reinterpret_cast<float*>(take(crec * 4));
+    B.c_dq = reinterpret_cast<float*>(take(crec * 4));
+    B.c_flag = reinterpret_cast<int*>(take(crec * 4));
+    B.nh = reinterpret_cast<int*>(take(per * 4));
+    B.ntot = reinterpret_cast<int*>(take(static_cast<size_t>(ncol) * 4));
+    B.nchunks = static_cast<int>(nc);
+    B.cstride = nc * kMwCap + kMwPad;
+    return B;
+}
+
+// ---- long mono sums: the iteration-0 scale of scans beyond kExactMaxPoints (lo_seqsum.h MwmBuf) ----
+__device__ __forceinline__ bool mwm_skip(const DevState* st, const MwmBuf& B) { return st->done || B.cnt[0] == 0 || B.cnt[1]; }
+template <bool SQ>
+__device__ __forceinline__ double mwm_term(const double* __restrict__ sorted, int j, int cnt, double m) {
+    if (j >= cnt) return 0.0;
+    const double v = sorted[j];
+    return SQ ? (v - m) * (v - m) : v;
+}
+
+// accepted residuals = the finite prefix of the sorted array (cnt[] zeroed by the host first)
+__global__ __launch_bounds__(256) void k_mwm_count(const double* __restrict__ sorted, int n, const DevState* st, MwmBuf B) {
+    if (st->done) return;
+    __shared__ int s_w[4];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const double v = i < n ? sorted[i] : __builtin_inf();
+    int fin;
+    (void)block_excl_scan<int, 256>(v != __builtin_inf() && !isnan(v) ? 1 : 0, s_w, fin);
+    const int nan = __syncthreads_or(isnan(v) ? 1 : 0);
+    if (threadIdx.x == 0) {
+        if (fin) atomicAdd(&B.cnt[0], fin);
+        if (nan) B.cnt[1] = 1;
+    }
+}
+
+template <bool SQ>
+__global__ __launch_bounds__(256) void k_mwm_chunk_sums(const double* __restrict__ sorted, const DevState* st, MwmBuf B) {
+    if (mwm_skip(st, B)) return;
+    __shared__ double s_w[4];
+    const int c = blockIdx.x, tid = threadIdx.x, cnt = B.cnt[0], c0 = c * kMwChunk;
+    const double m = SQ ? B.res[0] / cnt : 0.0;
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMwChunk / 256; ++k) v += mwm_term<SQ>(sorted, c0 + k * 256 + tid, cnt, m);
+    double tot;
+    (void)block_excl_scan<double, 256>(v, s_w, tot);
+    if (tid == 0) B.csum[c] = tot;
+}
+
+struct MwmScratch {
+    double wd[kMwWaves];
+    long long wl[kMwWaves];
+    int wi[kMwWaves];
+    int elast[kMwThreads];
+    int h_idx[kMwmCap];
+    int h_e[kMwmCap];
+    long long h_p[kMwmCap];
+};
+
+template <bool SQ>
+__global__ __launch_bounds__(kMwThreads) void k_mwm_classify(const double* __restrict__ sorted, const DevState* st, MwmBuf B) {
+    if (mwm_skip(st, B)) return;
+    __shared__ MwmScratch S;
+    const int c = blockIdx.x, tid = threadIdx.x, cnt = B.cnt[0], c0 = c * kMwChunk, mc = min(kMwChunk, cnt - c0);
+    if (mc <= 0) return;
+    const double m = SQ ? B.res[0] / cnt : 0.0;
+    double t0 = 0.0;
+    for (int k = tid; k < c; k += kMwThreads) t0 += B.csum[k];
+    double T0;
+    (void)block_excl_scan<double, kMwThreads>(t0, S.wd, T0);
+    const int base = tid * kMwPT;
+    double v[kMwPT];
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) v[a] = base + a < mc ? mwm_term<SQ>(sorted, c0 + base + a, cnt, m) : 0.0;
+    double run = 0.0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) run += v[a];
+    double ttot;
+    const double tex = T0 + block_excl_scan<double, kMwThreads>(run, S.wd, ttot);
+    S.elast[tid] = binade64(tex + run);
+    __syncthreads();
+    const int e_in = tid ? S.elast[tid - 1] : kExpNone;
+    // mono_seq_sum's classify; term 0 of every chunk heads a segment
+    auto classify = [&](int a, double T, int ep, int& E, long long& qa) -> bool {
+        const int j = base + a;
+        const double xv = v[a];
+        E = binade64(T);
+        qa = 0;
+        if (!(j < mc && (xv != 0.0 || j == 0))) return false;
+        if (E < -1000 || E != ep || j == 0) return true;
+        const double t = ldexp(xv, 52 - E);
+        const double f = floor(t), fr = t - f;
+        if (fr == 0.5) return true;
+        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
+        return false;
+    };
+    long long ql = 0;
+    int nhl = 0;
+    {
+        double tl = 0.0;
+        int ep = e_in;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) {
+            tl += v[a];
+            int E;
+            long long qa;
+            nhl += classify(a, tex + tl, ep, E, qa) ? 1 : 0;
+            ql += qa;
+            ep = E;
+        }
+    }
+    long long ptot;
+    const long long pex = block_excl_scan<long long, kMwThreads>(ql, S.wl, ptot);
+    int htot;
+    const int hbase = block_excl_scan<int, kMwThreads>(nhl, S.wi, htot);
+    const size_t rb = static_cast<size_t>(c) * kMwmCap;
+    if (htot > kMwmCap) {                                       // uniform: the whole chunk term by term
+        if (tid == 0) {
+            B.nh[c] = 1;
+            B.idx[rb] = c0;
+            B.end[rb] = c0 + mc;
+            B.flag[rb] = kMwFail;
+            B.x[rb] = mwm_term<SQ>(sorted, c0, cnt, m);
+            B.dq[rb] = -0.0;
+            B.dlo[rb] = __builtin_inf();
+            B.dhi[rb] = -__builtin_inf();
+        }
+        return;
+    }
+    {
+        double tl = 0.0;
+        int ep = e_in, hk = hbase;
+        long long prun = pex;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) {
+            tl += v[a];
+            int E;
+            long long qa;
+            const bool hd = classify(a, tex + tl, ep, E, qa);
+            prun += qa;
+            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; ++hk; }
+            ep = E;
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < htot; k += kMwThreads) {
+        const int hi = S.h_idx[k], E = S.h_e[k];
+        const long long hp = S.h_p[k];
+        const bool last = k + 1 >= htot;
+        const int hend = last ? mc : S.h_idx[k + 1];
+        const long long Q = (last ? ptot : S.h_p[k + 1]) - hp;
+        int flag = hend > hi + 1 ? 0 : 1;
+        double dq = -0.0, dlo = __builtin_inf(), dhi = -__builtin_inf();
+        if (!flag) {
+            if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
+                const double u = ldexp(1.0, E - 52);
+                dq = static_cast<double>(Q) * u;
+                dlo = ldexp(1.0, E);
+                dhi = (ldexp(1.0, E + 1) - u) - dq;            // exact: multiples of u below 2^(E+1)
+            } else {
+                flag = kMwFail;
+            }
+        }
+        const size_t r = rb + k;
+        B.idx[r] = c0 + hi;
+        B.end[r] = c0 + hend;
+        B.flag[r] = flag;
+        B.x[r] = mwm_term<SQ>(sorted, c0 + hi, cnt, m);
+        B.dq[r] = dq;
+        B.dlo[r] = dlo;
+        B.dhi[r] = dhi;
+    }
+    if (tid == 0) B.nh[c] = htot;
+}
+
+__global__ __launch_bounds__(256) void k_mwm_compact(const DevState* st, MwmBuf B) {
+    if (mwm_skip(st, B)) return;
+    __shared__ int s_w[4];
+    const int c = blockIdx.x, tid = threadIdx.x, cnt = B.cnt[0], nc = (cnt + kMwChunk - 1) / kMwChunk;
+    if (c >= nc) return;
+    int before = 0;
+    for (int k = tid; k < c; k += 256) before += B.nh[k];
+    int off;
+    (void)block_excl_scan<int, 256>(before, s_w, off);
+    const int h = B.nh[c];
+    const size_t src = static_cast<size_t>(c) * kMwmCap;
+    for (int k = tid; k < h; k += 256) {
+        B.c_idx[off + k] = B.idx[src + k];
+        B.c_end[off + k] = B.end[src + k];
+        B.c_flag[off + k] = B.flag[src + k];
+        B.c_x[off + k] = B.x[src + k];
+        B.c_dq[off + k] = B.dq[src + k];
+        B.c_dlo[off + k] = B.dlo[src + k];
+        B.c_dhi[off + k] = B.dhi[src + k];
+    }
+    if (c == nc - 1) {                                         // no-op records after the last head
+        if (tid < kMwPad) {
+            const int r = off + h + tid;
+            B.c_idx[r] = 0; B.c_end[r] = 0; B.c_flag[r] = 1; B.c_x[r] = -0.0; B.c_dq[r] = -0.0;
+            B.c_dlo[r] = 0.0; B.c_dhi[r] = 0.0;
+        }
+        if (tid == 0) B.cnt[2] = off + h;
+    }
+}
+
+// s + x[j0] + ... + x[j1 - 1] term by term, x = the (squared-deviation) terms, scalar loads as walk_terms
+template <bool SQ>
+__device__ __forceinline__ double walk_terms_m(const double* __restrict__ sorted, int j0, int j1, int cnt, double m, double s) {
+    constexpr int kB = 16;
+    j0 = __builtin_amdgcn_readfirstlane(j0);
+    j1 = __builtin_amdgcn_readfirstlane(j1);
+    const int lane = threadIdx.x & 63;
+    int j = j0;
+    {                                                          // to a 128-byte boundary: one load per lane
+        const int a = min(j1, (j0 + kB - 1) & ~(kB - 1));
+        const double v = lane < a - j0 ? mwm_term<SQ>(sorted, j0 + lane, cnt, m) : -0.0;
+        for (int l = 0; l < a - j0; ++l) s = s + rl64d(v, l);
+        j = a;
+    }
+    if (j + kB <= j1) {
+        double cur[kB], nxt[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) cur[u] = sorted[j + u];
+        for (; j + 2 * kB <= j1; j += kB) {
+#pragma unroll
+            for (int u = 0; u < kB; ++u) nxt[u] = sorted[j + kB + u];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) s = s + (SQ ? (cur[u] - m) * (cur[u] - m) : cur[u]);
+#pragma unroll
+            for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) s = s + (SQ ? (cur[u] - m) * (cur[u] - m) : cur[u]);
+        j += kB;
+    }
+    {                                                          // the rest (< kB terms): one load per lane
+        const double v = lane < j1 - j ? mwm_term<SQ>(sorted, j + lane, cnt, m) : -0.0;
+        for (int l = 0; l < j1 - j; ++l) s = s + rl64d(v, l);
+    }
+    return s;
+}
+
+// one wave: every head in order (as k_mw_walk, fp64); the sum into B.res[SQ]; SQ also writes the scale
+template <bool SQ>
+__global__ __launch_bounds__(64) void k_mwm_walk(const double* __restrict__ sorted, DevState* st, MwmBuf B) {
+    if (mwm_skip(st, B)) return;
+    const int lane = threadIdx.x, cnt = B.cnt[0], total = B.cnt[2];
+    const double m = SQ ? B.res[0] / cnt : 0.0;
+    struct Win { int hi, end, flag; double x, dq, dlo, dhi; };
+    auto load = [&](int k0) {                                  // records past the last head are no-ops (kMwPad)
+        const int k = k0 + lane;
+        return Win{B.c_idx[k], B.c_end[k], B.c_flag[k], B.c_x[k], B.c_dq[k], B.c_dlo[k], B.c_dhi[k]};
+    };
+    double s = 0.0;
+    int fbs = 0, fbt = 0;
+#ifdef LO_EXACT_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_terms = 0;
+#define LO_TT0 const unsigned long long t_a = __builtin_amdgcn_s_memtime();
+#define LO_TT1 t_terms += __builtin_amdgcn_s_memtime() - t_a;
+#else
+#define LO_TT0
+#define LO_TT1
+#endif
+    __shared__ double2 s_xd[64];                               // the window's (x, dq), read back as broadcasts
+    auto process = [&](const Win& cur, int k0) {
+        double rec = 0.0;
+        s_xd[lane] = make_double2(cur.x, cur.dq);
+        __syncthreads();
+        LO_TT0
+#pragma unroll
+        for (int l = 0; l < 64; ++l) {
+            const double2 xd = s_xd[l];
+            s = s + xd.x;
+            rec = lane == l ? s : rec;
+            s = s + xd.y;
+        }
+        LO_TT1
+        __syncthreads();
+        const bool ok = cur.flag == 1 || (cur.flag == 0 && rec >= cur.dlo && rec <= cur.dhi);
+        const unsigned long long badm = __ballot(!ok);
+        if (badm) {
+            const int f = __builtin_ctzll(badm);
+            s = rl64d(rec, f);                                  // exact: every head before f passed
+            s = walk_terms_m<SQ>(sorted, __builtin_amdgcn_readlane(cur.hi, f) + 1, __builtin_amdgcn_readlane(cur.end, f),
+                                 cnt, m, s);
+            ++fbs;
+            fbt += __builtin_amdgcn_readlane(cur.end, f) - __builtin_amdgcn_readlane(cur.hi, f) - 1;
+            const int mw = min(64, total - k0);
+            for (int l = f + 1; l < mw; ++l) {
+                s = s + rl64d(cur.x, l);
+                const int fl = __builtin_amdgcn_readlane(cur.flag, l);
+                const bool okl = fl == 1 || (fl == 0 && s >= rl64d(cur.dlo, l) && s <= rl64d(cur.dhi, l));
+                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) s = s + rl64d(cur.dq, l);
+                else {
+                    s = walk_terms_m<SQ>(sorted, __builtin_amdgcn_readlane(cur.hi, l) + 1,
+                                         __builtin_amdgcn_readlane(cur.end, l), cnt, m, s);
+                    ++fbs;
+                    fbt += __builtin_amdgcn_readlane(cur.end, l) - __builtin_amdgcn_readlane(cur.hi, l) - 1;
+                }
+            }
+        }
+    };
+    Win cur = load(0);                                         // the next window's records in flight
+    for (int k0 = 0; k0 < total; k0 += 64) {
+        const Win nxt = load(k0 + 64);
+        process(cur, k0);
+        cur = nxt;
+    }
+    if (lane == 0) {
+        B.res[SQ ? 1 : 0] = s;
+        if (SQ) st->scale = sqrt(s / cnt) / 6.0;
+        (void)fbs;
+        (void)fbt;
+#ifdef LO_EXACT_STAMPS
+        st->dbg[SQ ? 8 : 5] = static_cast<unsigned long long>(total);   // walk statistics of the last scan
+        st->dbg[SQ ? 9 : 6] = static_cast<unsigned long long>(fbs);
+        st->dbg[SQ ? 10 : 7] = static_cast<unsigned long long>(fbt);
+        if (!SQ) { st->dbg[11] = __builtin_amdgcn_s_memtime() - t_start; st->dbg[14] = t_terms; }
+#endif
+#undef LO_TT0
+#undef LO_TT1
+    }
+}
+
+// a NaN residual: the reference's sums are NaN and so is the scale (k_exact_scale's rule)
+__global__ void k_mwm_nan(const double* __restrict__ sorted, DevState* st, MwmBuf B) {
+    if (st->done || B.cnt[0] == 0 || !B.cnt[1]) return;      // no correspondence: the PKO launch reports it
+    st->scale = __builtin_nan("");
+}
+
+void launch_mwm_scale(KParams P, const double* sorted, const MwmBuf& B, hipStream_t s) {
+    const int n = P.n, nc = (n + kMwChunk - 1) / kMwChunk;
+    (void)hipMemsetAsync(B.cnt, 0, 3 * sizeof(int), s);
+    hipLaunchKernelGGL(k_mwm_count, dim3((n + 255) / 256), dim3(256), 0, s, sorted, n, P.st, B);
+    hipLaunchKernelGGL(k_mwm_nan, dim3(1), dim3(1), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_chunk_sums<false>, dim3(nc), dim3(256), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_classify<false>, dim3(nc), dim3(kMwThreads), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_compact, dim3(nc), dim3(256), 0, s, P.st, B);
+    hipLaunchKernelGGL(k_mwm_walk<false>, dim3(1), dim3(64), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_chunk_sums<true>, dim3(nc), dim3(256), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_classify<true>, dim3(nc), dim3(kMwThreads), 0, s, sorted, P.st, B);
+    hipLaunchKernelGGL(k_mwm_compact, dim3(nc), dim3(256), 0, s, P.st, B);
+    hipLaunchKernelGGL(k_mwm_walk<true>, dim3(1), dim3(64), 0, s, sorted, P.st, B);
+}
+size_t mwm_bytes(int n_cap) {
+    const size_t nc = static_cast<size_t>(std::max(1, (n_cap + kMwChunk - 1) / kMwChunk)), rec = nc * kMwmCap;
+    return (2 * rec + kMwPad) * (3 * sizeof(int) + 4 * sizeof(double)) + nc * (sizeof(int) + sizeof(double)) + 64 +
+           20 * 256;
+}
+MwmBuf mwm_layout(void* mem, int n_cap) {
+    MwmBuf B{};
+    const size_t nc = static_cast<size_t>(std::max(1, (n_cap + kMwChunk - 1) / kMwChunk)), rec = nc * kMwmCap;
+    char* p = static_cast<char*>(mem);
+    auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) / 256 * 256; return q; };
+    B.x = reinterpret_cast<double*>(take(rec * 8));
+    B.dq = reinterpret_cast<double*>(take(rec * 8));
+    B.dlo = reinterpret_cast<double*>(take(rec * 8));
+    B.dhi = reinterpret_cast<double*>(take(rec * 8));
+    B.c_x = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.c_dq = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.c_dlo = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.c_dhi = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.csum = reinterpret_cast<double*>(take(nc * 8));
+    B.res = reinterpret_cast<double*>(take(16));
+    B.idx = reinterpret_cast<int*>(take(rec * 4));
+    B.end = reinterpret_cast<int*>(take(rec * 4));
+    B.flag = reinterpret_cast<int*>(take(rec * 4));
+    B.c_idx = reinterpret_cast<int*>(take((rec + kMwPad) * 4));
+    B.c_end = reinterpret_cast<int*>(take((rec + kMwPad) * 4));
+    B.c_flag = reinterpret_cast<int*>(take((rec + kMwPad) * 4));
+    B.nh = reinterpret_cast<int*>(take(nc * 4));
+    B.cnt = reinterpret_cast<int*>(take(16));
+    B.nchunks = static_cast<int>(nc);
+    return B;
+}
+
+// large scans: the fp32 solve of the 43 column sums (launch_mw_sums), as k_exact_solve does it
 __global__ void k_exact_finish(KParams P, int it) {
     DevState* st = P.st;
     if (st->done || threadIdx.x != 0) return;

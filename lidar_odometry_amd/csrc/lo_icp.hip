@@ -25,6 +25,7 @@
 #include "lo_kdorder.h"
 #include "lo_math.h"
 #include "lo_pko_tables.h"
+#include "lo_seqsum.h"
 #include "lo_vfilter.h"
 
 namespace lo {
@@ -67,12 +68,16 @@ __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float t
                              FitOut* out);
 void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s);
 void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s);
-void launch_seq_sum_f32_diag(const float* x, int n, float* out, long long* stats, hipStream_t s);
+void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
+                    float* out, long long* stats, hipStream_t s);
+size_t mw_bytes(int ncol, int n_cap);
+MwBuf mw_layout(void* mem, int ncol, int n_cap);
+void launch_mwm_scale(KParams P, const double* sorted, const MwmBuf& B, hipStream_t s);
+size_t mwm_bytes(int n_cap);
+MwmBuf mwm_layout(void* mem, int n_cap);
 __global__ void k_exact_resid(KParams P, double* out);
-__global__ void k_exact_scale_g(KParams P, const double* sorted);
 __global__ void k_exact_terms(KParams P);
 __global__ void k_exact_solve(KParams P, int it);
-__global__ void k_exact_sum43(KParams P);
 __global__ void k_exact_finish(KParams P, int it);
 }  // namespace lo
 
@@ -119,8 +124,13 @@ struct lo_ctx {
     bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
     float* d_ex_terms = nullptr;
     size_t ex_cap = 0;              //   rows of d_ex_terms
-    float* d_ex_tot = nullptr;      //   large scans: the 43 sums (k_exact_sum43 -> k_exact_finish)
+    float* d_ex_tot = nullptr;      //   large scans: the 43 sums (launch_mw_sums -> k_exact_finish)
     double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints)
+    void* d_mw = nullptr;           //   large scans: head records of the 43 column sums (lo_seqsum.h MwBuf)
+    size_t mw_n_cap = 0;            //   the scan size d_mw is laid out for
+    MwBuf mw{};
+    void* d_mwm = nullptr;          //   large scans: head records of the iteration-0 scale's two sums (MwmBuf)
+    MwmBuf mwm{};
     double* d_ex_res = nullptr;     //   scans beyond kExactMaxPoints: residuals, sorted residuals, hipCUB scratch
     double* d_ex_sorted = nullptr;
     void* d_ex_sort_tmp = nullptr;
@@ -608,7 +618,7 @@ void lo_destroy(lo_ctx* c) {
                     c->grid.d_vpos, c->grid.d_nodes, c->lgrid.d_vpos, c->lgrid.d_nodes,
                     c->d_kd_nbr, c->d_kd_unres, c->d_kd_res, c->d_kd_plane, c->d_ex_terms, c->d_res_pko,
                     c->d_ex_res, c->d_ex_sorted, c->d_ex_sort_tmp, c->d_ex_tot, c->d_ex_rank,
-                    c->d_cand_rec, c->d_cand_cnt};
+                    c->d_mw, c->d_mwm, c->d_cand_rec, c->d_cand_cnt};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->grid.h_stage) (void)hipHostFree(c->grid.h_stage);
     if (c->lgrid.h_stage) (void)hipHostFree(c->lgrid.h_stage);
@@ -1192,7 +1202,7 @@ static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
 // Reference-exact mode (lo_exact.hip): device buffers on first use, then per GN iteration the correspondence stage,
 // (iteration 0) the sorted-order scale, the PKO, the per-point terms and the sequential sums + fp32 solve.  Scans of
 // at most kExactMaxPoints sort in one workgroup (*n2 = n: registers + LDS, lo_seqsum.h); larger scans (*n2 = 0)
-// write their residuals out, sort them with hipCUB's radix sort and sum from global memory (k_exact_scale_g).
+// write their residuals out, sort them with hipCUB's radix sort and sum them across the chip (launch_mwm_scale).
 static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     if (!c->d_ex_terms || c->ex_cap < std::max(n, static_cast<size_t>(kExactMaxPoints))) {
         if (c->d_ex_terms) LO_HIP(c, hipFree(c->d_ex_terms));
@@ -1205,6 +1215,17 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     P.scale_given = 1;
     if (n > static_cast<size_t>(kExactMaxPoints)) {
         if (!c->d_ex_tot) LO_HIP(c, hipMalloc(&c->d_ex_tot, 64 * sizeof(float)));
+        if (c->mw_n_cap < n) {                               // the column sums' head records
+            if (c->d_mw) LO_HIP(c, hipFree(c->d_mw));
+            c->d_mw = nullptr;
+            c->mw_n_cap = n;
+            LO_HIP(c, hipMalloc(&c->d_mw, mw_bytes(43, static_cast<int>(n))));
+            c->mw = mw_layout(c->d_mw, 43, static_cast<int>(n));
+            if (c->d_mwm) LO_HIP(c, hipFree(c->d_mwm));
+            c->d_mwm = nullptr;
+            LO_HIP(c, hipMalloc(&c->d_mwm, mwm_bytes(static_cast<int>(n))));
+            c->mwm = mwm_layout(c->d_mwm, static_cast<int>(n));
+        }
         P.ex_ld = static_cast<int>(n);                     // term-major: one coalesced column per sum
         P.ex_tot = c->d_ex_tot;
         if (c->ex_res_cap < n) {
@@ -1238,7 +1259,7 @@ static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStrea
     size_t tmp = c->ex_sort_tmp_bytes;
     (void)hipcub::DeviceRadixSort::SortKeys(c->d_ex_sort_tmp, tmp, c->d_ex_res, c->d_ex_sorted, n, 0,
                                             static_cast<int>(sizeof(double) * 8), s);
-    hipLaunchKernelGGL(k_exact_scale_g, dim3(1), dim3(1024), 0, s, P, c->d_ex_sorted);
+    launch_mwm_scale(P, c->d_ex_sorted, c->mwm, s);
 }
 static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P0, int it, int n2, bool kd) {
     launch_correspond(c, it == 0 ? P0 : P, 0, kd);
@@ -1246,7 +1267,7 @@ static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
     if (P.ex_ld) {                                           // large scan: 43 parallel sequential-sum reproductions
-        hipLaunchKernelGGL(k_exact_sum43, dim3(43), dim3(1024), 0, c->stream, P);
+        launch_mw_sums(P.ex_terms, P.ex_ld, 43, P.n, P.n_dev, P.st, c->mw, P.ex_tot, nullptr, c->stream);
         hipLaunchKernelGGL(k_exact_finish, dim3(1), dim3(64), 0, c->stream, P, it);
     } else {
         hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
@@ -1933,21 +1954,40 @@ int lo_seq_sum_f64(lo_ctx* c, const double* x, size_t n, int sort, double* out_s
 }
 
 int lo_seq_sum_f32(lo_ctx* c, const float* x, size_t n, float* out_sum, long long stats[4]) {
-    if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(INT32_MAX)) return LO_ERR_ARG;
+    if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(kMaxBlocks) * kBlock) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
-    float* d = nullptr;
-    const size_t st_off = ((n + 2) * sizeof(float) + 7) / 8 * 8;
-    LO_HIP(c, hipMalloc(&d, st_off + 4 * sizeof(long long)));
-    long long* d_st = reinterpret_cast<long long*>(reinterpret_cast<char*>(d) + st_off);
-    if (n > 0) LO_HIP(c, hipMemcpy(d, x, n * sizeof(float), hipMemcpyHostToDevice));
-    launch_seq_sum_f32_diag(d, static_cast<int>(n), d + n, d_st, c->stream);
-    hipError_t e = hipStreamSynchronize(c->stream);
-    long long st[4] = {0, 0, 0, 0};
-    if (e == hipSuccess) e = hipMemcpy(out_sum, d + n, sizeof(float), hipMemcpyDeviceToHost);
+    const int ni = static_cast<int>(n);
+    const size_t x_bytes = (n * sizeof(float) + 255) / 256 * 256, mwb = mw_bytes(1, ni);
+    char* d = nullptr;
+    LO_HIP(c, hipMalloc(&d, x_bytes + mwb + 256));
+    float* d_x = reinterpret_cast<float*>(d);
+    const MwBuf B = mw_layout(d + x_bytes, 1, ni);
+    float* d_out = reinterpret_cast<float*>(d + x_bytes + mwb);
+    long long* d_st = reinterpret_cast<long long*>(d + x_bytes + mwb + 64);
+    hipError_t e = hipSuccess;
+    if (n > 0) e = hipMemcpy(d_x, x, n * sizeof(float), hipMemcpyHostToDevice);
+    float ms = 0.0f;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) {
+        (void)hipEventRecord(e0, c->stream);
+        launch_mw_sums(d_x, ni, 1, ni, nullptr, nullptr, B, d_out, d_st, c->stream);
+        (void)hipEventRecord(e1, c->stream);
+        e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    long long st[3] = {0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(out_sum, d_out, sizeof(float), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) { c->err = std::string("lo_seq_sum_f32: ") + hipGetErrorString(e); return LO_ERR_HIP; }
-    if (stats) for (int k = 0; k < 4; ++k) stats[k] = st[k];
+    if (stats) {
+        for (int k = 0; k < 3; ++k) stats[k] = st[k];
+        stats[3] = static_cast<long long>(ms * 1e3);      // microseconds of the three launches
+    }
     return LO_OK;
 }
 

@@ -50,10 +50,11 @@ __device__ __forceinline__ long long rl64i(long long v, int l) {
     return static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
-// Exclusive prefix over the workgroup of one value per thread (wave scan by shuffles, wave totals through LDS), and
-// the total.  s_w: kSeqWaves entries, free again when the function returns.
-template <typename T>
+// Exclusive prefix over the workgroup (NT threads) of one value per thread (wave scan by shuffles, wave totals through
+// LDS), and the total.  s_w: NT / 64 entries, free again when the function returns.
+template <typename T, int NT = kSeqThreads>
 __device__ __forceinline__ T block_excl_scan(T v, T* s_w, T& total) {
+    constexpr int kNW = NT / kWave;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     T inc = v;
 #pragma unroll
@@ -67,7 +68,7 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s_w, T& total) {
     __syncthreads();
     T before = T(0), tot = T(0);
 #pragma unroll
-    for (int w = 0; w < kSeqWaves; ++w) {
+    for (int w = 0; w < kNW; ++w) {
         const T x = s_w[w];
         if (w < wid) before += x;
         tot += x;
@@ -265,30 +266,10 @@ namespace lo {
 // The partial sums of a segment are no longer monotone, so the prediction carries the proof: a term heads a segment
 // also when its predicted prefix T lies within M = 2^(E-9) of either edge of its binade.  Inside a segment every T_j
 // is then at least M from the edges, and the true partial sums differ from T_j by at most |s_h - T_h| (known once the
-// walk reaches the head) + (end - h) u / 2 (one half-ulp per step) + the fp64 error of T (< 2^(E-30)): when that total
-// stays below M - u, every partial sum of the segment is inside the binade, one ulp from its edges, and the integer
-// model is exact for each step.  The fp64 error of T is bounded per chunk by 2^-46 times the largest magnitude any of its
-// partial sums reaches (fewer than 64 roundings per predicted term), so a chunk whose sums cancel large values only
-// loses parallelism, never exactness.  Terms come in chunks (kSeqThreads * PT), each chunk starting a segment, with
-// the exact running sum carried in as the next chunk's prediction base.
+// walk reaches the head) + (end - h) u / 2 (one half-ulp per step) + the fp64 error of T: when that total stays below
+// M - u, every partial sum of the segment is inside the binade, one ulp from its edges, and the integer model is exact
+// for each step.  Implemented across the chip for long columns below (k_mw_* in lo_exact.hip).
 // ---------------------------------------------------------------------------------------------------------------------
-constexpr int kSHeadCap = 4096;
-
-struct SeqScratchS {
-    double wd[kSeqWaves];
-    long long wl[kSeqWaves];
-    int wi[kSeqWaves];
-    int elast[kSeqThreads];
-    int glast[kSeqThreads];
-    int h_idx[kSHeadCap];
-    int h_e[kSHeadCap];
-    long long h_p[kSHeadCap];
-    double h_t[kSHeadCap];
-    float result;
-    int e_carry, g_carry;
-    int nheads, fb_seg;
-};
-
 __device__ __forceinline__ int binade_abs(double v) {       // binade of |v| when it is a normal fp32 magnitude
     const double a = fabs(v);
     const uint64_t b = __builtin_bit_cast(uint64_t, a);
@@ -297,163 +278,99 @@ __device__ __forceinline__ int binade_abs(double v) {       // binade of |v| whe
     return (a > 0.0 && f != 0x7FF && e >= -120 && e <= 126) ? e : kExpNone;
 }
 
-// s_in + x_0 + ... + x_{cnt-1} in fp32, one rounding per addition in index order; thread t holds terms t*PT.. (zeros past
-// cnt), s_x[0, cnt) the same terms (LDS).  T0 / e0 / g0: the prediction base, binade and sign carried in from the
-// previous chunk; term 0 always starts a segment.  Every thread returns the sum and the carries; false (nothing
-// computed) when the chunk has more than kSHeadCap heads.
-template <int PT>
-__device__ __forceinline__ bool signed_seq_sum(int cnt, const float* s_x, SeqScratchS& S, double T0, int e0, int g0, float s_in,
-                               float& s_out, int& e_out, int& g_out) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int base = tid * PT;
-    auto term = [&](int a) { return base + a < cnt ? s_x[base + a] : 0.0f; };
-    double run = 0.0, amax = fabs(T0);
-#pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        run += static_cast<double>(term(a));
-        amax = fmax(amax, fabs(run));
-    }
-    double ttot;
-    const double tex = T0 + block_excl_scan<double>(run, S.wd, ttot);
-    {
-        const double Tl = tex + run;
-        S.elast[tid] = binade_abs(Tl);
-        S.glast[tid] = Tl > 0.0 ? 1 : (Tl < 0.0 ? -1 : 0);
-    }
-    __syncthreads();
-    const int e_in = tid ? S.elast[tid - 1] : e0, g_in = tid ? S.glast[tid - 1] : g0;
-    // predicted binade / sign of term a's prefix, whether it lies within M of its binade's edges, and its step
-    auto classify = [&](int a, double T, int ep, int gp, int& E, int& G, long long& qa) -> bool {
-        const int j = base + a;
-        const float xv = term(a);
-        E = binade_abs(T);
-        G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
-        qa = 0;
-        if (!(j < cnt && (xv != 0.0f || j == 0))) return false;          // a chunk's first term heads it even when zero
-        const double at = fabs(T), M = ldexp(1.0, E - 9);
-        const bool edge = E == kExpNone || at < ldexp(1.0, E) + M || at > ldexp(1.0, E + 1) - M;
-        if (edge || E != ep || G != gp || j == 0) return true;
-        const double t = ldexp(static_cast<double>(xv), 23 - E);         // exact
-        const double f = floor(t), fr = t - f;
-        if (fr == 0.5) return true;
-        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
-        return false;
-    };
-    long long ql = 0;
-    int nhl = 0;
-    {
-        double tl = 0.0;
-        int ep = e_in, gp = g_in;
-#pragma unroll
-        for (int a = 0; a < PT; ++a) {
-            tl += static_cast<double>(term(a));
-            const double T = tex + tl;
-            amax = fmax(amax, fabs(T));
-            int E, G;
-            long long qa;
-            nhl += classify(a, T, ep, gp, E, G, qa) ? 1 : 0;
-            ql += qa;
-            ep = E;
-            gp = G;
-        }
-    }
-    amax = fmax(amax, fabs(tex));
-    long long ptot;
-    const long long pex = block_excl_scan<long long>(ql, S.wl, ptot);
-    int htot;
-    const int hbase = block_excl_scan<int>(nhl, S.wi, htot);
-    if (htot > kSHeadCap) return false;
-    const double eps_t = ldexp(block_max(amax, S.wd), -46);    // bound on |T_j - exact prefix| for every term
-    {
-        double tl = 0.0;
-        int ep = e_in, gp = g_in, hk = hbase;
-        long long prun = pex;
-#pragma unroll
-        for (int a = 0; a < PT; ++a) {
-            tl += static_cast<double>(term(a));
-            const double T = tex + tl;
-            int E, G;
-            long long qa;
-            const bool hd = classify(a, T, ep, gp, E, G, qa);
-            prun += qa;
-            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; S.h_t[hk] = T; ++hk; }
-            ep = E;
-            gp = G;
-        }
-        if (tid == kSeqThreads - 1) { S.e_carry = ep; S.g_carry = gp; }
-    }
-    if (tid == 0) S.nheads = htot;
-    __syncthreads();
-    if (wid == 0) {
-        // lane l of a 64-head window precomputes head k0 + l's checks: the binade [2^E, 2^(E+1)), the allowed distance
-        // of the head's result from its prediction (M - the segment's rounding and T error budget), the segment's sum;
-        // a one-term segment or a lane past the last head passes (dq 0), a segment without a binade fails.  Eight heads
-        // at a time as a branch-free chain; a group with a failed check is redone head by head from its start
-        float s = s_in;
-        int fbs = 0;
-        for (int k0 = 0; k0 < htot; k0 += 64) {
-            const int kk = k0 + lane;
-            int hi = 0, hend = cnt, hg = 0, pass = 1;
-            double ht = 0.0, lo_e = __builtin_inf(), maxdev = -1.0, dq = -0.0;          // x + -0 == x, also for x = -0
-            float hx = -0.0f;
-            if (kk < htot) {
-                hi = S.h_idx[kk];
-                const int E = S.h_e[kk];
-                const long long hp = S.h_p[kk];
-                long long pend = ptot;
-                ht = S.h_t[kk];
-                hx = s_x[hi];
-                if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
-                pass = hend > hi + 1 ? 0 : 1;
-                if (!pass && E != kExpNone) {
-                    const double u = ldexp(1.0, E - 23);
-                    lo_e = ldexp(1.0, E);
-                    hg = ht > 0.0 ? 1 : -1;
-                    maxdev = ldexp(1.0, E - 9) - (static_cast<double>(hend - hi) * 0.5 + 1.0) * u - 2.0 * eps_t;
-                    dq = static_cast<double>(pend - hp) * u;
-                }
-            }
-            auto check = [&](double d, int l) -> bool {
-                const double ad = fabs(d), le = rl64d(lo_e, l);
-                const bool sgn = __builtin_amdgcn_readlane(hg, l) > 0 ? d > 0.0 : d < 0.0;
-                return __builtin_amdgcn_readlane(pass, l) != 0 ||
-                       (ad >= le && ad < 2.0 * le && sgn && fabs(d - rl64d(ht, l)) <= rl64d(maxdev, l));
-            };
-            auto rlf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
-            const int m = min(64, htot - k0);
-            for (int l0 = 0; l0 < m; l0 += 8) {
-                const float s0 = s;
-                int bad = 0;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    s = s + rlf(hx, l0 + u);
-                    const double d = static_cast<double>(s);
-                    bad |= check(d, l0 + u) ? 0 : 1;
-                    s = static_cast<float>(d + rl64d(dq, l0 + u));
-                }
-                if (__builtin_amdgcn_readfirstlane(bad)) {
-                    s = s0;
-                    for (int l = l0; l < min(l0 + 8, m); ++l) {
-                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
-                        s = s + rlf(hx, l);
-                        const double d = static_cast<double>(s);
-                        if (__builtin_amdgcn_readfirstlane(check(d, l) ? 1 : 0)) {
-                            s = static_cast<float>(d + rl64d(dq, l));
-                        } else {
-                            for (int j = h + 1; j < end; ++j) s = s + s_x[j];
-                            ++fbs;
-                        }
-                    }
-                }
-            }
-        }
-        if (lane == 0) { S.result = s; S.fb_seg = fbs; }
-    }
-    __syncthreads();
-    s_out = S.result;
-    e_out = S.e_carry;
-    g_out = S.g_carry;
-    return true;
-}
+}  // namespace lo
+
+namespace lo {
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Long signed fp32 columns across the chip (the exact mode's 43 normal-equation sums of scans beyond kExactMaxPoints,
+// up to 4M terms each).  The exact running sum is unknown until the walk reaches a term, so the phases run as
+// launches over every 4096-term chunk of every column at once:
+//   1. k_mw_chunk_sums: each chunk's fp64 sum and sum of magnitudes;
+//   2. k_mw_drift:      each chunk's modelled rounding error: the fp32 running sum drifts from the exact prefix by the
+//      sum of its step roundings, rint(x / u) u - x with u from the predicted binade -- over a long column of shrinking
+//      sums the drift outgrows the checks' margin, so the prediction carries it;
+//   3. k_mw_classify:   each chunk's prediction base T0 = the fp64 sum of the chunks before it plus their modelled drift,
+//      its heads and integer prefix, and for every head the record the walk needs (its term, the segment's sum u * Q,
+//      the check's interval) -- in HBM; k_mw_compact then lays the records out in walk order;
+//   4. k_mw_walk:       one wave per column walks every head in order, 64 at a time as a plain fp32 chain (operands
+//      broadcast from LDS, the next window's records in flight), then checks the 64 heads lane-parallel; from a failed
+//      check on, head by head, a failed segment term by term.
+// The prediction error bound eps_t is 2^-45 times (the column's sum of magnitudes up to the chunk's end + |T0|): only
+// the differences T_j - T_h within a chunk enter the proof, and the chunk's own fp64 prefix is a summation tree of depth
+// < 64 over its terms and T0.  Any T0 is correct -- the walk's check measures the real deviation at every head -- a good
+// one keeps the segments parallel.
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int kMwThreads = 256;                    // classification workgroup
+constexpr int kMwPT = 16;                          // consecutive terms per thread
+constexpr int kMwChunk = kMwThreads * kMwPT;       // terms per chunk
+constexpr int kMwCap = 1024;                       // head records per chunk (more: the chunk is one term-by-term run)
+constexpr int kMwMaxChunks = 1024;                 // chunks per column the walk's LDS offset table holds
+static_assert(static_cast<long long>(kMaxBlocks) * kBlock <= static_cast<long long>(kMwMaxChunks) * kMwChunk,
+              "a scan of the largest size must fit the walk's offset table");
+constexpr int kMwFail = 2;                         // record flag: the segment always goes term by term
+constexpr int kMwPad = 128;                        // no-op records after a column's last head (the walk's loads
+                                                   // run two windows ahead unconditionally)
+
+// Head records, structure of arrays, [column][chunk][kMwCap] as classified, then [column][k] compacted in walk order;
+// per-chunk sums and counts [column][chunk].  The walk's check of a multi-term segment is an interval test on the
+// running sum d right after the head's step: d in [dlo, dhi] <=> the sign, the binade [2^E, 2^(E+1)) and
+// |d - T| <= dev of the proof above all hold (bounds rounded inwards).
+struct MwBuf {
+    int* idx;          // the head's term index in the column
+    int* end;          // one past its segment's last term
+    float* x;          // the head's own term
+    float* dq;         // the rest of the segment, u * Q (exact in fp32 whenever the check passes; -0 for one term)
+    int* flag;         // 1: passes any check (one-term segment), kMwFail: never passes; else 0
+    double* dlo;       // the check's interval
+    double* dhi;
+    int* c_idx;        // the same records compacted: [column][k], k over every head of the column in order
+    int* c_end;
+    float* c_x;
+    float* c_dq;
+    int* c_flag;
+    double* c_dlo;
+    double* c_dhi;
+    int* nh;           // heads per chunk
+    int* ntot;         // heads per column (k_mw_compact)
+    double* csum;      // chunk sums (fp64)
+    double* cabs;      // chunk sums of magnitudes
+    double* dcorr;     // chunk sums of the modelled fp32 rounding errors (the prediction's drift correction)
+    int nchunks;       // chunks per column (the row stride of nh / csum / cabs; records: nchunks * kMwCap)
+    size_t cstride;    // column stride of the compacted records: nchunks * kMwCap + kMwPad
+};
+
+}  // namespace lo
+
+namespace lo {
+
+// Long non-negative fp64 sums across the chip (the iteration-0 scale of scans beyond kExactMaxPoints: the sorted
+// residuals' sum, then the sum of (r - mean)^2 -- IterativeClosestPointOptimizer.cpp:304-316).  mono_seq_sum's method
+// spread like the signed columns above: chunk sums -> classification (heads at predicted binade changes and halfway
+// ties, integer prefix sums) -> compaction -> one wave walking the heads.  A mono segment's check is exact and needs no
+// prediction bound: the sum right after the head's step lies in [2^E, 2^(E+1) - u - u * Q].
+constexpr int kMwmCap = kMwChunk;                  // mono: every term may head (halfway ties are common: residuals
+                                                   // carry ~40 significant bits), so no chunk runs term by term
+struct MwmBuf {
+    int* idx;          // records as classified, [chunk][kMwCap]
+    int* end;
+    int* flag;         // 1: passes any check, kMwFail: never passes, else 0
+    double* x;         // the head's own term
+    double* dq;        // u * Q (-0 for a one-term segment)
+    double* dlo;       // the check's interval on the sum right after the head's step
+    double* dhi;
+    int* c_idx;        // compacted in walk order
+    int* c_end;
+    int* c_flag;
+    double* c_x;
+    double* c_dq;
+    double* c_dlo;
+    double* c_dhi;
+    int* nh;           // heads per chunk
+    double* csum;      // chunk sums (fp64)
+    int* cnt;          // [0]: accepted residuals (the finite prefix of the sorted array); [1]: any NaN; [2]: heads in total
+    double* res;       // [0]: the sum; [1]: the variance sum
+    int nchunks;
+};
 
 }  // namespace lo

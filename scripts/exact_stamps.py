@@ -34,8 +34,18 @@ def main():
         icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
         d = (C.c_ulonglong * 16)()
         assert L.lo_debug_counters(icp.ctx, d) == 0
+        if len(wl["scans"][i]) > 16384:                      # large scan: k_exact_sum43 walk statistics (cumulative)
+            it = icp.get_last_stats().num_iterations
+            print("scan %d: %d pts, %d iterations | sum43 cumulative: %d heads, %d segments term by term, %d chained "
+                  "chunks | scale sums: %d / %d heads, %d / %d segments (%d / %d terms) term by term | mean walk %d cycles, "
+                  "%d in its unrolled 64-head chains" % (i, len(wl["scans"][i]), it, d[15], d[13], d[12], d[5], d[8], d[6],
+                                                         d[9], d[7], d[10], d[11], d[14]), flush=True)
+            continue
         rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3], d[6] - d[5], d[7] - d[6]])
         stats.append([d[14], d[8], d[9], d[10], d[11], d[12], d[13]])
+    if not rows:
+        icp.close()
+        return
     r = np.array(rows, dtype=np.float64)
     print("cycles (s_memtime) per phase, mean over", len(rows), "scans: scale load/count %.0f  store %.0f  mean-sum "
           "%.0f  var-sum %.0f | rank-sort WG 0: staging %.0f  compares %.0f" % tuple(r.mean(0)), flush=True)

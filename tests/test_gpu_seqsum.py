@@ -99,6 +99,10 @@ def _cases32():
     yield "tiny_and_huge", np.concatenate([rng.normal(0, 1e-30, 5000), rng.normal(0, 1e20, 100), rng.normal(0, 1, 5000)])
     yield "single", np.array([-0.5])
     yield "empty", np.zeros(0)
+    yield "negative_zeros", np.array([-0.0] * 9000 + [0.0] + [-0.0] * 5)
+    yield "sign_flips", np.tile([1.0, -1.0], 20_000) + rng.normal(0, 1e-3, 40_000)   # a head at every term
+    yield "grow_then_cancel", np.concatenate([rng.normal(5, 1, 500_000), rng.normal(-5, 1, 500_000)])
+    yield "large_products", rng.normal(0, 1, 1_000_000) * rng.normal(0, 1, 1_000_000) * 0.01
 
 
 def test_seq_sum_f32_bitwise(ctx):
@@ -107,4 +111,15 @@ def test_seq_sum_f32_bitwise(ctx):
         x32 = np.asarray(x, np.float32)
         ref = _seq32(x32)
         got, st = _dev_sum32(ctx, x32)
+        print(name, len(x32), "heads / term-by-term segments / term-by-term chunks / us:", st, flush=True)
         assert got.view(np.uint32) == ref.view(np.uint32), (name, got, ref, st)
+
+
+def test_seq_sum_f32_mostly_parallel(ctx):
+    """A 1M-term column of products (the C5 normal-equation terms' shape): a small fraction of the terms head a
+    segment and almost none is summed term by term."""
+    rng = np.random.default_rng(5)
+    x = (rng.normal(0, 1, 1_000_000) * rng.normal(0, 1, 1_000_000) * 0.01).astype(np.float32)
+    got, st = _dev_sum32(ctx, x)
+    assert got.view(np.uint32) == _seq32(x).view(np.uint32)
+    assert 0 < st[0] < 60_000 and st[1] < 400 and st[2] == 0, st
