@@ -658,6 +658,12 @@ def run_loop(args, world, rank, local):
             n_ok += int(ok)
             n_it += icp.get_last_stats().num_iterations
         el = time.perf_counter() - t0
+        gpu_res = []                                          # the parity pass (after the timed region)
+        for pr in pairs:
+            ok, Tr, inl = icp.optimize_loop(*pr)
+            st = icp.get_last_stats()
+            gpu_res.append({"ok": bool(ok), "T": np.asarray(Tr if ok else np.zeros(12), np.float32).reshape(12).copy(),
+                            "inlier": float(inl) if ok else None, "logs": st.iterations})
     finally:
         icp.close()
     result = {
@@ -681,6 +687,20 @@ def run_loop(args, world, rank, local):
         result["cpu_baseline"] = {"value": n_cpu / elc, "unit": "solves/s", "cores": 1, "kind": "port",
                                   "sample": f"{n_cpu} optimize_loop solves over {len(pairs)} pairs in {elc:.1f} s "
                                             f"(oracle restatement, kd-tree 5-NN, single thread)"}
+        ref = []
+        for pr in pairs:
+            ok_o, conv_o, Tr_o, inl_o, _, logs_o = oracle.icp_optimize_loop(*pr)
+            ok_r = ok_o and conv_o
+            ref.append({"ok": bool(ok_r), "T": np.asarray(Tr_o if ok_r else np.zeros(12), np.float32).reshape(12),
+                        "inlier": inl_o if ok_r else None, "logs": logs_o})
+        par = parity_vs_oracle(gpu_res, ref)
+        par["bitwise_equal"] = parity_bitwise(gpu_res, ref)
+        par["inlier_ratio_equal"] = sum(int(g["inlier"] == c["inlier"] or (g["inlier"] is not None and c["inlier"] is not None
+                                                                         and np.float32(g["inlier"]) == np.float32(c["inlier"])))
+                                        for g, c in zip(gpu_res, ref))
+        par["mode"] = args.mode
+        par["vs"] = "oracle.icp_optimize_loop on the same pairs: every GN iteration's pose, T_rel, status"
+        result["cpu_baseline"]["parity"] = par
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
     return result
 

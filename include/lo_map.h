@@ -66,7 +66,8 @@ size_t       lo_voxel_filter(const float* in_xyz, size_t n, float voxel_size, in
  * kernel launches on the context's stream and no host work, and the containers (L0 / L1 order, children order,
  * centroids, surfels) equal the host map's bit for bit.  Capacities are fixed at creation (max_l0 L0 voxels,
  * max_l0 / 2 L1 voxels, max_points per update); an overflow or a key beyond +-2^20 sets an error bit reported by
- * lo_devmap_counts.  hierarchy_factor 1 or 3.  Destroy the map before its context. */
+ * lo_devmap_counts / lo_devmap_status.  hierarchy_factor 1 or 3.  Destroy the map before its context.  The map
+ * follows the context's stream: after lo_set_stream its launches go to the new stream. */
 typedef struct lo_devmap lo_devmap;
 lo_devmap*  lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor, float planarity_threshold,
                              size_t max_l0, size_t max_points, int* err);
@@ -83,6 +84,9 @@ int         lo_devmap_update_from_scan(lo_devmap* m, const float T[12], double m
 int         lo_devmap_apply_transform(lo_devmap* m, const float T[12]);
 /* out = {L0 voxels, L1 voxels, surfels, error bits}; syncs the stream.  LO_ERR_CAPACITY when error bits are set. */
 int         lo_devmap_counts(lo_devmap* m, size_t out[4]);
+/* the error bits only (one 64-byte copy; syncs the stream): LO_OK, or LO_ERR_CAPACITY with lo_devmap_last_error set
+ * when an update overflowed a capacity or met a key beyond +-2^20 (the update aborted, the map is stale) */
+int         lo_devmap_status(lo_devmap* m);
 /* the containers in their order (tests / GetPointCloud): L0 keys, centroids, point counts; L1 keys, surfel flag,
  * normal, centroid, planarity, child count and children keys (27 per voxel) */
 size_t      lo_devmap_get_l0(lo_devmap* m, int32_t* keys, float* xyz, int32_t* point_counts, size_t cap);

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
     "lo_voxelmap_set_device_fit", "lo_devmap_create", "lo_devmap_destroy", "lo_devmap_last_error", "lo_devmap_update",
-    "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_get_l0", "lo_devmap_get_l1",
+    "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_status", "lo_devmap_get_l0", "lo_devmap_get_l1",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
     "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
@@ -165,6 +165,7 @@ def lib():
     L.lo_devmap_update_from_scan.argtypes = [vp, fp, C.c_double]
     L.lo_devmap_apply_transform.argtypes = [vp, fp]
     L.lo_devmap_counts.argtypes = [vp, C.POINTER(C.c_size_t)]
+    L.lo_devmap_status.argtypes = [vp]
     L.lo_devmap_get_l0.restype = C.c_size_t
     L.lo_devmap_get_l0.argtypes = [vp, ip, fp, ip, C.c_size_t]
     L.lo_devmap_get_l1.restype = C.c_size_t

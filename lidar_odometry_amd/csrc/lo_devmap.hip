@@ -1445,6 +1445,10 @@ static int dm_capture(lo_devmap* m, const int* d_scan_n, const float* d_scan) {
     return LO_OK;
 }
 
+// The map launches on its context's stream, looked up on every call (lo_set_stream may have replaced it; the captured
+// update graph is stream-independent).
+static void dm_stream(lo_devmap* m) { m->stream = static_cast<hipStream_t>(lo_stream(m->ctx)); }
+
 static int dm_update(lo_devmap* m, int n_host, bool from_scan, const float T[12], const double sensor[3],
                      double max_distance) {
     DM& M = m->M;
@@ -1484,6 +1488,7 @@ int lo_devmap_update(lo_devmap* m, const float* world_xyz, size_t n, int on_devi
     if (n == 0 || !is_keyframe) return LO_OK;           // UpdateVoxelMap returns before pruning (:135-142)
     if (n > static_cast<size_t>(m->M.NP)) { m->err = "more points than max_points"; return LO_ERR_CAPACITY; }
     DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
     DM_HIP(m, hipMemcpyAsync(m->d_in, world_xyz, n * 3 * sizeof(float),
                              on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, m->stream));
     return dm_update(m, static_cast<int>(n), false, nullptr, sensor, max_distance);
@@ -1492,6 +1497,7 @@ int lo_devmap_update(lo_devmap* m, const float* world_xyz, size_t n, int on_devi
 int lo_devmap_update_from_scan(lo_devmap* m, const float T[12], double max_distance) {
     if (!m || !T) return LO_ERR_ARG;
     DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
     const double sensor[3] = {T[3], T[7], T[11]};        // Vector3f -> Vector3d
     // an empty scan returns before the prune (UpdateVoxelMap :135-137): the kernels read the device count
     return dm_update(m, 0, true, T, sensor, max_distance);
@@ -1500,6 +1506,7 @@ int lo_devmap_update_from_scan(lo_devmap* m, const float T[12], double max_dista
 int lo_devmap_apply_transform(lo_devmap* m, const float T[12]) {
     if (!m || !T) return LO_ERR_ARG;
     DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
     int rc = dm_bind_table(m);
     if (rc != LO_OK) return rc;
     DM& M = m->M;
@@ -1520,9 +1527,20 @@ int lo_devmap_apply_transform(lo_devmap* m, const float T[12]) {
     return LO_OK;
 }
 
+int lo_devmap_status(lo_devmap* m) {
+    if (!m) return LO_ERR_ARG;
+    DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
+    DM_HIP(m, hipMemcpyAsync(m->h_cnt, m->M.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
+    DM_HIP(m, hipStreamSynchronize(m->stream));
+    if (m->h_cnt[C_ERR]) { m->err = "device map overflow / invalid key (error bits " + std::to_string(m->h_cnt[C_ERR]) + ")"; return LO_ERR_CAPACITY; }
+    return LO_OK;
+}
+
 int lo_devmap_counts(lo_devmap* m, size_t out[4]) {
     if (!m || !out) return LO_ERR_ARG;
     DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
     DM_HIP(m, hipMemcpyAsync(m->h_cnt, m->M.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
     DM_HIP(m, hipStreamSynchronize(m->stream));
     out[0] = static_cast<size_t>(m->h_cnt[C_N0]);
@@ -1540,8 +1558,9 @@ int lo_devmap_counts(lo_devmap* m, size_t out[4]) {
 }
 
 size_t lo_devmap_get_l0(lo_devmap* m, int32_t* keys, float* xyz, int32_t* point_counts, size_t cap) {
-    size_t c[4];
-    if (lo_devmap_counts(m, c) != LO_OK && c[0] == 0) return 0;
+    size_t c[4] = {0, 0, 0, 0};
+    const int rc = lo_devmap_counts(m, c);
+    if (rc != LO_OK && rc != LO_ERR_CAPACITY) return 0;
     const size_t n = std::min(c[0], cap);
     if (n == 0) return 0;
     std::vector<uint64_t> k(n);
@@ -1561,8 +1580,9 @@ size_t lo_devmap_get_l0(lo_devmap* m, int32_t* keys, float* xyz, int32_t* point_
 
 size_t lo_devmap_get_l1(lo_devmap* m, int32_t* keys, uint8_t* has_surfel, float* normals, float* centroids,
                         float* planarity, int32_t* child_counts, int32_t* children, size_t cap) {
-    size_t c[4];
-    if (lo_devmap_counts(m, c) != LO_OK && c[1] == 0) return 0;
+    size_t c[4] = {0, 0, 0, 0};
+    const int rc = lo_devmap_counts(m, c);
+    if (rc != LO_OK && rc != LO_ERR_CAPACITY) return 0;
     const size_t n = std::min(c[1], cap);
     if (n == 0) return 0;
     std::vector<uint64_t> k(n), kids(n * kKids);

@@ -30,16 +30,24 @@ struct lo_odometry {
     std::vector<float> feat, world;
 };
 
+static constexpr size_t kDevmapCheck = 8;
+
 static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info) {
     // create_keyframe (:370-530): world feature cloud -> UpdateVoxelMap(cloud, position, 1.2 max_range) -> device
     const auto t0 = std::chrono::steady_clock::now();
     if (o->dmap) {
         float T[12];
         lo::se3_to12(pose, T);
-        const int rc = lo_devmap_update_from_scan(o->dmap, T, o->cfg.max_range * 1.2);
+        int rc = lo_devmap_update_from_scan(o->dmap, T, o->cfg.max_range * 1.2);
         if (rc != LO_OK) { o->err = lo_devmap_last_error(o->dmap); return rc; }
         o->last_kf = pose;
         ++o->keyframes;
+        // the map's error bits (an update that overflowed a capacity aborted; tracking would go on against a stale
+        // map): read back every kDevmapCheck keyframes, one small copy and a stream sync
+        if (o->keyframes % kDevmapCheck == 0 && (rc = lo_devmap_status(o->dmap)) != LO_OK) {
+            o->err = lo_devmap_last_error(o->dmap);
+            return rc;
+        }
         if (info) {
             info->keyframe = 1;
             info->map_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

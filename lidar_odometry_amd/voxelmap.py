@@ -150,6 +150,10 @@ class DeviceVoxelMap:
                                  np.asarray(T, np.float32).reshape(12)).reshape(12)
         self._check(self._L.lo_devmap_apply_transform(self._h, _f(t)))
 
+    def status(self) -> int:
+        """lo_devmap_status: 0, or LO_ERR_CAPACITY when an update overflowed a capacity / met a key beyond +-2^20."""
+        return int(self._L.lo_devmap_status(self._h))
+
     def counts(self):
         """(L0 voxels, L1 voxels, surfels); raises on an overflow / key error bit."""
         out = (C.c_size_t * 4)()

@@ -155,3 +155,45 @@ def test_devmap_device_points_and_table_reupload():
         dm.close()
         A.close()
         B.close()
+
+
+def test_devmap_follows_context_stream_and_reports_overflow():
+    """The map launches on its context's current stream: after lo_set_stream (which destroys the context's own
+    stream) and back, updates still equal the host map.  An update beyond the map's capacity sets the error bits
+    that lo_devmap_status (read by the frame loop every 8 keyframes) reports as LO_ERR_CAPACITY."""
+    import ctypes as C
+
+    import torch
+
+    from lidar_odometry_amd import lib
+    from lidar_odometry_amd._lib import LO_ERR_CAPACITY
+    from lidar_odometry_amd.voxelmap import DeviceVoxelMap, VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=12)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A = _ctx()
+    dm = DeviceVoxelMap(A, 0.5, 3, 0.1, max_l0=1 << 18, max_points=1 << 16)
+    side = torch.cuda.Stream(device=0)
+    try:
+        for k in range(0, 11, 2):
+            if k == 4:
+                assert lib().lo_set_stream(A.ctx, C.c_void_p(side.cuda_stream)) == 0
+            if k == 8:
+                assert lib().lo_set_stream(A.ctx, None) == 0
+            T = seq.poses[k]
+            w = synth.transform(T, voxel_filter(seq.scan(k), 0.5, 8))
+            vm.update(w, T[:3, 3], 120.0, True)
+            dm.update(w, T[:3, 3], 120.0, True)
+            _same_maps(vm, dm)
+        assert dm.status() == 0
+    finally:
+        dm.close()
+        A.close()
+    B = _ctx()
+    small = DeviceVoxelMap(B, 0.5, 3, 0.1, max_l0=64, max_points=1 << 16)
+    try:
+        w = synth.transform(seq.poses[0], voxel_filter(seq.scan(0), 0.5, 8))
+        small.update(w, seq.poses[0][:3, 3], 120.0, True)
+        assert small.status() == LO_ERR_CAPACITY
+    finally:
+        small.close()
+        B.close()
