@@ -210,10 +210,11 @@ int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12]
  * (blockIdx.y = job).  Each job computes exactly what lo_icp_optimize computes on its context (bit-identical:
  * same kernels, same per-job reductions).  The reference has no batch entry point; this is the multi-sequence
  * form of IterativeClosestPointOptimizer::optimize (IterativeClosestPointOptimizer.cpp:255-463) called once
- * per sequence.  Requirements: surfel correspondence mode, one device, equal max_iterations, reference-exact mode
- * off (lo_set_exact has no batched form: create and optimize refuse such a context).  The batch runs
- * on its own stream; the contexts must be idle while it runs and each context's lo_icp_result() is not valid
- * for a batched scan (use lo_batch_result). */
+ * per sequence.  Requirements: surfel correspondence mode, one device, equal max_iterations.  A context in
+ * reference-exact mode (lo_set_exact) runs its own exact GN loop on its context stream inside the batch call (the
+ * sequential-sum reproductions have no lockstep form), ordered after the batch's uploads and before its record
+ * export, bit-identical to its lo_icp_optimize.  The batch runs on its own stream; the contexts must be idle while
+ * it runs and each context's lo_icp_result() is not valid for a batched scan (use lo_batch_result). */
 typedef struct lo_batch lo_batch;
 typedef struct lo_batch_rec {
     float  pose[12];       /* optimized pose (T_init when status != LO_OK, as lo_icp_optimize) */

@@ -2048,6 +2048,8 @@ struct lo_batch {
     struct Sig { const float* pts; int n; const Slot* tab; uint32_t log2cap; };
     std::vector<Sig> sig;            // what d_P currently holds, per active slot
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_go = nullptr;      // reference-exact jobs: the batch's uploads done (their streams wait on it)
+    std::vector<hipEvent_t> ev_ex;   //   and each exact job's scan finished (the batch stream waits on them)
     bool pending = false;
 };
 
@@ -2072,6 +2074,7 @@ static int batch_alloc(lo_batch* b) {
     LO_BHIP(b, hipHostMalloc(&b->h_rec, B * sizeof(lo_batch_rec), hipHostMallocDefault));
     LO_BHIP(b, hipEventCreate(&b->ev0));
     LO_BHIP(b, hipEventCreate(&b->ev1));
+    LO_BHIP(b, hipEventCreateWithFlags(&b->ev_go, hipEventDisableTiming));
     LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<4, false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
     LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<1, true>),
@@ -2094,7 +2097,6 @@ lo_batch* lo_batch_create(lo_ctx* const* ctxs, int count, int* err) {
         const lo_ctx* c = ctxs[j];
         if (!c) return fail(LO_ERR_ARG, "null context");
         if (c->kd) return fail(LO_ERR_ARG, "batched optimize needs surfel-mode contexts");
-        if (c->exact) return fail(LO_ERR_ARG, "batched optimize has no reference-exact mode (lo_set_exact)");
         if (c->device != ctxs[0]->device) return fail(LO_ERR_ARG, "contexts on different devices");
         if (c->cfg.max_iterations != ctxs[0]->cfg.max_iterations) return fail(LO_ERR_ARG, "max_iterations differ");
         for (int k = 0; k < j; ++k) if (ctxs[k] == c) return fail(LO_ERR_ARG, "a context appears twice");
@@ -2129,6 +2131,8 @@ void lo_batch_destroy(lo_batch* b) {
         if (p) (void)hipHostFree(p);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
+    if (b->ev_go) (void)hipEventDestroy(b->ev_go);
+    for (hipEvent_t e : b->ev_ex) (void)hipEventDestroy(e);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
@@ -2142,16 +2146,17 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
     const int B = static_cast<int>(b->ctx.size());
     for (int j = 0; j < B; ++j) {
         if (n[j] > static_cast<size_t>(b->ctx[j]->cfg.max_points)) { b->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
-        if (b->ctx[j]->exact) { b->err = "a context has reference-exact mode on (no batched form)"; return LO_ERR_STATE; }
     }
     LO_BHIP(b, hipSetDevice(b->device));
     std::memcpy(b->T_in.data(), T_init, sizeof(float) * 12 * B);
     b->act.clear();
     int max_nb = 1, max_acc = 1;
     bool same = true;
+    std::vector<int> ex;                                      // reference-exact jobs: their own GN path (below)
     for (int j = 0; j < B; ++j) {
         b->n[j] = n[j];
         if (n[j] == 0) continue;
+        if (b->ctx[j]->exact) { ex.push_back(j); continue; }
         lo_ctx* c = b->ctx[j];
         const float* pts = (d_pts && d_pts[j]) ? d_pts[j] : c->d_pts;
         const int a = static_cast<int>(b->act.size());
@@ -2169,11 +2174,48 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
         b->act.push_back(j);
     }
     const int nact = static_cast<int>(b->act.size());
-    if (static_cast<int>(b->sig.size()) != nact) { same = false; b->sig.resize(nact); }
+    // exact jobs after the batched ones: only their DevState pointer is read (k_export_batch)
+    for (int j : ex) {
+        b->h_P[b->act.size()] = make_params(b->ctx[j], b->ctx[j]->d_pts, static_cast<int>(n[j]));
+        b->act.push_back(j);
+    }
+    const int ntot = static_cast<int>(b->act.size());
+    if (!ex.empty()) same = false;
+    if (static_cast<int>(b->sig.size()) != ntot) { same = false; b->sig.resize(ntot); }
     LO_BHIP(b, hipEventRecord(b->ev0, b->stream));
+    if (ntot > 0) {
+        if (nact > 0) LO_BHIP(b, hipMemcpyAsync(b->d_T0, b->h_T0, sizeof(float) * 12 * nact, hipMemcpyHostToDevice, b->stream));
+        if (!same) LO_BHIP(b, hipMemcpyAsync(b->d_P, b->h_P, sizeof(KParams) * ntot, hipMemcpyHostToDevice, b->stream));
+    }
+    if (!ex.empty()) {
+        // reference-exact jobs run their context's own exact GN loop (the sequential-sum reproductions have no
+        // batched form) on the context stream, ordered after the batch's uploads (lo_batch_optimize copies their
+        // points on the batch stream) and before the batch's record export; the scan pipeline stays off for them,
+        // so every launch is on the context stream and the record is final when it ends
+        LO_BHIP(b, hipEventRecord(b->ev_go, b->stream));
+        while (b->ev_ex.size() < ex.size()) {
+            hipEvent_t e = nullptr;
+            LO_BHIP(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            b->ev_ex.push_back(e);
+        }
+        for (size_t q = 0; q < ex.size(); ++q) {
+            const int j = ex[q];
+            lo_ctx* c = b->ctx[j];
+            const float* pts = (d_pts && d_pts[j]) ? d_pts[j] : c->d_pts;
+            LO_BHIP(b, hipStreamWaitEvent(c->stream, b->ev_go, 0));
+            const bool pipe = c->pipe, sync_call = c->sync_call;
+            c->pipe = false;
+            c->sync_call = false;
+            const int rc = enqueue_optimize(c, pts, n[j], T_init + 12 * j);
+            c->pipe = pipe;
+            c->sync_call = sync_call;
+            c->pending = false;                               // the batch collects the record, not lo_icp_result
+            if (rc != LO_OK) { b->err = std::string("exact job: ") + c->err; return rc; }
+            LO_BHIP(b, hipEventRecord(b->ev_ex[q], c->stream));
+            LO_BHIP(b, hipStreamWaitEvent(b->stream, b->ev_ex[q], 0));
+        }
+    }
     if (nact > 0) {
-        LO_BHIP(b, hipMemcpyAsync(b->d_T0, b->h_T0, sizeof(float) * 12 * nact, hipMemcpyHostToDevice, b->stream));
-        if (!same) LO_BHIP(b, hipMemcpyAsync(b->d_P, b->h_P, sizeof(KParams) * nact, hipMemcpyHostToDevice, b->stream));
         const int pko_wgs = std::max(1, std::min(b->pko_max, b->pko_budget / nact));
         const size_t pre_bytes = static_cast<size_t>(max_nb) * sizeof(int);
         const dim3 blk(kBlock);
@@ -2195,9 +2237,11 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
                 hipLaunchKernelGGL(k_solve_b, dim3(nact), dim3(kSolveThreads), 0, b->stream, b->d_P, it);
             }
         }
-        hipLaunchKernelGGL(k_export_batch, dim3(nact), dim3(64), 0, b->stream, b->d_P, b->d_rec);
+    }
+    if (ntot > 0) {
+        hipLaunchKernelGGL(k_export_batch, dim3(ntot), dim3(64), 0, b->stream, b->d_P, b->d_rec);
         LO_BHIP(b, hipGetLastError());
-        LO_BHIP(b, hipMemcpyAsync(b->h_rec, b->d_rec, sizeof(lo_batch_rec) * nact, hipMemcpyDeviceToHost, b->stream));
+        LO_BHIP(b, hipMemcpyAsync(b->h_rec, b->d_rec, sizeof(lo_batch_rec) * ntot, hipMemcpyDeviceToHost, b->stream));
     }
     LO_BHIP(b, hipEventRecord(b->ev1, b->stream));
     b->pending = true;

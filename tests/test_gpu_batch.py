@@ -106,6 +106,29 @@ def test_batch_heterogeneous_bitwise_vs_single(pko_mode):
             o.close()
 
 
+def test_batch_exact_jobs_bitwise_vs_single():
+    """Reference-exact contexts in a batch (every other job): each exact job equals its context's own exact
+    lo_icp_optimize bit for bit (and so the oracle, tests/test_gpu_exact.py), each default job its default single run,
+    also when the batch runs twice."""
+    from lidar_odometry_amd import BatchOptimizer
+    jobs = _jobs()
+    ctxs = [_ctx(m, v) for (m, v, _, _) in jobs]
+    try:
+        for k, o in enumerate(ctxs):
+            o.set_exact(k % 2 == 0)
+        singles = _singles(ctxs, jobs)
+        b = BatchOptimizer(ctxs)
+        try:
+            for _ in range(2):
+                res = b.optimize(None, [j[2] for j in jobs], [j[3] for j in jobs])
+                _check_equal(res, singles)
+        finally:
+            b.close()
+    finally:
+        for o in ctxs:
+            o.close()
+
+
 def test_batch_many_jobs_and_repointed_scans(pko_mode):
     """64 jobs (fewer PKO workgroups per job than a single scan gets), then every job re-pointed at another scan."""
     from lidar_odometry_amd import BatchOptimizer
@@ -152,11 +175,9 @@ def test_batch_argument_checks():
                 b.optimize(None, [big], [np.eye(3, 4, dtype=np.float32)])   # exceeds max_points
             res = b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
             assert not res[0].success          # empty map: no correspondences
-            a.set_exact(True)                  # no batched exact mode: refused, not silently run on the fast path
-            with pytest.raises(RuntimeError):
-                b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
-            with pytest.raises(RuntimeError):
-                BatchOptimizer([a])
+            a.set_exact(True)                  # an exact-mode job runs its own exact GN loop inside the batch
+            res = b.optimize(None, [np.zeros((100, 3), np.float32)], [np.eye(3, 4, dtype=np.float32)])
+            assert not res[0].success
             a.set_exact(False)
         finally:
             b.close()
