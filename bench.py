@@ -430,7 +430,7 @@ def pko_roofline(em_live):
                     "iteration count for alpha to stay identical"}
 
 
-def c5_hbm_leg(local: int, dev, n_scans: int):
+def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False):
     """C5's data at one GPU's scale (BASELINE.json configs[4]: synthetic 1M-point scans, 1000 planar patches + 10 %
     outliers): n_scans DISTINCT scans, each on its own context (its own slot / residual outputs and table copy),
     launched round-robin on one stream.  Between two launches of a scan the other n_scans - 1 move their own ~24 MB
@@ -517,6 +517,15 @@ def c5_hbm_leg(local: int, dev, n_scans: int):
     in_ach = float(np.mean(alg)) / (in_t * 1e-6) / 1e9
     for o in ctxs:
         o.close()
+    # DRAM bytes of one 1M-point launch (live rocprofv3 --pmc passes in child processes, as the value line's): a
+    # 24 MB scan is far beyond the 4 MB L2 of an XCD, so isolated repeats of one scan miss L2 as the round-robin does
+    traffic_live = None
+    if pmc:
+        keys, normals, cents, _ = vm.surfels()
+        traffic_live = live_pmc({"pts": scans[0], "T": inits[0], "scale": it0[0][0], "alpha": it0[0][1], "keys": keys,
+                                 "normals": normals, "centroids": cents, "voxel": 0.5}, reps=50)
+        if traffic_live is not None:
+            traffic_live["alg_bytes_per_launch"] = float(alg[0])
     return {"workload": "C5 synthetic 1M-point scans (1000 planar patches + 10 % outliers, azimuth order), "
                         f"{n_scans} distinct scans, one context each, round-robin on one stream",
             "value": rounds * n_scans / el, "unit": "scans/s (1M points)", "gn_iters_per_scan_avg": float(np.mean(iters)),
@@ -524,6 +533,8 @@ def c5_hbm_leg(local: int, dev, n_scans: int):
             "roofline": {"kernel": "k_correspond", "bound": "hbm", "achieved": iso_ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": iso_ach / HBM_PEAK_GBS, "kernel_us": iso_t,
                          "alg_bytes_per_launch": float(np.mean(alg)), "launches": len(iso_us),
+                         "traffic": traffic_live["hbm_bytes_per_launch"] if traffic_live else None,
+                         "traffic_live": traffic_live,
                          "timing": "single launches (lo_bench_kernel id 4: no set-up pass), HIP events, each scan "
                                    f"last touched {n_scans - 1} scans earlier"},
             "in_step": {"kernel_us": in_t, "achieved": in_ach, "frac": in_ach / HBM_PEAK_GBS, "scans": int(n_in),
@@ -1347,7 +1358,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget, {args.mode: gpu_res, other: gpu_other}, args.mode)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and args.config == "kitti" and args.c5 > 0:
-        result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5)
+        result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5, pmc=args.pmc == "live")
     icp.close()
     if rank == 0:
         emit(result)
