@@ -100,6 +100,7 @@ struct SeqScratch {
     int h_idx[kSeqHeadCap];
     int h_e[kSeqHeadCap];
     long long h_p[kSeqHeadCap];
+    double2 xd[kWave];                         // the walk's window of (head term, segment sum), read as broadcasts
     double result;
     int e_carry;
     int nheads, fb_seg, fb_terms;              // walk statistics (heads; segments / terms summed term by term)
@@ -179,18 +180,19 @@ __device__ __forceinline__ bool mono_seq_sum(int cnt, const double* s_x, SeqScra
     }
     if (tid == 0) S.nheads = htot;
     __syncthreads();
-    // 3. the walk (wave 0, wave-uniform): lane l of a 64-head window holds head k0 + l and precomputes what the
-    //    sequential step needs -- the head's term, the segment's sum u * Q, the binade floor 2^E and the largest
-    //    result the segment may reach (2^(E+1) - u); a one-term segment, or a lane past the last head, passes any
-    //    check (its dq is 0), a segment without a valid binade fails every check.  Heads go eight at a time as a
-    //    branch-free chain of two adds each; a group in which any check failed is redone head by head from its start
+    // 3. the walk (wave 0, wave-uniform): lane l of a 64-head window holds head k0 + l and precomputes the head's
+    //    term, the segment's sum u * Q and the interval the sum right after the head's step must lie in for the
+    //    segment to stay in its binade, [2^E, 2^(E+1) - u - u * Q] (a one-term segment or a lane past the last head:
+    //    any sum; a segment without a valid binade: none).  The 64 heads run as a plain chain of two adds each, the
+    //    operands broadcast from LDS, lane l keeping the sum after head l's step; the checks then run lane-parallel,
+    //    and from a failed check on the window goes head by head (that head's sum is exact: the earlier ones passed)
     if (wid == 0) {
         double s = s_in;
         int fbs = 0, fbt = 0;
         for (int k0 = 0; k0 < htot; k0 += 64) {
             const int kk = k0 + lane;
             int hi = 0, hend = cnt;
-            double hx = -0.0, dq = -0.0, lo_e = -__builtin_inf(), top = __builtin_inf();   // x + -0 == x, also for x = -0
+            double hx = -0.0, dq = -0.0, dlo = -__builtin_inf(), dhi = __builtin_inf();   // x + -0 == x, also for x = -0
             if (kk < htot) {
                 hi = S.h_idx[kk];
                 const int E = S.h_e[kk];
@@ -200,40 +202,44 @@ __device__ __forceinline__ bool mono_seq_sum(int cnt, const double* s_x, SeqScra
                 if (kk + 1 < htot) { pend = S.h_p[kk + 1]; hend = S.h_idx[kk + 1]; }
                 const long long Q = pend - hp;
                 if (hend > hi + 1) {
-                    lo_e = __builtin_inf();
-                    top = 0.0;
+                    dlo = __builtin_inf();
+                    dhi = -__builtin_inf();
                     if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
                         const double u = ldexp(1.0, E - 52);
                         dq = static_cast<double>(Q) * u;
-                        lo_e = ldexp(1.0, E);
-                        top = ldexp(1.0, E + 1) - u;
+                        dlo = ldexp(1.0, E);
+                        dhi = (ldexp(1.0, E + 1) - u) - dq;      // exact: multiples of u below 2^(E+1)
                     }
                 }
             }
-            const int m = min(64, htot - k0);
-            for (int l0 = 0; l0 < m; l0 += 8) {
-                const double s0 = s;
-                int bad = 0;
+            S.xd[lane] = make_double2(hx, dq);
+            double rec = 0.0;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {                    // lanes past m are the no-op heads above
-                    const double s1 = s + rl64d(hx, l0 + u);     // the head's own step, as the reference does it
-                    const double R = s1 + rl64d(dq, l0 + u);     // exact when the segment stays in the binade
-                    bad |= (s1 >= rl64d(lo_e, l0 + u) && R <= rl64d(top, l0 + u)) ? 0 : 1;
-                    s = R;
+            for (int l = 0; l < 64; ++l) {                       // lanes past the window are no-op heads
+                const double2 v = S.xd[l];
+                s = s + v.x;                                     // the head's own step, as the reference does it
+                rec = lane == l ? s : rec;
+                s = s + v.y;                                     // exact when the segment stays in the binade
+            }
+            const unsigned long long badm = __ballot(!(rec >= dlo && rec <= dhi));
+            if (badm) {                                          // uniform
+                const int m = min(64, htot - k0), f = __builtin_ctzll(badm);
+                s = rl64d(rec, f);
+                {
+                    const int h = __builtin_amdgcn_readlane(hi, f), end = __builtin_amdgcn_readlane(hend, f);
+                    for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                    ++fbs;
+                    fbt += end - h - 1;
                 }
-                if (__builtin_amdgcn_readfirstlane(bad)) {       // uniform: redo the group head by head
-                    s = s0;
-                    for (int l = l0; l < min(l0 + 8, m); ++l) {
-                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
-                        s = s + rl64d(hx, l);
-                        const double R = s + rl64d(dq, l);
-                        if (__builtin_amdgcn_readfirstlane((s >= rl64d(lo_e, l) && R <= rl64d(top, l)) ? 1 : 0)) {
-                            s = R;
-                        } else {
-                            for (int j = h + 1; j < end; ++j) s = s + s_x[j];
-                            ++fbs;
-                            fbt += end - h - 1;
-                        }
+                for (int l = f + 1; l < m; ++l) {
+                    const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                    s = s + rl64d(hx, l);
+                    if (__builtin_amdgcn_readfirstlane((s >= rl64d(dlo, l) && s <= rl64d(dhi, l)) ? 1 : 0)) {
+                        s = s + rl64d(dq, l);
+                    } else {
+                        for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                        ++fbs;
+                        fbt += end - h - 1;
                     }
                 }
             }
