@@ -684,6 +684,9 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // indices two).  LDS: the dynamic buffer (after the prefix).
 __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
     if (c > P.NA) return;
+#ifdef LO_PKO_STAMPS
+    const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
+#endif
     float* s_f = dyn;                                      // [2][43][kXcStride]
     int* s_cnt = reinterpret_cast<int*>(dyn + 2 * kXcBuf); // [2][kXcRegions]
     float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
@@ -735,9 +738,9 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
                     buf[k * kXcStride + row] = f[fa] * f[fb];
                 }
             }
-            if (lane < ((cnt + 3) & ~3) - cnt) {                   // zero terms in rows cnt .. the next multiple of 4
-#pragma unroll
-                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + cnt + lane] = 0.0f;
+            if (lane < ((cnt + 3) & ~3) - cnt) {                   // -0 terms in rows cnt .. the next multiple of 4
+#pragma unroll                                                     // (s + -0 == s for every s, -0 included)
+                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + cnt + lane] = -0.0f;
             }
             if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = (cnt + 3) & ~3;
             // the next chunk's point / surfel / residual, and the slot of the one after
@@ -748,15 +751,18 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
             const int b = (ch - 1) & 1;
             const float* col = s_f + b * kXcBuf + (lane < kExactTerms ? lane : 0) * kXcStride;
 #pragma unroll
-            for (int r = 0; r < kXcRegions; ++r) {
-                const int cnt4 = s_cnt[b * kXcRegions + r];
+            for (int r = 0; r < kXcRegions; ++r) {             // a region's 16 row quads loaded at once, then added
+                const int q4 = s_cnt[b * kXcRegions + r] >> 2;
                 const float4* rows = reinterpret_cast<const float4*>(col + r * kWave);
-                for (int i = 0; i < cnt4 / 4; ++i) {
-                    const float4 v = rows[i];
-                    sum += v.x;
-                    sum += v.y;
-                    sum += v.z;
-                    sum += v.w;
+                float4 v[kWave / 4];
+#pragma unroll
+                for (int q = 0; q < kWave / 4; ++q) v[q] = q < q4 ? rows[q] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+#pragma unroll
+                for (int q = 0; q < kWave / 4; ++q) {
+                    sum += v[q].x;
+                    sum += v[q].y;
+                    sum += v[q].z;
+                    sum += v[q].w;
                 }
             }
         }
@@ -764,6 +770,9 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     }
     if (wid == 0 && lane < kExactTerms) s_tot[lane] = sum;
     __syncthreads();
+#ifdef LO_PKO_STAMPS
+    if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memtime() - c_t0);   // the slowest sums
+#endif
     if (tid == 0) {
         float tot[kExactTerms], pn[12], delta[6];
 #pragma unroll
@@ -781,6 +790,12 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     }
     __syncthreads();
     if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
+#ifdef LO_PKO_STAMPS
+    if (tid == 0 && c == 0) {                // diagnostic: candidate 0's cycles (dbg[7]); dbg[15]: the slowest sums
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        P.st->dbg[7] = __builtin_amdgcn_s_memtime() - c_t0;
+    }
+#endif
 }
 
 // Phase 1 of the PKO launch: correspondence count n_c, the exclusive rank -> block prefix of the per-block counts

@@ -51,13 +51,19 @@ def main():
     for k in range(10):
         step(k)
     L.lo_sync(icp.ctx)
+    em = (C.c_ulonglong * 3)()
+    L.lo_set_stage_timing(icp.ctx, 1)                          # (also clocks the lead PKO workgroup's EM)
+    L.lo_pko_em_stats(icp.ctx, em, 1)                          # zero the lead workgroup's EM clock sums
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(k)
     L.lo_sync(icp.ctx)
     el = time.perf_counter() - t0
+    L.lo_pko_em_stats(icp.ctx, em, 0)
     print(f"{a.config} {a.mode}: {a.steps / el:.1f} scans/s, {el / a.steps * 1e6:.1f} us/scan, "
-          f"{np.mean(iters):.2f} GN iters/scan, {np.mean([len(s) for s in wl['scans']]):.0f} pts/scan", flush=True)
+          f"{np.mean(iters):.2f} GN iters/scan, {np.mean([len(s) for s in wl['scans']]):.0f} pts/scan | EM of the lead "
+          f"PKO workgroup: {em[0] / max(em[1], 1):.0f} cycles per EM iteration, {em[1] / max(em[2], 1):.1f} "
+          f"iterations per fit, {em[2]} fits", flush=True)
     icp.close()
 
 
