@@ -3,7 +3,9 @@
 patch (lo_map_sync_voxelmap: the L1 voxels the update changed, async).  KITTI-like sequence, keyframe every 2 frames,
 pruning radius 120 m; times per keyframe over the second half (the map at its steady size).  Third column: the
 same map with device surfel fits (lo_voxelmap_set_device_fit: update without fits + patch + k_surfel_fit, the
-results applied at the next update)."""
+results applied at the next update).  Fourth: the reference-side sync (the adapter's sync_map ->
+lo_map_sync_surfels): the map's whole surfel set handed over each keyframe, diffed against the context's resident
+set, only the difference patched."""
 import ctypes as C
 import os
 import sys
@@ -26,7 +28,8 @@ vd = VoxelMap(0.5, 3, 0.1, True)
 vd.set_device_fit(True)
 A, B = IterativeClosestPointOptimizer(max_points=1 << 16), IterativeClosestPointOptimizer(max_points=1 << 16)
 D = IterativeClosestPointOptimizer(max_points=1 << 16)
-t_upd, t_full, t_patch, kinds, t_dev = [], [], [], [], []
+E = IterativeClosestPointOptimizer(max_points=1 << 16)
+t_upd, t_full, t_patch, kinds, t_dev, t_ref, sent = [], [], [], [], [], [], []
 patched = C.c_int(0)
 for k in range(0, n + 1, 2):
     T = seq.poses[k]
@@ -44,13 +47,21 @@ for k in range(0, n + 1, 2):
     assert lib().lo_map_sync_voxelmap(D.ctx, vd.handle, C.byref(patched)) == 0
     lib().lo_sync(D.ctx)
     t5 = time.perf_counter()
+    keys, normals, cents, _ = vm.surfels()
+    t6 = time.perf_counter()
+    sent.append(E.sync_surfels(keys, normals, cents))
+    lib().lo_sync(E.ctx)
+    t7 = time.perf_counter()
     t_upd.append(t1 - t0); t_full.append(t2 - t1); t_patch.append(t3 - t2); kinds.append(patched.value)
     t_dev.append(t5 - t4)
+    t_ref.append(t7 - t6)
 h = len(t_upd) // 2
 ms = lambda v: 1e3 * float(np.mean(v[h:]))  # noqa: E731
 print(f"keyframes {len(t_upd)}, surfels {vm.surfel_count()}, L0 {vm.l0_count()}: per keyframe (second half) "
       f"host map update {ms(t_upd):.3f} ms, full upload {ms(t_full):.3f} ms, patch {ms(t_patch):.3f} ms "
       f"(incl. stream sync); patched voxels per keyframe {np.mean([p for p in kinds[h:] if p >= 0]):.0f}, "
       f"full re-uploads in the second half {sum(p < 0 for p in kinds[h:])}; with device fits: update + sync "
-      f"{ms(t_dev):.3f} ms (host fits: {ms(t_upd) + ms(t_patch):.3f} ms)")
+      f"{ms(t_dev):.3f} ms (host fits: {ms(t_upd) + ms(t_patch):.3f} ms); reference-side sync_surfels of the full "
+      f"surfel set {ms(t_ref):.3f} ms, {np.mean([x for x in sent[h:] if x >= 0]):.0f} records sent per keyframe "
+      f"(full uploads in the second half: {sum(x < 0 for x in sent[h:])})")
 assert vd.surfel_count() == vm.surfel_count()
