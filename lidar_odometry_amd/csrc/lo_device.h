@@ -145,6 +145,8 @@ struct KParams {
     int ex_ld;                //   0: row-major [point][43]; > 0: term-major [43][ex_ld] (large scans, launch_mw_sums)
     float* ex_tot;            //   term-major path: the 43 sequential sums
     int scale_given;          // 1: the iteration-0 scale is already in DevState (k_exact_scale), the PKO reads it
+    uint64_t* presort;        // nullable (iteration 0, reference-exact mode): each correspondence block writes its 256
+                              //   residual keys sorted (lo_blocksort.h) for k_exact_scale_m's merge
     int exact_cand;           // 1: the PKO launch's candidates form the reference's sequential fp32 sums and solve
                               //   (reference-exact mode, acc_candidate_exact; one workgroup per candidate)
     const double* direct_res; // nullable: PKO on given residuals (parity entry point)
@@ -593,8 +595,10 @@ __device__ __forceinline__ void corr_epilogue(const KParams& P, bool valid, doub
 
 // find_correspondences' per-point step (IterativeClosestPointOptimizer.cpp:606-641) for point i at pose T, then the
 // block's ballots / count / (iteration 0) residual stats.
-__device__ __forceinline__ void correspond_tail(const KParams& P, const CorrOut& O, const float (&T)[12], float px,
-                                                float py, float pz, int i, int n, int with_stats, int blk) {
+// Returns the point's sort key for the exact iteration-0 scale (lo_blocksort.h): the accepted residual's bits, else
+// +inf's.
+__device__ __forceinline__ uint64_t correspond_tail(const KParams& P, const CorrOut& O, const float (&T)[12], float px,
+                                                    float py, float pz, int i, int n, int with_stats, int blk) {
     int slot = -1;
     double r = 0.0;
     if (i < n) {
@@ -611,10 +615,11 @@ __device__ __forceinline__ void correspond_tail(const KParams& P, const CorrOut&
         if (O.res) __builtin_nontemporal_store(r, &O.res[i]);
     }
     corr_epilogue(O, slot >= 0, r, with_stats, blk);
+    return slot >= 0 ? static_cast<uint64_t>(__double_as_longlong(r)) : 0x7FF0000000000000ull;
 }
-__device__ __forceinline__ void correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
-                                                int i, int n, int with_stats, int blk) {
-    correspond_tail(P, corr_out(P), T, px, py, pz, i, n, with_stats, blk);
+__device__ __forceinline__ uint64_t correspond_tail(const KParams& P, const float (&T)[12], float px, float py, float pz,
+                                                    int i, int n, int with_stats, int blk) {
+    return correspond_tail(P, corr_out(P), T, px, py, pz, i, n, with_stats, blk);
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cfloat>
 
+#include "lo_blocksort.h"
 #include "lo_device.h"
 #include "lo_math.h"
 #include "lo_seqsum.h"
@@ -154,6 +155,121 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const do
     if (tid == 0) st->scale = sqrt(var) / 6.0;
 }
 
+// ---- iteration 0, scans of at most kExactMergeMax points: the correspondence launch left one sorted run of 256 keys per
+// block (presort_block, lo_blocksort.h).  k_rank_runs (one workgroup per run, every run staged in LDS) places each key
+// at its rank -- its position in its own run plus, in every other run, the keys below it (later runs) or not above it
+// (earlier runs): nine probes per run, the runs' searches interleaved -- and k_exact_scale_s sums the sorted array in
+// one workgroup (mono_sum_tx: the halfway ties as two-state segment maps, a walk over ~25 binade heads). ----
+__global__ __launch_bounds__(kBlock) void k_rank_runs(KParams P, const uint64_t* __restrict__ runs, uint64_t* __restrict__ out) {
+    if (P.st->done) return;
+    extern __shared__ uint64_t s_r[];                        // P.nb runs
+    const int nb = P.nb, b = blockIdx.x, tid = threadIdx.x;
+    for (int e = tid; e < nb * kBlock; e += kBlock) s_r[e] = runs[e];
+    __syncthreads();
+    const uint64_t x = s_r[b * kBlock + tid];
+    int rank = tid;
+    for (int r = 0; r < nb; ++r) {                           // equal keys: earlier runs first, then this run's order
+        if (r == b) continue;
+        rank += r < b ? run_count<false>(s_r + r * kBlock, x) : run_count<true>(s_r + r * kBlock, x);
+    }
+    out[rank] = x;
+}
+
+template <int NT, int PT>
+__global__ __launch_bounds__(NT) void k_exact_scale_s(KParams P, const uint64_t* __restrict__ sorted) {
+    DevState* st = P.st;
+    if (st->done) return;
+    extern __shared__ double s_x[];                          // NT * PT terms
+    __shared__ MonoScratch<NT> S;
+    __shared__ int s_cnt[NT / kWave];
+    LO_XSTAMP(st, 0);
+    const int tid = threadIdx.x, base = tid * PT;
+    const int nfill = P.nb * kBlock;                         // sorted keys (finite residuals first, then +inf / NaN)
+    uint64_t v[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) v[q] = base + q < nfill ? sorted[base + q] : kInfKey;
+    // accepted residuals = the finite keys (a prefix); a NaN residual (accepted: the gate keeps NaN) makes the mean,
+    // the variance and the scale NaN
+    int nacc = 0;
+    bool nan = false;
+    uint64_t nan_key = 0;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        nacc += v[q] < kInfKey ? 1 : 0;
+        if (v[q] > kInfKey && !nan) { nan = true; nan_key = v[q]; }
+    }
+    int cnt = 0;
+    (void)block_excl_scan_dpp<NT>(nacc, 0, [](int a, int c) { return a + c; }, s_cnt, &cnt);
+    const bool any_nan = __syncthreads_or(nan ? 1 : 0) != 0;
+    if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
+    if (any_nan) {
+        if (nan) st->scale = sqrt(__longlong_as_double(static_cast<long long>(nan_key))) / 6.0;
+        return;
+    }
+    double x[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        x[q] = base + q < cnt ? __longlong_as_double(static_cast<long long>(v[q])) : 0.0;
+        s_x[base + q] = x[q];
+    }
+    __syncthreads();
+    LO_XSTAMP(st, 1);
+#ifdef LO_EXACT_STAMPS
+    unsigned long long* stp = st->dbg + 4;                  // dbg[4..6]: the mean sum's phases
+#else
+    unsigned long long* stp = nullptr;
+#endif
+    double sum;
+    if (!mono_sum_tx<NT, PT>(x, cnt, s_x, S, sum, stp)) sum = chain_sum_tx<NT>(s_x, cnt, S);
+    LO_XSTAMP(st, 2);
+    LO_XSTAT(st, 8, S.nheads);
+    LO_XSTAT(st, 9, S.fb_seg);
+    LO_XSTAT(st, 10, S.fb_terms);
+    LO_XSTAT(st, 14, cnt);
+    const double mean = sum / cnt;                           // std::accumulate(...) / residuals.size()
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        x[q] = base + q < cnt ? (x[q] - mean) * (x[q] - mean) : 0.0;
+        s_x[base + q] = x[q];                                // the walk's reads of s_x ended at mono_sum_tx's barrier
+    }
+    __syncthreads();
+    double var;
+    if (!mono_sum_tx<NT, PT>(x, cnt, s_x, S, var)) var = chain_sum_tx<NT>(s_x, cnt, S);
+    LO_XSTAMP(st, 3);
+    LO_XSTAT(st, 11, S.nheads);
+    LO_XSTAT(st, 12, S.fb_seg);
+    LO_XSTAT(st, 13, S.fb_terms);
+    var /= cnt;
+    if (tid == 0) st->scale = sqrt(var) / 6.0;               // :313-315
+}
+
+constexpr int kScaleThreads = 512;                           // k_exact_scale_s: 8 waves, PT = padded size / 512
+template <int PT>
+static hipError_t scale_s_attr() {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_s<kScaleThreads, PT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(PT * kScaleThreads * sizeof(double)));
+}
+// The kernels' dynamic LDS (up to 64 KB), set on the calling thread's current device (exact_prepare, per context).
+hipError_t exact_scale_m_prepare() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_rank_runs), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(kExactMergeMax * sizeof(uint64_t)));
+    for (hipError_t r : {scale_s_attr<1>(), scale_s_attr<2>(), scale_s_attr<4>(), scale_s_attr<8>(), scale_s_attr<16>()})
+        if (e == hipSuccess) e = r;
+    return e;
+}
+// P.nb runs of 256 sorted keys (P.nb * 256 <= kExactMergeMax) -> sorted (P.nb * 256 keys of scratch) -> the scale
+void launch_exact_scale_m(const KParams& P, const uint64_t* runs, uint64_t* sorted, hipStream_t s) {
+    const int need = P.nb * kBlock;
+    hipLaunchKernelGGL(k_rank_runs, dim3(P.nb), dim3(kBlock), static_cast<size_t>(need) * sizeof(uint64_t), s, P, runs, sorted);
+    const size_t lds = kScaleThreads * sizeof(double);
+    constexpr int T = kScaleThreads;
+    if (need <= T) hipLaunchKernelGGL((k_exact_scale_s<T, 1>), dim3(1), dim3(T), lds, s, P, sorted);
+    else if (need <= 2 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 2>), dim3(1), dim3(T), 2 * lds, s, P, sorted);
+    else if (need <= 4 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 4>), dim3(1), dim3(T), 4 * lds, s, P, sorted);
+    else if (need <= 8 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 8>), dim3(1), dim3(T), 8 * lds, s, P, sorted);
+    else hipLaunchKernelGGL((k_exact_scale_s<T, 16>), dim3(1), dim3(T), 16 * lds, s, P, sorted);
+}
+
 // ---- iteration 0 for scans beyond the one-workgroup sort (kExactMaxPoints < n): k_exact_resid writes every point's
 // residual (+inf without a correspondence) to global memory, the context sorts them ascending (hipCUB radix sort:
 // the same order as std::sort for the non-NaN values; -0 / +0 ties do not change any sum), and launch_mwm_scale runs
@@ -235,13 +351,20 @@ void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long
 // Host side: the scale of a scan of at most kExactMaxPoints points: k_rank_sort into `sorted` (n doubles of scratch),
 // then k_exact_scale<PT> (PT = the padded size / kSeqThreads).
 template <int PT>
+static hipError_t scale_attr() {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kSeqThreads * PT * 8);
+}
+// k_exact_scale's dynamic LDS (up to 128 KB), set on the calling thread's current device (exact_prepare, per context)
+hipError_t exact_scale_rank_prepare() {
+    hipError_t e = hipSuccess;
+    for (hipError_t r : {scale_attr<1>(), scale_attr<2>(), scale_attr<3>(), scale_attr<4>(), scale_attr<5>(), scale_attr<6>(),
+                         scale_attr<7>(), scale_attr<8>(), scale_attr<10>(), scale_attr<12>(), scale_attr<16>()})
+        if (e == hipSuccess) e = r;
+    return e;
+}
+template <int PT>
 static void launch_scale_pt(const KParams& P, const double* sorted, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale<PT>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kSeqThreads * PT * 8);
-        attr = true;
-    }
     hipLaunchKernelGGL(k_exact_scale<PT>, dim3(1), dim3(kSeqThreads), static_cast<size_t>(kSeqThreads) * PT * 8, s, P,
                        sorted);
 }

@@ -67,6 +67,9 @@ struct FitOut;
 __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float thr, Slot* tab, uint32_t log2cap,
                              FitOut* out);
 void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s);
+hipError_t exact_scale_rank_prepare();
+hipError_t exact_scale_m_prepare();
+void launch_exact_scale_m(const KParams& P, const uint64_t* runs, uint64_t* sorted, hipStream_t s);
 void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s);
 void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
                     float* out, long long* stats, hipStream_t s);
@@ -125,7 +128,10 @@ struct lo_ctx {
     float* d_ex_terms = nullptr;
     size_t ex_cap = 0;              //   rows of d_ex_terms
     float* d_ex_tot = nullptr;      //   large scans: the 43 sums (launch_mw_sums -> k_exact_finish)
-    double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints)
+    double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints), or
+                                    //   up to kExactMergeMax points: the correspondence blocks' sorted runs
+    bool ex_merge = false;          //   this scan's exact scale merges the presorted runs (k_exact_scale_m)
+    bool ex_attr = false;           //   the exact-scale kernels' dynamic-LDS attributes are set (per context)
     void* d_mw = nullptr;           //   large scans: head records of the 43 column sums (lo_seqsum.h MwBuf)
     size_t mw_n_cap = 0;            //   the scan size d_mw is laid out for
     MwBuf mw{};
@@ -1189,6 +1195,7 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
 
 static constexpr int kStageEvents = 1024;
 static constexpr int kExactMaxPoints = 16384;         // reference-exact mode: one-workgroup sort in LDS up to here
+static_assert(kExactMaxPoints >= 2 * kExactMergeMax, "d_ex_rank holds the presorted runs and the merged keys");
 
 // A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
 // (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
@@ -1211,8 +1218,16 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
         LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * 43 * sizeof(float)));
     }
     if (!c->d_ex_rank) LO_HIP(c, hipMalloc(&c->d_ex_rank, kExactMaxPoints * sizeof(double)));
+    if (!c->ex_attr) {
+        LO_HIP(c, exact_scale_rank_prepare());
+        LO_HIP(c, exact_scale_m_prepare());
+        c->ex_attr = true;
+    }
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
+    // up to kExactMergeMax points the iteration-0 correspondence launch presorts its blocks (P0.presort, set by the
+    // caller from ex_merge) and one workgroup merges and sums them
+    c->ex_merge = static_cast<size_t>(P.nb) * kBlock <= static_cast<size_t>(kExactMergeMax);
     if (n > static_cast<size_t>(kExactMaxPoints)) {
         if (!c->d_ex_tot) LO_HIP(c, hipMalloc(&c->d_ex_tot, 64 * sizeof(float)));
         if (c->mw_n_cap < n) {                               // the column sums' head records
@@ -1250,6 +1265,12 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
 }
 // the iteration-0 scale of reference-exact mode (between the scan's first correspondence launch and its first PKO)
 static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStream_t s) {
+    if (c->ex_merge) {
+        // runs in the first half of d_ex_rank, the sorted keys in the second (kExactMaxPoints = 2 kExactMergeMax)
+        launch_exact_scale_m(P, reinterpret_cast<const uint64_t*>(c->d_ex_rank),
+                             reinterpret_cast<uint64_t*>(c->d_ex_rank) + kExactMergeMax, s);
+        return;
+    }
     if (n2 > 0) {
         launch_exact_scale(P, n2, c->d_ex_rank, s);
         return;
@@ -1307,6 +1328,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             if (rc3 != LO_OK) return rc3;
             P0.ex_terms = P.ex_terms;
             P0.scale_given = P.scale_given;
+            if (c->ex_merge) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
             if (!(fused && P.cand_rec && !c->kd && n2 > 0)) {
                 // reference-exact GN loop without candidates (lo_exact.hip): correspondences, (iteration 0) sorted-order
                 // scale, PKO, per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
@@ -1516,6 +1538,7 @@ retry:
     if (c->exact && (rc = exact_prepare(c, P, n_curr, &n2)) != LO_OK) return rc;
     KParams P0 = P;
     P0.init = 1;
+    if (c->exact && c->ex_merge) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
     std::memcpy(P0.T0, T_curr, sizeof(float) * 12);
     const dim3 blk(kBlock);
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));

@@ -23,6 +23,7 @@
 // the grid) only when two distances are equal -- so the 5-NN lists, their order and their tie-breaks equal
 // nanoflann's (tests/test_gpu_kdtree.py against tests/golden/knn_golden.npz, written by nanoflann itself).
 // Non-finite queries find nothing (nanoflann only adds points with dist < worstDist = FLT_MAX).
+#include "lo_blocksort.h"
 #include "lo_device.h"
 #include "lo_solve.h"
 
@@ -537,6 +538,8 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
         if (P.res_dbg) P.res_dbg[i] = valid ? dist : 0.0;
     }
     corr_epilogue(P, valid, dist, with_stats, blockIdx.x);
+    if (P.presort)                                      // iteration 0, reference-exact mode (uniform branch)
+        presort_block(P.presort, blockIdx.x, valid ? static_cast<uint64_t>(__double_as_longlong(dist)) : kInfKey);
 }
 
 // optimize_loop's inlier ratio (:206-238): the curr cloud at the converged pose (t + R p, :220-221), each point an

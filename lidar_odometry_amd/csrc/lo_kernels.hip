@@ -20,6 +20,7 @@
 // Compiled with -ffp-contract=off: the correspondence set and the fp64 residuals are bit-identical to the
 // reference's fp32/fp64 expressions (DESIGN.md "fp order").  Sums are fixed-order trees (run-to-run
 // deterministic), not the reference's sequential order.
+#include "lo_blocksort.h"
 #include "lo_device.h"
 #include "lo_math.h"
 #include "lo_solve.h"
@@ -47,7 +48,8 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
     for (int k = 0; k < 12; ++k) T[k] = cst->pose[k];
     if (!init && done) return;
     scan_pose(P, init, blk, T);
-    correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
+    const uint64_t key = correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
+    if (P.presort) presort_block(P.presort, blk, key);      // iteration 0, reference-exact mode (uniform branch)
 }
 
 // XCD-aware block order: the hardware hands consecutive workgroups to the 8 XCDs round-robin; logical block

@@ -261,6 +261,336 @@ __device__ inline double chain_seq_sum(const double* s_x, int cnt, double s, Seq
     return S.result;
 }
 
+// ---------------------------------------------------------------------------------------------------------------------
+// Halfway ties without heads: the two-state form of a segment.
+// Inside binade E the running sum is s = Q u (u = 2^(E-52), Q in [2^52, 2^53)).  A term x with t = x / u adds
+// rint(t) to Q -- unless t is halfway (t = f + 1/2), where round-half-even gives Q + f when Q + f is even and
+// Q + f + 1 otherwise: the step depends on Q's parity and always leaves Q even.  So every step is a map on the
+// parity p = Q & 1 with an integer increment, Q -> Q + d_p, p -> p'_p, and a run of steps composes into one such map
+// (SeqTx) -- associative, so a segment's whole effect is a (segmented) scan, and ties no longer split segments.  The
+// walk then only stops where the running sum crosses a power of two or comes close to one (mono_sum_tx below): a
+// KITTI scan's ~200 tie heads drop to ~25.
+// ---------------------------------------------------------------------------------------------------------------------
+struct SeqTx {
+    long long d0, d1;        // Q increment for entry parity 0 / 1
+    int p;                   // bit q: the exit parity for entry parity q
+};
+constexpr long long kTxSat = 1ll << 61;        // saturated increment (never exact: fails every check)
+__device__ __forceinline__ SeqTx tx_ident() { return SeqTx{0, 0, 2}; }
+__device__ __forceinline__ SeqTx tx_then(const SeqTx& a, const SeqTx& b) {   // a, then b
+    const int a0 = a.p & 1, a1 = (a.p >> 1) & 1;
+    const long long e0 = a.d0 + (a0 ? b.d1 : b.d0);
+    const long long e1 = a.d1 + (a1 ? b.d1 : b.d0);
+    return SeqTx{e0 < kTxSat ? e0 : kTxSat, e1 < kTxSat ? e1 : kTxSat, ((b.p >> a0) & 1) | (((b.p >> a1) & 1) << 1)};
+}
+// One term's step on binade E appended to m (x >= +0, t = x / u < 2^53: the caller's head rule guarantees it):
+// t = f + r exactly; a halfway r rounds Q + f to even, otherwise Q gains rint(t).
+__device__ __forceinline__ void tx_push(SeqTx& m, double x, int E) {
+    const double t = ldexp(x, 52 - E);
+    const double f = floor(t), fr = t - f;
+    const long long fi = static_cast<long long>(f);
+    const int fb = static_cast<int>(fi & 1), p0 = m.p & 1, p1 = (m.p >> 1) & 1;
+    if (fr == 0.5) {
+        m.d0 += fi + (p0 ^ fb);
+        m.d1 += fi + (p1 ^ fb);
+        m.p = 0;
+    } else {
+        const long long q = fi + (fr > 0.5 ? 1 : 0);
+        const int b = static_cast<int>(q & 1);
+        m.d0 += q;
+        m.d1 += q;
+        m.p = (p0 ^ b) | ((p1 ^ b) << 1);
+    }
+}
+
+// Wave-wide inclusive scan of a POD of 32-bit words by DPP (row_shr 1/2/4/8, then row_bcast 15/31 into the upper
+// rows): the earlier lane's value is combined in front, op(earlier, later).  Lanes without a source keep `ident`.
+template <int N> struct Words { int w[N]; };
+template <int CTRL, int RM, typename T>
+__device__ __forceinline__ T dpp_pod(const T& v, const T& old) {
+    static_assert(sizeof(T) % 4 == 0, "32-bit words");
+    constexpr int N = sizeof(T) / 4;
+    const Words<N> a = __builtin_bit_cast(Words<N>, v), o = __builtin_bit_cast(Words<N>, old);
+    Words<N> r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.w[i] = __builtin_amdgcn_update_dpp(o.w[i], a.w[i], CTRL, RM, 0xf, false);
+    return __builtin_bit_cast(T, r);
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T v, const T& ident, Op op) {
+    v = op(dpp_pod<0x111, 0xf>(v, ident), v);       // row_shr:1
+    v = op(dpp_pod<0x112, 0xf>(v, ident), v);       // row_shr:2
+    v = op(dpp_pod<0x114, 0xf>(v, ident), v);       // row_shr:4
+    v = op(dpp_pod<0x118, 0xf>(v, ident), v);       // row_shr:8   (16-lane rows scanned)
+    v = op(dpp_pod<0x142, 0xa>(v, ident), v);       // row_bcast:15 into rows 1, 3
+    v = op(dpp_pod<0x143, 0xc>(v, ident), v);       // row_bcast:31 into rows 2, 3
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T readlane_pod(const T& v, int l) {
+    constexpr int N = sizeof(T) / 4;
+    Words<N> a = __builtin_bit_cast(Words<N>, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) a.w[i] = __builtin_amdgcn_readlane(a.w[i], l);
+    return __builtin_bit_cast(T, a);
+}
+template <typename T>
+__device__ __forceinline__ T shfl_up1_pod(const T& v, const T& ident) {
+    constexpr int N = sizeof(T) / 4;
+    const Words<N> a = __builtin_bit_cast(Words<N>, v);
+    Words<N> r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.w[i] = __shfl_up(a.w[i], 1, 64);
+    return (threadIdx.x & 63) == 0 ? ident : __builtin_bit_cast(T, r);
+}
+// Exclusive scan over a workgroup of NT threads (NT / 64 <= 16 waves): DPP wave scans; the wave totals meet in
+// s_w (NT / 64 entries), every wave scans them in its first row and takes its own prefix.  Barriers inside.
+template <int NT, typename T, typename Op>
+__device__ __forceinline__ T block_excl_scan_dpp(const T& v, const T& ident, Op op, T* s_w, T* total = nullptr) {
+    constexpr int NW = NT / kWave;
+    static_assert(NW >= 1 && NW <= 16, "waves");
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const T inc = wave_incl_scan(v, ident, op);
+    if (lane == 63) s_w[wid] = inc;
+    __syncthreads();
+    T w = lane < NW ? s_w[lane] : ident;
+    w = op(dpp_pod<0x111, 0xf>(w, ident), w);
+    w = op(dpp_pod<0x112, 0xf>(w, ident), w);
+    w = op(dpp_pod<0x114, 0xf>(w, ident), w);
+    w = op(dpp_pod<0x118, 0xf>(w, ident), w);
+    if (total) *total = readlane_pod(w, NW - 1);
+    const T wex = wid ? readlane_pod(w, wid - 1) : ident;
+    __syncthreads();                                // s_w free again
+    return op(wex, shfl_up1_pod(inc, ident));
+}
+
+struct SegAgg {                                    // segmented-scan element: a thread's terms as one map
+    long long d0, d1;
+    int pf;                                        // p | (a segment starts inside) << 2
+    int nh;                                        // heads inside
+};
+__device__ __forceinline__ SegAgg seg_ident() { return SegAgg{0, 0, 2, 0}; }
+__device__ __forceinline__ SegAgg seg_op(const SegAgg& a, const SegAgg& b) {
+    if (b.pf & 4) return SegAgg{b.d0, b.d1, b.pf, a.nh + b.nh};
+    const SeqTx t = tx_then(SeqTx{a.d0, a.d1, a.pf & 3}, SeqTx{b.d0, b.d1, b.pf & 3});
+    return SegAgg{t.d0, t.d1, t.p | (a.pf & 4), a.nh + b.nh};
+}
+
+constexpr int kTxHeadCap = 512;                    // heads per sum (more: the plain chain)
+constexpr int kExactMergeMax = 8192;               // exact scale from presorted runs (k_rank_runs + k_exact_scale_s)
+template <int NT>
+struct MonoScratch {
+    double wd[NT / kWave];
+    SegAgg wa[NT / kWave];
+    int elast[NT];                                 // predicted binade of each thread's last term
+    int hedge[NT];                                 // bit 0: the thread's first term heads, bit 1: its last term heads
+    int h_idx[kTxHeadCap];
+    int h_e[kTxHeadCap];
+    long long h_d0[kTxHeadCap];                    // the head's segment as a two-state map
+    long long h_d1[kTxHeadCap];
+    double result;
+    int nheads, fb_seg, fb_terms;
+};
+
+// The plain chain (mono_sum_tx's fallback beyond kTxHeadCap heads): wave 0 adds s_x[0, cnt) to +0 in order.
+template <int NT>
+__device__ inline double chain_sum_tx(const double* s_x, int cnt, MonoScratch<NT>& S) {
+    if ((threadIdx.x >> 6) == 0) {
+        double s = 0.0;
+        for (int j = 0; j < cnt; ++j) s = s + s_x[j];
+        if (threadIdx.x == 0) S.result = s;
+    }
+    __syncthreads();
+    return S.result;
+}
+
+// Does the prefix T lie within 2^-30 of either end of its binade?  (The true running sum differs from the predicted
+// prefix by < n 2^-53 relative; terms this close to a power of two head their own segment.)
+__device__ __forceinline__ bool near_edge(double T) {
+    const uint64_t m = __builtin_bit_cast(uint64_t, T) & ((1ull << 52) - 1);
+    return m < (1ull << 22) || m > (1ull << 52) - (1ull << 22);
+}
+
+// acc = fma(v of lane N of this 16-lane row, 1.0, acc): rounds exactly as acc + v; no LDS, no readlane.
+template <int N>
+__device__ __forceinline__ void bcast_add(double& acc, double v, double one) {
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(v), "v"(one), "i"(N));
+}
+// Heads N.. of a 16-head window (every 16-lane row holds the window's heads in lanes 0-15): the head's own step, the
+// sum right after it recorded in lane N of each row, then the segment as s + u d_p (p = the low bit of s's mantissa:
+// Q's parity while s lies in the head's binade, which the check afterwards confirms).
+template <int N>
+__device__ __forceinline__ void walk_row(double& s, double& rec, double hx, double q0, double q1, double one, int left,
+                                         int n16) {
+    if constexpr (N < 16) {
+        if (N < left) {
+            bcast_add<N>(s, hx, one);
+            rec = n16 == N ? s : rec;
+            double s0 = s, s1 = s;
+            bcast_add<N>(s0, q0, one);
+            bcast_add<N>(s1, q1, one);
+            s = (__double2loint(s) & 1) ? s1 : s0;
+            walk_row<N + 1>(s, rec, hx, q0, q1, one, left, n16);
+        }
+    }
+}
+
+// +0 + x_0 + x_1 + ... + x_{cnt-1} in index order, one fp64 rounding per addition, for x_j >= +0 (no NaN).
+// One workgroup of NT threads; thread t holds terms t*PT .. t*PT + PT - 1 in x (zero past cnt) and the same terms sit in
+// s_x (LDS: the walk's head terms, term-by-term fallbacks).  Heads: the first non-zero term, every non-zero term whose
+// predicted binade differs from its predecessor's, lies within 2^-30 of a binade end, or is too large for the integer
+// model; every other term is a step of its head's segment map.  The walk (wave 0) does a head's step directly, then its
+// segment as s + u d_p when s lies in the predicted binade and the result stays below 2^(E+1); else the segment term by
+// term.  False when the heads exceed kTxHeadCap (the caller sums the chain).  stamps (nullable, diagnostic builds):
+// thread 0 stores s_memtime after the head count, the segmented scan and the records.
+template <int NT, int PT>
+__device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, const double* s_x, MonoScratch<NT>& S,
+                                            double& out, unsigned long long* stamps = nullptr) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, base = tid * PT;
+    // 1. approximate prefix (fp64, tree order): the prediction of each step's binade
+    double run = 0.0;
+#pragma unroll
+    for (int a = 0; a < PT; ++a) run += x[a];
+    const double tex = block_excl_scan_dpp<NT>(run, 0.0, [](double a, double b) { return a + b; }, S.wd);
+    S.elast[tid] = binade64(tex + run);
+    __syncthreads();
+    // 2. predicted binades and heads (a term's predecessor's binade as its owner computed it)
+    int E[PT];
+    bool hd[PT];
+    int nh = 0;
+    {
+        double tl = 0.0;
+        int ep = tid ? S.elast[tid - 1] : kExpNone;
+#pragma unroll
+        for (int a = 0; a < PT; ++a) {
+            tl += x[a];
+            const double T = tex + tl;
+            E[a] = binade64(T);
+            const bool act = base + a < cnt && x[a] != 0.0;
+            bool h = act && (E[a] == kExpNone || E[a] != ep || near_edge(T));
+            if (act && !h) h = !(ldexp(x[a], 52 - E[a]) < 0x1p53);
+            hd[a] = h;
+            nh += h ? 1 : 0;
+            ep = E[a];
+        }
+    }
+    S.hedge[tid] = (hd[0] ? 1 : 0) | (hd[PT - 1] ? 2 : 0);
+    __syncthreads();
+    const bool prev_head = tid ? (S.hedge[tid - 1] & 2) != 0 : false;
+    const bool next_head = tid + 1 < NT ? (S.hedge[tid + 1] & 1) != 0 : false;
+    if (stamps && tid == 0) stamps[0] = __builtin_amdgcn_s_memtime();
+    // 3. the thread's terms as one segmented map (a head's own step is the walk's: identity here), with its head count
+    SegAgg agg{0, 0, 2, nh};
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        if (hd[a] || (a ? hd[a - 1] : prev_head)) { agg.d0 = 0; agg.d1 = 0; agg.pf = 2 | 4; }   // a segment starts
+        if (base + a < cnt && x[a] != 0.0 && !hd[a]) {
+            SeqTx m{agg.d0, agg.d1, agg.pf & 3};
+            tx_push(m, x[a], E[a]);
+            agg.d0 = m.d0; agg.d1 = m.d1; agg.pf = m.p | (agg.pf & 4);
+        }
+    }
+    SegAgg tot;
+    const SegAgg ex = block_excl_scan_dpp<NT>(agg, seg_ident(), seg_op, S.wa, &tot);
+    const int htot = tot.nh;
+    if (stamps && tid == 0) stamps[1] = __builtin_amdgcn_s_memtime();
+    if (htot > kTxHeadCap) return false;                       // uniform
+    // 4. head records and each segment's map (written by the thread holding the segment's last term)
+    {
+        SeqTx cur{ex.d0, ex.d1, ex.pf & 3};
+        int hk = ex.nh;
+#pragma unroll
+        for (int a = 0; a < PT; ++a) {
+            const int j = base + a;
+            if (hd[a] || (a ? hd[a - 1] : prev_head)) cur = tx_ident();
+            if (j < cnt && x[a] != 0.0 && !hd[a]) tx_push(cur, x[a], E[a]);
+            if (hd[a]) { S.h_idx[hk] = j; S.h_e[hk] = E[a]; ++hk; }
+            const bool last = j == cnt - 1 || (j < cnt && (a + 1 < PT ? hd[a + 1] : next_head));
+            if (last && hk > 0) { S.h_d0[hk - 1] = cur.d0; S.h_d1[hk - 1] = cur.d1; }
+        }
+    }
+    __syncthreads();
+    if (stamps && tid == 0) stamps[2] = __builtin_amdgcn_s_memtime();
+    // 5. the walk (wave 0, wave-uniform): windows of 16 heads, every 16-lane row holding the window; a head costs a
+    //    dependent fma, a parity select and a second fma (row_newbcast operands); the checks run lane-parallel after the
+    //    window, and from a failed check on it goes head by head (the failed head's segment term by term)
+    if (wid == 0) {
+        const double one = 1.0;
+        const int n16 = lane & 15;
+        double s = 0.0;
+        int fbs = 0, fbt = 0;
+        for (int k0 = 0; k0 < htot; k0 += 16) {
+            const int kk = k0 + n16;
+            int hi = 0, hend = 0, E0 = kExpNone;
+            long long d0 = 0, d1 = 0;
+            double hx = -0.0, q0 = -0.0, q1 = -0.0;              // past the window: a no-op head (x + -0 == x)
+            bool seg = false, bad = false;
+            if (kk < htot) {
+                hi = S.h_idx[kk];
+                hend = kk + 1 < htot ? S.h_idx[kk + 1] : cnt;
+                E0 = S.h_e[kk];
+                hx = s_x[hi];
+                seg = hend > hi + 1;
+                if (seg) {
+                    d0 = S.h_d0[kk];
+                    d1 = S.h_d1[kk];
+                    bad = E0 == kExpNone || d0 >= (1ll << 53) || d1 >= (1ll << 53);
+                    if (!bad) {
+                        const double u = ldexp(1.0, E0 - 52);
+                        q0 = static_cast<double>(d0) * u;
+                        q1 = static_cast<double>(d1) * u;
+                    }
+                }
+            }
+            // the check on the sum right after head kk's own step: s in [2^E, 2^(E+1)) and Q + d_parity <= 2^53 - 1
+            auto check = [&](double sv) -> bool {
+                if (!seg) return true;
+                if (bad || binade64(sv) != E0) return false;
+                const long long Q = static_cast<long long>((__builtin_bit_cast(uint64_t, sv) & ((1ull << 52) - 1)) | (1ull << 52));
+                return Q + ((Q & 1) ? d1 : d0) <= (1ll << 53) - 1;
+            };
+            const int left = min(16, htot - k0);
+            double rec = 0.0;
+            walk_row<0>(s, rec, hx, q0, q1, one, left, n16);
+            const unsigned long long badm = __ballot(!check(rec)) & 0xFFFFull;
+            if (badm) {                                          // uniform
+                const int f = __builtin_ctzll(badm);
+                s = rl64d(rec, f);
+                for (int l = f; l < left; ++l) {
+                    if (l > f) s = s + rl64d(hx, l);
+                    const bool ok = l > f && ((__ballot(check(s)) >> l) & 1ull) != 0ull;   // head l's own check
+                    if (ok) {
+                        s = s + ((__double2loint(s) & 1) ? rl64d(q1, l) : rl64d(q0, l));
+                    } else {
+                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                        for (int j = h + 1; j < end; ++j) s = s + s_x[j];
+                        fbs += end > h + 1 ? 1 : 0;
+                        fbt += end - h - 1;
+                    }
+                }
+            }
+        }
+        if (lane == 0) { S.result = s; S.fb_seg = fbs; S.fb_terms = fbt; S.nheads = htot; }
+    }
+    __syncthreads();
+    out = S.result;
+    return true;
+}
+
+// Sorting support for the exact scale (k_rank_runs): the number of keys of a sorted 256-key run below x (STRICT) or
+// not above x -- nine probes, no branch.
+template <bool STRICT>
+__device__ __forceinline__ int run_count(const uint64_t* R, uint64_t x) {
+    int p = 0;
+#pragma unroll
+    for (int s = 128; s >= 1; s >>= 1) {
+        const uint64_t v = R[p + s - 1];
+        p += (STRICT ? v < x : v <= x) ? s : 0;
+    }
+    const uint64_t v = R[p];
+    return p + ((STRICT ? v < x : v <= x) ? 1 : 0);
+}
+
 }  // namespace lo
 
 namespace lo {

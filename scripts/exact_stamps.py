@@ -29,7 +29,7 @@ def main():
     L = lib()
     assert L.lo_map_set_from_voxelmap(icp.ctx, wl["vm"].handle) == 0
     icp.set_exact(True)
-    rows, stats = [], []
+    rows, stats, mrows = [], [], []
     for i in range(len(wl["scans"])):
         icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
         d = (C.c_ulonglong * 16)()
@@ -41,9 +41,20 @@ def main():
                   "%d in its unrolled 64-head chains" % (i, len(wl["scans"][i]), it, d[15], d[13], d[12], d[5], d[8], d[6],
                                                          d[9], d[7], d[10], d[11], d[14]), flush=True)
             continue
+        if len(wl["scans"][i]) <= 8192:                       # merge path (k_exact_scale_m): 0 start, 1 merged,
+            mrows.append([d[1] - d[0], d[4] - d[1], d[5] - d[4], d[6] - d[5], d[2] - d[6], d[3] - d[2]])  # 4-6 sum phases
+            stats.append([d[14], d[8], d[9], d[10], d[11], d[12], d[13]])
+            continue
         rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3], d[6] - d[5], d[7] - d[6]])
         stats.append([d[14], d[8], d[9], d[10], d[11], d[12], d[13]])
+    if mrows:
+        m = np.array(mrows, dtype=np.float64)
+        print("merge path, cycles per phase, mean over %d scans: load + count %.0f | mean sum: heads %.0f  segmented "
+              "scan %.0f  records %.0f  walk %.0f | variance sum %.0f" % (len(mrows), *m.mean(0)), flush=True)
     if not rows:
+        for k, t in enumerate(stats):
+            print("scan %d: %d accepted | mean sum: %d heads, %d segments / %d terms term by term | variance: %d heads, "
+                  "%d / %d" % (k, *t), flush=True)
         icp.close()
         return
     r = np.array(rows, dtype=np.float64)
