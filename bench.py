@@ -219,7 +219,7 @@ def parity_bitwise(gpu, ref) -> int:
 
 MODE_NOTE = {"exact": "lo_set_exact: the reference's fp32 operation order (sequential sums in correspondence order, "
                       "sorted-order iteration-0 scale, fp32 LDLT, JacobiSVD-projected SO3)",
-             "default": "fp64 tree sums, Chan-merged iteration-0 scale, fp64 LDLT + polar SO3"}
+             "fast": "lo_set_exact(ctx, 0): fp64 tree sums, Chan-merged iteration-0 scale, fp64 LDLT + polar SO3"}
 
 
 def oracle_reference(wl):
@@ -430,7 +430,7 @@ def pko_roofline(em_live):
                     "iteration count for alpha to stay identical"}
 
 
-def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False):
+def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "exact"):
     """C5's data at one GPU's scale (BASELINE.json configs[4]: synthetic 1M-point scans, 1000 planar patches + 10 %
     outliers): n_scans DISTINCT scans, each on its own context (its own slot / residual outputs and table copy),
     launched round-robin on one stream.  Between two launches of a scan the other n_scans - 1 move their own ~24 MB
@@ -456,6 +456,7 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False):
         pts = synth.azimuth_order(synth.transform(np.linalg.inv(T), synth.sample_patches(sc, 1_000_000, 2011 + f)))
         o = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=0.5),
                                            device=local, max_points=len(pts))
+        o.set_exact(mode == "exact")
         assert L.lo_map_set_from_voxelmap(o.ctx, vm.handle) == 0
         ctxs.append(o)
         scans.append(pts)
@@ -528,7 +529,7 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False):
             traffic_live["alg_bytes_per_launch"] = float(alg[0])
     return {"workload": "C5 synthetic 1M-point scans (1000 planar patches + 10 % outliers, azimuth order), "
                         f"{n_scans} distinct scans, one context each, round-robin on one stream",
-            "value": rounds * n_scans / el, "unit": "scans/s (1M points)", "gn_iters_per_scan_avg": float(np.mean(iters)),
+            "value": rounds * n_scans / el, "unit": "scans/s (1M points)", "mode": mode, "gn_iters_per_scan_avg": float(np.mean(iters)),
             "working_set_bytes": float(ws), "in_cache": bool(ws <= MALL_BYTES), "map_surfels": vm.surfel_count(),
             "roofline": {"kernel": "k_correspond", "bound": "hbm", "achieved": iso_ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": iso_ach / HBM_PEAK_GBS, "kernel_us": iso_t,
@@ -840,13 +841,13 @@ def main():
                     help="extra measurement with --config kitti: this many distinct 1M-point scans (C5), one context "
                          "each, rotated so each launch reads its scan from HBM; 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="auto", choices=["auto", "exact", "default"],
-                    help="arithmetic order of the timed GN step: exact = the reference's own fp32 order (lo_set_exact: "
-                         "sequential sums, fp32 LDLT, JacobiSVD SO3; bit-identical to the oracle), default = fp64 tree "
-                         "sums + fp64 solve (within ~1e-7 per step, but a near-tie in the PKO's JS argmin can flip "
-                         "alpha); auto = default when its every iteration on the workload's scans is within the "
-                         "north_star's 1e-4 m / 1e-4 rad of the oracle, else exact.  The other mode is timed beside it "
-                         "as other_mode")
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast", "auto", "default"],
+                    help="arithmetic order of the timed GN step: exact (the library's default) = the reference's own "
+                         "fp32 order (sequential sums, fp32 LDLT, JacobiSVD SO3; bit-identical to the oracle), fast = "
+                         "fp64 tree sums + fp64 solve (lo_set_exact(ctx, 0): within ~1e-7 per step, but a near-tie in "
+                         "the PKO's JS argmin can flip alpha; 'default' is its old name); auto = fast when, on EVERY "
+                         "rank, its every iteration on the workload's scans is within the north_star's 1e-4 m / 1e-4 "
+                         "rad of the oracle, else exact.  The other mode is timed beside it as other_mode")
     ap.add_argument("--order", default="azimuth", choices=["azimuth", "random"], help="patch1m scan point order")
     ap.add_argument("--sequences", type=int, default=8,
                     help="extra measurement: independent sequences sharing this GPU, one context + HIP stream each "
@@ -860,6 +861,8 @@ def main():
                          "contexts advanced in lockstep, one launch per kernel per GN iteration); '' = skip; "
                          "reported as batched, never as value")
     args = ap.parse_args()
+    if args.mode == "default":
+        args.mode = "fast"
     global ORDER
     ORDER = args.order
     if args.pmc_child:
@@ -934,14 +937,17 @@ def main():
         p_sel = parity_vs_oracle(sel, ref_sel)
         passes = bool(p_sel["within_1e-4"] and p_sel["iteration_count_equal"] == p_sel["scans"]
                       and p_sel["status_equal"] == p_sel["scans"])
-        args.mode = "default" if passes else "exact"
-        mode_selection = {"rule": "default arithmetic when its every iteration on this workload's scans is within "
-                                  "1e-4 m / 1e-4 rad of the oracle with equal iteration counts and status, else "
-                                  "reference-exact", "default_parity": p_sel, "chosen": args.mode,
-                          "seconds": time.perf_counter() - t_sel}
-        log(f"[rank {rank}] mode auto -> {args.mode} (default within 1e-4: {p_sel['within_1e-4']})")
+        # every rank decides on its own scans; all ranks time the same mode (all-reduce MIN of the verdicts)
+        from lidar_odometry_amd.parallel import all_ranks_agree
+        agreed = all_ranks_agree(passes, world, None if (world == 1 or args.dist_backend == "gloo") else dev)
+        args.mode = "fast" if agreed else "exact"
+        mode_selection = {"rule": "fast arithmetic when, on every rank, its every iteration on that rank's scans is "
+                                  "within 1e-4 m / 1e-4 rad of the oracle with equal iteration counts and status, else "
+                                  "reference-exact", "fast_parity": p_sel, "this_rank_passes": passes,
+                          "all_ranks_pass": agreed, "chosen": args.mode, "seconds": time.perf_counter() - t_sel}
+        log(f"[rank {rank}] mode auto -> {args.mode} (fast within 1e-4 here: {p_sel['within_1e-4']}, all ranks: {agreed})")
     icp.set_exact(args.mode == "exact")
-    other = "default" if args.mode == "exact" else "exact"
+    other = "fast" if args.mode == "exact" else "exact"
     # one stream shared by the ICP context and torch (pose-record copies, the gather's events): a dedicated stream,
     # because handle 0 (torch's legacy default stream) means "the context's own non-blocking stream" to
     # lo_set_stream, which the default stream does not order against
@@ -1215,7 +1221,7 @@ def main():
     if sizes:
         from lidar_odometry_amd import BatchOptimizer
         from lidar_odometry_amd._lib import LoBatchRec
-        batched = {"unit": "scans/s", "runs": [], "mode": "default",
+        batched = {"unit": "scans/s", "runs": [], "mode": args.mode, "mode_note": MODE_NOTE[args.mode],
                    "note": "B independent sequences on one GPU (one context each: own map copy, scan, GN state), "
                            "advanced in lockstep by lo_batch_optimize_async; aggregate throughput, not value"}
         pool = []
@@ -1228,6 +1234,7 @@ def main():
             while len(pool) < B:
                 o = IterativeClosestPointOptimizer(ICPConfig(), AdaptiveMEstimatorConfig(), MapGeometry(voxel_size=wl["voxel"]),
                                                    device=local, max_points=max_pts)
+                o.set_exact(args.mode == "exact")
                 assert L.lo_map_set_from_voxelmap(o.ctx, wl["vm"].handle) == 0
                 pool.append(o)
             bo = BatchOptimizer(pool[:B])
@@ -1358,7 +1365,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget, {args.mode: gpu_res, other: gpu_other}, args.mode)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
     if rank == 0 and world == 1 and args.config == "kitti" and args.c5 > 0:
-        result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5, pmc=args.pmc == "live")
+        result["c5_hbm"] = c5_hbm_leg(local, dev, args.c5, pmc=args.pmc == "live", mode=args.mode)
     icp.close()
     if rank == 0:
         emit(result)

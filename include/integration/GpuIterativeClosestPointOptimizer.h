@@ -152,7 +152,8 @@ public:
         m_config = config;
     }
     const ICPConfig& get_config() const { return m_config; }
-    lo_ctx* context() const { return m_ctx; }                // e.g. lo_set_exact(context(), 1)
+    lo_ctx* context() const { return m_ctx; }                // reference-exact by default; lo_set_exact(context(), 0) =
+                                                             // the opt-in fast mode (not parity-safe)
 
 private:
     lo_config make_config(const ICPConfig& cfg) const {

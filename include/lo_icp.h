@@ -156,12 +156,15 @@ void* lo_stream(lo_ctx* ctx);   /* hipStream_t of the context */
 /* Run the context on a caller stream (e.g. the framework's current stream); NULL = own stream again (a fresh
  * hipStreamNonBlocking stream -- so the legacy default stream, handle 0, cannot be selected: pass a created stream). */
 int lo_set_stream(lo_ctx* ctx, void* hip_stream);
-/* Reference-exact arithmetic (default off): H, g and the cost summed SEQUENTIALLY in fp32 over the correspondences
- * in scan order, the iteration-0 scale from the sorted residuals, the fp32 LDLT and SO3 re-projection through
- * JacobiSVD -- the reference's own operation order (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99),
- * so the per-iteration logs equal the oracle restatement's bit for bit.  Slower (a sequential sum and two fp32 SVDs per
- * GN iteration); up to 16384 points the iteration-0 residuals are sorted in one workgroup's LDS, larger scans (up to
- * max_points) sort them with hipCUB's radix sort in device memory. */
+/* Arithmetic mode.  enable = 1 (THE DEFAULT of every context): reference-exact -- H, g and the cost summed
+ * SEQUENTIALLY in fp32 over the correspondences in scan order, the iteration-0 scale from the sorted residuals, the
+ * fp32 LDLT and SO3 re-projection through JacobiSVD: the reference's own operation order
+ * (IterativeClosestPointOptimizer.cpp:304-449, MathUtils.cpp:23-99), so the per-iteration logs equal the oracle
+ * restatement's bit for bit (the sequential sums are reproduced in parallel, lo_seqsum.h).  enable = 0: the fast mode
+ * (opt-in) -- fixed-order fp64 tree sums, a Chan-merged scale, an fp64 LDLT with a polar SO3 projection; within 1e-7
+ * of the reference per step, but a PKO alpha near-tie or a correspondence on a voxel face can then resolve the other way
+ * and move the pose by 1e-4 .. 4e-4 (measured on the MID360-like and 1M-point workloads): NOT parity-safe.
+ * LO_EXACT=0 in the environment starts contexts in the fast mode (A/B runs). */
 int lo_set_exact(lo_ctx* ctx, int enable);
 /* Scan pipeline (default on; LO_PIPE=0 in the environment turns it off at lo_create).  The reference's optimize
  * runs GN iterations until convergence (IterativeClosestPointOptimizer.cpp:281-449); the device loop enqueues all

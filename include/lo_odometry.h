@@ -53,9 +53,9 @@ void          lo_odom_destroy(lo_odometry* o);
 const char*   lo_odom_last_error(const lo_odometry* o);
 /* Pose of the first frame (LidarFrame::get_initial_pose); identity by default. */
 int           lo_odom_set_initial_pose(lo_odometry* o, const float T[12]);
-/* Reference-exact ICP arithmetic for every frame (lo_set_exact on the frame loop's context).  Feature clouds whose
- * bound ceil(n_raw / point_stride) exceeds 16384 take the exact mode's device radix-sort path for the iteration-0
- * scale (slower, same bits). */
+/* The frame loop's ICP arithmetic mode (lo_set_exact on its context): 1 = reference-exact, the default; 0 = the
+ * opt-in fast mode (not parity-safe, see lo_set_exact).  Feature clouds whose bound ceil(n_raw / point_stride) exceeds
+ * 16384 take the exact mode's device radix-sort path for the iteration-0 scale (slower, same bits). */
 int           lo_odom_set_exact(lo_odometry* o, int enable);
 /* One raw scan (AoS float3, host memory) -> its world pose (row-major 3x4).  Returns LO_OK / LO_INSUFFICIENT
  * (the guess was kept, as :304-307) or a negative error. */

@@ -162,17 +162,24 @@ __global__ __launch_bounds__(kSeqThreads) void k_exact_scale(KParams P, const do
 // one workgroup (mono_sum_tx: the halfway ties as two-state segment maps, a walk over ~25 binade heads). ----
 __global__ __launch_bounds__(kBlock) void k_rank_runs(KParams P, const uint64_t* __restrict__ runs, uint64_t* __restrict__ out) {
     if (P.st->done) return;
+    if (blockIdx.x == 0) LO_XSTAMP(P.st, 15);
     extern __shared__ uint64_t s_r[];                        // P.nb runs
     const int nb = P.nb, b = blockIdx.x, tid = threadIdx.x;
-    for (int e = tid; e < nb * kBlock; e += kBlock) s_r[e] = runs[e];
-    __syncthreads();
-    const uint64_t x = s_r[b * kBlock + tid];
-    int rank = tid;
-    for (int r = 0; r < nb; ++r) {                           // equal keys: earlier runs first, then this run's order
-        if (r == b) continue;
-        rank += r < b ? run_count<false>(s_r + r * kBlock, x) : run_count<true>(s_r + r * kBlock, x);
+    {                                                        // every run's key of this lane in flight at once
+        constexpr int kRuns = kExactMergeMax / kBlock;
+        uint64_t v[kRuns];
+#pragma unroll
+        for (int r = 0; r < kRuns; ++r) v[r] = runs[(r < nb ? r : 0) * kBlock + tid];
+#pragma unroll
+        for (int r = 0; r < kRuns; ++r) if (r < nb) s_r[r * kBlock + tid] = v[r];
     }
+    __syncthreads();
+    if (b == 0) LO_XSTAMP(P.st, 12);
+    const uint64_t x = s_r[b * kBlock + tid];
+    // equal keys: earlier runs first, then this run's order
+    const int rank = tid + (nb <= 16 ? runs_rank<16>(s_r, nb, b, x) : runs_rank<kExactMergeMax / kBlock>(s_r, nb, b, x));
     out[rank] = x;
+    if (b == 0) LO_XSTAMP(P.st, 13);
 }
 
 template <int NT, int PT>
@@ -216,15 +223,18 @@ __global__ __launch_bounds__(NT) void k_exact_scale_s(KParams P, const uint64_t*
     LO_XSTAMP(st, 1);
 #ifdef LO_EXACT_STAMPS
     unsigned long long* stp = st->dbg + 4;                  // dbg[4..6]: the mean sum's phases
+    {                                                        // diagnostic: the same sum once more from a warm
+        double warm;                                         // instruction cache (dbg[8..10] phases, dbg[11] end)
+        LO_XSTAMP(st, 7);
+        (void)mono_sum_tx<NT, PT>(x, cnt, s_x, S, warm, st->dbg + 8);
+        LO_XSTAMP(st, 11);
+    }
 #else
     unsigned long long* stp = nullptr;
 #endif
     double sum;
     if (!mono_sum_tx<NT, PT>(x, cnt, s_x, S, sum, stp)) sum = chain_sum_tx<NT>(s_x, cnt, S);
     LO_XSTAMP(st, 2);
-    LO_XSTAT(st, 8, S.nheads);
-    LO_XSTAT(st, 9, S.fb_seg);
-    LO_XSTAT(st, 10, S.fb_terms);
     LO_XSTAT(st, 14, cnt);
     const double mean = sum / cnt;                           // std::accumulate(...) / residuals.size()
 #pragma unroll
@@ -236,14 +246,180 @@ __global__ __launch_bounds__(NT) void k_exact_scale_s(KParams P, const uint64_t*
     double var;
     if (!mono_sum_tx<NT, PT>(x, cnt, s_x, S, var)) var = chain_sum_tx<NT>(s_x, cnt, S);
     LO_XSTAMP(st, 3);
-    LO_XSTAT(st, 11, S.nheads);
-    LO_XSTAT(st, 12, S.fb_seg);
-    LO_XSTAT(st, 13, S.fb_terms);
     var /= cnt;
     if (tid == 0) st->scale = sqrt(var) / 6.0;               // :313-315
 }
 
-constexpr int kScaleThreads = 512;                           // k_exact_scale_s: 8 waves, PT = padded size / 512
+// ---- iteration 0, scans of at most kExactMergeMax points, in ONE launch after the correspondence launch: the accepted
+// residuals' keys sorted by a counting sort in LDS -- bins over [min, max] of the finite keys (monotone in the key, so
+// bin order is sort order), a histogram, its scan, an atomic scatter into the bins, then each key's rank inside its
+// bin by comparing it with the bin's members (a bin holds a few keys: the bins are as many as the keys) -- and both
+// sums by mono_sum_tx.  No chip-wide pass, no presort. ----
+struct KeyStat {
+    uint64_t mn, mx;                                         // min / max finite key
+    int cnt, nan;                                            // finite keys; NaN keys
+};
+__device__ __forceinline__ KeyStat keystat_op(KeyStat a, KeyStat b) {
+    return KeyStat{a.mn < b.mn ? a.mn : b.mn, a.mx > b.mx ? a.mx : b.mx, a.cnt + b.cnt, a.nan | b.nan};
+}
+constexpr int kScaleC = 1024;                                // k_exact_scale_c threads
+template <int PT>
+__host__ __device__ constexpr int scale_c_bins() { return PT * kScaleC <= 4096 ? PT * kScaleC : 2048; }
+template <int PT>
+__host__ __device__ constexpr size_t scale_c_lds() {
+    return 2 * static_cast<size_t>(PT) * kScaleC * sizeof(uint64_t) + 2 * static_cast<size_t>(scale_c_bins<PT>()) * sizeof(int);
+}
+
+template <int PT>
+__device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
+    DevState* st = P.st;
+    if (st->done) return;
+    constexpr int NT = kScaleC, N = PT * NT, NB = scale_c_bins<PT>();
+    extern __shared__ uint64_t s_dyn[];
+    uint64_t* s_tmp = s_dyn;                                 // keys in bin order
+    uint64_t* s_srt = s_dyn + N;                             // keys sorted
+    int* s_cnt = reinterpret_cast<int*>(s_dyn + 2 * N);      // per-bin count
+    int* s_end = s_cnt + NB;                                 // per-bin start, then end (after the scatter)
+    __shared__ MonoScratch<NT> S;
+    __shared__ KeyStat s_ks[NT / kWave];
+    LO_XSTAMP(st, 0);
+    const int tid = threadIdx.x, n = scan_n(P);
+    const int32_t* slot = P.slot;
+    const double* res = P.kd_res ? P.kd_res : P.res_out;
+    // the keys, coalesced: element e = q NT + tid (the accepted residual's bits, else +inf)
+    uint64_t key[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        const int e = q * NT + tid, ec = e < n ? e : 0;
+        const int sl = slot[ec];
+        const uint64_t r = static_cast<uint64_t>(__double_as_longlong(res[ec]));
+        key[q] = (e < n && sl >= 0) ? r : kInfKey;
+    }
+    KeyStat ks{~0ull, 0ull, 0, 0};
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        if (key[q] < kInfKey) { ks.mn = key[q] < ks.mn ? key[q] : ks.mn; ks.mx = key[q] > ks.mx ? key[q] : ks.mx; ++ks.cnt; }
+        if (key[q] > kInfKey) ks.nan = 1;
+    }
+    for (int b = tid; b < NB; b += NT) s_cnt[b] = 0;
+    KeyStat tot;
+    (void)block_excl_scan_dpp<NT>(ks, KeyStat{~0ull, 0ull, 0, 0}, keystat_op, s_ks, &tot);
+    const int cnt = tot.cnt;
+    if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
+    if (tot.nan) {                                           // a NaN residual (accepted: the gate keeps NaN): the mean,
+        uint64_t nk = ~0ull;                                 // the variance and the scale are NaN
+#pragma unroll
+        for (int q = 0; q < PT; ++q) if (key[q] > kInfKey && key[q] < nk) nk = key[q];
+        if (nk != ~0ull) st->scale = sqrt(__longlong_as_double(static_cast<long long>(nk))) / 6.0;
+        return;
+    }
+    const uint64_t range = tot.mx - tot.mn;
+    const int bl = range ? 64 - __clzll(static_cast<long long>(range)) : 0;
+    int lb = 0;
+    while ((1 << (lb + 1)) <= NB) ++lb;                      // log2(NB)
+    const int shift = bl > lb ? bl - lb : 0;
+    auto bin_of = [&](uint64_t k) { return static_cast<int>((k - tot.mn) >> shift); };
+    // histogram, its exclusive scan (NB / NT consecutive bins per thread), the scatter
+#pragma unroll
+    for (int q = 0; q < PT; ++q) if (key[q] < kInfKey) atomicAdd(&s_cnt[bin_of(key[q])], 1);
+    __syncthreads();
+    constexpr int BPT = NB / NT;
+    int bsum = 0;
+    for (int i = 0; i < BPT; ++i) bsum += s_cnt[tid * BPT + i];
+    int bex = block_excl_scan_dpp<NT>(bsum, 0, [](int a, int b) { return a + b; }, S.wi);
+    for (int i = 0; i < BPT; ++i) { s_end[tid * BPT + i] = bex; bex += s_cnt[tid * BPT + i]; }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PT; ++q)
+        if (key[q] < kInfKey) s_tmp[atomicAdd(&s_end[bin_of(key[q])], 1)] = key[q];
+    __syncthreads();
+    // each key's rank in its bin: the members below it, and the equal ones placed before it
+    for (int p = tid; p < cnt; p += NT) {
+        const uint64_t k = s_tmp[p];
+        const int b = bin_of(k), e = s_end[b], s0 = e - s_cnt[b];
+        int r = 0;
+        for (int q = s0; q < e; ++q) {
+            const uint64_t o = s_tmp[q];
+            r += (o < k || (o == k && q < p)) ? 1 : 0;
+        }
+        s_srt[s0 + r] = k;
+    }
+    __syncthreads();
+    LO_XSTAMP(st, 12);
+    double* s_x = reinterpret_cast<double*>(s_tmp);          // the bin-ordered keys are no longer read
+    const int base = tid * PT;
+    double x[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+        x[q] = base + q < cnt ? __longlong_as_double(static_cast<long long>(s_srt[base + q])) : 0.0;
+        s_x[base + q] = x[q];
+    }
+    __syncthreads();
+    LO_XSTAMP(st, 1);
+    double sum, var;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {                   // the mean's sum, then the variance's (same code)
+#ifdef LO_EXACT_STAMPS
+        unsigned long long* stp = st->dbg + (pass ? 8 : 4);  // dbg[4..6] / dbg[8..10]: the sums' phases
+#else
+        unsigned long long* stp = nullptr;
+#endif
+        double v;
+        if (!mono_sum_tx<NT, PT>(x, cnt, s_x, S, v, stp)) v = chain_sum_tx<NT>(s_x, cnt, S);
+        if (pass == 0) {
+            LO_XSTAMP(st, 2);
+            sum = v;
+            const double mean = sum / cnt;                   // std::accumulate(...) / residuals.size()
+#pragma unroll
+            for (int q = 0; q < PT; ++q) {
+                x[q] = base + q < cnt ? (x[q] - mean) * (x[q] - mean) : 0.0;
+                s_x[base + q] = x[q];                        // the walk's reads of s_x ended at mono_sum_tx's barrier
+            }
+            __syncthreads();
+        } else {
+            var = v;
+        }
+    }
+    (void)sum;
+    LO_XSTAMP(st, 3);
+    var /= cnt;
+    if (tid == 0) st->scale = sqrt(var) / 6.0;               // :313-315
+}
+template <int PT>
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_c(KParams P) { exact_scale_c_body<PT>(P); }
+// batched (lo_batch_* over reference-exact contexts): one workgroup per job
+template <int PT>
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_cb(const KParams* __restrict__ PB) { exact_scale_c_body<PT>(PB[blockIdx.x]); }
+template <int PT>
+static hipError_t scale_c_attr() {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cb<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(scale_c_lds<PT>()));
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_c<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(scale_c_lds<PT>()));
+}
+hipError_t exact_scale_c_prepare() {
+    hipError_t e = hipSuccess;
+    for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>()})
+        if (e == hipSuccess) e = r;
+    return e;
+}
+// jobs [0, njobs) of PB, every job's P.n <= n_max <= kExactMergeMax
+void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t s) {
+    const dim3 g(njobs), b(kScaleC);
+    if (n_max <= kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<1>, g, b, scale_c_lds<1>(), s, PB);
+    else if (n_max <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<2>, g, b, scale_c_lds<2>(), s, PB);
+    else if (n_max <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<4>, g, b, scale_c_lds<4>(), s, PB);
+    else hipLaunchKernelGGL(k_exact_scale_cb<8>, g, b, scale_c_lds<8>(), s, PB);
+}
+// the bound P.n (a device-counted scan: its upper bound) <= kExactMergeMax
+void launch_exact_scale_c(const KParams& P, hipStream_t s) {
+    if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
+    else if (P.n <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<2>, dim3(1), dim3(kScaleC), scale_c_lds<2>(), s, P);
+    else if (P.n <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<4>, dim3(1), dim3(kScaleC), scale_c_lds<4>(), s, P);
+    else hipLaunchKernelGGL(k_exact_scale_c<8>, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
+}
+
+constexpr int kScaleThreads = 256;                           // k_exact_scale_s: 4 waves, PT = padded size / 256
 template <int PT>
 static hipError_t scale_s_attr() {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_s<kScaleThreads, PT>),
@@ -253,7 +429,8 @@ static hipError_t scale_s_attr() {
 hipError_t exact_scale_m_prepare() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_rank_runs), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        static_cast<int>(kExactMergeMax * sizeof(uint64_t)));
-    for (hipError_t r : {scale_s_attr<1>(), scale_s_attr<2>(), scale_s_attr<4>(), scale_s_attr<8>(), scale_s_attr<16>()})
+    for (hipError_t r : {scale_s_attr<1>(), scale_s_attr<2>(), scale_s_attr<4>(), scale_s_attr<8>(), scale_s_attr<16>(),
+                         scale_s_attr<32>()})
         if (e == hipSuccess) e = r;
     return e;
 }
@@ -267,7 +444,8 @@ void launch_exact_scale_m(const KParams& P, const uint64_t* runs, uint64_t* sort
     else if (need <= 2 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 2>), dim3(1), dim3(T), 2 * lds, s, P, sorted);
     else if (need <= 4 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 4>), dim3(1), dim3(T), 4 * lds, s, P, sorted);
     else if (need <= 8 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 8>), dim3(1), dim3(T), 8 * lds, s, P, sorted);
-    else hipLaunchKernelGGL((k_exact_scale_s<T, 16>), dim3(1), dim3(T), 16 * lds, s, P, sorted);
+    else if (need <= 16 * T) hipLaunchKernelGGL((k_exact_scale_s<T, 16>), dim3(1), dim3(T), 16 * lds, s, P, sorted);
+    else hipLaunchKernelGGL((k_exact_scale_s<T, 32>), dim3(1), dim3(T), 32 * lds, s, P, sorted);
 }
 
 // ---- iteration 0 for scans beyond the one-workgroup sort (kExactMaxPoints < n): k_exact_resid writes every point's

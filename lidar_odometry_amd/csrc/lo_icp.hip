@@ -57,6 +57,8 @@ template <bool SOLVE> __global__ void k_accumulate_b1(const KParams* PB, int it)
 __global__ void k_solve_b1(const KParams* PB, int it);
 __global__ void k_solve_b(const KParams* PB, int it);
 __global__ void k_export_batch(const KParams* PB, lo_batch_rec* out);
+__global__ void k_exact_acc_b(const KParams* PB, int it);
+void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t s);
 struct MapPatchRec;
 __global__ void k_map_patch(Slot* tab, uint32_t log2cap, const MapPatchRec* rec, int n);
 struct FitJob {
@@ -69,6 +71,8 @@ __global__ void k_surfel_fit(const FitJob* jobs, const float* cs, int n, float t
 void launch_exact_scale(const KParams& P, int n, double* sorted, hipStream_t s);
 hipError_t exact_scale_rank_prepare();
 hipError_t exact_scale_m_prepare();
+hipError_t exact_scale_c_prepare();
+void launch_exact_scale_c(const KParams& P, hipStream_t s);
 void launch_exact_scale_m(const KParams& P, const uint64_t* runs, uint64_t* sorted, hipStream_t s);
 void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s);
 void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
@@ -124,13 +128,17 @@ struct lo_ctx {
     float* d_cand_rec = nullptr;    //   and each candidate's solved GN step [NA + 1][kCandWords]
     unsigned* d_cand_cnt = nullptr; //   per-candidate workgroup arrivals (zero between launches)
     bool presolve = true;           //   candidates solve inside the PKO launch (LO_PRESOLVE=0: k_solve_* instead)
-    bool exact = false;             // lo_set_exact: the reference's fp32 arithmetic order (lo_exact.hip)
+    bool exact = true;              // lo_set_exact: the reference's own arithmetic order (lo_exact.hip) -- the default;
+                                    //   lo_set_exact(ctx, 0) opts into the fast mode (fp64 tree sums, not parity-safe)
+    uint64_t cfg_gen = 0;           // bumped by lo_update_config and by (re)allocations of the PKO / candidate buffers: a
+                                    //   batch's cached device KParams of this context are stale once it changes
     float* d_ex_terms = nullptr;
     size_t ex_cap = 0;              //   rows of d_ex_terms
     float* d_ex_tot = nullptr;      //   large scans: the 43 sums (launch_mw_sums -> k_exact_finish)
     double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints), or
                                     //   up to kExactMergeMax points: the correspondence blocks' sorted runs
-    bool ex_merge = false;          //   this scan's exact scale merges the presorted runs (k_exact_scale_m)
+    bool ex_merge = false;          //   this scan's exact scale runs in one launch (k_exact_scale_c: counting sort + sums)
+    bool ex_merge_presort = false;  //   ... or from the correspondence blocks' presorted runs (LO_EXACT_PRESORT, A/B)
     bool ex_attr = false;           //   the exact-scale kernels' dynamic-LDS attributes are set (per context)
     void* d_mw = nullptr;           //   large scans: head records of the 43 column sums (lo_seqsum.h MwBuf)
     size_t mw_n_cap = 0;            //   the scan size d_mw is laid out for
@@ -299,6 +307,7 @@ static int ensure_acc_part(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_cand_rec, cand * kCandWords * sizeof(float)));
     LO_HIP(c, hipMalloc(&c->d_cand_cnt, cand * sizeof(unsigned)));
     LO_HIP(c, hipMemset(c->d_cand_cnt, 0, cand * sizeof(unsigned)));
+    ++c->cfg_gen;
     // the exact candidates' staging sits in the PKO launch's dynamic LDS (beyond the 64 KB default with the static part)
     LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(kXcLdsBytes + 16384)));
@@ -498,30 +507,45 @@ static int kd_alloc(lo_ctx* c) {
 }
 
 // PKO tables (alpha grid, Z(alpha), the shuffle tables, the k-means draws), host-built for the context's config
-static int upload_pko_tables(lo_ctx* c) {
-    const lo_config& g = c->cfg;
-    for (void* p : {static_cast<void*>(c->d_alphas), static_cast<void*>(c->d_Z), static_cast<void*>(c->d_tabs_i)})
-        if (p) LO_HIP(c, hipFree(p));
-    c->d_alphas = nullptr;
-    c->d_Z = nullptr;
-    c->d_tabs_i = nullptr;
-    build_pko_tables(c->tables, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
+// Built for config g into new buffers first; the context's tables and pointers change only once everything succeeded
+// (a failed update leaves the old ones in place).
+static int upload_pko_tables(lo_ctx* c, const lo_config& g) {
+    PkoTables t;
+    build_pko_tables(t, g.gmm_sample_size, g.gmm_components, g.max_points, g.min_scale_factor,
                      g.max_scale_factor, g.num_alpha_segments, g.truncated_threshold, g.pko_kernel);
-    const PkoTables& t = c->tables;
-    LO_HIP(c, hipMalloc(&c->d_alphas, t.alphas.size() * sizeof(double)));
-    LO_HIP(c, hipMalloc(&c->d_Z, t.Z.size() * sizeof(double)));
-    LO_HIP(c, hipMemcpy(c->d_alphas, t.alphas.data(), t.alphas.size() * sizeof(double), hipMemcpyHostToDevice));
-    LO_HIP(c, hipMemcpy(c->d_Z, t.Z.data(), t.Z.size() * sizeof(double), hipMemcpyHostToDevice));
     std::vector<int32_t> all;
-    auto append = [&](const std::vector<int32_t>& v, size_t& off) { off = all.size(); all.insert(all.end(), v.begin(), v.end()); all.push_back(0); };
-    append(t.small_off, c->off_small_off);
-    append(t.small_perm, c->off_small_perm);
-    append(t.base, c->off_base);
-    append(t.ev_off, c->off_ev_off);
-    append(t.ev_steps, c->off_ev_steps);
-    append(t.km_draws, c->off_km);
-    LO_HIP(c, hipMalloc(&c->d_tabs_i, all.size() * sizeof(int32_t)));
-    LO_HIP(c, hipMemcpy(c->d_tabs_i, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    size_t off[6];
+    auto append = [&](const std::vector<int32_t>& v, size_t& o) { o = all.size(); all.insert(all.end(), v.begin(), v.end()); all.push_back(0); };
+    append(t.small_off, off[0]);
+    append(t.small_perm, off[1]);
+    append(t.base, off[2]);
+    append(t.ev_off, off[3]);
+    append(t.ev_steps, off[4]);
+    append(t.km_draws, off[5]);
+    double *a = nullptr, *z = nullptr;
+    int32_t* ti = nullptr;
+    auto fail = [&](hipError_t e, const char* what) {
+        for (void* p : {static_cast<void*>(a), static_cast<void*>(z), static_cast<void*>(ti)}) if (p) (void)hipFree(p);
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+        return LO_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&a, t.alphas.size() * sizeof(double))) != hipSuccess) return fail(e, "hipMalloc alphas");
+    if ((e = hipMalloc(&z, t.Z.size() * sizeof(double))) != hipSuccess) return fail(e, "hipMalloc Z");
+    if ((e = hipMalloc(&ti, all.size() * sizeof(int32_t))) != hipSuccess) return fail(e, "hipMalloc tables");
+    if ((e = hipMemcpy(a, t.alphas.data(), t.alphas.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(z, t.Z.data(), t.Z.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(ti, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e, "hipMemcpy PKO tables");
+    for (void* p : {static_cast<void*>(c->d_alphas), static_cast<void*>(c->d_Z), static_cast<void*>(c->d_tabs_i)})
+        if (p) (void)hipFree(p);
+    c->d_alphas = a;
+    c->d_Z = z;
+    c->d_tabs_i = ti;
+    c->off_small_off = off[0]; c->off_small_perm = off[1]; c->off_base = off[2];
+    c->off_ev_off = off[3]; c->off_ev_steps = off[4]; c->off_km = off[5];
+    c->tables = std::move(t);
+    ++c->cfg_gen;
     return LO_OK;
 }
 
@@ -549,7 +573,7 @@ static int ctx_alloc(lo_ctx* c) {
     c->log2cap = 1;
     LO_HIP(c, hipMalloc(&c->d_tab, c->tab_cap * sizeof(Slot)));
     LO_HIP(c, hipMemset(c->d_tab, 0xff, c->tab_cap * sizeof(Slot)));
-    const int rc_t = upload_pko_tables(c);
+    const int rc_t = upload_pko_tables(c, c->cfg);
     if (rc_t != LO_OK) return rc_t;
     LO_HIP(c, hipEventCreate(&c->ev0));
     LO_HIP(c, hipEventCreate(&c->ev1));
@@ -592,6 +616,7 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
     if (const char* pw = std::getenv("LO_PIPE_WAIT_MS")) c->pipe_bound = 100000ull * std::max(1, std::atoi(pw));
     if (const char* pg = std::getenv("LO_PKO_GROUPS")) c->pko_groups = std::max(0, std::atoi(pg));
+    if (const char* ex = std::getenv("LO_EXACT")) c->exact = std::atoi(ex) != 0;   // A/B runs: LO_EXACT=0 = fast mode
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
         std::fprintf(stderr, "lo_create: %s\n", c->err.c_str());
@@ -1030,11 +1055,12 @@ int lo_update_config(lo_ctx* c, const lo_config* cfg) {
                              cfg->num_alpha_segments != o.num_alpha_segments ||
                              cfg->truncated_threshold != o.truncated_threshold || cfg->pko_kernel != o.pko_kernel;
     const bool na_changed = cfg->num_alpha_segments != o.num_alpha_segments;
-    c->cfg = *cfg;
-    if (pko_changed) {
-        rc = upload_pko_tables(c);
+    if (pko_changed) {                                   // the new tables first: a failure leaves the context unchanged
+        rc = upload_pko_tables(c, *cfg);
         if (rc != LO_OK) return rc;
     }
+    c->cfg = *cfg;
+    ++c->cfg_gen;                                        // batches re-upload this context's parameters
     if (na_changed || (cfg->use_adaptive_m_estimator && !c->d_acc_part)) {
         // the candidate buffers are sized by the alpha grid: re-made on the next optimize
         if (c->d_acc_part) LO_HIP(c, hipFree(c->d_acc_part));
@@ -1221,13 +1247,15 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     if (!c->ex_attr) {
         LO_HIP(c, exact_scale_rank_prepare());
         LO_HIP(c, exact_scale_m_prepare());
+        LO_HIP(c, exact_scale_c_prepare());
         c->ex_attr = true;
     }
     P.ex_terms = c->d_ex_terms;
     P.scale_given = 1;
     // up to kExactMergeMax points the iteration-0 correspondence launch presorts its blocks (P0.presort, set by the
     // caller from ex_merge) and one workgroup merges and sums them
-    c->ex_merge = static_cast<size_t>(P.nb) * kBlock <= static_cast<size_t>(kExactMergeMax);
+    c->ex_merge = n <= static_cast<size_t>(kExactMergeMax);
+    c->ex_merge_presort = c->ex_merge && std::getenv("LO_EXACT_PRESORT") != nullptr;   // A/B: the presorted-runs path
     if (n > static_cast<size_t>(kExactMaxPoints)) {
         if (!c->d_ex_tot) LO_HIP(c, hipMalloc(&c->d_ex_tot, 64 * sizeof(float)));
         if (c->mw_n_cap < n) {                               // the column sums' head records
@@ -1265,6 +1293,10 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
 }
 // the iteration-0 scale of reference-exact mode (between the scan's first correspondence launch and its first PKO)
 static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStream_t s) {
+    if (c->ex_merge && !c->ex_merge_presort) {
+        launch_exact_scale_c(P, s);                          // counting sort + sums in one workgroup
+        return;
+    }
     if (c->ex_merge) {
         // runs in the first half of d_ex_rank, the sorted keys in the second (kExactMaxPoints = 2 kExactMergeMax)
         launch_exact_scale_m(P, reinterpret_cast<const uint64_t*>(c->d_ex_rank),
@@ -1328,7 +1360,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             if (rc3 != LO_OK) return rc3;
             P0.ex_terms = P.ex_terms;
             P0.scale_given = P.scale_given;
-            if (c->ex_merge) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
+            if (c->ex_merge_presort) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
             if (!(fused && P.cand_rec && !c->kd && n2 > 0)) {
                 // reference-exact GN loop without candidates (lo_exact.hip): correspondences, (iteration 0) sorted-order
                 // scale, PKO, per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
@@ -1538,7 +1570,7 @@ retry:
     if (c->exact && (rc = exact_prepare(c, P, n_curr, &n2)) != LO_OK) return rc;
     KParams P0 = P;
     P0.init = 1;
-    if (c->exact && c->ex_merge) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
+    if (c->exact && c->ex_merge_presort) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
     std::memcpy(P0.T0, T_curr, sizeof(float) * 12);
     const dim3 blk(kBlock);
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -2068,11 +2100,12 @@ struct lo_batch {
     std::vector<float> T_in;         // count x 12 (T_out of failed / skipped jobs)
     std::vector<int> act;            // active job -> job index
     std::vector<size_t> n;
-    struct Sig { const float* pts; int n; const Slot* tab; uint32_t log2cap; };
+    struct Sig { const lo_ctx* ctx; uint64_t gen; const float* pts; int n; const Slot* tab; uint32_t log2cap; int exact; };
     std::vector<Sig> sig;            // what d_P currently holds, per active slot
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_go = nullptr;      // reference-exact jobs: the batch's uploads done (their streams wait on it)
     std::vector<hipEvent_t> ev_ex;   //   and each exact job's scan finished (the batch stream waits on them)
+    int nlock = 0;                   // jobs of the last call that ran in lockstep (the first nlock params)
     bool pending = false;
 };
 
@@ -2102,6 +2135,8 @@ static int batch_alloc(lo_batch* b) {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
     LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tb<1, true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
+    LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_acc_b), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   static_cast<int>(kXcLdsBytes)));
     b->T_in.assign(B * 12, 0.0f);
     b->n.assign(B, 0);
     return LO_OK;
@@ -2169,35 +2204,60 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
     const int B = static_cast<int>(b->ctx.size());
     for (int j = 0; j < B; ++j) {
         if (n[j] > static_cast<size_t>(b->ctx[j]->cfg.max_points)) { b->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+        if (b->ctx[j]->cfg.max_iterations != b->max_iters) {   // lo_update_config after lo_batch_create
+            b->err = "a context's max_iterations no longer matches the batch's";
+            return LO_ERR_STATE;
+        }
     }
     LO_BHIP(b, hipSetDevice(b->device));
+    for (int j = 0; j < B; ++j) {                      // PKO / candidate buffers first (their pointers go into the params)
+        if (n[j] == 0) continue;
+        const int rc = ensure_acc_part(b->ctx[j]);
+        if (rc != LO_OK) { b->err = b->ctx[j]->err; return rc; }
+    }
     std::memcpy(b->T_in.data(), T_init, sizeof(float) * 12 * B);
     b->act.clear();
-    int max_nb = 1, max_acc = 1;
+    int max_nb = 1, max_acc = 1, n_max_ex = 1;
     bool same = true;
-    std::vector<int> ex;                                      // reference-exact jobs: their own GN path (below)
+    // job order in the device params: the fast-mode jobs, then the reference-exact ones (both in lockstep), then the
+    // exact jobs too large for the one-workgroup scale (kExactMergeMax): those run their context's own exact GN loop
+    std::vector<int> fast, exl, ex;
     for (int j = 0; j < B; ++j) {
         b->n[j] = n[j];
         if (n[j] == 0) continue;
-        if (b->ctx[j]->exact) { ex.push_back(j); continue; }
         lo_ctx* c = b->ctx[j];
-        const float* pts = (d_pts && d_pts[j]) ? d_pts[j] : c->d_pts;
-        const int a = static_cast<int>(b->act.size());
-        KParams P = make_params(c, pts, static_cast<int>(n[j]));
-        P.T0p = b->d_T0 + 12 * a;
-        max_nb = std::max(max_nb, P.nb);
-        max_acc = std::max(max_acc, P.nb_acc);
-        const lo_batch::Sig sg{pts, P.n, P.tab, P.log2cap};
-        if (a >= static_cast<int>(b->sig.size()) || std::memcmp(&b->sig[a], &sg, sizeof(sg)) != 0) same = false;
-        if (!same) {
-            if (a < static_cast<int>(b->sig.size())) b->sig[a] = sg; else b->sig.push_back(sg);
+        if (!c->exact) fast.push_back(j);
+        else if (n[j] <= static_cast<size_t>(kExactMergeMax)) exl.push_back(j);
+        else ex.push_back(j);
+    }
+    const int nfast = static_cast<int>(fast.size()), nexl = static_cast<int>(exl.size());
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int j : pass ? exl : fast) {
+            lo_ctx* c = b->ctx[j];
+            const float* pts = (d_pts && d_pts[j]) ? d_pts[j] : c->d_pts;
+            const int a = static_cast<int>(b->act.size());
+            KParams P = make_params(c, pts, static_cast<int>(n[j]));
+            P.T0p = b->d_T0 + 12 * a;
+            if (pass) {                                       // the scale comes from k_exact_scale_cb (iteration 0)
+                P.scale_given = 1;
+                n_max_ex = std::max(n_max_ex, P.n);
+            } else {
+                max_acc = std::max(max_acc, P.nb_acc);
+            }
+            max_nb = std::max(max_nb, P.nb);
+            const lo_batch::Sig sg{c, c->cfg_gen, pts, P.n, P.tab, P.log2cap, pass};
+            if (a >= static_cast<int>(b->sig.size()) || std::memcmp(&b->sig[a], &sg, sizeof(sg)) != 0) same = false;
+            if (!same) {
+                if (a < static_cast<int>(b->sig.size())) b->sig[a] = sg; else b->sig.push_back(sg);
+            }
+            b->h_P[a] = P;
+            std::memcpy(b->h_T0 + 12 * a, T_init + 12 * j, sizeof(float) * 12);
+            b->act.push_back(j);
         }
-        b->h_P[a] = P;
-        std::memcpy(b->h_T0 + 12 * a, T_init + 12 * j, sizeof(float) * 12);
-        b->act.push_back(j);
     }
     const int nact = static_cast<int>(b->act.size());
-    // exact jobs after the batched ones: only their DevState pointer is read (k_export_batch)
+    b->nlock = nact;
+    // large exact jobs after the lockstep ones: only their DevState pointer is read (k_export_batch)
     for (int j : ex) {
         b->h_P[b->act.size()] = make_params(b->ctx[j], b->ctx[j]->d_pts, static_cast<int>(n[j]));
         b->act.push_back(j);
@@ -2211,10 +2271,10 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
         if (!same) LO_BHIP(b, hipMemcpyAsync(b->d_P, b->h_P, sizeof(KParams) * ntot, hipMemcpyHostToDevice, b->stream));
     }
     if (!ex.empty()) {
-        // reference-exact jobs run their context's own exact GN loop (the sequential-sum reproductions have no
-        // batched form) on the context stream, ordered after the batch's uploads (lo_batch_optimize copies their
-        // points on the batch stream) and before the batch's record export; the scan pipeline stays off for them,
-        // so every launch is on the context stream and the record is final when it ends
+        // large reference-exact jobs run their context's own exact GN loop (the chip-wide sequential-sum
+        // reproductions) on the context stream, ordered after the batch's uploads (lo_batch_optimize copies their
+        // points on the batch stream) and before its record export; the scan pipeline stays off for them, so every
+        // launch is on the context stream and the record is final when it ends
         LO_BHIP(b, hipEventRecord(b->ev_go, b->stream));
         while (b->ev_ex.size() < ex.size()) {
             hipEvent_t e = nullptr;
@@ -2244,20 +2304,24 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
         const dim3 blk(kBlock);
         for (int it = 0; it < b->max_iters; ++it) {
             hipLaunchKernelGGL(k_correspond_b, dim3(max_nb, nact), blk, 0, b->stream, b->d_P, it == 0 ? 1 : 0, it == 0 ? 1 : 0);
+            if (it == 0 && nexl > 0) launch_exact_scale_cb(b->d_P + nfast, nexl, n_max_ex, b->stream);
             if (nact >= b->one_wave_min)
                 hipLaunchKernelGGL((k_pko_tb<1, true>), dim3(1, nact), dim3(64), pre_bytes, b->stream, b->d_P, it);
             else
                 hipLaunchKernelGGL((k_pko_tb<4, false>), dim3(pko_wgs, nact), dim3(256), pre_bytes, b->stream, b->d_P, it);
+            if (nexl > 0)
+                hipLaunchKernelGGL(k_exact_acc_b, dim3(nexl), dim3(256), kXcLdsBytes, b->stream, b->d_P + nfast, it);
+            if (nfast == 0) continue;
             if (max_acc <= kFuseMaxBlocks) {           // small jobs: one 8-wave workgroup accumulates + solves
-                if (nact < b->split_solve_min) {
-                    hipLaunchKernelGGL(k_accumulate_b1<true>, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
+                if (nfast < b->split_solve_min) {
+                    hipLaunchKernelGGL(k_accumulate_b1<true>, dim3(1, nfast), dim3(512), 0, b->stream, b->d_P, it);
                 } else {
-                    hipLaunchKernelGGL(k_accumulate_b1<false>, dim3(1, nact), dim3(512), 0, b->stream, b->d_P, it);
-                    hipLaunchKernelGGL(k_solve_b1, dim3(nact), dim3(kBlock), 0, b->stream, b->d_P, it);
+                    hipLaunchKernelGGL(k_accumulate_b1<false>, dim3(1, nfast), dim3(512), 0, b->stream, b->d_P, it);
+                    hipLaunchKernelGGL(k_solve_b1, dim3(nfast), dim3(kBlock), 0, b->stream, b->d_P, it);
                 }
             } else {
-                hipLaunchKernelGGL(k_accumulate_b, dim3(max_acc, nact), blk, 0, b->stream, b->d_P, it);
-                hipLaunchKernelGGL(k_solve_b, dim3(nact), dim3(kSolveThreads), 0, b->stream, b->d_P, it);
+                hipLaunchKernelGGL(k_accumulate_b, dim3(max_acc, nfast), blk, 0, b->stream, b->d_P, it);
+                hipLaunchKernelGGL(k_solve_b, dim3(nfast), dim3(kSolveThreads), 0, b->stream, b->d_P, it);
             }
         }
     }
@@ -2297,8 +2361,8 @@ int lo_batch_result(lo_batch* b, lo_batch_rec* out, double* gpu_ms) {
 int lo_batch_bench_correspond(lo_batch* b, int reps, float* avg_ms) {
     if (!b || reps < 1 || !avg_ms) return LO_ERR_ARG;
     if (b->pending) { b->err = "batch in flight: call lo_batch_result first"; return LO_ERR_STATE; }
-    const int nact = static_cast<int>(b->act.size());
-    if (nact == 0) { b->err = "no batch has run yet"; return LO_ERR_STATE; }
+    const int nact = b->nlock;
+    if (nact == 0) { b->err = "no lockstep batch has run yet"; return LO_ERR_STATE; }
     LO_BHIP(b, hipSetDevice(b->device));
     int max_nb = 1;
     for (int a = 0; a < nact; ++a) max_nb = std::max(max_nb, b->h_P[a].nb);

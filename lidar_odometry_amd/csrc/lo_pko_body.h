@@ -682,23 +682,15 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // adds term k of every staged row to its running sum, one rounding per addition, four rows per ds_read_b128, one
 // chunk behind the producers (double-buffered, one barrier per chunk).  The producers' loads run a chunk ahead (slot
 // indices two).  LDS: the dynamic buffer (after the prefix).
-__device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
-    if (c > P.NA) return;
-#ifdef LO_PKO_STAMPS
-    const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
-#endif
+// The 43 sequential sums of build_ne with Huber delta dl at pose T into s_tot (LDS, kExactTerms floats), by one 256-thread
+// workgroup (waves 1-3 produce, wave 0 adds); dyn: kXcLdsBytes of LDS.  Every thread of the workgroup calls it.
+__device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double scale, float dl, float* dyn, float* s_tot) {
     float* s_f = dyn;                                      // [2][43][kXcStride]
     int* s_cnt = reinterpret_cast<int*>(dyn + 2 * kXcBuf); // [2][kXcRegions]
-    float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
-    float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n = scan_n(P);
     const int nch = (n + kXcChunk - 1) / kXcChunk;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
-    const float dl = cand_delta(P, c);
-    __syncthreads();                                       // the prefix's use of the dynamic buffer is over
+    __syncthreads();                                       // earlier uses of the dynamic buffer are over
     // producer state: this lane's point of the current chunk (loaded) and the slot of the next
     int sl_cur = -1, sl_nxt = -1;
     float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -727,7 +719,11 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
             const bool valid = sl_cur >= 0;
             const uint64_t m = __ballot(valid);
             const int cnt = __popcll(m);
+#if defined(LO_XC_EXP) && LO_XC_EXP == 1
+            if (false) {                                   // diagnostic: producers skip the terms (consumer alone)
+#else
             if (valid) {
+#endif
                 float f[14];
                 exact_point_factors(P, T, scale, dl, rv, px, py, pz, sv, f);
                 const int row = r * kWave + __popcll(m & ((1ull << lane) - 1ull));
@@ -747,7 +743,11 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
             sl_cur = sl_nxt;
             sl_nxt = slot_at(ch + 2);
             load_pt(ch + 1, sl_cur);
+#if defined(LO_XC_EXP) && LO_XC_EXP == 2
+        } else if (false) {                                // diagnostic: no adds (producers alone)
+#else
         } else if (wid == 0 && ch > 0) {
+#endif
             const int b = (ch - 1) & 1;
             const float* col = s_f + b * kXcBuf + (lane < kExactTerms ? lane : 0) * kXcStride;
 #pragma unroll
@@ -770,6 +770,20 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     }
     if (wid == 0 && lane < kExactTerms) s_tot[lane] = sum;
     __syncthreads();
+}
+
+__device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
+    if (c > P.NA) return;
+#ifdef LO_PKO_STAMPS
+    const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
+    float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
+    const int tid = threadIdx.x;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+    exact_sums_wg(P, T, scale, cand_delta(P, c), dyn, s_tot);
 #ifdef LO_PKO_STAMPS
     if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memtime() - c_t0);   // the slowest sums
 #endif

@@ -262,52 +262,50 @@ __device__ inline double chain_seq_sum(const double* s_x, int cnt, double s, Seq
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
-// Halfway ties without heads: the two-state form of a segment.
-// Inside binade E the running sum is s = Q u (u = 2^(E-52), Q in [2^52, 2^53)).  A term x with t = x / u adds
-// rint(t) to Q -- unless t is halfway (t = f + 1/2), where round-half-even gives Q + f when Q + f is even and
-// Q + f + 1 otherwise: the step depends on Q's parity and always leaves Q even.  So every step is a map on the
-// parity p = Q & 1 with an integer increment, Q -> Q + d_p, p -> p'_p, and a run of steps composes into one such map
-// (SeqTx) -- associative, so a segment's whole effect is a (segmented) scan, and ties no longer split segments.  The
-// walk then only stops where the running sum crosses a power of two or comes close to one (mono_sum_tx below): a
-// KITTI scan's ~200 tie heads drop to ~25.
+// Halfway ties without heads (mono_sum_tx below).
+// Inside binade E the running sum is s = Q u (u = 2^(E-52), Q in [2^52, 2^53)), and a term x = m 2^(e-52) (m its 53-bit
+// integer mantissa) adds t = x / u = m 2^(e-E): Q gains f = m >> (E-e), plus one when the dropped bits are above half --
+// unless they are exactly half (a tie), where round-half-even gives Q + f when Q + f is even and Q + f + 1 otherwise,
+// and leaves Q even.  So inside a segment (the steps after a head, all in the head's predicted binade) only the FIRST
+// tie depends on the parity Q had when the segment started: every later tie sees Q even after the previous tie, plus
+// the parities of the plain steps since.  A term's increment is thus known from its own bits and the XOR of the
+// increment parities back to the last tie or head (a segmented XOR scan of single bits), except the first tie's +1,
+// which the walk decides from the entry parity (the segment record keeps c1 = that XOR ^ the tie's f parity).  Segment
+// totals are differences of one int64 prefix sum; everything per term is integer arithmetic on the mantissa bits.
 // ---------------------------------------------------------------------------------------------------------------------
-struct SeqTx {
-    long long d0, d1;        // Q increment for entry parity 0 / 1
-    int p;                   // bit q: the exit parity for entry parity q
+struct TermBits {
+    long long f;             // floor(x / u); 2^62 when x / u >= 2^53 (never a segment step: the head rule)
+    int tie, up;             // the dropped bits are exactly half / above half
 };
-constexpr long long kTxSat = 1ll << 61;        // saturated increment (never exact: fails every check)
-__device__ __forceinline__ SeqTx tx_ident() { return SeqTx{0, 0, 2}; }
-__device__ __forceinline__ SeqTx tx_then(const SeqTx& a, const SeqTx& b) {   // a, then b
-    const int a0 = a.p & 1, a1 = (a.p >> 1) & 1;
-    const long long e0 = a.d0 + (a0 ? b.d1 : b.d0);
-    const long long e1 = a.d1 + (a1 ? b.d1 : b.d0);
-    return SeqTx{e0 < kTxSat ? e0 : kTxSat, e1 < kTxSat ? e1 : kTxSat, ((b.p >> a0) & 1) | (((b.p >> a1) & 1) << 1)};
+__device__ __forceinline__ TermBits term_bits(double x, int E) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const int ef = static_cast<int>((b >> 52) & 0x7FF);
+    const uint64_t m = (b & ((1ull << 52) - 1)) | (ef ? (1ull << 52) : 0ull);
+    const int k = E - (ef ? ef - 1023 : -1022);             // x = m 2^(e-52): t = m 2^-k
+    TermBits r{0, 0, 0};
+    if (k <= 0) {
+        r.f = k == 0 ? static_cast<long long>(m) : (1ll << 62);
+    } else if (k < 54) {
+        r.f = static_cast<long long>(m >> k);
+        const uint64_t rem = m & ((1ull << k) - 1), half = 1ull << (k - 1);
+        r.tie = rem == half ? 1 : 0;
+        r.up = rem > half ? 1 : 0;
+    }                                                         // k >= 54: t < 1/2 (m < 2^53 <= the half bit)
+    return r;
 }
-// One term's step on binade E appended to m (x >= +0, t = x / u < 2^53: the caller's head rule guarantees it):
-// t = f + r exactly; a halfway r rounds Q + f to even, otherwise Q gains rint(t).
-__device__ __forceinline__ void tx_push(SeqTx& m, double x, int E) {
-    const double t = ldexp(x, 52 - E);
-    const double f = floor(t), fr = t - f;
-    const long long fi = static_cast<long long>(f);
-    const int fb = static_cast<int>(fi & 1), p0 = m.p & 1, p1 = (m.p >> 1) & 1;
-    if (fr == 0.5) {
-        m.d0 += fi + (p0 ^ fb);
-        m.d1 += fi + (p1 ^ fb);
-        m.p = 0;
-    } else {
-        const long long q = fi + (fr > 0.5 ? 1 : 0);
-        const int b = static_cast<int>(q & 1);
-        m.d0 += q;
-        m.d1 += q;
-        m.p = (p0 ^ b) | ((p1 ^ b) << 1);
-    }
+// The segmented XOR-scan state, four bits: 1 a reset (tie or head) inside, 2 the XOR of plain-step parities since the
+// last reset (or since the start), 4 a head inside, 8 a tie since the last head (or since the start).
+__device__ __forceinline__ int xs_op(int a, int b) {       // a, then b
+    const int x = (b & 1) ? (b & 2) : ((a ^ b) & 2);
+    const int t = (b & 4) ? (b & 8) : ((a | b) & 8);
+    return ((a | b) & 5) | x | t;
 }
 
 // Wave-wide inclusive scan of a POD of 32-bit words by DPP (row_shr 1/2/4/8, then row_bcast 15/31 into the upper
 // rows): the earlier lane's value is combined in front, op(earlier, later).  Lanes without a source keep `ident`.
 template <int N> struct Words { int w[N]; };
 template <int CTRL, int RM, typename T>
-__device__ __forceinline__ T dpp_pod(const T& v, const T& old) {
+__device__ __forceinline__ T dpp_pod(T v, T old) {
     static_assert(sizeof(T) % 4 == 0, "32-bit words");
     constexpr int N = sizeof(T) / 4;
     const Words<N> a = __builtin_bit_cast(Words<N>, v), o = __builtin_bit_cast(Words<N>, old);
@@ -317,7 +315,7 @@ __device__ __forceinline__ T dpp_pod(const T& v, const T& old) {
     return __builtin_bit_cast(T, r);
 }
 template <typename T, typename Op>
-__device__ __forceinline__ T wave_incl_scan(T v, const T& ident, Op op) {
+__device__ __forceinline__ T wave_incl_scan(T v, T ident, Op op) {
     v = op(dpp_pod<0x111, 0xf>(v, ident), v);       // row_shr:1
     v = op(dpp_pod<0x112, 0xf>(v, ident), v);       // row_shr:2
     v = op(dpp_pod<0x114, 0xf>(v, ident), v);       // row_shr:4
@@ -327,7 +325,7 @@ __device__ __forceinline__ T wave_incl_scan(T v, const T& ident, Op op) {
     return v;
 }
 template <typename T>
-__device__ __forceinline__ T readlane_pod(const T& v, int l) {
+__device__ __forceinline__ T readlane_pod(T v, int l) {
     constexpr int N = sizeof(T) / 4;
     Words<N> a = __builtin_bit_cast(Words<N>, v);
 #pragma unroll
@@ -335,59 +333,67 @@ __device__ __forceinline__ T readlane_pod(const T& v, int l) {
     return __builtin_bit_cast(T, a);
 }
 template <typename T>
-__device__ __forceinline__ T shfl_up1_pod(const T& v, const T& ident) {
+__device__ __forceinline__ T shfl_up1_pod(T v, T ident) {
     constexpr int N = sizeof(T) / 4;
-    const Words<N> a = __builtin_bit_cast(Words<N>, v);
+    const Words<N> a = __builtin_bit_cast(Words<N>, v), o = __builtin_bit_cast(Words<N>, ident);
+    const bool first = (threadIdx.x & 63) == 0;
     Words<N> r;
 #pragma unroll
-    for (int i = 0; i < N; ++i) r.w[i] = __shfl_up(a.w[i], 1, 64);
-    return (threadIdx.x & 63) == 0 ? ident : __builtin_bit_cast(T, r);
+    for (int i = 0; i < N; ++i) {
+        const int t = __shfl_up(a.w[i], 1, 64);
+        r.w[i] = first ? o.w[i] : t;
+    }
+    return __builtin_bit_cast(T, r);
 }
 // Exclusive scan over a workgroup of NT threads (NT / 64 <= 16 waves): DPP wave scans; the wave totals meet in
-// s_w (NT / 64 entries), every wave scans them in its first row and takes its own prefix.  Barriers inside.
+// s_w (NT / 64 entries), every wave scans them in its first row and takes its own prefix.  Two barriers.
 template <int NT, typename T, typename Op>
-__device__ __forceinline__ T block_excl_scan_dpp(const T& v, const T& ident, Op op, T* s_w, T* total = nullptr) {
+__device__ __forceinline__ T block_excl_scan_dpp(T v, T ident, Op op, T* s_w, T* total = nullptr) {
     constexpr int NW = NT / kWave;
     static_assert(NW >= 1 && NW <= 16, "waves");
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const T inc = wave_incl_scan(v, ident, op);
+    const T ex = shfl_up1_pod(inc, ident);
+    if constexpr (NW == 1) {
+        if (total) *total = readlane_pod(inc, 63);
+        return ex;
+    }
     if (lane == 63) s_w[wid] = inc;
     __syncthreads();
     T w = lane < NW ? s_w[lane] : ident;
-    w = op(dpp_pod<0x111, 0xf>(w, ident), w);
-    w = op(dpp_pod<0x112, 0xf>(w, ident), w);
-    w = op(dpp_pod<0x114, 0xf>(w, ident), w);
-    w = op(dpp_pod<0x118, 0xf>(w, ident), w);
+#pragma unroll
+    for (int sh = 1; sh < NW; sh <<= 1) {
+        if (sh == 1) w = op(dpp_pod<0x111, 0xf>(w, ident), w);
+        if (sh == 2) w = op(dpp_pod<0x112, 0xf>(w, ident), w);
+        if (sh == 4) w = op(dpp_pod<0x114, 0xf>(w, ident), w);
+        if (sh == 8) w = op(dpp_pod<0x118, 0xf>(w, ident), w);
+    }
     if (total) *total = readlane_pod(w, NW - 1);
     const T wex = wid ? readlane_pod(w, wid - 1) : ident;
     __syncthreads();                                // s_w free again
-    return op(wex, shfl_up1_pod(inc, ident));
+    return wid ? op(wex, ex) : ex;
 }
 
-struct SegAgg {                                    // segmented-scan element: a thread's terms as one map
-    long long d0, d1;
-    int pf;                                        // p | (a segment starts inside) << 2
-    int nh;                                        // heads inside
-};
-__device__ __forceinline__ SegAgg seg_ident() { return SegAgg{0, 0, 2, 0}; }
-__device__ __forceinline__ SegAgg seg_op(const SegAgg& a, const SegAgg& b) {
-    if (b.pf & 4) return SegAgg{b.d0, b.d1, b.pf, a.nh + b.nh};
-    const SeqTx t = tx_then(SeqTx{a.d0, a.d1, a.pf & 3}, SeqTx{b.d0, b.d1, b.pf & 3});
-    return SegAgg{t.d0, t.d1, t.p | (a.pf & 4), a.nh + b.nh};
-}
-
-constexpr int kTxHeadCap = 512;                    // heads per sum (more: the plain chain)
+constexpr int kTxHeadCap = 256;                    // heads per sum (more: the plain chain)
+constexpr int kTxAny = 100000;                     // walk record: a head without a segment (every check passes)
 constexpr int kExactMergeMax = 8192;               // exact scale from presorted runs (k_rank_runs + k_exact_scale_s)
 template <int NT>
 struct MonoScratch {
     double wd[NT / kWave];
-    SegAgg wa[NT / kWave];
-    int elast[NT];                                 // predicted binade of each thread's last term
-    int hedge[NT];                                 // bit 0: the thread's first term heads, bit 1: its last term heads
+    long long wl[NT / kWave];
+    int wi[NT / kWave];
+    int welast[NT / kWave];                        // predicted binade of each wave's last term
     int h_idx[kTxHeadCap];
     int h_e[kTxHeadCap];
-    long long h_d0[kTxHeadCap];                    // the head's segment as a two-state map
-    long long h_d1[kTxHeadCap];
+    long long h_p[kTxHeadCap];                     // the int64 prefix of the increments at the head
+    int h_c1[kTxHeadCap];                          // bit 1: the segment has a tie, bit 0: c1 of its first tie
+    double w_hx[kTxHeadCap];                       // the walk's records: the head's term, u d_0, u d_1,
+    double w_q0[kTxHeadCap];
+    double w_q1[kTxHeadCap];
+    long long w_d0[kTxHeadCap];                    //   d_0, d_1, the check's binade (kTxAny: no segment), the segment's end
+    long long w_d1[kTxHeadCap];
+    int w_e[kTxHeadCap];
+    int w_end[kTxHeadCap];
     double result;
     int nheads, fb_seg, fb_terms;
 };
@@ -438,80 +444,148 @@ __device__ __forceinline__ void walk_row(double& s, double& rec, double hx, doub
 // +0 + x_0 + x_1 + ... + x_{cnt-1} in index order, one fp64 rounding per addition, for x_j >= +0 (no NaN).
 // One workgroup of NT threads; thread t holds terms t*PT .. t*PT + PT - 1 in x (zero past cnt) and the same terms sit in
 // s_x (LDS: the walk's head terms, term-by-term fallbacks).  Heads: the first non-zero term, every non-zero term whose
-// predicted binade differs from its predecessor's, lies within 2^-30 of a binade end, or is too large for the integer
-// model; every other term is a step of its head's segment map.  The walk (wave 0) does a head's step directly, then its
-// segment as s + u d_p when s lies in the predicted binade and the result stays below 2^(E+1); else the segment term by
-// term.  False when the heads exceed kTxHeadCap (the caller sums the chain).  stamps (nullable, diagnostic builds):
-// thread 0 stores s_memtime after the head count, the segmented scan and the records.
+// predicted binade differs from its predecessor's, lies within 2^-30 of a binade end, or steps by 2^49 units or more;
+// every other term is an integer step of its head's segment.  Three block scans (the fp64 prediction, the 4-bit XOR
+// state, the int64 increments), then the walk (wave 0): a head's step done directly, its segment as s + u d_p (p = Q's
+// parity at the segment's start, d_p = the segment's increments with the first tie's +1 for that parity) when s lies in
+// the predicted binade and the result stays below 2^(E+1); else the segment term by term.  False when the heads exceed
+// kTxHeadCap (the caller sums the chain).  stamps (nullable, diagnostic builds): thread 0 stores s_memtime after the
+// heads, the scans and the records.
 template <int NT, int PT>
 __device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, const double* s_x, MonoScratch<NT>& S,
                                             double& out, unsigned long long* stamps = nullptr) {
+    constexpr int NW = NT / kWave;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, base = tid * PT;
-    // 1. approximate prefix (fp64, tree order): the prediction of each step's binade
+    // 1. approximate prefix (fp64): the prediction of each step's binade
     double run = 0.0;
 #pragma unroll
     for (int a = 0; a < PT; ++a) run += x[a];
     const double tex = block_excl_scan_dpp<NT>(run, 0.0, [](double a, double b) { return a + b; }, S.wd);
-    S.elast[tid] = binade64(tex + run);
-    __syncthreads();
-    // 2. predicted binades and heads (a term's predecessor's binade as its owner computed it)
+    // 2. predicted binades, integer steps and heads; a term's predecessor's binade as its owner computed it (lane
+    //    l - 1's last term; lane 0: the previous wave's, through LDS)
     int E[PT];
+    TermBits tb[PT];
     bool hd[PT];
     int nh = 0;
+    double tl = 0.0;
+#pragma unroll
+    for (int a = 0; a < PT; ++a) {
+        tl += x[a];
+        E[a] = binade64(tex + tl);
+    }
+    const int e_up = __shfl_up(E[PT - 1], 1, 64);
+    if (lane == 63) S.welast[wid] = E[PT - 1];
+    __syncthreads();
     {
-        double tl = 0.0;
-        int ep = tid ? S.elast[tid - 1] : kExpNone;
+        int ep = lane ? e_up : (wid ? S.welast[wid - 1] : kExpNone);
+        tl = 0.0;
 #pragma unroll
         for (int a = 0; a < PT; ++a) {
             tl += x[a];
-            const double T = tex + tl;
-            E[a] = binade64(T);
             const bool act = base + a < cnt && x[a] != 0.0;
-            bool h = act && (E[a] == kExpNone || E[a] != ep || near_edge(T));
-            if (act && !h) h = !(ldexp(x[a], 52 - E[a]) < 0x1p53);
+            tb[a] = term_bits(x[a], E[a] == kExpNone ? 0 : E[a]);
+            const bool h = act && (E[a] == kExpNone || E[a] != ep || near_edge(tex + tl) || tb[a].f >= (1ll << 49));
             hd[a] = h;
             nh += h ? 1 : 0;
             ep = E[a];
         }
     }
-    S.hedge[tid] = (hd[0] ? 1 : 0) | (hd[PT - 1] ? 2 : 0);
-    __syncthreads();
-    const bool prev_head = tid ? (S.hedge[tid - 1] & 2) != 0 : false;
-    const bool next_head = tid + 1 < NT ? (S.hedge[tid + 1] & 1) != 0 : false;
-    if (stamps && tid == 0) stamps[0] = __builtin_amdgcn_s_memtime();
-    // 3. the thread's terms as one segmented map (a head's own step is the walk's: identity here), with its head count
-    SegAgg agg{0, 0, 2, nh};
+    // 3. the segmented XOR state over the thread's terms (bits 0-3, xs_op) with the thread's head count above them
+    auto bits_of = [&](int a) -> int {                      // a term's own 4-bit state
+        if (hd[a]) return 1 | 4;
+        if (!(base + a < cnt && x[a] != 0.0)) return 0;
+        if (tb[a].tie) return 1 | 8;
+        return static_cast<int>((tb[a].f + tb[a].up) & 1) << 1;
+    };
+    int xs = 0;
 #pragma unroll
-    for (int a = 0; a < PT; ++a) {
-        if (hd[a] || (a ? hd[a - 1] : prev_head)) { agg.d0 = 0; agg.d1 = 0; agg.pf = 2 | 4; }   // a segment starts
-        if (base + a < cnt && x[a] != 0.0 && !hd[a]) {
-            SeqTx m{agg.d0, agg.d1, agg.pf & 3};
-            tx_push(m, x[a], E[a]);
-            agg.d0 = m.d0; agg.d1 = m.d1; agg.pf = m.p | (agg.pf & 4);
+    for (int a = 0; a < PT; ++a) xs = xs_op(xs, bits_of(a));
+    int xtot = 0;
+    const int xex = block_excl_scan_dpp<NT>(xs | (nh << 4), 0,
+                                            [](int a, int b) { return xs_op(a & 15, b & 15) | (((a >> 4) + (b >> 4)) << 4); },
+                                            S.wi, &xtot);
+    const int hbase = xex >> 4, htot = xtot >> 4;
+    if (stamps && tid == 0) stamps[0] = __builtin_amdgcn_s_memtime();
+    // 4. each term's increment (a tie after another tie of its segment: f + (XOR ^ f's parity); the first tie: f, the
+    //    +1 left to the walk), the thread's total, the int64 prefix
+    long long inc_tot = 0;
+    {
+        int st = xex & 15;
+#pragma unroll
+        for (int a = 0; a < PT; ++a) {
+            const bool act = base + a < cnt && x[a] != 0.0 && !hd[a];
+            long long inc = 0;
+            if (act) {
+                if (tb[a].tie) inc = tb[a].f + ((st & 8) ? (((st >> 1) ^ static_cast<int>(tb[a].f)) & 1) : 0);
+                else inc = tb[a].f + tb[a].up;
+            }
+            inc_tot += inc;
+            st = xs_op(st, bits_of(a));
         }
     }
-    SegAgg tot;
-    const SegAgg ex = block_excl_scan_dpp<NT>(agg, seg_ident(), seg_op, S.wa, &tot);
-    const int htot = tot.nh;
-    if (stamps && tid == 0) stamps[1] = __builtin_amdgcn_s_memtime();
     if (htot > kTxHeadCap) return false;                       // uniform
-    // 4. head records and each segment's map (written by the thread holding the segment's last term)
+    for (int k = tid; k < htot; k += NT) S.h_c1[k] = 0;       // ordered before step 5 by the scan's barriers
+    long long ptot = 0;
+    const long long pex = block_excl_scan_dpp<NT>(inc_tot, 0ll, [](long long a, long long b) { return a + b; }, S.wl, &ptot);
+    if (stamps && tid == 0) stamps[1] = __builtin_amdgcn_s_memtime();
+    // 5. head records (index, binade, the prefix at the head) and each segment's first tie (c1)
     {
-        SeqTx cur{ex.d0, ex.d1, ex.pf & 3};
-        int hk = ex.nh;
+        int st = xex & 15;
+        long long P = pex;
+        int hk = hbase;
 #pragma unroll
         for (int a = 0; a < PT; ++a) {
             const int j = base + a;
-            if (hd[a] || (a ? hd[a - 1] : prev_head)) cur = tx_ident();
-            if (j < cnt && x[a] != 0.0 && !hd[a]) tx_push(cur, x[a], E[a]);
-            if (hd[a]) { S.h_idx[hk] = j; S.h_e[hk] = E[a]; ++hk; }
-            const bool last = j == cnt - 1 || (j < cnt && (a + 1 < PT ? hd[a + 1] : next_head));
-            if (last && hk > 0) { S.h_d0[hk - 1] = cur.d0; S.h_d1[hk - 1] = cur.d1; }
+            const bool act = j < cnt && x[a] != 0.0 && !hd[a];
+            if (hd[a]) { S.h_idx[hk] = j; S.h_e[hk] = E[a]; S.h_p[hk] = P; ++hk; }
+            long long inc = 0;
+            if (act) {
+                if (tb[a].tie) {
+                    if (st & 8) inc = tb[a].f + (((st >> 1) ^ static_cast<int>(tb[a].f)) & 1);
+                    else {
+                        inc = tb[a].f;
+                        if (hk > 0) S.h_c1[hk - 1] = 2 | (((st >> 1) ^ static_cast<int>(tb[a].f)) & 1);
+                    }
+                } else {
+                    inc = tb[a].f + tb[a].up;
+                }
+            }
+            P += inc;
+            st = xs_op(st, bits_of(a));
         }
     }
     __syncthreads();
+    // 6. every head's walk record, in parallel: its term, its segment's increments for either entry parity as fp64
+    //    multiples of u (exact below 2^53), the check's binade and increments (E = kExpNone: never passes; a head
+    //    without a segment: always passes)
+    for (int k = tid; k < htot; k += NT) {
+        const int hi = S.h_idx[k], hend = k + 1 < htot ? S.h_idx[k + 1] : cnt, E0 = S.h_e[k];
+        double q0 = -0.0, q1 = -0.0;                           // x + -0 == x for every x
+        int e = kTxAny;
+        long long d0 = 0, d1 = 0;
+        if (hend > hi + 1) {
+            const long long D = (k + 1 < htot ? S.h_p[k + 1] : ptot) - S.h_p[k];
+            const int c = S.h_c1[k];
+            d0 = D + ((c & 2) ? (c & 1) : 0);
+            d1 = D + ((c & 2) ? ((c & 1) ^ 1) : 0);
+            e = (E0 == kExpNone || D < 0 || d0 >= (1ll << 53) || d1 >= (1ll << 53)) ? kExpNone : E0;
+            if (e != kExpNone) {
+                const double u = ldexp(1.0, E0 - 52);
+                q0 = static_cast<double>(d0) * u;
+                q1 = static_cast<double>(d1) * u;
+            }
+        }
+        S.w_hx[k] = s_x[hi];
+        S.w_q0[k] = q0;
+        S.w_q1[k] = q1;
+        S.w_e[k] = e;
+        S.w_end[k] = hend;
+        S.w_d0[k] = d0;
+        S.w_d1[k] = d1;
+    }
+    __syncthreads();
     if (stamps && tid == 0) stamps[2] = __builtin_amdgcn_s_memtime();
-    // 5. the walk (wave 0, wave-uniform): windows of 16 heads, every 16-lane row holding the window; a head costs a
+    // 7. the walk (wave 0, wave-uniform): windows of 16 heads, every 16-lane row holding the window; a head costs a
     //    dependent fma, a parity select and a second fma (row_newbcast operands); the checks run lane-parallel after the
     //    window, and from a failed check on it goes head by head (the failed head's segment term by term)
     if (wid == 0) {
@@ -521,31 +595,14 @@ __device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, cons
         int fbs = 0, fbt = 0;
         for (int k0 = 0; k0 < htot; k0 += 16) {
             const int kk = k0 + n16;
-            int hi = 0, hend = 0, E0 = kExpNone;
-            long long d0 = 0, d1 = 0;
-            double hx = -0.0, q0 = -0.0, q1 = -0.0;              // past the window: a no-op head (x + -0 == x)
-            bool seg = false, bad = false;
-            if (kk < htot) {
-                hi = S.h_idx[kk];
-                hend = kk + 1 < htot ? S.h_idx[kk + 1] : cnt;
-                E0 = S.h_e[kk];
-                hx = s_x[hi];
-                seg = hend > hi + 1;
-                if (seg) {
-                    d0 = S.h_d0[kk];
-                    d1 = S.h_d1[kk];
-                    bad = E0 == kExpNone || d0 >= (1ll << 53) || d1 >= (1ll << 53);
-                    if (!bad) {
-                        const double u = ldexp(1.0, E0 - 52);
-                        q0 = static_cast<double>(d0) * u;
-                        q1 = static_cast<double>(d1) * u;
-                    }
-                }
-            }
+            const bool in = kk < htot;
+            const double hx = in ? S.w_hx[kk] : -0.0, q0 = in ? S.w_q0[kk] : -0.0, q1 = in ? S.w_q1[kk] : -0.0;
+            const int e = in ? S.w_e[kk] : kTxAny;
+            const long long d0 = in ? S.w_d0[kk] : 0, d1 = in ? S.w_d1[kk] : 0;
             // the check on the sum right after head kk's own step: s in [2^E, 2^(E+1)) and Q + d_parity <= 2^53 - 1
             auto check = [&](double sv) -> bool {
-                if (!seg) return true;
-                if (bad || binade64(sv) != E0) return false;
+                if (e == kTxAny) return true;
+                if (binade64(sv) != e) return false;               // also kExpNone (never a valid binade)
                 const long long Q = static_cast<long long>((__builtin_bit_cast(uint64_t, sv) & ((1ull << 52) - 1)) | (1ull << 52));
                 return Q + ((Q & 1) ? d1 : d0) <= (1ll << 53) - 1;
             };
@@ -562,7 +619,7 @@ __device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, cons
                     if (ok) {
                         s = s + ((__double2loint(s) & 1) ? rl64d(q1, l) : rl64d(q0, l));
                     } else {
-                        const int h = __builtin_amdgcn_readlane(hi, l), end = __builtin_amdgcn_readlane(hend, l);
+                        const int h = S.h_idx[k0 + l], end = S.w_end[k0 + l];
                         for (int j = h + 1; j < end; ++j) s = s + s_x[j];
                         fbs += end > h + 1 ? 1 : 0;
                         fbt += end - h - 1;
@@ -578,18 +635,35 @@ __device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, cons
 }
 
 // Sorting support for the exact scale (k_rank_runs): the number of keys of a sorted 256-key run below x (STRICT) or
-// not above x -- nine probes, no branch.
-template <bool STRICT>
-__device__ __forceinline__ int run_count(const uint64_t* R, uint64_t x) {
-    int p = 0;
+// not above x, for every run at once (the runs' nine-probe binary searches interleaved: NR loads in flight per probe).
+template <int NR>
+__device__ __forceinline__ int runs_rank(const uint64_t* s_r, int nb, int b, uint64_t x) {
+    int p[NR];
+    bool use[NR], le[NR];
 #pragma unroll
-    for (int s = 128; s >= 1; s >>= 1) {
-        const uint64_t v = R[p + s - 1];
-        p += (STRICT ? v < x : v <= x) ? s : 0;
+    for (int r = 0; r < NR; ++r) {
+        p[r] = (r < nb ? r : 0) * 256;                     // a row past nb reads row 0 and is not counted
+        use[r] = r < nb && r != b;
+        le[r] = r < b;                                     // earlier runs: keys not above x; later runs: below x
     }
-    const uint64_t v = R[p];
-    return p + ((STRICT ? v < x : v <= x) ? 1 : 0);
+#pragma unroll
+    for (int st = 128; st >= 1; st >>= 1) {
+        uint64_t v[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) v[r] = s_r[p[r] + st - 1];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) p[r] += (le[r] ? v[r] <= x : v[r] < x) ? st : 0;
+    }
+    int rank = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const uint64_t v = s_r[p[r]];
+        const int c = (p[r] & 255) + ((le[r] ? v <= x : v < x) ? 1 : 0);
+        rank += use[r] ? c : 0;
+    }
+    return rank;
 }
+
 
 }  // namespace lo
 

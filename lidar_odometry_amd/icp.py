@@ -137,7 +137,9 @@ class IterativeClosestPointOptimizer:
         return int(self._L.lo_map_surfel_count(self.ctx))
 
     def set_exact(self, enable: bool = True):
-        """Reference-exact arithmetic order (sequential fp32 sums, sorted-order scale, fp32 LDLT / SVD SO3); default off."""
+        """Arithmetic mode (lo_set_exact): True = reference-exact (sequential fp32 sums, sorted-order scale, fp32 LDLT /
+        SVD SO3; bit-identical to the reference restatement) -- the DEFAULT of every context; False = the opt-in fast mode
+        (fp64 tree sums; within 1e-7 per step but not parity-safe where a PKO alpha nearly ties)."""
         rc = self._L.lo_set_exact(self.ctx, int(bool(enable)))
         if rc != 0:
             raise RuntimeError(f"lo_set_exact failed ({rc})")
@@ -195,12 +197,14 @@ class IterativeClosestPointOptimizer:
                                               len(k), C.byref(patched)))
         return int(patched.value)
 
-    def update_config(self, config: ICPConfig):
+    def update_config(self, config: ICPConfig, adaptive: AdaptiveMEstimatorConfig | None = None):
         """IterativeClosestPointOptimizer::update_config (IterativeClosestPointOptimizer.h:220): new parameters, same
-        context -- the device map stays (lo_update_config)."""
-        cfg = make_config(config, self.adaptive, self.geometry, self._cfg.max_points)
+        context -- the device map stays (lo_update_config).  adaptive: new PKO parameters too (the estimator's config)."""
+        ad = adaptive or self.adaptive
+        cfg = make_config(config, ad, self.geometry, self._cfg.max_points)
         self._check(self._L.lo_update_config(self.ctx, C.byref(cfg)))
         self.config = config
+        self.adaptive = ad
         self._cfg = cfg
 
     def get_config(self) -> ICPConfig:

@@ -29,7 +29,7 @@ class LidarOdometry:
     def __init__(self, device: int = 0, max_points: int = 1 << 17, use_surfel_correspondence: bool = True,
                  point_stride: int = 8, voxel_size: float = 0.5, map_voxel_size: float = 0.5, max_range: float = 100.0,
                  keyframe_distance: float = 1.0, keyframe_rotation: float = 0.3, initial_pose=None,
-                 exact: bool = False):
+                 exact: bool = True):
         cfg = LoOdomConfig()
         lib().lo_odom_config_default_kitti(C.byref(cfg))
         cfg.icp.max_points = int(max_points)
@@ -48,8 +48,8 @@ class LidarOdometry:
         if initial_pose is not None:
             T = np.ascontiguousarray(np.asarray(initial_pose, np.float32)[:3, :4].reshape(12))
             lib().lo_odom_set_initial_pose(self._o, T.ctypes.data_as(C.POINTER(C.c_float)))
-        if exact:                                  # the reference's fp32 ICP arithmetic order (lo_set_exact)
-            lib().lo_odom_set_exact(self._o, 1)
+        # the ICP arithmetic mode: reference-exact (the library default, lo_set_exact) or the opt-in fast mode
+        lib().lo_odom_set_exact(self._o, 1 if exact else 0)
 
     def close(self):
         h = getattr(self, "_o", None)

@@ -35,6 +35,19 @@ def scan_of(step: int, rank: int, world: int) -> int:
     return step * world + rank
 
 
+def all_ranks_agree(flag: bool, world: int, device=None) -> bool:
+    """True only if `flag` holds on every rank: one all-reduce (MIN) of a 0/1 int.  bench.py's --mode auto takes the
+    fast arithmetic only when every rank's own parity check passed, so all ranks time the same mode (the per-rank
+    parity verdicts stay in the line).  world == 1 needs no process group."""
+    if world == 1:
+        return bool(flag)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
 class PoseAllGather:
     """All-gather of one RECORD_FLOATS record per rank into a preallocated [world * 16] tensor.
 

@@ -17,9 +17,12 @@ TOL_T = 1e-4
 TOL_R = 1e-4
 
 
-def _ctx(m, voxel=0.5, max_points=1 << 16):
+def _ctx(m, voxel=0.5, max_points=1 << 16, exact=False):
+    """A context for a batch job; the fast mode unless exact (the lockstep kernels' own tests -- the library default is
+    reference-exact, whose batch form test_batch_exact_* covers)."""
     from lidar_odometry_amd import IterativeClosestPointOptimizer, MapGeometry
     o = IterativeClosestPointOptimizer(geometry=MapGeometry(voxel_size=voxel), max_points=max_points)
+    o.set_exact(exact)
     if m is not None:
         k, n, c = _data.surfels(m)
         o.set_surfels(k, n, c)
@@ -106,12 +109,17 @@ def test_batch_heterogeneous_bitwise_vs_single(pko_mode):
             o.close()
 
 
-def test_batch_exact_jobs_bitwise_vs_single():
+def test_batch_exact_jobs_bitwise_vs_single(pko_mode):
     """Reference-exact contexts in a batch (every other job): each exact job equals its context's own exact
-    lo_icp_optimize bit for bit (and so the oracle, tests/test_gpu_exact.py), each default job its default single run,
-    also when the batch runs twice."""
+    lo_icp_optimize bit for bit (and so the oracle, tests/test_gpu_exact.py), each fast-mode job its fast single run,
+    also when the batch runs twice.  The exact jobs of at most kExactMergeMax (8192) points run in lockstep
+    (k_exact_scale_cb + k_exact_acc_b); the appended 11k-point exact job runs its context's own exact GN loop."""
     from lidar_odometry_amd import BatchOptimizer
     jobs = _jobs()
+    m, pts, Ti, _ = _data.kitti_case(11)
+    big = np.concatenate([pts, pts + np.float32(0.01), pts - np.float32(0.01)])
+    assert len(big) > 8192
+    jobs.append((m, 0.5, big, Ti))
     ctxs = [_ctx(m, v) for (m, v, _, _) in jobs]
     try:
         for k, o in enumerate(ctxs):
@@ -129,13 +137,42 @@ def test_batch_exact_jobs_bitwise_vs_single():
             o.close()
 
 
-def test_batch_many_jobs_and_repointed_scans(pko_mode):
-    """64 jobs (fewer PKO workgroups per job than a single scan gets), then every job re-pointed at another scan."""
+def test_batch_follows_update_config():
+    """lo_update_config on a context that belongs to a batch (IterativeClosestPointOptimizer::update_config): the next
+    batch uses the new parameters -- a new alpha grid (the PKO tables and candidate buffers are re-made) and a new
+    correspondence gate -- and stays bit-identical to the contexts' single optimize; a changed max_iterations (fixed at
+    lo_batch_create) is refused."""
+    from lidar_odometry_amd import BatchOptimizer
+    from lidar_odometry_amd.icp import AdaptiveMEstimatorConfig, ICPConfig
+    jobs = _jobs()[:4]
+    ctxs = [_ctx(m, v) for (m, v, _, _) in jobs]
+    try:
+        b = BatchOptimizer(ctxs)
+        try:
+            pts, Ts = [j[2] for j in jobs], [j[3] for j in jobs]
+            _check_equal(b.optimize(None, pts, Ts), _singles(ctxs, jobs))
+            ctxs[1].update_config(ICPConfig(max_correspondence_distance=0.5), AdaptiveMEstimatorConfig(num_alpha_segments=60))
+            ctxs[2].update_config(ICPConfig(max_correspondence_distance=0.7))
+            _check_equal(b.optimize(None, pts, Ts), _singles(ctxs, jobs))
+            ctxs[3].update_config(ICPConfig(max_iterations=6))
+            with pytest.raises(RuntimeError):
+                b.optimize(None, pts, Ts)
+        finally:
+            b.close()
+    finally:
+        for o in ctxs:
+            o.close()
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["fast", "exact"])
+def test_batch_many_jobs_and_repointed_scans(pko_mode, exact):
+    """64 jobs (fewer PKO workgroups per job than a single scan gets), then every job re-pointed at another scan; in
+    both modes (all-exact: the lockstep exact scale + sums of 64 jobs)."""
     from lidar_odometry_amd import BatchOptimizer
     frames = [11, 13, 15, 17, 19, 21, 23, 25]
     cases = [_data.kitti_case(f) for f in frames]
     m = cases[0][0]
-    ctxs = [_ctx(m) for _ in range(64)]
+    ctxs = [_ctx(m, exact=exact) for _ in range(64)]
     try:
         b = BatchOptimizer(ctxs)
         try:

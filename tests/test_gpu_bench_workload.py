@@ -1,12 +1,12 @@
 """Parity on the bench's own workloads -- the exact inputs the `value` lines time: KITTI-07-like city map after 660
 frames (331 keyframes, 12.8k surfels, 120k L0 voxels) with its 20 measured scans (C2), the MID360-like rosette
 sequence (C3, 20 scans) and the synthetic 1M-point patch scans (C5, 4 scans), each with its perturbed initial poses.
-In reference-exact mode every iteration's pose, alpha and correspondence count is bit-identical to the oracle's on
-all three; in the default (fp64 tree-sum) mode the KITTI workload stays within the north_star tolerance (1e-4 m /
-1e-4 rad per iteration) with equal iteration counts, status and alpha at every iteration.  The default mode is not
-required to pass on C3 / C5: an alpha near-tie there flips with the summation order (DESIGN.md "parity per config"),
-which is why bench.py's auto mode reports exact mode as the value on those configs.  (The bench line repeats these
-comparisons in `cpu_baseline.parity` / `parity_other` on every run; this makes them part of the GPU test tier.)"""
+The PRODUCT DEFAULT (a context as lo_create makes it: reference-exact arithmetic) is bit-identical to the oracle at
+every iteration -- pose, alpha, correspondence count -- on all three, so it meets the north_star tolerance (1e-4 m /
+1e-4 rad per iteration) everywhere.  The opt-in fast mode (lo_set_exact(ctx, 0): fp64 tree sums) stays within the
+tolerance on C2; on C3 / C5 an alpha near-tie flips with the summation order and moves the pose by up to ~4e-4
+(DESIGN.md "parity per config") -- documented and bounded here, which is why the fast mode is not the default.  (The
+bench line repeats these comparisons in `cpu_baseline.parity` / `parity_other` on every run.)"""
 import numpy as np
 import pytest
 
@@ -31,7 +31,8 @@ def workload(request):
     return wl, inits, ref
 
 
-def _gpu_results(wl, inits, exact: bool):
+def _gpu_results(wl, inits, exact):
+    """exact: True / False set the mode, None keeps the product default (lo_create's)."""
     from lidar_odometry_amd import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
     from lidar_odometry_amd._lib import lib
     o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=True), AdaptiveMEstimatorConfig(),
@@ -39,7 +40,8 @@ def _gpu_results(wl, inits, exact: bool):
                                        max_points=max(len(s) for s in wl["scans"]))   # as bench.py builds it
     try:
         assert lib().lo_map_set_from_voxelmap(o.ctx, wl["vm"].handle) == 0
-        o.set_exact(exact)
+        if exact is not None:
+            o.set_exact(exact)
         out = []
         for pts, Ti in zip(wl["scans"], inits):
             ok, To = o.optimize(None, pts, Ti)
@@ -61,13 +63,25 @@ def test_bench_workload_size(workload):
         assert len(wl["scans"]) == 20
 
 
-def test_bench_workload_default_parity(workload):
+def test_bench_workload_product_default_parity(workload):
+    """The product default on every bench workload: within 1e-4 with equal status, iteration counts and alpha at every
+    iteration (it is bit-identical: test_bench_workload_exact_bitwise)."""
     wl, inits, ref = workload
-    if wl["key"] != "kitti":
-        pytest.skip("default mode is only required on C2; C3 / C5 report exact mode (see module docstring)")
-    p = bench.parity_vs_oracle(_gpu_results(wl, inits, exact=False), ref)
+    p = bench.parity_vs_oracle(_gpu_results(wl, inits, exact=None), ref)
     assert p["within_1e-4"], p
     assert p["status_equal"] == p["iteration_count_equal"] == p["alpha_every_iteration_equal"] == len(ref), p
+
+
+def test_bench_workload_fast_mode(workload):
+    """The opt-in fast mode: within 1e-4 on C2; on C3 / C5 bounded by 1e-3 (alpha near-ties resolve differently)."""
+    wl, inits, ref = workload
+    p = bench.parity_vs_oracle(_gpu_results(wl, inits, exact=False), ref)
+    assert p["status_equal"] == len(ref), p
+    if wl["key"] == "kitti":
+        assert p["within_1e-4"], p
+        assert p["iteration_count_equal"] == p["alpha_every_iteration_equal"] == len(ref), p
+    else:
+        assert p["per_iteration_max_dt_m"] <= 1e-3 and p["per_iteration_max_dR_rad"] <= 1e-3, p
 
 
 def test_bench_workload_exact_bitwise(workload):

@@ -69,6 +69,33 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # bench.py --mode auto: a rank whose own parity check failed keeps every rank on reference-exact
+        q.put((rank, [parallel.all_ranks_agree(f, world) for f in
+                      ([True, rank == 0, rank == 1, False])]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mode_agreement_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1] == [True, False, False, False]
+    assert parallel.all_ranks_agree(True, 1) and not parallel.all_ranks_agree(False, 1)
+
+
 def test_assignment_covers_all_scans():
     for n in (1, 2, 5, 8, 17):
         for w in (1, 2, 3, 8):
