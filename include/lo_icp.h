@@ -164,7 +164,11 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * (opt-in) -- fixed-order fp64 tree sums, a Chan-merged scale, an fp64 LDLT with a polar SO3 projection; within 1e-7
  * of the reference per step, but a PKO alpha near-tie or a correspondence on a voxel face can then resolve the other way
  * and move the pose by 1e-4 .. 4e-4 (measured on the MID360-like and 1M-point workloads): NOT parity-safe.
- * LO_EXACT=0 in the environment starts contexts in the fast mode (A/B runs). */
+ * LO_EXACT=0 in the environment starts contexts in the fast mode (A/B runs).
+ * Device memory of the exact mode, allocated at the first scan that needs it and kept: up to 16384 points a fixed
+ * ~1 MB; a larger scan adds ~0.95 KB per point of the largest such scan (the 43 fp32 term columns, 172 B, and the
+ * sequential-sum head records, 2 x 1024 per 4096-term chunk of every column at 36 B, ~775 B) -- ~0.95 GB at 1M points,
+ * ~3.8 GB at the 4M-point max_points.  An allocation failure there returns LO_ERR_HIP from that optimize call. */
 int lo_set_exact(lo_ctx* ctx, int enable);
 /* Scan pipeline (default on; LO_PIPE=0 in the environment turns it off at lo_create).  The reference's optimize
  * runs GN iterations until convergence (IterativeClosestPointOptimizer.cpp:281-449); the device loop enqueues all
@@ -186,7 +190,11 @@ int lo_set_pko_groups(lo_ctx* ctx, int groups);
 /* Scan-pipeline state: out[0] enabled, out[1] main iterations, out[2] timeouts (a device-side wait gave up -- the two
  * streams were not run concurrently -- and the pipeline was switched off), out[3] synchronous scans re-run on one
  * stream after a timeout.  A scan whose wait timed out reports LO_ERR_PIPELINE in its device status (the exported
- * record of an async scan); lo_icp_result re-runs it on one stream instead of returning that status. */
+ * record of an async scan); lo_icp_result re-runs it on one stream instead of returning that status.  That re-run reads
+ * the points of the context's LAST enqueued scan again: after lo_icp_optimize_async / lo_icp_optimize_raw_async the
+ * caller's device buffer (d_pts / d_raw, and the device count) must therefore stay valid and unchanged until
+ * lo_icp_result has returned -- the same lifetime a stream-ordered reader of the buffer needs anyway.  Earlier async
+ * scans are never re-run: their exported records keep LO_ERR_PIPELINE. */
 int lo_pipeline_status(lo_ctx* ctx, int out[4]);
 /* In-step timing: with enable, each optimize brackets its FIRST correspondence launch (k_correspond, or the KDTree
  * k_knn + k_knn_brute + k_plane) with HIP events on the context stream (up to 1024 scans; enabling resets them).
@@ -315,6 +323,8 @@ int lo_seq_sum_f64(lo_ctx* ctx, const double* x, size_t n, int sort, double* out
 int lo_seq_sum_f32(lo_ctx* ctx, const float* x, size_t n, float* out_sum, long long stats[4]);
 /* Diagnostic: 16 device counters (phase timestamps of the -DLO_PKO_STAMPS build; zeros otherwise). */
 int lo_debug_counters(lo_ctx* ctx, unsigned long long out[16]);
+/* Diagnostic: the first n (<= 24) device counters. */
+int lo_debug_counters_ex(lo_ctx* ctx, unsigned long long* out, int n);
 /* Context-free host variant (no GPU needed): sample_size = gmm_sample_size. */
 int lo_pko_sample_indices_host(size_t n, int sample_size, int32_t* out);
 

@@ -87,6 +87,12 @@ int         lo_devmap_counts(lo_devmap* m, size_t out[4]);
 /* the error bits only (one 64-byte copy; syncs the stream): LO_OK, or LO_ERR_CAPACITY with lo_devmap_last_error set
  * when an update overflowed a capacity or met a key beyond +-2^20 (the update aborted, the map is stale) */
 int         lo_devmap_status(lo_devmap* m);
+/* the same check without a stream sync: _async enqueues the copy of the error bits (pinned memory + an event) behind
+ * the work enqueued so far; _poll returns LO_ERR_CAPACITY once that copy has landed and shows error bits, else LO_OK
+ * (also while it is still in flight).  The frame loop enqueues after every keyframe's update and polls after each
+ * frame's synchronous ICP, so an aborted update is reported at the first frame tracked after it. */
+int         lo_devmap_status_async(lo_devmap* m);
+int         lo_devmap_status_poll(lo_devmap* m);
 /* the containers in their order (tests / GetPointCloud): L0 keys, centroids, point counts; L1 keys, surfel flag,
  * normal, centroid, planarity, child count and children keys (27 per voxel) */
 size_t      lo_devmap_get_l0(lo_devmap* m, int32_t* keys, float* xyz, int32_t* point_counts, size_t cap);

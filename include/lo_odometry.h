@@ -48,6 +48,9 @@ typedef struct {
 typedef struct lo_odometry lo_odometry;
 
 void          lo_odom_config_default_kitti(lo_odom_config* cfg);
+/* The device map holds up to 2^21 L0 voxels (LO_DEVMAP_MAX_L0 in the environment overrides it).  An update that
+ * overflows a capacity aborts and sets the map's error bits; lo_odom_process reports it (LO_ERR_CAPACITY) at the first
+ * frame after that keyframe, read without a stream sync (lo_devmap_status_async / _poll). */
 lo_odometry*  lo_odom_create(const lo_odom_config* cfg, int device, int* err);
 void          lo_odom_destroy(lo_odometry* o);
 const char*   lo_odom_last_error(const lo_odometry* o);

@@ -42,9 +42,15 @@ constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv =
 // in the PKO launch's dynamic LDS (4 consecutive rows of one term per ds_read_b128)
 constexpr int kXcRegions = 3;                              // 64-point regions per chunk (one per producer wave)
 constexpr int kXcChunk = kXcRegions * kWave;              // 192 points
-constexpr int kXcStride = kXcChunk + 4;                    // floats per term row (+4: b128 reads of 16 lanes hit 64 banks)
-constexpr int kXcBuf = 43 * kXcStride;
-constexpr size_t kXcLdsBytes = (2 * kXcBuf + 2 * kXcRegions + 43 + kCandWords) * sizeof(float);
+constexpr int kXcPad = 16;                                 // a chunk's staged rows padded to a multiple of 16
+constexpr int kXcFactors = 14;                             // a point's factors (J, wJ, wr, r): every term is fa * fb
+// floats per factor row: a chunk's rows + padding, and 212 = 20 mod 64 puts the 14 rows' 16-B reads on disjoint banks
+constexpr int kXcStride = 212;
+static_assert(kXcStride >= kXcChunk + kXcPad - 1, "a padded chunk fits a factor row");
+constexpr int kXcBuf = kXcFactors * kXcStride;             // one chunk's factor rows
+constexpr int kXcCntOff = 2 * kXcBuf;                      // [4][kXcRegions] valid rows per region (ints)
+constexpr int kXcTotOff = kXcCntOff + 4 * kXcRegions;      // [43] the sums, then the candidate record
+constexpr size_t kXcLdsBytes = (kXcTotOff + 43 + kCandWords) * sizeof(float);
 
 struct __attribute__((aligned(32))) Slot {
     uint64_t key;
@@ -69,7 +75,7 @@ struct DevState {
     double g_out[6];
     double cost_out;
     double gmm_out[3 * kMaxK];
-    unsigned long long dbg[16];     // diagnostic build only (-DLO_PKO_STAMPS): phase timestamps / counters
+    unsigned long long dbg[24];     // diagnostic build only (-DLO_PKO_STAMPS): phase timestamps / counters
     unsigned long long em_stat[3];  // with stage timing: EM s_memtime cycles, EM iterations, fits (lead workgroup)
     lo_iter_log logs[LO_MAX_ITERS];
 };
@@ -234,6 +240,25 @@ __device__ __forceinline__ ScanBufs own_bufs(const KParams& P) {
 // ---------------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
+
+// A load through the global address space (global_load, counted by vmcnt only).  Pointers read from a KParams in
+// memory (the batch kernels) or passed through helpers are generic, and a generic (flat) load is counted by lgkmcnt as
+// well: then every wait for an LDS write before a barrier also waits for the loads in flight -- prefetches included.
+template <typename T> __device__ __forceinline__ T gld(const T* p) {
+    return *(const __attribute__((address_space(1))) T*)(p);
+}
+
+// a whole 32-B slot as two 16-B global loads (a builtin vector type: a class type's copy would bind a generic
+// reference and load through flat again)
+__device__ __forceinline__ Slot gld_slot(const Slot* p) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f a = gld(reinterpret_cast<const v4f*>(p)), b = gld(reinterpret_cast<const v4f*>(p) + 1);
+    Slot s;
+    s.key = static_cast<uint64_t>(__float_as_uint(a.x)) | (static_cast<uint64_t>(__float_as_uint(a.y)) << 32);
+    s.n[0] = a.z; s.n[1] = a.w; s.n[2] = b.x;
+    s.c[0] = b.y; s.c[1] = b.z; s.c[2] = b.w;
+    return s;
+}
 
 template <bool SC1> struct Mem;
 template <> struct Mem<false> {

@@ -1260,6 +1260,9 @@ struct lo_devmap {
     const int* g_scan_n = nullptr;
     std::string err;
     int* h_cnt = nullptr;                // pinned copy of the counters
+    int* h_err = nullptr;                // pinned copy of the counters for lo_devmap_status_async / _poll
+    hipEvent_t ev_err = nullptr;         //   recorded after that copy
+    bool err_pending = false;
     size_t updates = 0;
 };
 
@@ -1368,6 +1371,8 @@ lo_devmap* lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor,
     if (rc == LO_OK) rc = dm_fill_int(m, M.ttfirst, HP, INT_MAX);
     if (rc == LO_OK) rc = dm_fill_int(m, M.tqfirst, HP, INT_MAX);
     if (rc == LO_OK && hipHostMalloc(&m->h_cnt, 16 * sizeof(int), hipHostMallocDefault) != hipSuccess) rc = LO_ERR_HIP;
+    if (rc == LO_OK && hipHostMalloc(&m->h_err, 16 * sizeof(int), hipHostMallocDefault) != hipSuccess) rc = LO_ERR_HIP;
+    if (rc == LO_OK && hipEventCreateWithFlags(&m->ev_err, hipEventDisableTiming) != hipSuccess) rc = LO_ERR_HIP;
     if (rc == LO_OK) rc = dm_bind_table(m);
     if (rc == LO_OK && hipStreamSynchronize(m->stream) != hipSuccess) rc = LO_ERR_HIP;
     if (rc != LO_OK) return fail(rc, "allocation", m);
@@ -1389,6 +1394,8 @@ void lo_devmap_destroy(lo_devmap* m) {
     if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
     for (void* p : m->bufs) (void)hipFree(p);
     if (m->h_cnt) (void)hipHostFree(m->h_cnt);
+    if (m->h_err) (void)hipHostFree(m->h_err);
+    if (m->ev_err) (void)hipEventDestroy(m->ev_err);
     delete m;
 }
 
@@ -1534,6 +1541,27 @@ int lo_devmap_status(lo_devmap* m) {
     DM_HIP(m, hipMemcpyAsync(m->h_cnt, m->M.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
     DM_HIP(m, hipStreamSynchronize(m->stream));
     if (m->h_cnt[C_ERR]) { m->err = "device map overflow / invalid key (error bits " + std::to_string(m->h_cnt[C_ERR]) + ")"; return LO_ERR_CAPACITY; }
+    return LO_OK;
+}
+
+int lo_devmap_status_async(lo_devmap* m) {
+    if (!m) return LO_ERR_ARG;
+    DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
+    DM_HIP(m, hipMemcpyAsync(m->h_err, m->M.cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, m->stream));
+    DM_HIP(m, hipEventRecord(m->ev_err, m->stream));
+    m->err_pending = true;
+    return LO_OK;
+}
+
+int lo_devmap_status_poll(lo_devmap* m) {
+    if (!m) return LO_ERR_ARG;
+    if (!m->err_pending) return LO_OK;
+    const hipError_t q = hipEventQuery(m->ev_err);
+    if (q == hipErrorNotReady) return LO_OK;             // still in flight: the next poll reads it
+    DM_HIP(m, q);
+    m->err_pending = false;
+    if (m->h_err[C_ERR]) { m->err = "device map overflow / invalid key (error bits " + std::to_string(m->h_err[C_ERR]) + ")"; return LO_ERR_CAPACITY; }
     return LO_OK;
 }
 

@@ -267,7 +267,7 @@ template <int PT>
 __host__ __device__ constexpr int scale_c_bins() { return PT * kScaleC <= 4096 ? PT * kScaleC : 2048; }
 template <int PT>
 __host__ __device__ constexpr size_t scale_c_lds() {
-    return 2 * static_cast<size_t>(PT) * kScaleC * sizeof(uint64_t) + 2 * static_cast<size_t>(scale_c_bins<PT>()) * sizeof(int);
+    return static_cast<size_t>(PT) * kScaleC * sizeof(uint64_t) + 2 * static_cast<size_t>(scale_c_bins<PT>()) * sizeof(int);
 }
 
 template <int PT>
@@ -276,9 +276,8 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
     if (st->done) return;
     constexpr int NT = kScaleC, N = PT * NT, NB = scale_c_bins<PT>();
     extern __shared__ uint64_t s_dyn[];
-    uint64_t* s_tmp = s_dyn;                                 // keys in bin order
-    uint64_t* s_srt = s_dyn + N;                             // keys sorted
-    int* s_cnt = reinterpret_cast<int*>(s_dyn + 2 * N);      // per-bin count
+    uint64_t* s_tmp = s_dyn;                                 // keys in bin order, then sorted (in place)
+    int* s_cnt = reinterpret_cast<int*>(s_dyn + N);          // per-bin count
     int* s_end = s_cnt + NB;                                 // per-bin start, then end (after the scatter)
     __shared__ MonoScratch<NT> S;
     __shared__ KeyStat s_ks[NT / kWave];
@@ -333,20 +332,34 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
     for (int q = 0; q < PT; ++q)
         if (key[q] < kInfKey) s_tmp[atomicAdd(&s_end[bin_of(key[q])], 1)] = key[q];
     __syncthreads();
-    // each key's rank in its bin: the members below it, and the equal ones placed before it
-    for (int p = tid; p < cnt; p += NT) {
-        const uint64_t k = s_tmp[p];
-        const int b = bin_of(k), e = s_end[b], s0 = e - s_cnt[b];
-        int r = 0;
-        for (int q = s0; q < e; ++q) {
-            const uint64_t o = s_tmp[q];
-            r += (o < k || (o == k && q < p)) ? 1 : 0;
+    // each key's rank in its bin: the members below it, and the equal ones placed before it; every key is read before
+    // any moves (the barrier), so the sorted order goes back into the same array
+    uint64_t kk[PT];
+    int pos[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int p = tid + i * NT;
+        pos[i] = -1;
+        if (p < cnt) {
+            const uint64_t k = s_tmp[p];
+            const int b = bin_of(k), e = s_end[b], s0 = e - s_cnt[b];
+            int r = 0;
+            for (int q = s0; q < e; ++q) {
+                const uint64_t o = s_tmp[q];
+                r += (o < k || (o == k && q < p)) ? 1 : 0;
+            }
+            kk[i] = k;
+            pos[i] = s0 + r;
         }
-        s_srt[s0 + r] = k;
     }
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+        if (pos[i] >= 0) s_tmp[pos[i]] = kk[i];
+    __syncthreads();
+    const uint64_t* s_srt = s_tmp;
     LO_XSTAMP(st, 12);
-    double* s_x = reinterpret_cast<double*>(s_tmp);          // the bin-ordered keys are no longer read
+    double* s_x = reinterpret_cast<double*>(s_tmp);          // each thread overwrites only the keys it reads
     const int base = tid * PT;
     double x[PT];
 #pragma unroll

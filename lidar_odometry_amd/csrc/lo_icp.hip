@@ -225,6 +225,8 @@ struct lo_ctx {
     bool pipe = true;
     int pipe_main = 2;
     int pko_groups = 0;             // EM workgroups per PKO launch (lo_set_pko_groups / LO_PKO_GROUPS; 0 = one per alpha)
+    bool pko_solo = false;          // LO_PKO_SOLO=1 (A/B): the speculative PKO launch asks for enough LDS that one
+                                    //   workgroup holds a CU alone (no other launch's waves on its SIMDs)
     hipStream_t s_tail = nullptr;
     uint32_t pipe_seq = 0;
     uint32_t* d_fin = nullptr;      // [0] the last scan whose result is final (publish_final), [1] main part done,
@@ -270,6 +272,7 @@ static void launch_pko(lo_ctx* c, const KParams& P, int it) {
 // solves the selected one.
 static bool spec_ok(const KParams& P) { return P.use_pko && P.acc_part && P.nb_acc <= kFuseMaxBlocks; }
 
+constexpr size_t kPkoSoloBytes = 64 * 1024;   // + the ~22-27 KB static part: more than half of a CU's 160 KB
 static void launch_pko_spec(lo_ctx* c, const KParams& P, int it, hipStream_t s = nullptr) {
     size_t pre_bytes = static_cast<size_t>(std::max(P.nb, 1)) * sizeof(int);
     const int G = pko_grid(c);
@@ -278,6 +281,7 @@ static void launch_pko_spec(lo_ctx* c, const KParams& P, int it, hipStream_t s =
         W = 1;
         pre_bytes = std::max(pre_bytes, kXcLdsBytes);
     }
+    if (c->pko_solo) pre_bytes = std::max(pre_bytes, kPkoSoloBytes);
     if (P.exact_cand) hipLaunchKernelGGL(k_pko_tx, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
     else hipLaunchKernelGGL(k_pko_t<4>, dim3(G + (P.NA + 1) * W), dim3(256), pre_bytes, s ? s : c->stream, P, it, G);
 }
@@ -310,7 +314,9 @@ static int ensure_acc_part(lo_ctx* c) {
     ++c->cfg_gen;
     // the exact candidates' staging sits in the PKO launch's dynamic LDS (beyond the 64 KB default with the static part)
     LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(kXcLdsBytes + 16384)));
+                                  static_cast<int>(std::max(kXcLdsBytes + 16384, kPkoSoloBytes))));
+    LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_t<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(kPkoSoloBytes)));
     return LO_OK;
 }
 
@@ -616,6 +622,7 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
     if (const char* pw = std::getenv("LO_PIPE_WAIT_MS")) c->pipe_bound = 100000ull * std::max(1, std::atoi(pw));
     if (const char* pg = std::getenv("LO_PKO_GROUPS")) c->pko_groups = std::max(0, std::atoi(pg));
+    if (const char* ps = std::getenv("LO_PKO_SOLO")) c->pko_solo = std::atoi(ps) != 0;
     if (const char* ex = std::getenv("LO_EXACT")) c->exact = std::atoi(ex) != 0;   // A/B runs: LO_EXACT=0 = fast mode
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
@@ -2052,6 +2059,14 @@ int lo_debug_counters(lo_ctx* c, unsigned long long out[16]) {
     const DevState* st = c->d_st;
     LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(st) + offsetof(DevState, dbg), 16 * sizeof(unsigned long long),
                         hipMemcpyDeviceToHost));
+    return LO_OK;
+}
+
+int lo_debug_counters_ex(lo_ctx* c, unsigned long long* out, int n) {
+    if (!c || !out || n < 1 || n > 24) return LO_ERR_ARG;
+    LO_HIP(c, sync_all(c));
+    LO_HIP(c, hipMemcpy(out, reinterpret_cast<const char*>(c->d_st) + offsetof(DevState, dbg),
+                        static_cast<size_t>(n) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return LO_OK;
 }
 

@@ -30,8 +30,6 @@ struct lo_odometry {
     std::vector<float> feat, world;
 };
 
-static constexpr size_t kDevmapCheck = 8;
-
 static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info) {
     // create_keyframe (:370-530): world feature cloud -> UpdateVoxelMap(cloud, position, 1.2 max_range) -> device
     const auto t0 = std::chrono::steady_clock::now();
@@ -43,8 +41,8 @@ static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info
         o->last_kf = pose;
         ++o->keyframes;
         // the map's error bits (an update that overflowed a capacity aborted; tracking would go on against a stale
-        // map): read back every kDevmapCheck keyframes, one small copy and a stream sync
-        if (o->keyframes % kDevmapCheck == 0 && (rc = lo_devmap_status(o->dmap)) != LO_OK) {
+        // map): copied back behind the update without a sync, read after the next frame's ICP (lo_odom_process)
+        if ((rc = lo_devmap_status_async(o->dmap)) != LO_OK) {
             o->err = lo_devmap_last_error(o->dmap);
             return rc;
         }
@@ -100,8 +98,10 @@ lo_odometry* lo_odom_create(const lo_odom_config* cfg, int device, int* err) {
     const char* hm = std::getenv("LO_HOST_MAP");
     if (cfg->icp.use_surfel_correspondence && !(hm && std::atoi(hm))) {
         int e = LO_OK;
+        size_t max_l0 = size_t(1) << 21;                                   // LO_DEVMAP_MAX_L0: capacity override
+        if (const char* cap = std::getenv("LO_DEVMAP_MAX_L0"); cap && std::atoll(cap) > 0) max_l0 = std::atoll(cap);
         o->dmap = lo_devmap_create(o->icp, cfg->icp.voxel_size, cfg->icp.hierarchy_factor, cfg->planarity_threshold,
-                                   size_t(1) << 21, static_cast<size_t>(std::max(cfg->icp.max_points, 16)), &e);
+                                   max_l0, static_cast<size_t>(std::max(cfg->icp.max_points, 16)), &e);
         if (!o->dmap) { lo_voxelmap_destroy(o->map); lo_destroy(o->icp); delete o; if (err) *err = e; return nullptr; }
     }
     if (err) *err = LO_OK;
@@ -171,6 +171,10 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
     lo_stats st{};
     int rc = lo_icp_optimize_raw(o->icp, raw, n, stride, voxel, g12, p12, logs, &st);
     if (rc < 0) { o->err = lo_last_error(o->icp); return rc; }
+    if (o->dmap) {      // the last keyframe's map update: the ICP's sync has drained it (same stream), so no wait here
+        const int mrc = lo_devmap_status_poll(o->dmap);
+        if (mrc != LO_OK) { o->err = lo_devmap_last_error(o->dmap); return mrc; }
+    }
     fi->status = rc;
     fi->icp_iterations = st.iterations;
     fi->n_corr = st.n_corr;

@@ -45,8 +45,8 @@ __global__ __launch_bounds__(256) void k_exact_acc_b(const KParams* __restrict__
     const KParams& P = PB[blockIdx.x];
     DevState* st = P.st;
     if (st->done) return;
-    extern __shared__ float s_dyn[];                       // kXcLdsBytes
-    float* s_tot = s_dyn + 2 * kXcBuf + 2 * kXcRegions;
+    extern __shared__ __attribute__((aligned(16))) float s_dyn[];   // kXcLdsBytes (16-B aligned: ds_read_b128)
+    float* s_tot = s_dyn + kXcTotOff;
     __shared__ double s_alpha;
     const int tid = threadIdx.x, lane = tid & 63;
     if (tid < kWave) {

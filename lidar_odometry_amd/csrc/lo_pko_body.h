@@ -675,19 +675,20 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // Reference-exact candidates (lo_set_exact, scans with nb_acc <= kFuseMaxBlocks): candidate c's GN step exactly as the
 // reference forms it -- the 43 running fp32 sums of build_ne in correspondence (scan) order (:345-410), Eigen's fp32
 // LDLT and the re-projected update (:417-448; lo_exact.h) -- in ONE workgroup while the EM runs, written as the same
-// 48-word record acc_candidate writes, so k_pick_correspond / k_pick take it unchanged.  Waves 1-3 form each accepted
-// point's 43 terms (exact_point_factors, then the products exactly as build_ne forms them) for a chunk of 192 points
-// and stage them term-major in LDS, compacted per 64-point region in point order and padded with zero terms to a
-// multiple of 4 (adding +0 leaves a running sum unchanged: the sums start at +0 and never become -0); wave 0's lane k
-// adds term k of every staged row to its running sum, one rounding per addition, four rows per ds_read_b128, one
-// chunk behind the producers (double-buffered, one barrier per chunk).  The producers' loads run a chunk ahead (slot
-// indices two).  LDS: the dynamic buffer (after the prefix).
-// The 43 sequential sums of build_ne with Huber delta dl at pose T into s_tot (LDS, kExactTerms floats), by one 256-thread
-// workgroup (waves 1-3 produce, wave 0 adds); dyn: kXcLdsBytes of LDS.  Every thread of the workgroup calls it.
+// 48-word record acc_candidate writes, so k_pick_correspond / k_pick take it unchanged.
+// exact_sums_wg: the 43 sequential sums of build_ne with Huber delta dl at pose T into s_tot (LDS), by one 256-thread
+// workgroup; dyn: kXcLdsBytes of LDS; every thread calls it.  Per chunk of 192 points, waves 1-3 form each accepted
+// point's 14 factors (exact_point_factors: J, wJ, wr, r) and stage them factor-major in LDS, compacted over the whole
+// chunk in point order (each region's valid count is published one chunk ahead, from the slot indices the producers
+// hold two chunks ahead) and padded with zero factors to a multiple of 16 rows; wave 0's lane k forms term k of every
+// staged row as fa * fb (the same fp32 product build_ne forms) and adds it to its running sum, one rounding per
+// addition, a chunk behind the producers (double-buffered, one barrier per chunk).  A zero pad row adds +0, which
+// leaves a running sum unchanged: the sums start at +0 and never become -0 (x + -x rounds to +0).  The consumer's loop
+// is uniform (no per-row test) with the next 16 rows' reads issued before the current 16 adds.
 __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double scale, float dl, float* dyn, float* s_tot) {
-    float* s_f = dyn;                                      // [2][43][kXcStride]
-    int* s_cnt = reinterpret_cast<int*>(dyn + 2 * kXcBuf); // [2][kXcRegions]
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float* s_f = dyn;                                      // [2][kXcFactors][kXcStride]
+    int* s_cnt = reinterpret_cast<int*>(dyn + kXcCntOff);  // [4][kXcRegions]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = wid - 1;
     const int n = scan_n(P);
     const int nch = (n + kXcChunk - 1) / kXcChunk;
     __syncthreads();                                       // earlier uses of the dynamic buffer are over
@@ -696,78 +697,121 @@ __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double sca
     float px = 0.0f, py = 0.0f, pz = 0.0f;
     Slot sv{};
     double rv = 0.0;
-    auto pidx = [&](int ch) { return ch * kXcChunk + (wid - 1) * kWave + lane; };
-    auto slot_at = [&](int ch) { const int i = pidx(ch); return (ch < nch && i < n) ? P.slot[i] : -1; };
+    auto pidx = [&](int ch) { return ch * kXcChunk + r * kWave + lane; };
+    // global (not flat) loads: a flat load in flight would hold up every LDS wait of the chunk (gld)
+    const double* res = P.kd_res ? P.kd_res : P.res_out;   // the stored fp64 residual (same bits as recomputing)
+    auto slot_at = [&](int ch) { const int i = pidx(ch); return (ch < nch && i < n) ? gld(P.slot + i) : -1; };
     auto load_pt = [&](int ch, int s) {
         if (s >= 0) {
             const int i = pidx(ch);
-            px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2];
-            sv = P.tab[s];
-            rv = P.kd_res ? P.kd_res[i] : P.res_out[i];     // the stored fp64 residual (same bits as recomputing)
+            px = gld(P.pts + 3 * i); py = gld(P.pts + 3 * i + 1); pz = gld(P.pts + 3 * i + 2);
+            sv = gld_slot(P.tab + s);
+            rv = gld(res + i);
         }
     };
     if (wid > 0) {
         sl_cur = slot_at(0);
         sl_nxt = slot_at(1);
         load_pt(0, sl_cur);
+        const int c0 = __popcll(__ballot(sl_cur >= 0));
+        if (lane == 0) s_cnt[r] = c0;                      // chunk 0's region counts (buffer 0)
     }
+    // consumer: lane k's factor rows (lanes >= 43 repeat term 0 and discard it)
+    int fa, fb;
+    exact_term_factors(lane < kExactTerms ? lane : 0, fa, fb);
+    __syncthreads();
     float sum = 0.0f;                                      // consumer: lane k's running sum of term k
+#ifdef LO_PKO_STAMPS
+    unsigned long long t_work = 0, t_wait = 0;             // diagnostic: this wave's cycles in its part / at the barrier
+#endif
     for (int ch = 0; ch <= nch; ++ch) {
+#ifdef LO_PKO_STAMPS
+        const unsigned long long t_c0 = __builtin_amdgcn_s_memtime();
+#endif
         if (wid > 0 && ch < nch) {
             float* buf = s_f + (ch & 1) * kXcBuf;
-            const int r = wid - 1;
+            const int* cn = s_cnt + (ch & 3) * kXcRegions;
+            const int c0 = cn[0], c1 = cn[1], tot = c0 + c1 + cn[2];
+            const int off = r == 0 ? 0 : (r == 1 ? c0 : c0 + c1);
             const bool valid = sl_cur >= 0;
             const uint64_t m = __ballot(valid);
-            const int cnt = __popcll(m);
 #if defined(LO_XC_EXP) && LO_XC_EXP == 1
-            if (false) {                                   // diagnostic: producers skip the terms (consumer alone)
+            if (false) {                                   // diagnostic: producers skip the factors (consumer alone)
 #else
             if (valid) {
 #endif
-                float f[14];
+                float f[kXcFactors];
                 exact_point_factors(P, T, scale, dl, rv, px, py, pz, sv, f);
-                const int row = r * kWave + __popcll(m & ((1ull << lane) - 1ull));
+                const int row = off + __popcll(m & ((1ull << lane) - 1ull));
 #pragma unroll
-                for (int k = 0; k < kExactTerms; ++k) {
-                    int fa, fb;
-                    exact_term_factors(k, fa, fb);
-                    buf[k * kXcStride + row] = f[fa] * f[fb];
-                }
+                for (int j = 0; j < kXcFactors; ++j) buf[j * kXcStride + row] = f[j];
             }
-            if (lane < ((cnt + 3) & ~3) - cnt) {                   // -0 terms in rows cnt .. the next multiple of 4
-#pragma unroll                                                     // (s + -0 == s for every s, -0 included)
-                for (int k = 0; k < kExactTerms; ++k) buf[k * kXcStride + r * kWave + cnt + lane] = -0.0f;
+            const int pad = ((tot + kXcPad - 1) & ~(kXcPad - 1)) - tot;
+            if (r == kXcRegions - 1 && lane < pad) {       // zero factor rows up to the next multiple of 16
+#pragma unroll
+                for (int j = 0; j < kXcFactors; ++j) buf[j * kXcStride + tot + lane] = 0.0f;
             }
-            if (lane == 0) s_cnt[(ch & 1) * kXcRegions + r] = (cnt + 3) & ~3;
-            // the next chunk's point / surfel / residual, and the slot of the one after
+            // the next chunk's point / surfel / residual, the slot of the one after, and the next chunk's count
             sl_cur = sl_nxt;
             sl_nxt = slot_at(ch + 2);
             load_pt(ch + 1, sl_cur);
+            const int cn1 = __popcll(__ballot(sl_cur >= 0));
+            if (lane == 0) s_cnt[((ch + 1) & 3) * kXcRegions + r] = cn1;
 #if defined(LO_XC_EXP) && LO_XC_EXP == 2
         } else if (false) {                                // diagnostic: no adds (producers alone)
 #else
         } else if (wid == 0 && ch > 0) {
 #endif
-            const int b = (ch - 1) & 1;
-            const float* col = s_f + b * kXcBuf + (lane < kExactTerms ? lane : 0) * kXcStride;
+            const float* base = s_f + ((ch - 1) & 1) * kXcBuf;
+            const float4* A = reinterpret_cast<const float4*>(base + fa * kXcStride);
+            const float4* B = reinterpret_cast<const float4*>(base + fb * kXcStride);
+            const int* cn = s_cnt + ((ch - 1) & 3) * kXcRegions;
+            const int ng = (cn[0] + cn[1] + cn[2] + kXcPad - 1) / kXcPad;   // groups of 16 rows (uniform)
+            float4 a[4], b[4];
+            if (ng > 0) {
 #pragma unroll
-            for (int r = 0; r < kXcRegions; ++r) {             // a region's 16 row quads loaded at once, then added
-                const int q4 = s_cnt[b * kXcRegions + r] >> 2;
-                const float4* rows = reinterpret_cast<const float4*>(col + r * kWave);
-                float4 v[kWave / 4];
+                for (int q = 0; q < 4; ++q) { a[q] = A[q]; b[q] = B[q]; }
+            }
+            for (int g = 0; g < ng; ++g) {
+                float4 an[4], bn[4];
+                const int gn = g + 1 < ng ? g + 1 : g;     // the next group's rows (the last group re-reads itself)
 #pragma unroll
-                for (int q = 0; q < kWave / 4; ++q) v[q] = q < q4 ? rows[q] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+                for (int q = 0; q < 4; ++q) { an[q] = A[4 * gn + q]; bn[q] = B[4 * gn + q]; }
 #pragma unroll
-                for (int q = 0; q < kWave / 4; ++q) {
-                    sum += v[q].x;
-                    sum += v[q].y;
-                    sum += v[q].z;
-                    sum += v[q].w;
+                for (int q = 0; q < 4; ++q) {
+                    sum += a[q].x * b[q].x;
+                    sum += a[q].y * b[q].y;
+                    sum += a[q].z * b[q].z;
+                    sum += a[q].w * b[q].w;
                 }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { a[q] = an[q]; b[q] = bn[q]; }
             }
         }
+#ifdef LO_PKO_STAMPS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long t_c1 = __builtin_amdgcn_s_memtime();
         __syncthreads();
+        const unsigned long long t_c2 = __builtin_amdgcn_s_memtime();
+        t_work += t_c1 - t_c0;
+        t_wait += t_c2 - t_c1;
+#else
+        __syncthreads();
+#endif
     }
+#ifdef LO_PKO_STAMPS
+    // diagnostic sums over every exact candidate of the launch: dbg[16] calls, dbg[17] / [18] the consumer wave's add /
+    // barrier cycles, dbg[19] / [20] producer wave 1's term / barrier cycles (lo_debug_counters_ex)
+    if (lane == 0 && wid == 0) {
+        atomicAdd(&P.st->dbg[16], 1ull);
+        atomicAdd(&P.st->dbg[17], t_work);
+        atomicAdd(&P.st->dbg[18], t_wait);
+    }
+    if (lane == 0 && wid == 1) {
+        atomicAdd(&P.st->dbg[19], t_work);
+        atomicAdd(&P.st->dbg[20], t_wait);
+    }
+#endif
     if (wid == 0 && lane < kExactTerms) s_tot[lane] = sum;
     __syncthreads();
 }
@@ -777,7 +821,7 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
 #ifdef LO_PKO_STAMPS
     const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    float* s_tot = dyn + 2 * kXcBuf + 2 * kXcRegions;      // [kExactTerms]
+    float* s_tot = dyn + kXcTotOff;                        // [kExactTerms]
     float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
     const int tid = threadIdx.x;
     float T[12];
@@ -1210,7 +1254,9 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     if (wg == 0) dbg = st->dbg;
 #endif
     LO_STAMP(dbg, 0);
-    extern __shared__ int s_pre[];                   // dynamic, nb ints: exclusive prefix of block counts
+    // dynamic, nb ints: exclusive prefix of block counts (16-B aligned: the exact candidates read it with ds_read_b128,
+    // and a misaligned 16-B LDS read is split -- the static part ends at a multiple of 8 only)
+    extern __shared__ __attribute__((aligned(16))) int s_pre[];
     __shared__ PkoLds<NW> L;
     PkoPrefetch pf;
     pko_prefetch<NW>(P, wg, G, pf, L);

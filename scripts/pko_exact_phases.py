@@ -26,6 +26,8 @@ def main():
     for mode in ("default", "exact"):
         icp.set_exact(mode == "exact")
         lead, cand, sums = [], [], []
+        acc = np.zeros(24)
+        prev = None
         for i in range(len(wl["scans"])):
             icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
             d = (C.c_ulonglong * 16)()
@@ -33,9 +35,19 @@ def main():
             lead.append(d[6] - d[0])
             cand.append(d[7])
             sums.append(d[15])
+            d2 = (C.c_ulonglong * 24)()
+            assert L.lo_debug_counters_ex(icp.ctx, d2, 24) == 0
+            cur = np.array(list(d2), dtype=np.float64)
+            if prev is not None and mode == "exact":
+                acc += cur - prev
+            prev = cur
         print(f"{mode}: lead PKO workgroup prefix..JS {np.mean(lead):.0f} cycles, candidate 0 {np.mean(cand):.0f} "
               f"cycles, slowest candidate's sums done at {np.mean(sums):.0f} (exact mode; mean over {len(lead)} scans' last launch)",
               flush=True)
+        if mode == "exact" and acc[16] > 0:
+            k = acc[16]
+            print(f"  exact_sums_wg per call ({k:.0f} calls): consumer adds {acc[17] / k:.0f} + barrier {acc[18] / k:.0f} "
+                  f"cycles; producer wave 1 terms {acc[19] / k:.0f} + barrier {acc[20] / k:.0f}", flush=True)
     icp.close()
 
 

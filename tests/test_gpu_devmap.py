@@ -160,7 +160,8 @@ def test_devmap_device_points_and_table_reupload():
 def test_devmap_follows_context_stream_and_reports_overflow():
     """The map launches on its context's current stream: after lo_set_stream (which destroys the context's own
     stream) and back, updates still equal the host map.  An update beyond the map's capacity sets the error bits
-    that lo_devmap_status (read by the frame loop every 8 keyframes) reports as LO_ERR_CAPACITY."""
+    that lo_devmap_status reports as LO_ERR_CAPACITY, and so does lo_devmap_status_poll once the copy enqueued by
+    lo_devmap_status_async has landed (the frame loop's per-keyframe check)."""
     import ctypes as C
 
     import torch
@@ -193,6 +194,13 @@ def test_devmap_follows_context_stream_and_reports_overflow():
     try:
         w = synth.transform(seq.poses[0], voxel_filter(seq.scan(0), 0.5, 8))
         small.update(w, seq.poses[0][:3, 3], 120.0, True)
+        L = lib()
+        assert L.lo_devmap_status_poll(small._h) == 0           # nothing enqueued yet
+        assert L.lo_devmap_status_async(small._h) == 0
+        torch.cuda.synchronize()
+        assert L.lo_sync(B.ctx) == 0
+        assert L.lo_devmap_status_poll(small._h) == LO_ERR_CAPACITY
+        assert L.lo_devmap_status_poll(small._h) == 0           # reported once per enqueued check
         assert small.status() == LO_ERR_CAPACITY
     finally:
         small.close()

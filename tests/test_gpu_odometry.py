@@ -114,3 +114,22 @@ def test_empty_first_frame_never_starts_a_map():
         assert info.status == 0 and not info.keyframe
         np.testing.assert_array_equal(T.reshape(12), ref[k])
         np.testing.assert_array_equal(T.reshape(12), np.asarray(T0, np.float32)[:3, :4].reshape(12))
+
+
+def test_map_overflow_reported_at_next_frame(monkeypatch):
+    """A keyframe whose device-map update overflows (LO_DEVMAP_MAX_L0 = 64 L0 voxels) aborts the update; the frame loop
+    copies the error bits back behind every keyframe's update without a sync and reports LO_ERR_CAPACITY at the very
+    next frame (previously only every 8th keyframe was checked)."""
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.odometry import LidarOdometry
+    monkeypatch.setenv("LO_DEVMAP_MAX_L0", "64")
+    seq = synth.KittiLikeSequence(seed=7, n_frames=3)
+    od = LidarOdometry(initial_pose=seq.poses[0])
+    try:
+        _, info = od.process(seq.scan(0))                 # the first keyframe: its update overflows on the device
+        assert info.keyframe
+        from lidar_odometry_amd._lib import LO_ERR_CAPACITY
+        with pytest.raises(RuntimeError, match=f"error {LO_ERR_CAPACITY}"):
+            od.process(seq.scan(1))
+    finally:
+        od.close()
