@@ -515,7 +515,7 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
         n_in += cnt.value
         L.lo_set_stage_timing(o.ctx, 0)
     in_t = tot_us / max(n_in, 1)
-    in_ach = float(np.mean(alg)) / (in_t * 1e-6) / 1e9
+    in_ach = float(np.mean(alg)) / (in_t * 1e-6) / 1e9 if in_t > 0 else None
     for o in ctxs:
         o.close()
     # DRAM bytes of one 1M-point launch (live rocprofv3 --pmc passes in child processes, as the value line's): a
@@ -538,7 +538,8 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
                          "traffic_live": traffic_live,
                          "timing": "single launches (lo_bench_kernel id 4: no set-up pass), HIP events, each scan "
                                    f"last touched {n_scans - 1} scans earlier"},
-            "in_step": {"kernel_us": in_t, "achieved": in_ach, "frac": in_ach / HBM_PEAK_GBS, "scans": int(n_in),
+            "in_step": {"kernel_us": in_t, "achieved": in_ach, "frac": in_ach / HBM_PEAK_GBS if in_ach else None,
+                        "scans": int(n_in),
                         "timing": "each scan's first correspondence launch inside its GN loop (HIP events)"}}
 
 

@@ -1232,10 +1232,10 @@ static_assert(kExactMaxPoints >= 2 * kExactMergeMax, "d_ex_rank holds the presor
 
 // A scan's first correspondence launch, bracketed by HIP events on the context stream when stage timing is on
 // (the kernel's in-step duration, as opposed to lo_bench_kernel's back-to-back launches).
-static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd) {
+static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd, int with_stats = 1) {
     const bool timed = c->stage_timing && c->st_n < kStageEvents;
     if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n], c->stream);
-    launch_correspond(c, P0, 1, kd);
+    launch_correspond(c, P0, with_stats, kd);
     if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n++ + 1], c->stream);
 }
 
@@ -1322,7 +1322,8 @@ static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStrea
     launch_mwm_scale(P, c->d_ex_sorted, c->mwm, s);
 }
 static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P0, int it, int n2, bool kd) {
-    launch_correspond(c, it == 0 ? P0 : P, 0, kd);
+    if (it == 0) launch_correspond_first(c, P0, kd, 0);   // (stage timing: the scan's first correspondence launch)
+    else launch_correspond(c, P, 0, kd);
     if (it == 0) launch_exact_scale_any(c, P, n2, c->stream);
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
