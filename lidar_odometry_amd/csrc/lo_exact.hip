@@ -1188,14 +1188,20 @@ struct MwmScratch {
     int elast[kMwThreads];
     int h_idx[kMwmCap];
     int h_e[kMwmCap];
+    int h_c1[kMwmCap];                                         // bit 1: the segment has a tie, bit 0: c1 of its first
     long long h_p[kMwmCap];
 };
 
+// A chunk's heads and records (mono_sum_tx's rules, chunk-local: term 0 of every chunk heads a segment, so the
+// segmented XOR state starts afresh in every chunk).  Heads: the chunk's first term, every non-zero term whose
+// predicted binade differs from its predecessor's, and steps of 2^49 units or more; a halfway tie inside a segment is
+// not a head -- its increment follows from the XOR of the increment parities since the segment's previous tie, or, for
+// the segment's first tie, from Q's parity at the segment's start (the record's two increments d_0 / d_1).
 template <bool SQ>
 __global__ __launch_bounds__(kMwThreads) void k_mwm_classify(const double* __restrict__ sorted, const DevState* st, MwmBuf B) {
     if (mwm_skip(st, B)) return;
     __shared__ MwmScratch S;
-    const int c = blockIdx.x, tid = threadIdx.x, cnt = B.cnt[0], c0 = c * kMwChunk, mc = min(kMwChunk, cnt - c0);
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, cnt = B.cnt[0], c0 = c * kMwChunk, mc = min(kMwChunk, cnt - c0);
     if (mc <= 0) return;
     const double m = SQ ? B.res[0] / cnt : 0.0;
     double t0 = 0.0;
@@ -1214,83 +1220,104 @@ __global__ __launch_bounds__(kMwThreads) void k_mwm_classify(const double* __res
     S.elast[tid] = binade64(tex + run);
     __syncthreads();
     const int e_in = tid ? S.elast[tid - 1] : kExpNone;
-    // mono_seq_sum's classify; term 0 of every chunk heads a segment
-    auto classify = [&](int a, double T, int ep, int& E, long long& qa) -> bool {
-        const int j = base + a;
-        const double xv = v[a];
-        E = binade64(T);
-        qa = 0;
-        if (!(j < mc && (xv != 0.0 || j == 0))) return false;
-        if (E < -1000 || E != ep || j == 0) return true;
-        const double t = ldexp(xv, 52 - E);
-        const double f = floor(t), fr = t - f;
-        if (fr == 0.5) return true;
-        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
-        return false;
-    };
-    long long ql = 0;
-    int nhl = 0;
+    // predicted binades, term bits, heads
+    int E[kMwPT];
+    TermBits tb[kMwPT];
+    bool hd[kMwPT];
+    int nh = 0;
     {
         double tl = 0.0;
         int ep = e_in;
 #pragma unroll
         for (int a = 0; a < kMwPT; ++a) {
             tl += v[a];
-            int E;
-            long long qa;
-            nhl += classify(a, tex + tl, ep, E, qa) ? 1 : 0;
-            ql += qa;
-            ep = E;
+            const int j = base + a;
+            E[a] = binade64(tex + tl);
+            const bool act = j < mc && v[a] != 0.0;
+            tb[a] = term_bits(v[a], E[a] == kExpNone ? 0 : E[a]);
+            hd[a] = j < mc && (j == 0 || (act && (E[a] < -1000 || E[a] != ep || tb[a].f >= (1ll << 49))));
+            nh += hd[a] ? 1 : 0;
+            ep = E[a];
         }
     }
-    long long ptot;
-    const long long pex = block_excl_scan<long long, kMwThreads>(ql, S.wl, ptot);
-    int htot;
-    const int hbase = block_excl_scan<int, kMwThreads>(nhl, S.wi, htot);
-    const size_t rb = static_cast<size_t>(c) * kMwmCap;
-    if (htot > kMwmCap) {                                       // uniform: the whole chunk term by term
-        if (tid == 0) {
-            B.nh[c] = 1;
-            B.idx[rb] = c0;
-            B.end[rb] = c0 + mc;
-            B.flag[rb] = kMwFail;
-            B.x[rb] = mwm_term<SQ>(sorted, c0, cnt, m);
-            B.dq[rb] = -0.0;
-            B.dlo[rb] = __builtin_inf();
-            B.dhi[rb] = -__builtin_inf();
-        }
-        return;
-    }
+    auto bits_of = [&](int a) -> int {                          // a term's own 4-bit XOR-scan state (xs_op)
+        if (hd[a]) return 1 | 4;
+        if (!(base + a < mc && v[a] != 0.0)) return 0;
+        if (tb[a].tie) return 1 | 8;
+        return static_cast<int>((tb[a].f + tb[a].up) & 1) << 1;
+    };
+    int xs = 0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) xs = xs_op(xs, bits_of(a));
+    int xtot = 0;
+    const int xex = block_excl_scan_dpp<kMwThreads>(xs | (nh << 4), 0,
+                                                    [](int a, int b) { return xs_op(a & 15, b & 15) | (((a >> 4) + (b >> 4)) << 4); },
+                                                    S.wi, &xtot);
+    const int hbase = xex >> 4, htot = xtot >> 4;
+    // increments (a later tie of its segment: f + (XOR ^ f's parity); the first: f, its +1 left to the walk)
+    long long inc_tot = 0;
     {
-        double tl = 0.0;
-        int ep = e_in, hk = hbase;
-        long long prun = pex;
+        int st4 = xex & 15;
 #pragma unroll
         for (int a = 0; a < kMwPT; ++a) {
-            tl += v[a];
-            int E;
-            long long qa;
-            const bool hd = classify(a, tex + tl, ep, E, qa);
-            prun += qa;
-            if (hd) { S.h_idx[hk] = base + a; S.h_e[hk] = E; S.h_p[hk] = prun; ++hk; }
-            ep = E;
+            const bool act = base + a < mc && v[a] != 0.0 && !hd[a];
+            long long inc = 0;
+            if (act) {
+                if (tb[a].tie) inc = tb[a].f + ((st4 & 8) ? (((st4 >> 1) ^ static_cast<int>(tb[a].f)) & 1) : 0);
+                else inc = tb[a].f + tb[a].up;
+            }
+            inc_tot += inc;
+            st4 = xs_op(st4, bits_of(a));
+        }
+    }
+    for (int k = tid; k < htot; k += kMwThreads) S.h_c1[k] = 0;    // ordered before the records by the scan's barriers
+    long long ptot = 0;
+    const long long pex = block_excl_scan_dpp<kMwThreads>(inc_tot, 0ll, [](long long a, long long b) { return a + b; }, S.wl, &ptot);
+    (void)lane;
+    {
+        int st4 = xex & 15;
+        long long P = pex;
+        int hk = hbase;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) {
+            const int j = base + a;
+            const bool act = j < mc && v[a] != 0.0 && !hd[a];
+            if (hd[a]) { S.h_idx[hk] = j; S.h_e[hk] = E[a]; S.h_p[hk] = P; ++hk; }
+            long long inc = 0;
+            if (act) {
+                if (tb[a].tie) {
+                    if (st4 & 8) inc = tb[a].f + (((st4 >> 1) ^ static_cast<int>(tb[a].f)) & 1);
+                    else {
+                        inc = tb[a].f;
+                        if (hk > 0) S.h_c1[hk - 1] = 2 | (((st4 >> 1) ^ static_cast<int>(tb[a].f)) & 1);
+                    }
+                } else {
+                    inc = tb[a].f + tb[a].up;
+                }
+            }
+            P += inc;
+            st4 = xs_op(st4, bits_of(a));
         }
     }
     __syncthreads();
+    const size_t rb = static_cast<size_t>(c) * kMwmCap;
     for (int k = tid; k < htot; k += kMwThreads) {
-        const int hi = S.h_idx[k], E = S.h_e[k];
-        const long long hp = S.h_p[k];
+        const int hi = S.h_idx[k], E0 = S.h_e[k];
         const bool last = k + 1 >= htot;
         const int hend = last ? mc : S.h_idx[k + 1];
-        const long long Q = (last ? ptot : S.h_p[k + 1]) - hp;
+        const long long D = (last ? ptot : S.h_p[k + 1]) - S.h_p[k];
+        const int cc = S.h_c1[k];
+        const long long d0 = D + ((cc & 2) ? (cc & 1) : 0), d1 = D + ((cc & 2) ? ((cc & 1) ^ 1) : 0);
         int flag = hend > hi + 1 ? 0 : 1;
-        double dq = -0.0, dlo = __builtin_inf(), dhi = -__builtin_inf();
+        double dq = -0.0, dq1 = -0.0, dlo = __builtin_inf(), dhi = -__builtin_inf(), dhi1 = -__builtin_inf();
         if (!flag) {
-            if (E >= -1000 && Q >= 0 && Q < (1ll << 53)) {
-                const double u = ldexp(1.0, E - 52);
-                dq = static_cast<double>(Q) * u;
-                dlo = ldexp(1.0, E);
-                dhi = (ldexp(1.0, E + 1) - u) - dq;            // exact: multiples of u below 2^(E+1)
+            if (E0 >= -1000 && D >= 0 && d0 < (1ll << 53) && d1 < (1ll << 53)) {
+                const double u = ldexp(1.0, E0 - 52), top = ldexp(1.0, E0 + 1) - u;
+                dq = static_cast<double>(d0) * u;
+                dq1 = static_cast<double>(d1) * u;
+                dlo = ldexp(1.0, E0);
+                dhi = top - dq;                                // exact: multiples of u below 2^(E0+1)
+                dhi1 = top - dq1;
             } else {
                 flag = kMwFail;
             }
@@ -1301,8 +1328,10 @@ __global__ __launch_bounds__(kMwThreads) void k_mwm_classify(const double* __res
         B.flag[r] = flag;
         B.x[r] = mwm_term<SQ>(sorted, c0 + hi, cnt, m);
         B.dq[r] = dq;
+        B.dq1[r] = dq1;
         B.dlo[r] = dlo;
         B.dhi[r] = dhi;
+        B.dhi1[r] = dhi1;
     }
     if (tid == 0) B.nh[c] = htot;
 }
@@ -1324,14 +1353,16 @@ __global__ __launch_bounds__(256) void k_mwm_compact(const DevState* st, MwmBuf 
         B.c_flag[off + k] = B.flag[src + k];
         B.c_x[off + k] = B.x[src + k];
         B.c_dq[off + k] = B.dq[src + k];
+        B.c_dq1[off + k] = B.dq1[src + k];
         B.c_dlo[off + k] = B.dlo[src + k];
         B.c_dhi[off + k] = B.dhi[src + k];
+        B.c_dhi1[off + k] = B.dhi1[src + k];
     }
     if (c == nc - 1) {                                         // no-op records after the last head
         if (tid < kMwPad) {
             const int r = off + h + tid;
-            B.c_idx[r] = 0; B.c_end[r] = 0; B.c_flag[r] = 1; B.c_x[r] = -0.0; B.c_dq[r] = -0.0;
-            B.c_dlo[r] = 0.0; B.c_dhi[r] = 0.0;
+            B.c_idx[r] = 0; B.c_end[r] = 0; B.c_flag[r] = 1; B.c_x[r] = -0.0; B.c_dq[r] = -0.0; B.c_dq1[r] = -0.0;
+            B.c_dlo[r] = 0.0; B.c_dhi[r] = 0.0; B.c_dhi1[r] = 0.0;
         }
         if (tid == 0) B.cnt[2] = off + h;
     }
@@ -1380,11 +1411,13 @@ __global__ __launch_bounds__(64) void k_mwm_walk(const double* __restrict__ sort
     if (mwm_skip(st, B)) return;
     const int lane = threadIdx.x, cnt = B.cnt[0], total = B.cnt[2];
     const double m = SQ ? B.res[0] / cnt : 0.0;
-    struct Win { int hi, end, flag; double x, dq, dlo, dhi; };
+    struct Win { int hi, end, flag; double x, dq, dq1, dlo, dhi, dhi1; };
     auto load = [&](int k0) {                                  // records past the last head are no-ops (kMwPad)
         const int k = k0 + lane;
-        return Win{B.c_idx[k], B.c_end[k], B.c_flag[k], B.c_x[k], B.c_dq[k], B.c_dlo[k], B.c_dhi[k]};
+        return Win{B.c_idx[k], B.c_end[k], B.c_flag[k], B.c_x[k], B.c_dq[k], B.c_dq1[k], B.c_dlo[k], B.c_dhi[k], B.c_dhi1[k]};
     };
+    // the segment's increments for Q's parity at its start: the low bit of the mantissa of the sum after the head
+    auto odd = [](double v) { return (__double2loint(v) & 1) != 0; };
     double s = 0.0;
     int fbs = 0, fbt = 0;
 #ifdef LO_EXACT_STAMPS
@@ -1397,21 +1430,24 @@ __global__ __launch_bounds__(64) void k_mwm_walk(const double* __restrict__ sort
 #define LO_TT1
 #endif
     __shared__ double2 s_xd[64];                               // the window's (x, dq), read back as broadcasts
+    __shared__ double s_d1[64];                                //   and dq1
     auto process = [&](const Win& cur, int k0) {
         double rec = 0.0;
         s_xd[lane] = make_double2(cur.x, cur.dq);
+        s_d1[lane] = cur.dq1;
         __syncthreads();
         LO_TT0
 #pragma unroll
         for (int l = 0; l < 64; ++l) {
             const double2 xd = s_xd[l];
+            const double d1 = s_d1[l];
             s = s + xd.x;
             rec = lane == l ? s : rec;
-            s = s + xd.y;
+            s = s + (odd(s) ? d1 : xd.y);
         }
         LO_TT1
         __syncthreads();
-        const bool ok = cur.flag == 1 || (cur.flag == 0 && rec >= cur.dlo && rec <= cur.dhi);
+        const bool ok = cur.flag == 1 || (cur.flag == 0 && rec >= cur.dlo && rec <= (odd(rec) ? cur.dhi1 : cur.dhi));
         const unsigned long long badm = __ballot(!ok);
         if (badm) {
             const int f = __builtin_ctzll(badm);
@@ -1424,8 +1460,8 @@ __global__ __launch_bounds__(64) void k_mwm_walk(const double* __restrict__ sort
             for (int l = f + 1; l < mw; ++l) {
                 s = s + rl64d(cur.x, l);
                 const int fl = __builtin_amdgcn_readlane(cur.flag, l);
-                const bool okl = fl == 1 || (fl == 0 && s >= rl64d(cur.dlo, l) && s <= rl64d(cur.dhi, l));
-                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) s = s + rl64d(cur.dq, l);
+                const bool okl = fl == 1 || (fl == 0 && s >= rl64d(cur.dlo, l) && s <= (odd(s) ? rl64d(cur.dhi1, l) : rl64d(cur.dhi, l)));
+                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) s = s + (odd(s) ? rl64d(cur.dq1, l) : rl64d(cur.dq, l));
                 else {
                     s = walk_terms_m<SQ>(sorted, __builtin_amdgcn_readlane(cur.hi, l) + 1,
                                          __builtin_amdgcn_readlane(cur.end, l), cnt, m, s);
@@ -1479,8 +1515,8 @@ void launch_mwm_scale(KParams P, const double* sorted, const MwmBuf& B, hipStrea
 }
 size_t mwm_bytes(int n_cap) {
     const size_t nc = static_cast<size_t>(std::max(1, (n_cap + kMwChunk - 1) / kMwChunk)), rec = nc * kMwmCap;
-    return (2 * rec + kMwPad) * (3 * sizeof(int) + 4 * sizeof(double)) + nc * (sizeof(int) + sizeof(double)) + 64 +
-           20 * 256;
+    return (2 * rec + kMwPad) * (3 * sizeof(int) + 6 * sizeof(double)) + nc * (sizeof(int) + sizeof(double)) + 64 +
+           24 * 256;
 }
 MwmBuf mwm_layout(void* mem, int n_cap) {
     MwmBuf B{};
@@ -1489,12 +1525,16 @@ MwmBuf mwm_layout(void* mem, int n_cap) {
     auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) / 256 * 256; return q; };
     B.x = reinterpret_cast<double*>(take(rec * 8));
     B.dq = reinterpret_cast<double*>(take(rec * 8));
+    B.dq1 = reinterpret_cast<double*>(take(rec * 8));
     B.dlo = reinterpret_cast<double*>(take(rec * 8));
     B.dhi = reinterpret_cast<double*>(take(rec * 8));
+    B.dhi1 = reinterpret_cast<double*>(take(rec * 8));
     B.c_x = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
     B.c_dq = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.c_dq1 = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
     B.c_dlo = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
     B.c_dhi = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
+    B.c_dhi1 = reinterpret_cast<double*>(take((rec + kMwPad) * 8));
     B.csum = reinterpret_cast<double*>(take(nc * 8));
     B.res = reinterpret_cast<double*>(take(16));
     B.idx = reinterpret_cast<int*>(take(rec * 4));

@@ -756,26 +756,31 @@ namespace lo {
 
 // Long non-negative fp64 sums across the chip (the iteration-0 scale of scans beyond kExactMaxPoints: the sorted
 // residuals' sum, then the sum of (r - mean)^2 -- IterativeClosestPointOptimizer.cpp:304-316).  mono_seq_sum's method
-// spread like the signed columns above: chunk sums -> classification (heads at predicted binade changes and halfway
-// ties, integer prefix sums) -> compaction -> one wave walking the heads.  A mono segment's check is exact and needs no
-// prediction bound: the sum right after the head's step lies in [2^E, 2^(E+1) - u - u * Q].
-constexpr int kMwmCap = kMwChunk;                  // mono: every term may head (halfway ties are common: residuals
-                                                   // carry ~40 significant bits), so no chunk runs term by term
+// spread like the signed columns above: chunk sums -> classification (heads at predicted binade changes, integer
+// prefix sums; halfway ties inside a segment as mono_sum_tx's two-state segments: the record carries the segment's
+// increments for either parity of Q at its start) -> compaction -> one wave walking the heads.  A mono segment's check
+// is exact and needs no prediction bound: the sum right after the head's step lies in [2^E, 2^(E+1) - u - u * d_p],
+// p = that sum's mantissa parity.
+constexpr int kMwmCap = kMwChunk;                  // mono: every term may head, so no chunk runs term by term
 struct MwmBuf {
     int* idx;          // records as classified, [chunk][kMwCap]
     int* end;
     int* flag;         // 1: passes any check, kMwFail: never passes, else 0
     double* x;         // the head's own term
-    double* dq;        // u * Q (-0 for a one-term segment)
-    double* dlo;       // the check's interval on the sum right after the head's step
+    double* dq;        // u * d_0: the segment's increments when Q is even at its start (-0 for a one-term segment)
+    double* dq1;       // u * d_1: ... when Q is odd
+    double* dlo;       // the check's interval on the sum right after the head's step: [dlo, dhi_p]
     double* dhi;
+    double* dhi1;
     int* c_idx;        // compacted in walk order
     int* c_end;
     int* c_flag;
     double* c_x;
     double* c_dq;
+    double* c_dq1;
     double* c_dlo;
     double* c_dhi;
+    double* c_dhi1;
     int* nh;           // heads per chunk
     double* csum;      // chunk sums (fp64)
     int* cnt;          // [0]: accepted residuals (the finite prefix of the sorted array); [1]: any NaN; [2]: heads in total

@@ -1,0 +1,7 @@
+cd /root/repo && export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) echo "fatal rc $1 in $2"; exit 4;; esac; }
+timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_exact.py tests/test_gpu_seqsum.py tests/test_gpu_bench_workload.py > gpurun_out/t3.log 2>&1
+rc=$?; echo "tests rc $rc"; fatal $rc tests; [ $rc -eq 0 ] || exit 3
+LO_ICP_LIB=lidar_odometry_amd/liblo_icp_diagx.so timeout -k 10 400 python scripts/exact_stamps.py --config patch1m > gpurun_out/st_1m.log 2>&1
+rc=$?; echo "stamps rc $rc"; fatal $rc stamps
+bash scripts/gpu_r05_prof.sh patch1m exact 40
