@@ -478,15 +478,19 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
     tab_bytes = 32 * 4 * vm.surfel_count()
     ws = sum(len(p) * (12 + 4 + 8) for p in scans) + n_scans * tab_bytes
     # isolated: one launch per call, no set-up pass, round-robin over the scans (each last touched n_scans - 1 ago)
-    iso_us, iso_bytes = [], []
+    # timed two ways: the launch's own span (lo_bench_kernel 5: first block's start to last block's end, what a kernel
+    # trace reports) and HIP events around the single launch (4: adds the dispatch latency, several us here)
+    iso_us, iso_ev_us, iso_bytes = [], [], []
     for r in range(4):
-        for i, o in enumerate(ctxs):
-            ms = C.c_float(0.0)
-            assert L.lo_bench_kernel(o.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]),
-                                     C.c_double(it0[i][0]), C.c_double(it0[i][1]), 4, 1, C.byref(ms)) == 0
-            if r > 0:
-                iso_us.append(ms.value * 1e3)
-                iso_bytes.append(alg[i])
+        for kid in (5, 4):
+            for i, o in enumerate(ctxs):
+                ms = C.c_float(0.0)
+                assert L.lo_bench_kernel(o.ctx, C.c_void_p(d_scans[i].data_ptr()), d_scans[i].shape[0], fptr(inits[i]),
+                                         C.c_double(it0[i][0]), C.c_double(it0[i][1]), kid, 1, C.byref(ms)) == 0
+                if r > 0 and ms.value > 0:
+                    (iso_us if kid == 5 else iso_ev_us).append(ms.value * 1e3)
+                    if kid == 5:
+                        iso_bytes.append(alg[i])
     iso_t = float(np.mean(iso_us))
     iso_ach = float(np.mean(iso_bytes)) / (iso_t * 1e-6) / 1e9
 
@@ -507,14 +511,18 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
         L.lo_set_stage_timing(o.ctx, 1)
     for _ in range(3):
         enqueue_round()
-    tot_us = n_in = 0.0
+    tot_us = n_in = tot_ev = n_ev = 0.0
     for o in ctxs:
         us, cnt = C.c_double(0.0), C.c_int(0)
-        assert L.lo_stage_time(o.ctx, C.byref(us), C.byref(cnt)) == 0
+        assert L.lo_stage_span(o.ctx, C.byref(us), C.byref(cnt)) == 0
         tot_us += us.value * cnt.value
         n_in += cnt.value
+        assert L.lo_stage_time(o.ctx, C.byref(us), C.byref(cnt)) == 0
+        tot_ev += us.value * cnt.value
+        n_ev += cnt.value
         L.lo_set_stage_timing(o.ctx, 0)
     in_t = tot_us / max(n_in, 1)
+    in_ev = tot_ev / max(n_ev, 1)
     in_ach = float(np.mean(alg)) / (in_t * 1e-6) / 1e9 if in_t > 0 else None
     for o in ctxs:
         o.close()
@@ -536,11 +544,15 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
                          "alg_bytes_per_launch": float(np.mean(alg)), "launches": len(iso_us),
                          "traffic": traffic_live["hbm_bytes_per_launch"] if traffic_live else None,
                          "traffic_live": traffic_live,
-                         "timing": "single launches (lo_bench_kernel id 4: no set-up pass), HIP events, each scan "
-                                   f"last touched {n_scans - 1} scans earlier"},
+                         "kernel_us_events": float(np.mean(iso_ev_us)) if iso_ev_us else None,
+                         "timing": "single launches with no set-up pass, each scan last touched "
+                                   f"{n_scans - 1} scans earlier; kernel_us = the launch's own span (first block's start "
+                                   "to last block's end, s_memrealtime in k_correspond: lo_bench_kernel 5), "
+                                   "kernel_us_events = HIP events around the launch (adds the dispatch latency)"},
             "in_step": {"kernel_us": in_t, "achieved": in_ach, "frac": in_ach / HBM_PEAK_GBS if in_ach else None,
-                        "scans": int(n_in),
-                        "timing": "each scan's first correspondence launch inside its GN loop (HIP events)"}}
+                        "scans": int(n_in), "kernel_us_events": in_ev,
+                        "timing": "each scan's first correspondence launch inside its GN loop: its own span "
+                                  "(lo_stage_span); kernel_us_events = HIP events around it (lo_stage_time)"}}
 
 
 # --------------------------------------------------------------------------------------------------
@@ -548,6 +560,7 @@ def c5_hbm_leg(local: int, dev, n_scans: int, pmc: bool = False, mode: str = "ex
 # --------------------------------------------------------------------------------------------------
 def run_e2e(args, world, rank, local):
     import torch
+    kd = args.config == "kitti_e2e_kdtree"
     from lidar_odometry_amd import synth
     from lidar_odometry_amd.odometry import LidarOdometry
     n_frames = 60
@@ -562,7 +575,8 @@ def run_e2e(args, world, rank, local):
         pinned.append(a)
 
     def epoch(timed, scans=pinned):
-        od = LidarOdometry(device=local, initial_pose=seq.poses[0], exact=args.mode == "exact")
+        od = LidarOdometry(device=local, initial_pose=seq.poses[0], exact=args.mode == "exact",
+                           use_surfel_correspondence=not kd)
         dt, poses, kf, dev_ms, map_ms = 0.0, [], 0, 0.0, 0.0
         try:
             for r in scans:
@@ -604,7 +618,9 @@ def run_e2e(args, world, rank, local):
         "dtype": "f32 (pose, J, H) + f64 (residuals, PKO)",
         "data": "synthetic raw HDL-64 sequence from rest (60 frames), raw scans in pinned host memory (lo_host_alloc)",
         "config": {"workload": "Estimator::process_frame loop (no loop closure / PGO), config/kitti.yaml, device filter + ICP, "
-                               "device-resident VoxelMap update at keyframes (lo_devmap)",
+                               "device-resident VoxelMap update at keyframes (lo_devmap)" +
+                               (", KDTree correspondences (RebuildKdTree as a device grid from the map's L0 centroids, "
+                                "lo_devmap_sync_points)" if kd else ", surfel correspondences"),
                    "raw_points_per_frame_avg": float(np.mean([len(r) for r in raws])),
                    "keyframes_per_frame": kfs / frames, "parallelism": "single GPU per sequence",
                    "mode": args.mode, "mode_note": MODE_NOTE[args.mode]},
@@ -616,7 +632,10 @@ def run_e2e(args, world, rank, local):
                         "poses_bitwise_equal": True,
                         "what": "same loop with the host VoxelMap + patch sync at keyframes (LO_HOST_MAP=1)"},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if kd:                                                    # no CPU restatement of the KDTree frame loop: parity of
+        result["parity"] = {"vs": "the same loop on the host map (host_map_ab, bitwise); the KDTree correspondence "
+                                  "stage itself is bitwise vs the oracle in tests/test_gpu_kdtree.py"}   # this loop
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not kd:
         import oracle
         t = time.perf_counter()
         n_cpu = 0
@@ -836,7 +855,7 @@ def main():
     ap.add_argument("--data-rank", type=int, default=None, help="diagnostic: build the workload of this rank")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS) + ["kitti_e2e", "kitti_loop"])
+    ap.add_argument("--config", default="kitti", choices=sorted(WORKLOADS) + ["kitti_e2e", "kitti_e2e_kdtree", "kitti_loop"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work for cpu_baseline")
     ap.add_argument("--c5", type=int, default=12,
                     help="extra measurement with --config kitti: this many distinct 1M-point scans (C5), one context "
@@ -897,10 +916,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    if args.config in ("kitti_e2e", "kitti_loop"):
+    if args.config in ("kitti_e2e", "kitti_e2e_kdtree", "kitti_loop"):
         if args.mode == "auto":           # the frame loop and the loop-closure solve: reference-exact arithmetic
             args.mode = "exact"
-        result = (run_e2e if args.config == "kitti_e2e" else run_loop)(args, world, rank, local)
+        result = (run_loop if args.config == "kitti_loop" else run_e2e)(args, world, rank, local)
         if rank == 0:
             emit(result)
         if world > 1:

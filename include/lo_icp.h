@@ -136,6 +136,9 @@ size_t lo_map_surfel_count(const lo_ctx* ctx);
  * VoxelMap::RebuildKdTree (:420-438, called at Estimator.cpp:461) with a device grid built from it.
  * Neighbour ties are broken by this order (index).  LO_ERR_STATE on a surfel-mode context. */
 int lo_map_set_points(lo_ctx* ctx, const float* xyz, size_t m);
+/* Scans re-run because a device-built KDTree grid (the device map's, lo_devmap_sync_points) met a deciding distance
+ * tie: lo_icp_result then builds the kd visit order on the host and optimizes the scan again. */
+int lo_kd_reruns(const lo_ctx* ctx);
 size_t lo_map_point_count(const lo_ctx* ctx);
 
 /* ---- the optimize boundary ----
@@ -201,6 +204,10 @@ int lo_pipeline_status(lo_ctx* ctx, int out[4]);
  * lo_stage_time syncs the stream and returns the average in-step duration (us) and the number of timed scans. */
 int lo_set_stage_timing(lo_ctx* ctx, int enable);
 int lo_stage_time(lo_ctx* ctx, double* avg_us, int* count);
+/* The same timed launches' own execution spans (surfel correspondence: first block's start to last block's end,
+ * s_memrealtime at 100 MHz inside k_correspond) -- what a kernel trace reports, without the dispatch latency the HIP
+ * events add (several us, a large share of a ~13 us 1M-point launch).  Syncs the stream. */
+int lo_stage_span(lo_ctx* ctx, double* avg_us, int* count);
 /* With stage timing on, the lead PKO workgroup also clocks its EM loop (s_memtime): out = {cycles, EM iterations, fits}
  * summed over the optimize calls since the last reset (the dominant kernel's cycles per EM iteration, measured in the
  * running GN loop).  Syncs the stream; reset != 0 zeroes the sums. */
@@ -210,7 +217,8 @@ int lo_pko_em_stats(lo_ctx* ctx, unsigned long long out[3], int reset);
 int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);
 /* Timing harness: reps back-to-back launches of one kernel (0 correspond, 1 accumulate, 2 pko, 3 solve; 4 correspond
  * without the set-up pass the others get, so a scan last touched long ago is read from HBM) on a device-resident scan
- * at pose T; writes the average device time per launch (HIP events). */
+ * at pose T; writes the average device time per launch (HIP events).  5: as 4, timed by the last launch's own span
+ * (lo_stage_span's clock: the first blocks' start to the last blocks' end; surfel correspondence only). */
 int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
                     int kernel_id, int reps, float* avg_ms);
 

@@ -92,6 +92,11 @@ int         lo_devmap_status(lo_devmap* m);
  * (also while it is still in flight).  The frame loop enqueues after every keyframe's update and polls after each
  * frame's synchronous ICP, so an aborted update is reported at the first frame tracked after it. */
 int         lo_devmap_status_async(lo_devmap* m);
+/* KDTree-mode context (use_surfel_correspondence = 0): RebuildKdTree (VoxelMap.cpp:420-438) on the device -- the
+ * context's correspondence grid rebuilt from the map's L0 centroids in L0 (GetPointCloud) order, equal to
+ * lo_map_set_points on the same points; one small readback (count, bounds) per call.  Distance ties that the
+ * reference's kd visit order would decide re-run the scan with that order (lo_kd_reruns). */
+int         lo_devmap_sync_points(lo_devmap* m);
 int         lo_devmap_status_poll(lo_devmap* m);
 /* the containers in their order (tests / GetPointCloud): L0 keys, centroids, point counts; L1 keys, surfel flag,
  * normal, centroid, planarity, child count and children keys (27 per voxel) */

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
     "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_set_pko_groups", "lo_update_config", "lo_map_sync_surfels", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
-    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters", "lo_debug_counters_ex", "lo_seq_sum_f64", "lo_seq_sum_f32",
+    "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters", "lo_debug_counters_ex", "lo_stage_span", "lo_seq_sum_f64", "lo_seq_sum_f32",
     "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
     "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
     # include/lo_map.h
@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
     "lo_voxelmap_set_device_fit", "lo_devmap_create", "lo_devmap_destroy", "lo_devmap_last_error", "lo_devmap_update",
-    "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_status", "lo_devmap_status_async", "lo_devmap_status_poll", "lo_devmap_get_l0", "lo_devmap_get_l1",
+    "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_status", "lo_devmap_status_async", "lo_devmap_status_poll", "lo_devmap_sync_points", "lo_kd_reruns", "lo_devmap_get_l0", "lo_devmap_get_l1",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
     "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
@@ -168,6 +168,8 @@ def lib():
     L.lo_devmap_status.argtypes = [vp]
     L.lo_devmap_status_async.argtypes = [vp]
     L.lo_devmap_status_poll.argtypes = [vp]
+    L.lo_devmap_sync_points.argtypes = [vp]
+    L.lo_kd_reruns.argtypes = [vp]
     L.lo_devmap_get_l0.restype = C.c_size_t
     L.lo_devmap_get_l0.argtypes = [vp, ip, fp, ip, C.c_size_t]
     L.lo_devmap_get_l1.restype = C.c_size_t
@@ -205,6 +207,7 @@ def lib():
     L.lo_set_pipeline.argtypes = [vp, C.c_int, C.c_int]
     L.lo_set_stage_timing.argtypes = [vp, C.c_int]
     L.lo_stage_time.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    L.lo_stage_span.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     L.lo_pko_em_stats.argtypes = [vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lo_icp_export_pose.argtypes = [vp, vp]
     L.lo_bench_kernel.argtypes = [vp, vp, C.c_size_t, fp, C.c_double, C.c_double, C.c_int, C.c_int, fp]

@@ -33,4 +33,11 @@ int ctx_reserve_table(lo_ctx* c, size_t min_slots, void** tab, uint32_t* log2cap
 // The device-filtered scan of the last lo_icp_optimize_raw / lo_voxel_filter_gpu: device points and the device
 // count (stream-ordered; no sync).
 int ctx_filtered_device(lo_ctx* c, const float** d_pts, const int** d_n);
+// KDTree contexts (use_surfel_correspondence = 0): the correspondence grid (lo_map_set_points' RebuildKdTree
+// equivalent) built on the device from a device point array -- the device map's L0 centroids in GetPointCloud order:
+// xyz (3 floats per point), *d_count of them (<= cap).  One small readback (count and bounds) sizes the grid; the
+// cell sort is a stable device radix sort, so the grid equals lo_map_set_points' on the same points.  No kd visit
+// order is built: a query that meets a deciding distance tie flags it, and lo_icp_result rebuilds the grid with the
+// order on the host and re-runs that scan (rare: equal distances between distinct centroids).
+int ctx_grid_from_device(lo_ctx* c, const float* d_xyz, const int* d_count, size_t cap);
 }  // namespace lo

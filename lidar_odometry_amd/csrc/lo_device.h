@@ -40,6 +40,8 @@ constexpr int kCandWords = 48;      // a candidate's solved GN step: pose[12] | 
 constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv = 46;
 // reference-exact candidates (lo_pko_body.h acc_candidate_exact): the 43 terms of a chunk's points staged term-major
 // in the PKO launch's dynamic LDS (4 consecutive rows of one term per ds_read_b128)
+constexpr int kSpanStarts = 16, kSpanEnds = 256;            // KParams::span: plain per-block stores, no atomics
+constexpr int kSpanWords = kSpanStarts + kSpanEnds;
 constexpr int kXcRegions = 3;                              // 64-point regions per chunk (one per producer wave)
 constexpr int kXcChunk = kXcRegions * kWave;              // 192 points
 constexpr int kXcPad = 16;                                 // a chunk's staged rows padded to a multiple of 16
@@ -145,6 +147,8 @@ struct KParams {
     unsigned* cand_cnt;       //   per-candidate arrivals of its W workgroups (the last one solves and re-zeroes it)
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
+    unsigned long long* span; // nullable (timing, kSpanWords): start stamps of blocks 0-15, end stamps of the last 256
+                              //   blocks of this correspondence launch, s_memrealtime (100 MHz); preset ~0 / 0
     double* res_out;          // nullable: per-point fp64 residual of the accepted correspondences (k_correspond /
                               //   k_solve_correspond), read back by the PKO sample instead of recomputing it
     float* ex_terms;          // reference-exact mode (lo_exact.hip): per point the 43 fp32 normal-equation terms

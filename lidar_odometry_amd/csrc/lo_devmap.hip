@@ -63,6 +63,8 @@ struct DM {
     uint32_t h0l, h1l, hpl;              // log2 capacities: L0 index, L1 index, per-update point / parent hashes
     float voxel, l1scale, thr;
     int factor;
+    int surfels;                         // SetComputeSurfels (Estimator.cpp:79): 0 for a KDTree-mode context -- no
+                                         //   surfel decisions, so no planarity erases (VoxelMap.cpp:182-185)
     // L0 (insertion order)
     uint64_t* k0;
     float* c0;                           // xyz per voxel
@@ -928,6 +930,7 @@ __device__ void dm_touched_one(const DM& M, int t, float* cs) {
     const int lp = idx_find(M.i1k, M.i1v, M.h1l, M.T[t]);
     M.tlp[t] = lp;
     if (lp < 0) return;                                    // cannot happen: every touched key registered above
+    if (!M.surfels) return;                                // UpdateVoxelMap returns before the surfel pass
     const int cnt = M.nk[lp];
     if (cnt < 5) { M.has[lp] = 0; return; }
     if (M.has[lp] && M.last[lp] == cnt) return;
@@ -1324,8 +1327,9 @@ lo_devmap* lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor,
         max_l0 > (size_t(1) << 26) || max_points < 1 || max_points > (size_t(1) << 24))
         return fail(LO_ERR_ARG, "bad arguments (factor 1 or 3, 16 <= max_l0 <= 2^26, max_points <= 2^24)", nullptr);
     lo_config cfg;
-    if (lo_get_config(ctx, &cfg) != LO_OK || !cfg.use_surfel_correspondence)
-        return fail(LO_ERR_ARG, "the context must use surfel correspondences", nullptr);
+    if (lo_get_config(ctx, &cfg) != LO_OK) return fail(LO_ERR_ARG, "bad context", nullptr);
+    // a KDTree-mode context reads the map's L0 centroids through its grid (lo_devmap_sync_points); the surfel table
+    // the map keeps is then unused by its ICP
     lo_devmap* m = new lo_devmap();
     m->ctx = ctx;
     m->device = lo_device(ctx);
@@ -1342,6 +1346,7 @@ lo_devmap* lo_devmap_create(lo_ctx* ctx, float voxel_size, int hierarchy_factor,
     M.l1scale = voxel_size * static_cast<float>(hierarchy_factor);
     M.thr = planarity_threshold;
     M.factor = hierarchy_factor;
+    M.surfels = cfg.use_surfel_correspondence ? 1 : 0;
     const size_t C0 = M.C0, C1 = M.C1, NP = M.NP;
     const size_t H0 = size_t(1) << M.h0l, H1 = size_t(1) << M.h1l, HP = size_t(1) << M.hpl;
     const size_t HT = std::max(HP, H0);                  // the point hash doubles as ApplyTransform's key hash
@@ -1542,6 +1547,15 @@ int lo_devmap_status(lo_devmap* m) {
     DM_HIP(m, hipStreamSynchronize(m->stream));
     if (m->h_cnt[C_ERR]) { m->err = "device map overflow / invalid key (error bits " + std::to_string(m->h_cnt[C_ERR]) + ")"; return LO_ERR_CAPACITY; }
     return LO_OK;
+}
+
+int lo_devmap_sync_points(lo_devmap* m) {
+    if (!m) return LO_ERR_ARG;
+    DM_HIP(m, hipSetDevice(m->device));
+    dm_stream(m);
+    const int rc = ctx_grid_from_device(m->ctx, m->M.c0, m->M.cnt + C_N0, static_cast<size_t>(m->M.C0));
+    if (rc != LO_OK) m->err = std::string("sync_points: ") + lo_last_error(m->ctx);
+    return rc;
 }
 
 int lo_devmap_status_async(lo_devmap* m) {

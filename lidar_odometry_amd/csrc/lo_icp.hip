@@ -109,6 +109,18 @@ struct PointGrid {
     float h = 1.0f;
 };
 
+// ctx_grid_from_device's scratch: the bounds readback, keys / values (and their sorted copies), cell counts, hipCUB temp
+struct DevGridScratch {
+    float* d_bounds = nullptr;
+    float* h_bounds = nullptr;
+    uint32_t* d_keys = nullptr;
+    size_t keys_cap = 0;
+    uint32_t* d_counts = nullptr;
+    size_t counts_cap = 0;
+    unsigned char* d_tmp = nullptr;
+    size_t tmp_cap = 0;
+};
+
 struct lo_ctx {
     lo_config cfg{};
     int device = 0;
@@ -191,7 +203,10 @@ struct lo_ctx {
     float fit_thr = 0.0f;
     // KDTree variant: dense grid over the L0 centroids + per-point neighbour / plane / residual buffers
     bool kd = false;
-    PointGrid grid;                 // the map's L0 centroids (lo_map_set_points)
+    PointGrid grid;                 // the map's L0 centroids (lo_map_set_points, or ctx_grid_from_device)
+    DevGridScratch gscr;
+    bool grid_dev = false;          // the grid was built on the device (no kd visit order; ties re-run, lo_icp_result)
+    int kd_reruns = 0;              //   scans re-run with the order after such a tie (lo_kd_reruns)
     PointGrid lgrid;                // loop closure: the matched keyframe's local map (lo_icp_optimize_loop)
     uint64_t loop_reruns = 0;       //   solves rerun with the kd visit order (a deciding distance tie)
     int32_t* d_kd_nbr = nullptr;
@@ -214,6 +229,8 @@ struct lo_ctx {
     bool stage_timing = false;
     std::vector<hipEvent_t> st_ev;  // pairs: [2 i] before, [2 i + 1] after
     int st_n = 0;
+    unsigned long long* d_span = nullptr;   // in-kernel span stamps (kSpanWords per launch): stage-timed launch i at
+                                            //   kSpanWords i; lo_bench_kernel 5 at kSpanWords kStageEvents
     float T_init[12];
     size_t last_n = 0;
     bool pending = false;
@@ -666,6 +683,7 @@ void lo_destroy(lo_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->st_ev) (void)hipEventDestroy(e);
+    if (c->d_span) (void)hipFree(c->d_span);
     if (c->ev_patch) (void)hipEventDestroy(c->ev_patch);
     if (c->h_patch) (void)hipHostFree(c->h_patch);
     if (c->d_patch) (void)hipFree(c->d_patch);
@@ -1200,11 +1218,167 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
     return LO_OK;
 }
 
+}  // extern "C"
+
+namespace lo {
+// ---- the same grid built on the device (ctx_grid_from_device: the device map's L0 centroids) ----
+__global__ __launch_bounds__(1024) void k_grid_bounds(const float* __restrict__ xyz, const int* __restrict__ d_count,
+                                                     float* __restrict__ out) {
+    __shared__ float s[6][16];
+    const int m = *d_count, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = tid; i < m; i += 1024)
+        for (int a = 0; a < 3; ++a) { const float v = xyz[3 * i + a]; lo[a] = fminf(lo[a], v); hi[a] = fmaxf(hi[a], v); }
+    for (int o = 32; o > 0; o >>= 1)
+        for (int a = 0; a < 3; ++a) { lo[a] = fminf(lo[a], __shfl_xor(lo[a], o, 64)); hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], o, 64)); }
+    if (lane == 0) for (int a = 0; a < 3; ++a) { s[a][wid] = lo[a]; s[3 + a][wid] = hi[a]; }
+    __syncthreads();
+    if (tid < 6) {
+        float r = s[tid][0];
+        for (int w = 1; w < 16; ++w) r = tid < 3 ? fminf(r, s[tid][w]) : fmaxf(r, s[tid][w]);
+        out[tid] = r;
+    }
+    if (tid == 0) out[6] = __int_as_float(m);
+}
+struct GridGeom {
+    float h;
+    int org[3], dim[3];
+};
+// grid_build's cell of a coordinate: floor(v / h) in fp32, as an int64 (the same operations)
+__device__ __forceinline__ long long grid_cell(float v, float h) { return static_cast<long long>(floorf(v / h)); }
+__global__ void k_grid_keys(const float* __restrict__ xyz, const int* __restrict__ d_count, GridGeom g,
+                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *d_count) return;
+    const long long x = grid_cell(xyz[3 * i], g.h) - g.org[0], y = grid_cell(xyz[3 * i + 1], g.h) - g.org[1],
+                    z = grid_cell(xyz[3 * i + 2], g.h) - g.org[2];
+    const uint32_t lin = static_cast<uint32_t>((static_cast<unsigned long long>(z) * g.dim[1] + y) * g.dim[0] + x);
+    keys[i] = lin;
+    vals[i] = static_cast<uint32_t>(i);
+    atomicAdd(&counts[lin], 1u);
+}
+__global__ void k_grid_scatter(const float* __restrict__ xyz, const int* __restrict__ d_count,
+                               const uint32_t* __restrict__ svals, float4* __restrict__ pts) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= *d_count) return;
+    const uint32_t i = svals[p];
+    pts[p] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __int_as_float(static_cast<int>(i)));
+}
+
+int ctx_grid_from_device(lo_ctx* c, const float* d_xyz, const int* d_count, size_t cap) {
+    if (!c || !d_xyz || !d_count) return LO_ERR_ARG;
+    if (!c->kd) { c->err = "ctx_grid_from_device: a KDTree-mode context"; return LO_ERR_STATE; }
+    LO_HIP(c, hipSetDevice(c->device));
+    PointGrid& G = c->grid;
+    DevGridScratch& S = c->gscr;
+    if (!S.d_bounds) LO_HIP(c, hipMalloc(&S.d_bounds, 8 * sizeof(float)));
+    if (!S.h_bounds) LO_HIP(c, hipHostMalloc(&S.h_bounds, 8 * sizeof(float), hipHostMallocDefault));
+    hipLaunchKernelGGL(k_grid_bounds, dim3(1), dim3(1024), 0, c->stream, d_xyz, d_count, S.d_bounds);
+    LO_HIP(c, hipMemcpyAsync(S.h_bounds, S.d_bounds, 8 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    int mi = 0;
+    std::memcpy(&mi, &S.h_bounds[6], sizeof(int));
+    const size_t m = static_cast<size_t>(std::max(mi, 0));
+    if (m > cap) { c->err = "ctx_grid_from_device: count beyond the array"; return LO_ERR_CAPACITY; }
+    // grid_build's geometry loop, from the bounds (floor(v / h) is monotone in v, so the cells' extremes are the
+    // extremes' cells)
+    float h = 2.0f * c->cfg.voxel_size;
+    int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
+    auto cell = [&](float v) { return static_cast<int64_t>(std::floor(v / h)); };
+    for (;;) {
+        int64_t lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = m ? cell(S.h_bounds[a]) : 0;
+            hi[a] = m ? cell(S.h_bounds[3 + a]) : 0;
+        }
+        size_t ncell = 1;
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) {
+            const int64_t d = hi[a] - lo[a] + 1;
+            if (d > static_cast<int64_t>(kKdMaxCells) || lo[a] < INT32_MIN / 2 || hi[a] > INT32_MAX / 2) { ok = false; break; }
+            ncell *= static_cast<size_t>(d);
+            if (ncell > kKdMaxCells) { ok = false; break; }
+        }
+        if (ok) { for (int a = 0; a < 3; ++a) { org[a] = static_cast<int>(lo[a]); dim[a] = static_cast<int>(hi[a] - lo[a] + 1); } break; }
+        h *= 2.0f;
+    }
+    const size_t ncell = static_cast<size_t>(dim[0]) * dim[1] * dim[2];
+    auto grow = [&](auto*& p, size_t& capv, size_t need) -> int {
+        if (need <= capv) return LO_OK;
+        if (p) LO_HIP(c, hipFree(p));
+        p = nullptr;
+        LO_HIP(c, hipMalloc(&p, need * sizeof(*p)));
+        capv = need;
+        return LO_OK;
+    };
+    const size_t mm = std::max<size_t>(m, 1);
+    int rc;
+    if ((rc = grow(G.d_pts, G.pts_cap, mm)) != LO_OK) return rc;
+    if ((rc = grow(G.d_start, G.start_cap, ncell + 1)) != LO_OK) return rc;
+    if ((rc = grow(S.d_keys, S.keys_cap, 4 * mm)) != LO_OK) return rc;       // keys, vals, sorted keys, sorted vals
+    if ((rc = grow(S.d_counts, S.counts_cap, ncell + 1)) != LO_OK) return rc;
+    uint32_t *keys = S.d_keys, *vals = keys + mm, *skeys = vals + mm, *svals = skeys + mm;
+    int bits = 1;
+    while (bits < 32 && (size_t(1) << bits) < ncell) ++bits;
+    size_t tmp_sort = 0, tmp_scan = 0;
+    LO_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, keys, skeys, vals, svals, static_cast<int>(mm), 0, bits,
+                                                 c->stream));
+    LO_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, S.d_counts, G.d_start, static_cast<int>(ncell + 1),
+                                               c->stream));
+    if ((rc = grow(S.d_tmp, S.tmp_cap, std::max(tmp_sort, tmp_scan))) != LO_OK) return rc;
+    LO_HIP(c, hipMemsetAsync(S.d_counts, 0, (ncell + 1) * sizeof(uint32_t), c->stream));
+    GridGeom g{h, {org[0], org[1], org[2]}, {dim[0], dim[1], dim[2]}};
+    if (m > 0) {
+        const dim3 grid((m + 255) / 256), blk(256);
+        hipLaunchKernelGGL(k_grid_keys, grid, blk, 0, c->stream, d_xyz, d_count, g, keys, vals, S.d_counts);
+        size_t t = S.tmp_cap;
+        LO_HIP(c, hipcub::DeviceRadixSort::SortPairs(S.d_tmp, t, keys, skeys, vals, svals, static_cast<int>(m), 0, bits,
+                                                     c->stream));
+        hipLaunchKernelGGL(k_grid_scatter, grid, blk, 0, c->stream, d_xyz, d_count, svals, G.d_pts);
+    }
+    size_t t2 = S.tmp_cap;                               // start[cell] = points in the cells before it; start[ncell] = m
+    LO_HIP(c, hipcub::DeviceScan::ExclusiveSum(S.d_tmp, t2, S.d_counts, G.d_start, static_cast<int>(ncell + 1), c->stream));
+    LO_HIP(c, hipGetLastError());
+    G.m = static_cast<int>(m);
+    G.has_order = false;
+    G.h = h;
+    for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
+    c->grid_dev = true;
+    return LO_OK;
+}
+
+}  // namespace lo
+
+extern "C" {
+
 int lo_map_set_points(lo_ctx* c, const float* xyz, size_t m) {
     if (!c) return LO_ERR_ARG;
     if (!c->kd) { c->err = "lo_map_set_points needs use_surfel_correspondence = 0"; return LO_ERR_STATE; }
+    c->grid_dev = false;
     return grid_build(c, c->grid, xyz, m);
 }
+
+// The kd visit order for a device-built grid (ctx_grid_from_device): its points back in index order (each grid
+// point carries its index), then the host build with the order -- the same grid plus the order.
+static int grid_add_order(lo_ctx* c) {
+    PointGrid& G = c->grid;
+    const size_t m = static_cast<size_t>(G.m);
+    std::vector<float4> p(std::max<size_t>(m, 1));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    if (m > 0) LO_HIP(c, hipMemcpy(p.data(), G.d_pts, m * sizeof(float4), hipMemcpyDeviceToHost));
+    std::vector<float> xyz(3 * std::max<size_t>(m, 1));
+    for (size_t k = 0; k < m; ++k) {
+        int i;
+        std::memcpy(&i, &p[k].w, sizeof(int));
+        if (i < 0 || static_cast<size_t>(i) >= m) { c->err = "device grid: bad point index"; return LO_ERR_STATE; }
+        xyz[3 * i] = p[k].x; xyz[3 * i + 1] = p[k].y; xyz[3 * i + 2] = p[k].z;
+    }
+    const int rc = grid_build(c, G, xyz.data(), m, true);
+    if (rc == LO_OK) c->grid_dev = true;                 // still the device map's grid (the next keyframe rebuilds it)
+    return rc;
+}
+
+int lo_kd_reruns(const lo_ctx* c) { return c ? c->kd_reruns : -1; }
 
 size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->grid.m) : 0; }
 
@@ -1235,7 +1409,13 @@ static_assert(kExactMaxPoints >= 2 * kExactMergeMax, "d_ex_rank holds the presor
 static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd, int with_stats = 1) {
     const bool timed = c->stage_timing && c->st_n < kStageEvents;
     if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n], c->stream);
-    launch_correspond(c, P0, with_stats, kd);
+    if (timed && !kd && c->d_span) {                     // and its own execution span (k_correspond, P.span)
+        KParams Pt = P0;
+        Pt.span = c->d_span + static_cast<size_t>(kSpanWords) * c->st_n;
+        launch_correspond(c, Pt, with_stats, kd);
+    } else {
+        launch_correspond(c, P0, with_stats, kd);
+    }
     if (timed) (void)hipEventRecord(c->st_ev[2 * c->st_n++ + 1], c->stream);
 }
 
@@ -1487,6 +1667,23 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
         LO_HIP(c, hipStreamSynchronize(c->stream));
         c->pending = false;
         ++c->pipe_reruns;
+        status = hs->status;
+    }
+    if (c->kd && c->grid_dev && !c->grid.has_order && hs->kd_tie && c->last_n > 0) {
+        // a deciding distance tie was ranked by index (a device-built grid has no kd visit order): the order built on
+        // the host from the grid's own points, then the same scan again (its points are still the caller's)
+        int rc = grid_add_order(c);
+        if (rc != LO_OK) return rc;
+        float T0[12];
+        std::memcpy(T0, c->T_init, sizeof(T0));
+        const bool timed = c->sync_call;
+        rc = enqueue_optimize(c, c->last_pts, c->last_n, T0, c->last_ndev);
+        c->sync_call = timed;
+        if (rc != LO_OK) return rc;
+        LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
+        LO_HIP(c, hipStreamSynchronize(c->stream));
+        c->pending = false;
+        ++c->kd_reruns;
         status = hs->status;
     }
     const int iters = hs->iter;
@@ -1880,14 +2077,59 @@ int lo_pko_sample_indices(lo_ctx* c, size_t n, int32_t* out) {
     return k;
 }
 
+// start stamps ~0, end stamps 0, in every launch's record (kStageEvents + 1 records)
+static int reset_spans(lo_ctx* c) {
+    const size_t words = static_cast<size_t>(kSpanWords) * (kStageEvents + 1);
+    if (!c->d_span) LO_HIP(c, hipMalloc(&c->d_span, words * sizeof(unsigned long long)));
+    std::vector<unsigned long long> h(words, 0ull);
+    for (size_t r = 0; r < words; r += kSpanWords)
+        for (int k = 0; k < kSpanStarts; ++k) h[r + k] = ~0ull;
+    LO_HIP(c, hipMemcpyAsync(c->d_span, h.data(), h.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    return LO_OK;
+}
+
+// a launch's span record: the latest end stamp minus the earliest start stamp (0 if it did not run)
+static unsigned long long span_of(const unsigned long long* r) {
+    unsigned long long s = ~0ull, e = 0;
+    for (int k = 0; k < kSpanStarts; ++k) s = std::min(s, r[k]);
+    for (int k = 0; k < kSpanEnds; ++k) e = std::max(e, r[kSpanStarts + k]);
+    return e > s ? e - s : 0ull;
+}
+
 int lo_set_stage_timing(lo_ctx* c, int enable) {
     if (!c) return LO_ERR_ARG;
     if (enable && c->st_ev.empty()) {
         c->st_ev.resize(2 * kStageEvents, nullptr);
         for (hipEvent_t& e : c->st_ev) LO_HIP(c, hipEventCreate(&e));
     }
+    if (enable) {
+        LO_HIP(c, hipSetDevice(c->device));
+        const int rc = reset_spans(c);
+        if (rc != LO_OK) return rc;
+    }
     c->stage_timing = enable != 0;
     c->st_n = 0;
+    return LO_OK;
+}
+
+int lo_stage_span(lo_ctx* c, double* avg_us, int* count) {
+    if (!c || !avg_us) return LO_ERR_ARG;
+    *avg_us = 0.0;
+    if (count) *count = 0;
+    if (!c->d_span || c->st_n == 0) return LO_OK;
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> h(static_cast<size_t>(kSpanWords) * c->st_n);
+    LO_HIP(c, hipMemcpy(h.data(), c->d_span, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    double tot = 0.0;
+    int k = 0;
+    for (int i = 0; i < c->st_n; ++i) {
+        const unsigned long long d = span_of(h.data() + static_cast<size_t>(kSpanWords) * i);
+        if (d) { tot += static_cast<double>(d); ++k; }
+    }
+    *avg_us = k ? tot / k * 0.01 : 0.0;                  // s_memrealtime: 100 MHz
+    if (count) *count = k;
     return LO_OK;
 }
 
@@ -1963,7 +2205,8 @@ int lo_icp_export_pose(lo_ctx* c, float* d_out16) {
 
 int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
                     int kernel_id, int reps, float* avg_ms) {
-    if (!c || !d_pts || !T || !avg_ms || n == 0 || reps < 1 || kernel_id < 0 || kernel_id > 4) return LO_ERR_ARG;
+    if (!c || !d_pts || !T || !avg_ms || n == 0 || reps < 1 || kernel_id < 0 || kernel_id > 5) return LO_ERR_ARG;
+    if (kernel_id == 5 && c->kd) { c->err = "kernel 5: surfel correspondence only"; return LO_ERR_STATE; }
     if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
     LO_HIP(c, hipSetDevice(c->device));
     int rc = reset_state(c, T, scale, alpha);
@@ -1974,7 +2217,12 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     const dim3 grid(P.nb), blk(kBlock);
     // set up the inputs every kernel reads: slots / block stats (k_correspond), alpha (k_pko), partials; kernel 4 (the
     // correspondence launch with NO setup pass: its inputs not pre-read into the caches) skips it
-    if (kernel_id != 4) {
+    if (kernel_id == 5) {                                // the launches' own span (P.span), not the events'
+        rc = reset_spans(c);
+        if (rc != LO_OK) return rc;
+        P.span = c->d_span + static_cast<size_t>(kSpanWords) * kStageEvents;
+    }
+    if (kernel_id < 4) {
         launch_correspond(c, P, 1, c->kd);
         hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0, 0);
     }
@@ -1982,7 +2230,7 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     for (int r = 0; r < reps; ++r) {
         switch (kernel_id) {
-            case 0: case 4: launch_correspond(c, P, 0, c->kd); break;         // KDTree: kNN + fallback + plane fit
+            case 0: case 4: case 5: launch_correspond(c, P, 0, c->kd); break;   // KDTree: kNN + fallback + plane fit
             case 1: hipLaunchKernelGGL(k_accumulate, dim3(P.nb_acc), blk, 0, c->stream, P, 0,
                                        P.nb_acc <= kFuseMaxBlocks ? 2 : 0); break;
             case 2: if (spec_ok(P)) launch_pko_spec(c, P, 1); else launch_pko(c, P, 1); break;
@@ -1995,6 +2243,13 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     float ms = 0.0f;
     LO_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     *avg_ms = ms / reps;
+    if (kernel_id == 5) {
+        std::vector<unsigned long long> h(kSpanWords);
+        LO_HIP(c, hipMemcpy(h.data(), c->d_span + static_cast<size_t>(kSpanWords) * kStageEvents,
+                            kSpanWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        const unsigned long long d = span_of(h.data());
+        *avg_ms = d ? static_cast<float>(static_cast<double>(d) * 1e-5) : -1.0f;   // the last launch's span
+    }
     return LO_OK;
 }
 

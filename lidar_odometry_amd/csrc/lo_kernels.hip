@@ -37,6 +37,11 @@ namespace lo {
 // The point load is issued before the DevState loads (done flag, pose) so the three latencies overlap
 // instead of serialising at the start of every wave.
 __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats, int init, int blk) {
+    // timing (P.span, lo_set_stage_timing / lo_bench_kernel 5): the launch's own execution span, without the dispatch
+    // latency a pair of HIP events around it includes -- the first blocks' starts and the last blocks' ends, plain
+    // stores (one address hit by every block's atomic serialises: ~80 us at 1M points)
+    if (P.span && threadIdx.x == 0 && blk < kSpanStarts)
+        P.span[blk] = static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime());
     const int i = blk * kBlock + threadIdx.x;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -50,6 +55,11 @@ __device__ __forceinline__ void correspond_body(const KParams& P, int with_stats
     scan_pose(P, init, blk, T);
     const uint64_t key = correspond_tail(P, T, px, py, pz, i, n, with_stats, blk);
     if (P.presort) presort_block(P.presort, blk, key);      // iteration 0, reference-exact mode (uniform branch)
+    if (P.span) {                                           // after every thread's stores of the block have issued
+        const int e = blk - (P.nb > kSpanEnds ? P.nb - kSpanEnds : 0);
+        __syncthreads();
+        if (threadIdx.x == 0 && e >= 0) P.span[kSpanStarts + e] = static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 // XCD-aware block order: the hardware hands consecutive workgroups to the 8 XCDs round-robin; logical block

@@ -37,6 +37,8 @@ static int create_keyframe(lo_odometry* o, const SE3f& pose, lo_odom_frame* info
         float T[12];
         lo::se3_to12(pose, T);
         int rc = lo_devmap_update_from_scan(o->dmap, T, o->cfg.max_range * 1.2);
+        if (rc == LO_OK && !o->cfg.icp.use_surfel_correspondence)
+            rc = lo_devmap_sync_points(o->dmap);         // RebuildKdTree (Estimator.cpp:460-462) on the device
         if (rc != LO_OK) { o->err = lo_devmap_last_error(o->dmap); return rc; }
         o->last_kf = pose;
         ++o->keyframes;
@@ -96,7 +98,7 @@ lo_odometry* lo_odom_create(const lo_odom_config* cfg, int device, int* err) {
     if (!o->map) { lo_destroy(o->icp); delete o; if (err) *err = LO_ERR_ARG; return nullptr; }
     if (cfg->icp.use_surfel_correspondence) lo_voxelmap_set_device_fit(o->map, 1);   // refits run in the sync's patch
     const char* hm = std::getenv("LO_HOST_MAP");
-    if (cfg->icp.use_surfel_correspondence && !(hm && std::atoi(hm))) {
+    if (!(hm && std::atoi(hm))) {                        // both correspondence modes (KDTree: lo_devmap_sync_points)
         int e = LO_OK;
         size_t max_l0 = size_t(1) << 21;                                   // LO_DEVMAP_MAX_L0: capacity override
         if (const char* cap = std::getenv("LO_DEVMAP_MAX_L0"); cap && std::atoll(cap) > 0) max_l0 = std::atoll(cap);

@@ -133,3 +133,33 @@ def test_map_overflow_reported_at_next_frame(monkeypatch):
             od.process(seq.scan(1))
     finally:
         od.close()
+
+
+def test_kdtree_frame_loop_device_map_matches_host_map(monkeypatch):
+    """KDTree correspondences (use_surfel_correspondence = false): the frame loop on the device map -- the map update
+    without surfel decisions (SetComputeSurfels(false), so no planarity erases) and RebuildKdTree as a device grid
+    from the L0 centroids (lo_devmap_sync_points) -- gives the same poses, bit for bit, and the same keyframes as
+    the same loop on the host map (LO_HOST_MAP=1: host VoxelMap + lo_map_set_points, kd visit order built on the
+    host)."""
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.odometry import LidarOdometry
+    n = 16
+    seq = synth.KittiLikeSequence(seed=7, n_frames=n, ramp_s=2.0)
+    raws = [seq.scan(k) for k in range(n)]
+
+    def run():
+        od = LidarOdometry(initial_pose=seq.poses[0], use_surfel_correspondence=False)
+        try:
+            return [od.process(r) for r in raws], od.keyframes
+        finally:
+            od.close()
+    dev, kf_dev = run()
+    monkeypatch.setenv("LO_HOST_MAP", "1")
+    host, kf_host = run()
+    assert kf_dev == kf_host >= 3
+    for k, ((Td, idv), (Th, ih)) in enumerate(zip(dev, host)):
+        assert idv.keyframe == ih.keyframe and idv.status == ih.status, f"frame {k}"
+        np.testing.assert_array_equal(np.asarray(Td, np.float32).view(np.uint32), np.asarray(Th, np.float32).view(np.uint32),
+                                      err_msg=f"frame {k}")
+    err = max(float(np.linalg.norm(np.asarray(T)[:3, 3] - seq.poses[k][:3, 3])) for k, (T, _) in enumerate(dev))
+    assert err < 0.05
