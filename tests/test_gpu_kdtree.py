@@ -183,3 +183,50 @@ def test_kdtree_optimize_repeatable(kd_icp):
     outs = [kd_icp.optimize(None, pts, Ti)[1] for _ in range(3)]
     for o in outs[1:]:
         np.testing.assert_array_equal(o, outs[0])
+
+
+def test_device_grid_tie_reruns_with_kd_order():
+    """A device-built grid (the device map's RebuildKdTree, lo_devmap_sync_points) carries no kd visit order: a scan
+    whose 5-NN search meets a deciding distance tie is re-run by lo_icp_result with the order built on the host, and
+    then equals, bit for bit, the same scan on the host-built grid of the same points (lo_map_set_points)."""
+    import ctypes as C
+
+    from lidar_odometry_amd import ICPConfig, IterativeClosestPointOptimizer, lib
+    from lidar_odometry_amd.voxelmap import DeviceVoxelMap, VoxelMap
+    # map points at L0 voxel centres on three orthogonal planes: the lattice makes equal distances everywhere
+    g = np.arange(-12, 12) * 0.5 + 0.25
+    A2, B2 = np.meshgrid(g, g)
+    a, b = A2.ravel(), B2.ravel()
+    c = np.full(a.size, 0.25)
+    world = np.ascontiguousarray(np.concatenate([np.stack([a, b, c - 3.0], 1), np.stack([c + 3.0, a, b], 1),
+                                                 np.stack([a, c + 3.0, b], 1)]), dtype=np.float32)
+    # the scan: points halfway between lattice neighbours, slightly off the initial pose
+    rng = np.random.default_rng(3)
+    scan = world[rng.choice(len(world), 600, replace=False)] + np.float32(0.25) * np.array([1, 0, 0], np.float32)
+    scan = np.ascontiguousarray(scan, dtype=np.float32)
+    T0 = np.eye(3, 4, dtype=np.float32)
+    T0[:, 3] = [0.02, -0.01, 0.01]
+    dev = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), max_points=4096)
+    host = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=False), max_points=4096)
+    dm = DeviceVoxelMap(dev, 0.5, 3, 0.1, max_l0=1 << 14, max_points=1 << 14)
+    try:
+        dm.update(world, np.zeros(3), 1000.0, True)
+        L = lib()
+        assert L.lo_devmap_sync_points(dm._h) == 0
+        hv = VoxelMap(0.5, 3, 0.1, False)                   # the host map without surfels: its GetPointCloud
+        hv.update(world, np.zeros(3), 1000.0, True)
+        host.set_map_points(hv.l0_cloud())
+        ok_d, T_d = dev.optimize(None, scan, T0)
+        ok_h, T_h = host.optimize(None, scan, T0)
+        assert L.lo_kd_reruns(dev.ctx) >= 1                 # the lattice forced the tie path
+        assert ok_d == ok_h
+        np.testing.assert_array_equal(np.asarray(T_d, np.float32).view(np.uint32), np.asarray(T_h, np.float32).view(np.uint32))
+        n_d, v_d, r_d = dev.find_correspondences(scan, T0)
+        n_h, v_h, r_h = host.find_correspondences(scan, T0)
+        assert n_d == n_h
+        np.testing.assert_array_equal(v_d, v_h)
+        np.testing.assert_array_equal(np.asarray(r_d).view(np.uint64), np.asarray(r_h).view(np.uint64))
+    finally:
+        dm.close()
+        dev.close()
+        host.close()
