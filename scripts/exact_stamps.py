@@ -43,7 +43,8 @@ def main():
             continue
         if len(wl["scans"][i]) <= 8192:                       # one-launch path (k_exact_scale_c): 0 start, 12 sorted,
             mrows.append([d[12] - d[0], d[1] - d[12], d[4] - d[1], d[5] - d[4], d[6] - d[5], d[2] - d[6],   # 1 terms,
-                          d[8] - d[2], d[9] - d[8], d[10] - d[9], d[3] - d[10]])                           # 2 / 3 sums
+                          d[8] - d[2], d[9] - d[8], d[10] - d[9], d[3] - d[10],                            # 2 / 3 sums
+                          d[13] - d[0], d[14] - d[13], d[15] - d[14], d[12] - d[15]])   # the sort's parts
             continue
         rows.append([d[1] - d[0], d[2] - d[1], d[3] - d[2], d[4] - d[3], d[6] - d[5], d[7] - d[6]])
         stats.append([d[14], d[8], d[9], d[10], d[11], d[12], d[13]])
@@ -51,7 +52,8 @@ def main():
         m = np.array(mrows, dtype=np.float64)
         print("one-launch exact scale, cycles per phase, mean over %d scans: counting sort %.0f  terms %.0f | mean sum: "
               "heads + xor scan %.0f  increments scan %.0f  records %.0f  walk %.0f | variance sum: heads + xor scan "
-              "%.0f  increments scan %.0f  records %.0f  walk %.0f" % (len(mrows), *m.mean(0)), flush=True)
+              "%.0f  increments scan %.0f  records %.0f  walk %.0f | sort: loads + key stats %.0f  histogram + scan + "
+              "scatter %.0f  rank in bin %.0f  write back %.0f" % (len(mrows), *m.mean(0)), flush=True)
     if not rows:
         for k, t in enumerate(stats):
             print("scan %d: %d accepted | mean sum: %d heads, %d segments / %d terms term by term | variance: %d heads, "
