@@ -304,6 +304,7 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
     KeyStat tot;
     (void)block_excl_scan_dpp<NT>(ks, KeyStat{~0ull, 0ull, 0, 0}, keystat_op, s_ks, &tot);
     const int cnt = tot.cnt;
+    LO_XSTAMP(st, 13);
     if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
     if (tot.nan) {                                           // a NaN residual (accepted: the gate keeps NaN): the mean,
         uint64_t nk = ~0ull;                                 // the variance and the scale are NaN
@@ -332,6 +333,7 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
     for (int q = 0; q < PT; ++q)
         if (key[q] < kInfKey) s_tmp[atomicAdd(&s_end[bin_of(key[q])], 1)] = key[q];
     __syncthreads();
+    LO_XSTAMP(st, 14);
     // each key's rank in its bin: the members below it, and the equal ones placed before it; every key is read before
     // any moves (the barrier), so the sorted order goes back into the same array
     uint64_t kk[PT];
@@ -352,6 +354,7 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
             pos[i] = s0 + r;
         }
     }
+    LO_XSTAMP(st, 15);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PT; ++i)

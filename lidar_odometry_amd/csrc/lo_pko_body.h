@@ -197,7 +197,11 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         // for issue with a component wave on the same SIMD in workgroups of more than 4 waves)
         __syncthreads();
         int buf = 0;
+#if defined(LO_XC_EXP) && LO_XC_EXP == 3
+        for (int em = 0; em < 1; ++em) {
+#else
         for (int em = 0; em < 100; ++em) {
+#endif
             __syncthreads();
             double change = 0.0;
 #pragma unroll
@@ -311,7 +315,12 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
         for (int s = 0; s < SPL; ++s) pv[q][s] = s_p[q * kStride + 64 * s + lane];
     int buf = 0;
     int n_em = 100;
-    for (int em = 0; em < 100; ++em) {
+#if defined(LO_XC_EXP) && LO_XC_EXP == 3
+    constexpr int kEmMax = 1;                              // diagnostic: one EM iteration (the launch without its EM)
+#else
+    constexpr int kEmMax = 100;
+#endif
+    for (int em = 0; em < kEmMax; ++em) {
         double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
@@ -1252,8 +1261,8 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     unsigned long long* dbg = nullptr;
 #ifdef LO_PKO_STAMPS
     if (wg == 0) dbg = st->dbg;
+    const unsigned long long t_launch = __builtin_amdgcn_s_memtime();   // dbg[0], stored by working launches only
 #endif
-    LO_STAMP(dbg, 0);
     // dynamic, nb ints: exclusive prefix of block counts (16-B aligned: the exact candidates read it with ds_read_b128,
     // and a misaligned 16-B LDS read is split -- the static part ends at a multiple of 8 only)
     extern __shared__ __attribute__((aligned(16))) int s_pre[];
@@ -1292,6 +1301,9 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     }
     if (lead && tid == 0) st->n_corr = nc;
     if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
+#ifdef LO_PKO_STAMPS
+    if (dbg && tid == 0) dbg[0] = t_launch;
+#endif
     LO_STAMP(dbg, 1);
     pko_fit_js<NW, ONE_WAVE>(P, B, wg, G, nc, s_scale, pf, s_pre, s_wmask, L, dbg);
 }
