@@ -707,6 +707,16 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
 }
 
 // ---- long columns across the chip (lo_seqsum.h "Long signed fp32 columns"): chunk sums -> classification -> walk ----
+// The edge margin M = 2^(E - kMwEdgeBits) of a predicted binade E (lo_seqsum.h): a term whose predicted prefix lies
+// closer to an edge heads a segment, and a segment's check allows a deviation of M minus its length's half-ulps.  A
+// narrower margin trades heads for failed checks (segments summed term by term); same-box A/B on the C5 scans
+// (`make edge`, scripts/gpu_r05_edge.sh): 9 / 10 / 11 bits -> 434 / 462 / 448 scans/s, heads per scan 355k / 225k /
+// 145k, chunks run term by term 78 / 47 / 44, failed segments 950 / 1447 / 2301 (bitwise the same).
+#ifndef LO_MW_EDGE_BITS
+#define LO_MW_EDGE_BITS 10
+#endif
+constexpr int kMwEdgeBits = LO_MW_EDGE_BITS;
+static_assert(kMwEdgeBits >= 1 && kMwEdgeBits <= 11, "a 4096-term segment must fit the margin: 2^(23 - bits) > 2049");
 __device__ __forceinline__ int mw_n(int n_cap, const int* n_dev) { return n_dev ? *n_dev : n_cap; }
 
 __global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__ col0, int ld, int n_cap,
@@ -799,7 +809,7 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict
     if (tid == 0) B.dcorr[co + c] = dtot;
 }
 
-__global__ __launch_bounds__(kMwThreads) void k_mw_classify(const float* __restrict__ col0, int ld, int n_cap,
+__global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __restrict__ col0, int ld, int n_cap,
                                                              const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
     __shared__ MwScratch S;
@@ -838,7 +848,7 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_classify(const float* __restr
         G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
         qa = 0;
         if (!(j < mc && (xv != 0.0f || j == 0))) return false;
-        const double at = fabs(T), M = ldexp(1.0, E - 9);
+        const double at = fabs(T), M = ldexp(1.0, E - kMwEdgeBits);
         const bool edge = E == kExpNone || at < ldexp(1.0, E) + M || at > ldexp(1.0, E + 1) - M;
         if (edge || E != ep || G != gp || j == 0) return true;
         const double t = ldexp(static_cast<double>(xv), 23 - E);
@@ -863,6 +873,10 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_classify(const float* __restr
             gp = G;
         }
     }
+    // the record pass below recomputes every term's classification: opaque copies of the terms keep the compiler from
+    // carrying the first pass's per-term values across the scans (190 -> fewer VGPRs, more waves per SIMD)
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) asm volatile("" : "+v"(v[a]));
     long long ptot;
     const long long pex = block_excl_scan<long long, kMwThreads>(ql, S.wl, ptot);
     int htot;
@@ -913,7 +927,7 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_classify(const float* __restr
             flag = kMwFail;
             if (E != kExpNone) {
                 const double u = ldexp(1.0, E - 23), lo = ldexp(1.0, E);
-                const double dev = ldexp(1.0, E - 9) - (static_cast<double>(hend - hi) * 0.5 + 1.0) * u - 2.0 * eps_t;
+                const double dev = ldexp(1.0, E - kMwEdgeBits) - (static_cast<double>(hend - hi) * 0.5 + 1.0) * u - 2.0 * eps_t;
                 if (dev >= 0.0) {
                     // |d - ht| <= dev, rounded inwards; the binade of the head's sign, its top end exclusive
                     const double slack = ldexp(fabs(ht) + dev, -51);

@@ -674,7 +674,7 @@ namespace lo {
 // IterativeClosestPointOptimizer.cpp:359-415).  The same idea as mono_seq_sum, for terms of either sign: while the
 // running sum s keeps its sign and binade [2^E, 2^(E+1)) in magnitude, fl(s + x) = s + u rint(x / u), u = 2^(E-23).
 // The partial sums of a segment are no longer monotone, so the prediction carries the proof: a term heads a segment
-// also when its predicted prefix T lies within M = 2^(E-9) of either edge of its binade.  Inside a segment every T_j
+// also when its predicted prefix T lies within M = 2^(E-10) of either edge of its binade (kMwEdgeBits, lo_exact.hip).  Inside a segment every T_j
 // is then at least M from the edges, and the true partial sums differ from T_j by at most |s_h - T_h| (known once the
 // walk reaches the head) + (end - h) u / 2 (one half-ulp per step) + the fp64 error of T: when that total stays below
 // M - u, every partial sum of the segment is inside the binade, one ulp from its edges, and the integer model is exact

@@ -117,9 +117,10 @@ def test_seq_sum_f32_bitwise(ctx):
 
 def test_seq_sum_f32_mostly_parallel(ctx):
     """A 1M-term column of products (the C5 normal-equation terms' shape): a small fraction of the terms head a
-    segment and almost none is summed term by term."""
+    segment and almost none is summed term by term (the edge margin 2^-10 trades heads for a few hundred failed
+    checks: kMwEdgeBits in lo_exact.hip)."""
     rng = np.random.default_rng(5)
     x = (rng.normal(0, 1, 1_000_000) * rng.normal(0, 1, 1_000_000) * 0.01).astype(np.float32)
     got, st = _dev_sum32(ctx, x)
     assert got.view(np.uint32) == _seq32(x).view(np.uint32)
-    assert 0 < st[0] < 60_000 and st[1] < 400 and st[2] == 0, st
+    assert 0 < st[0] < 60_000 and st[1] < 1000 and st[2] == 0, st
