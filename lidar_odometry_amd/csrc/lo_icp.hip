@@ -251,6 +251,7 @@ struct lo_ctx {
     uint32_t* h_broken = nullptr;   // pinned, device-mapped: the seq of the scan whose wait timed out (0: none)
     uint32_t* d_hbroken = nullptr;
     unsigned long long pipe_bound = 200000000ull;   // wait bound in 100 MHz ticks (2 s; LO_PIPE_WAIT_MS)
+    uint32_t pipe_fail_at = 0;      // test hook (LO_PIPE_FAIL_AT=k): the k-th pipelined scan's tail wait gives up at once
     unsigned pipe_timeouts = 0;     // times a wait timed out and the pipeline was switched off (lo_pipeline_status)
     unsigned pipe_reruns = 0;       // synchronous scans re-run on one stream after such a timeout
     const float* last_pts = nullptr;   // the scan in flight (a re-run after a pipeline timeout)
@@ -638,6 +639,7 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     if (const char* pp = std::getenv("LO_PIPE")) c->pipe = std::atoi(pp) != 0;
     if (const char* pm = std::getenv("LO_PIPE_MAIN")) c->pipe_main = std::max(1, std::atoi(pm));
     if (const char* pw = std::getenv("LO_PIPE_WAIT_MS")) c->pipe_bound = 100000ull * std::max(1, std::atoi(pw));
+    if (const char* pf = std::getenv("LO_PIPE_FAIL_AT")) c->pipe_fail_at = static_cast<uint32_t>(std::max(0, std::atoi(pf)));
     if (const char* pg = std::getenv("LO_PKO_GROUPS")) c->pko_groups = std::max(0, std::atoi(pg));
     if (const char* ps = std::getenv("LO_PKO_SOLO")) c->pko_solo = std::atoi(ps) != 0;
     if (const char* ex = std::getenv("LO_EXACT")) c->exact = std::atoi(ex) != 0;   // A/B runs: LO_EXACT=0 = fast mode
@@ -1585,9 +1587,9 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             if (c->exact) launch_exact_scale_any(c, P, n2, c->stream);
             for (int it = 0; it < g.max_iterations; ++it) {
                 const bool tail = it >= c->pipe_main;
-                if (it == c->pipe_main)
+                if (it == c->pipe_main)                   // bound 0: the test hook's forced timeout
                     hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin, seq, c->d_st, c->d_hbroken,
-                                       c->pipe_bound);
+                                       seq == c->pipe_fail_at ? 0ull : c->pipe_bound);
                 const hipStream_t s = tail ? c->s_tail : c->stream;
                 const KParams& Pi = tail ? Pt : (it + 1 == c->pipe_main ? Ph : P);
                 launch_pko_spec(c, Pi, it, s);

@@ -525,7 +525,8 @@ __device__ __forceinline__ void pipe_fail(uint32_t* fin, uint32_t* hbroken, uint
 }
 __global__ void k_wait_seq(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound) {
     if (threadIdx.x != 0) return;
-    if (!wait_word2(fin, fin + 1, seq, fin + 3, bound)) pipe_fail(fin, hbroken, seq, st);
+    // bound 0 (LO_PIPE_FAIL_AT, tests): the timeout path taken without waiting
+    if (bound == 0 || !wait_word2(fin, fin + 1, seq, fin + 3, bound)) pipe_fail(fin, hbroken, seq, st);
 }
 __global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound) {
     if (threadIdx.x != 0) return;

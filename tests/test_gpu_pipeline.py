@@ -215,6 +215,47 @@ def test_pipeline_tail_insufficient_queued():
         o.close()
 
 
+def test_pipeline_forced_timeout_is_deterministic(monkeypatch):
+    """The timeout path on demand (LO_PIPE_FAIL_AT=3: the third pipelined scan's tail wait gives up at once, the rest
+    wait normally): a synchronous call re-runs that scan on one stream, bit-identical to the pipeline switched off,
+    the pipeline stays off from then on, and lo_pipeline_status counts one timeout and one re-run; an async queue
+    flags exactly the forced scan's record LO_ERR_PIPELINE and keeps every other record bit-identical."""
+    cs = _cases()[:6]
+    monkeypatch.setenv("LO_PIPE", "1")
+    monkeypatch.setenv("LO_PIPE_FAIL_AT", "3")
+    o = _ctx(cs[0][0])
+    try:
+        o.set_pipeline(False)
+        ref = [_run(o, pts, Ti) for _, pts, Ti in cs]
+        o.set_pipeline(True, 2)
+        got = [_run(o, pts, Ti) for _, pts, Ti in cs]
+        st = (C.c_int * 4)()
+        o._L.lo_pipeline_status(o.ctx, st)
+        assert got == ref
+        assert st[0] == 0 and st[2] == 1 and st[3] == 1, list(st)   # off after the timeout, 1 timeout, 1 re-run
+    finally:
+        o.close()
+    import torch
+    o = _ctx(cs[0][0])
+    try:
+        d_scans = [torch.from_numpy(np.ascontiguousarray(p, np.float32).reshape(-1, 3)).to("cuda:0") for _, p, _ in cs]
+        inits = [Ti for _, _, Ti in cs]
+        order = list(range(len(cs)))
+        o.set_pipeline(False)
+        ref_q = _queued(o, d_scans, inits, order)
+        o.set_pipeline(True, 2)
+        got_q = _queued(o, d_scans, inits, order)
+        flagged = [k for k in range(len(order)) if int(got_q[k, 12]) == -5]
+        # the six scans are all pipelined: the third one's wait was forced to time out; the scans queued behind it
+        # may find the pipeline broken (flagged) -- never a silently different record
+        assert 2 in flagged and min(flagged) == 2, (flagged, got_q[:, 12])
+        for k in range(len(order)):
+            if k not in flagged:
+                np.testing.assert_array_equal(got_q[k].view(np.uint32), ref_q[k].view(np.uint32), err_msg=f"scan {k}")
+    finally:
+        o.close()
+
+
 def test_pipeline_timeout_under_counter_collection():
     """The failure the device-side waits had: under `rocprofv3 --pmc` dispatches are serialised across queues, and a
     wait can run before the work it waits for.  Forced on (LO_PIPE=1) with a 20 ms bound, a timed-out wait marks its
