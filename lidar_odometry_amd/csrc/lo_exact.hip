@@ -725,6 +725,7 @@ __global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__
     __shared__ double s_w[2][4];
     const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
+    if (mc <= 0) return;                                       // chunks past the end publish nothing
     const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
     double v = 0.0, a = 0.0;
 #pragma unroll
@@ -748,6 +749,7 @@ __global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__
 constexpr int kMwWaves = kMwThreads / kWave;
 struct MwScratch {
     double wd[kMwWaves];
+    double wd2[2 * kMwWaves];
     long long wl[kMwWaves];
     int wi[kMwWaves];
     int elast[kMwThreads];
@@ -771,6 +773,22 @@ __device__ __forceinline__ void mw_base(const MwBuf& B, size_t co, int c, double
     (void)block_excl_scan<double, kMwThreads>(a0, s_w, A);
 }
 
+// One thread's share of a chunk's modelled drift: each step's rounding in its predicted binade (tex: the predicted sum
+// before the thread's first term).
+__device__ __forceinline__ double mw_drift_terms(const float (&v)[kMwPT], double tex) {
+    double d = 0.0, tl = 0.0;
+#pragma unroll
+    for (int a = 0; a < kMwPT; ++a) {
+        tl += static_cast<double>(v[a]);
+        const int E = binade_abs(tex + tl);
+        if (E != kExpNone) {
+            const double x = static_cast<double>(v[a]);
+            d += ldexp(rint(ldexp(x, 23 - E)), E - 23) - x;
+        }
+    }
+    return d;
+}
+
 __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict__ col0, int ld, int n_cap,
                                                         const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
@@ -778,10 +796,7 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict
     const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x;
     const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
     const size_t co = static_cast<size_t>(colI) * B.nchunks;
-    if (mc <= 0) {
-        if (tid == 0) B.dcorr[co + c] = 0.0;
-        return;
-    }
+    if (mc <= 0) return;
     const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
     double T0, A;
     mw_base<false>(B, co, c, s_w, T0, A);
@@ -794,21 +809,53 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict
     for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
     double ttot;
     const double tex = T0 + block_excl_scan<double, kMwThreads>(run, s_w, ttot);
-    double d = 0.0, tl = 0.0;
-#pragma unroll
-    for (int a = 0; a < kMwPT; ++a) {                          // each step's rounding in its predicted binade
-        tl += static_cast<double>(v[a]);
-        const int E = binade_abs(tex + tl);
-        if (E != kExpNone) {
-            const double x = static_cast<double>(v[a]);
-            d += ldexp(rint(ldexp(x, 23 - E)), E - 23) - x;
-        }
-    }
     double dtot;
-    (void)block_excl_scan<double, kMwThreads>(d, s_w, dtot);
+    (void)block_excl_scan<double, kMwThreads>(mw_drift_terms(v, tex), s_w, dtot);
     if (tid == 0) B.dcorr[co + c] = dtot;
 }
 
+// Chunk values handed from one classification workgroup to the later chunks of its column inside the launch (the fused
+// path below): csum / cabs / dcorr hold kMwUnset until their chunk publishes them with an sc1 store; a reader polls
+// with sc1 loads (lo_device.h Mem<true>).  k_mw_compact puts kMwUnset back after the launch, mw_clear sets it at
+// allocation.  Computed values are never kMwUnset (a NaN is published as the canonical quiet NaN).  A wait is bounded
+// by kMwWaitTicks of the 100 MHz clock and then reads 0: any prediction is correct (the walk checks every head), a
+// wrong one only costs term-by-term segments, so no value can hang or corrupt a sum.
+constexpr unsigned long long kMwUnset = ~0ull;
+constexpr unsigned long long kMwWaitTicks = 10000000ull;      // 0.1 s
+__device__ __forceinline__ void mw_publish(double* p, double v) {
+    Mem<true>::st(p, v != v ? __builtin_bit_cast(double, 0x7FF8000000000000ull) : v);
+}
+__device__ __forceinline__ double mw_await(const double* p) {
+    unsigned long long b = Mem<true>::ld(reinterpret_cast<const unsigned long long*>(p));
+    if (b == kMwUnset) {
+        const unsigned long long t0 = wall_clock64();
+        do {
+            __builtin_amdgcn_s_sleep(1);
+            b = Mem<true>::ld(reinterpret_cast<const unsigned long long*>(p));
+        } while (b == kMwUnset && wall_clock64() - t0 <= kMwWaitTicks);
+    }
+    return b == kMwUnset ? 0.0 : __builtin_bit_cast(double, b);
+}
+// Two sums over the workgroup (every thread gets both; s_w: 2 * kMwWaves entries, free again on return).
+__device__ __forceinline__ void mw_block_sum2(double& x, double& y, double* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64); }
+    if (lane == 0) { s_w[wid] = x; s_w[kMwWaves + wid] = y; }
+    __syncthreads();
+    x = 0.0;
+    y = 0.0;
+#pragma unroll
+    for (int w = 0; w < kMwWaves; ++w) { x += s_w[w]; y += s_w[kMwWaves + w]; }
+    __syncthreads();
+}
+
+// FUSED (the default): one launch computes each chunk's sums, publishes them, takes the sums of the chunks before it from
+// their workgroups (a look-back: every workgroup waits only for lower chunks of its own column, dispatched before it),
+// then its modelled drift the same way, then classifies -- k_mw_chunk_sums and k_mw_drift fold in.  The prediction
+// base is the same quantity summed in another order (T0 = chunk sums + drift corrections of the chunks before).
+// !FUSED: the three-launch path (LO_MW_SPLIT=1, A/B).
+template <bool FUSED>
 __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __restrict__ col0, int ld, int n_cap,
                                                              const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
@@ -821,9 +868,6 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
         return;
     }
     const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
-    double T0, A;
-    mw_base<true>(B, co, c, S.wd, T0, A);
-    const double eps_t = ldexp(A + fabs(T0), -45);             // bound on the in-chunk prediction error (see above)
     const int base = tid * kMwPT;
     float v[kMwPT];
 #pragma unroll
@@ -831,8 +875,31 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
     double run = 0.0;
 #pragma unroll
     for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
-    double ttot;
-    const double tex = T0 + block_excl_scan<double, kMwThreads>(run, S.wd, ttot);
+    double T0, A, ttot, ex;
+    if constexpr (FUSED) {
+        ex = block_excl_scan<double, kMwThreads>(run, S.wd, ttot);
+        double ab = 0.0, unused = 0.0;
+#pragma unroll
+        for (int a = 0; a < kMwPT; ++a) ab += fabs(static_cast<double>(v[a]));
+        mw_block_sum2(ab, unused, S.wd2);
+        if (tid == 0) { mw_publish(B.csum + co + c, ttot); mw_publish(B.cabs + co + c, ab); }
+        double t0 = 0.0, a0 = 0.0;
+        for (int k = tid; k < c; k += kMwThreads) { t0 += mw_await(B.csum + co + k); a0 += mw_await(B.cabs + co + k); }
+        mw_block_sum2(t0, a0, S.wd2);
+        A = a0 + ab;
+        double d = mw_drift_terms(v, t0 + ex), dp = 0.0;
+        mw_block_sum2(d, dp, S.wd2);
+        if (tid == 0) mw_publish(B.dcorr + co + c, d);
+        for (int k = tid; k < c; k += kMwThreads) dp += mw_await(B.dcorr + co + k);
+        double unused2 = 0.0;
+        mw_block_sum2(dp, unused2, S.wd2);
+        T0 = t0 + dp;
+    } else {
+        mw_base<true>(B, co, c, S.wd, T0, A);
+        ex = block_excl_scan<double, kMwThreads>(run, S.wd, ttot);
+    }
+    const double eps_t = ldexp(A + fabs(T0), -45);             // bound on the in-chunk prediction error (see above)
+    const double tex = T0 + ex;
     {
         const double Tl = tex + run;
         S.elast[tid] = binade_abs(Tl);
@@ -1003,6 +1070,12 @@ __global__ __launch_bounds__(256) void k_mw_compact(int n_cap, const int* n_dev,
     int off;
     (void)block_excl_scan<int, 256>(before, s_w, off);
     const int h = B.nh[co + c];
+    if (tid == 0) {                                            // the chunk's handed-off values back to unset
+        const double u = __builtin_bit_cast(double, kMwUnset);
+        B.csum[co + c] = u;
+        B.cabs[co + c] = u;
+        B.dcorr[co + c] = u;
+    }
     const size_t src = (co + c) * kMwCap, dst = static_cast<size_t>(colI) * B.cstride + off;
     for (int k = tid; k < h; k += 256) {
         B.c_idx[dst + k] = B.idx[src + k];
@@ -1113,10 +1186,15 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
 void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
                     float* out, long long* stats, hipStream_t s) {
     const int nc = (n_cap + kMwChunk - 1) / kMwChunk;
+    static const bool split = std::getenv("LO_MW_SPLIT") != nullptr;   // A/B: the three-launch classification
     if (nc > 0) {
-        hipLaunchKernelGGL(k_mw_chunk_sums, dim3(nc, ncol), dim3(256), 0, s, col0, ld, n_cap, n_dev, st, B);
-        hipLaunchKernelGGL(k_mw_drift, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
-        hipLaunchKernelGGL(k_mw_classify, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+        if (split) {
+            hipLaunchKernelGGL(k_mw_chunk_sums, dim3(nc, ncol), dim3(256), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL(k_mw_drift, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL(k_mw_classify<false>, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+        } else {
+            hipLaunchKernelGGL(k_mw_classify<true>, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+        }
         hipLaunchKernelGGL(k_mw_compact, dim3(nc, ncol), dim3(256), 0, s, n_cap, n_dev, st, B);
     }
     hipLaunchKernelGGL(k_mw_walk, dim3(ncol), dim3(64), 0, s, col0, ld, n_cap, n_dev, st, B, out, stats);
@@ -1158,6 +1236,13 @@ MwBuf mw_layout(void* mem, int ncol, int n_cap) {
     B.nchunks = static_cast<int>(nc);
     B.cstride = nc * kMwCap + kMwPad;
     return B;
+}
+// The handed-off chunk values to kMwUnset (once per allocation; k_mw_compact keeps them so).
+hipError_t mw_clear(const MwBuf& B, int ncol, hipStream_t s) {
+    const size_t per = static_cast<size_t>(ncol) * B.nchunks;
+    const char* lo = reinterpret_cast<const char*>(B.csum);
+    const char* hi = reinterpret_cast<const char*>(B.dcorr + per);
+    return hipMemsetAsync(B.csum, 0xFF, static_cast<size_t>(hi - lo), s);
 }
 
 // ---- long mono sums: the iteration-0 scale of scans beyond kExactMaxPoints (lo_seqsum.h MwmBuf) ----

@@ -79,6 +79,7 @@ void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n
                     float* out, long long* stats, hipStream_t s);
 size_t mw_bytes(int ncol, int n_cap);
 MwBuf mw_layout(void* mem, int ncol, int n_cap);
+hipError_t mw_clear(const MwBuf& B, int ncol, hipStream_t s);
 void launch_mwm_scale(KParams P, const double* sorted, const MwmBuf& B, hipStream_t s);
 size_t mwm_bytes(int n_cap);
 MwmBuf mwm_layout(void* mem, int n_cap);
@@ -1453,6 +1454,8 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
             c->mw_n_cap = n;
             LO_HIP(c, hipMalloc(&c->d_mw, mw_bytes(43, static_cast<int>(n))));
             c->mw = mw_layout(c->d_mw, 43, static_cast<int>(n));
+            LO_HIP(c, mw_clear(c->mw, 43, c->stream));
+            LO_HIP(c, hipStreamSynchronize(c->stream));
             if (c->d_mwm) LO_HIP(c, hipFree(c->d_mwm));
             c->d_mwm = nullptr;
             LO_HIP(c, hipMalloc(&c->d_mwm, mwm_bytes(static_cast<int>(n))));
@@ -2286,6 +2289,7 @@ int lo_seq_sum_f32(lo_ctx* c, const float* x, size_t n, float* out_sum, long lon
     long long* d_st = reinterpret_cast<long long*>(d + x_bytes + mwb + 64);
     hipError_t e = hipSuccess;
     if (n > 0) e = hipMemcpy(d_x, x, n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mw_clear(B, 1, c->stream);
     float ms = 0.0f;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess) e = hipEventCreate(&e0);
