@@ -781,10 +781,9 @@ __device__ __forceinline__ double mw_drift_terms(const float (&v)[kMwPT], double
     for (int a = 0; a < kMwPT; ++a) {
         tl += static_cast<double>(v[a]);
         const int E = binade_abs(tex + tl);
-        if (E != kExpNone) {
-            const double x = static_cast<double>(v[a]);
-            d += ldexp(rint(ldexp(x, 23 - E)), E - 23) - x;
-        }
+        const double x = static_cast<double>(v[a]);
+        const double q = ldexp(rint(ldexp(x, 23 - E)), E - 23) - x;   // branch-free: no binade -> not counted
+        d += E != kExpNone ? q : 0.0;
     }
     return d;
 }
@@ -913,16 +912,17 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
         const float xv = v[a];
         E = binade_abs(T);
         G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
-        qa = 0;
-        if (!(j < mc && (xv != 0.0f || j == 0))) return false;
-        const double at = fabs(T), M = ldexp(1.0, E - kMwEdgeBits);
-        const bool edge = E == kExpNone || at < ldexp(1.0, E) + M || at > ldexp(1.0, E + 1) - M;
-        if (edge || E != ep || G != gp || j == 0) return true;
-        const double t = ldexp(static_cast<double>(xv), 23 - E);
-        const double f = floor(t), fr = t - f;
-        if (fr == 0.5) return true;
-        qa = static_cast<long long>(f) + (fr > 0.5 ? 1 : 0);
-        return false;
+        // branch-free.  Edge proximity on the mantissa: |T| = 2^E (1 + m) lies within M = 2^(E - kMwEdgeBits) of an
+        // edge <=> m's top kMwEdgeBits bits are all zero, or all one with a nonzero rest
+        const uint64_t mb = __builtin_bit_cast(uint64_t, T) & ((1ull << 52) - 1);
+        const uint64_t top = mb >> (52 - kMwEdgeBits), rest = mb & ((1ull << (52 - kMwEdgeBits)) - 1);
+        const bool edge = E == kExpNone || top == 0 || (top == (1ull << kMwEdgeBits) - 1 && rest != 0);
+        const double t = ldexp(static_cast<double>(xv), 23 - E);   // |t| < 2^24 whenever the term does not head
+        const double r = rint(t);
+        const bool live = j < mc && (xv != 0.0f || j == 0);
+        const bool head = live && (edge || E != ep || G != gp || j == 0 || fabs(t - r) == 0.5);   // |t - r| = 1/2: a tie
+        qa = static_cast<long long>(static_cast<int>(live && !head ? r : 0.0));
+        return head;
     };
     long long ql = 0;
     int nhl = 0;
