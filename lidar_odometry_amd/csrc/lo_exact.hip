@@ -902,7 +902,7 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
     {
         const double Tl = tex + run;
         S.elast[tid] = binade_abs(Tl);
-        S.glast[tid] = Tl > 0.0 ? 1 : (Tl < 0.0 ? -1 : 0);
+        S.glast[tid] = static_cast<int>(__builtin_bit_cast(uint64_t, Tl) >> 63);
     }
     __syncthreads();
     const int e_in = tid ? S.elast[tid - 1] : kExpNone, g_in = tid ? S.glast[tid - 1] : 0;
@@ -910,13 +910,17 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
     auto classify = [&](int a, double T, int ep, int gp, int& E, int& G, long long& qa) -> bool {
         const int j = base + a;
         const float xv = v[a];
+        // branch-free, on T's bits.  G: the sign bit (it matters only where E and the previous E are binades -- else
+        // the term heads anyway -- and there it is the sign).  Edge proximity: |T| = 2^E (1 + m) lies within
+        // M = 2^(E - kMwEdgeBits) of an edge <=> m's top kMwEdgeBits bits are all zero, or all one with a nonzero rest
+        // (kMwEdgeBits <= 11: the top bits sit in the high word)
+        const uint64_t tb = __builtin_bit_cast(uint64_t, T);
+        const uint32_t hi = static_cast<uint32_t>(tb >> 32), lo32 = static_cast<uint32_t>(tb);
         E = binade_abs(T);
-        G = T > 0.0 ? 1 : (T < 0.0 ? -1 : 0);
-        // branch-free.  Edge proximity on the mantissa: |T| = 2^E (1 + m) lies within M = 2^(E - kMwEdgeBits) of an
-        // edge <=> m's top kMwEdgeBits bits are all zero, or all one with a nonzero rest
-        const uint64_t mb = __builtin_bit_cast(uint64_t, T) & ((1ull << 52) - 1);
-        const uint64_t top = mb >> (52 - kMwEdgeBits), rest = mb & ((1ull << (52 - kMwEdgeBits)) - 1);
-        const bool edge = E == kExpNone || top == 0 || (top == (1ull << kMwEdgeBits) - 1 && rest != 0);
+        G = static_cast<int>(hi >> 31);
+        const uint32_t top = (hi >> (20 - kMwEdgeBits)) & ((1u << kMwEdgeBits) - 1);
+        const bool rest = ((hi & ((1u << (20 - kMwEdgeBits)) - 1)) | lo32) != 0;
+        const bool edge = E == kExpNone || top == 0 || (top == (1u << kMwEdgeBits) - 1 && rest);
         const double t = ldexp(static_cast<double>(xv), 23 - E);   // |t| < 2^24 whenever the term does not head
         const double r = rint(t);
         const bool live = j < mc && (xv != 0.0f || j == 0);
@@ -1054,6 +1058,9 @@ __device__ __forceinline__ float walk_terms(const float* __restrict__ col, int j
         const float v = lane < j1 - j ? col[j + lane] : -0.0f;
         for (int l = 0; l < j1 - j; ++l) s = s + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
     }
+    // every load above complete (vmcnt(0)): a caller's loop then carries no possibly-pending register, which would make
+    // the compiler wait for ALL loads at the loop head -- the walk's next-window prefetch included
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     return s;
 }
 
@@ -1098,9 +1105,9 @@ __global__ __launch_bounds__(256) void k_mw_compact(int n_cap, const int* n_dev,
 
 // One wave per column: every head in order, a window of 64 heads at a time (the next window's records in flight).
 // The fast path adds the window's heads as a plain fp32 chain -- s += x (the head's own step), s += dq (its segment)
-// -- lane l keeping the sum right after head l's step; the 64 checks then run lane-parallel.  A failed check at head f
-// restarts from its recorded sum (exact: every earlier head passed), sums f's segment term by term and takes the rest
-// of the window head by head.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
+// -- storing the sum right after head l's step to LDS (lane l reads it back); the 64 checks then run lane-parallel.  A
+// failed check at head f restarts from its recorded sum (exact: every earlier head passed), sums f's segment term by
+// term and takes the rest of the window head by head.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
 // term-by-term run.
 __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, int ld, int n_cap, const int* n_dev,
                                                 const DevState* st, MwBuf B, float* out, long long* stats) {
@@ -1118,54 +1125,84 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
     auto rlf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
     float s = 0.0f;
     int fbs = 0, chained = 0;
-    // one window: the plain chain, the lane-parallel checks, the slow path from the first failure
+#ifdef LO_EXACT_STAMPS
+    // cycle split: chained chunks / failed segments (walk_terms) / the slow paths in all, and the whole walk
+    unsigned long long t_ch = 0, t_fs = 0, t_slow = 0;
+    const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
+#define LO_WALK_TERMS(isch, expr) do { const unsigned long long t_w0 = __builtin_amdgcn_s_memtime(); expr; \
+        const unsigned long long t_w = __builtin_amdgcn_s_memtime() - t_w0; if (isch) t_ch += t_w; else t_fs += t_w; } while (0)
+#else
+#define LO_WALK_TERMS(isch, expr) expr
+#endif
+    // one window: the plain chain, the lane-parallel checks; from a failed check at head f: its segment term by term,
+    // then the rest of the window head by head (running the chain again over the rest measured slower: 498 against
+    // 547 scans/s on the C5 scans, same box)
     __shared__ float2 s_xd[64];                                // the window's (x, dq), read back as broadcasts
-    auto process = [&](const Win& cur, int k0) {
-        float rec = 0.0f;
-        s_xd[lane] = make_float2(cur.x, cur.dq);
+    __shared__ float s_rec[64 * 64];                           // [head l][lane]: the sum right after head l's step
+    auto chain = [&]() -> float {
         __syncthreads();
+        float2 xd[64];                                         // every operand in registers before the chain starts:
+#pragma unroll                                                 // the chain's LDS stores share the loads' counter
+        for (int l = 0; l < 64; ++l) xd[l] = s_xd[l];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int l = 0; l < 64; ++l) {                          // lanes past the window's end are no-ops
-            const float2 xd = s_xd[l];
-            s = s + xd.x;
-            rec = lane == l ? s : rec;
-            s = s + xd.y;
+        for (int l = 0; l < 64; ++l) {                          // no-op records add -0: s + -0 = s bitwise
+            s = s + xd[l].x;
+            s_rec[l * 64 + lane] = s;                          // every lane its own word: no bank conflicts
+            s = s + xd[l].y;
         }
         __syncthreads();
+        return s_rec[lane * 64 + lane];
+    };
+    auto process = [&](const Win& cur, int k0) {
+        s_xd[lane] = make_float2(cur.x, cur.dq);
+        const float rec = chain();
         const double d = static_cast<double>(rec);
         const bool ok = cur.flag == 1 || (cur.flag == 0 && d >= cur.dlo && d <= cur.dhi);
         const unsigned long long badm = __ballot(!ok);
-        if (badm) {                                            // uniform
-            const int f = __builtin_ctzll(badm);
-            s = rlf(rec, f);                                   // exact: every head before f passed
-            {
-                const int h = __builtin_amdgcn_readlane(cur.hi, f), end = __builtin_amdgcn_readlane(cur.end, f);
-                chained += __builtin_amdgcn_readlane(cur.flag, f) == kMwFail && end - h > 1 ? 1 : 0;
-                s = walk_terms(col, h + 1, end, s);
+        if (!badm) return;                                     // uniform
+#ifdef LO_EXACT_STAMPS
+        const unsigned long long t_s0 = __builtin_amdgcn_s_memtime();
+#endif
+        const int f = __builtin_ctzll(badm);
+        s = rlf(rec, f);                                       // exact: every head before f passed
+        {
+            const int h = __builtin_amdgcn_readlane(cur.hi, f), end = __builtin_amdgcn_readlane(cur.end, f);
+            const bool ch = __builtin_amdgcn_readlane(cur.flag, f) == kMwFail && end - h > 1;
+            chained += ch ? 1 : 0;
+            LO_WALK_TERMS(ch, s = walk_terms(col, h + 1, end, s));
+            ++fbs;
+        }
+        const int m = min(64, total - k0);
+        for (int l = f + 1; l < m; ++l) {                      // the rest of the window head by head
+            const int h = __builtin_amdgcn_readlane(cur.hi, l), end = __builtin_amdgcn_readlane(cur.end, l);
+            s = s + rlf(cur.x, l);
+            const double dl = static_cast<double>(s);
+            const int fl = __builtin_amdgcn_readlane(cur.flag, l);
+            const bool okl = fl == 1 || (fl == 0 && dl >= rl64d(cur.dlo, l) && dl <= rl64d(cur.dhi, l));
+            if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) {
+                s = s + rlf(cur.dq, l);
+            } else {
+                const bool ch = fl == kMwFail && end - h > 1;
+                chained += ch ? 1 : 0;
+                LO_WALK_TERMS(ch, s = walk_terms(col, h + 1, end, s));
                 ++fbs;
             }
-            const int m = min(64, total - k0);
-            for (int l = f + 1; l < m; ++l) {                   // the rest of the window head by head
-                const int h = __builtin_amdgcn_readlane(cur.hi, l), end = __builtin_amdgcn_readlane(cur.end, l);
-                s = s + rlf(cur.x, l);
-                const double dl = static_cast<double>(s);
-                const int fl = __builtin_amdgcn_readlane(cur.flag, l);
-                const bool okl = fl == 1 || (fl == 0 && dl >= rl64d(cur.dlo, l) && dl <= rl64d(cur.dhi, l));
-                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) {
-                    s = s + rlf(cur.dq, l);
-                } else {
-                    chained += fl == kMwFail && end - h > 1 ? 1 : 0;
-                    s = walk_terms(col, h + 1, end, s);
-                    ++fbs;
-                }
-            }
         }
+#ifdef LO_EXACT_STAMPS
+        t_slow += __builtin_amdgcn_s_memtime() - t_s0;
+#endif
     };
-    Win cur = load(0);                                         // the next window's records in flight
-    for (int k0 = 0; k0 < total; k0 += 64) {
-        const Win nxt = load(k0 + 64);
-        process(cur, k0);
-        cur = nxt;
+#undef LO_WALK_TERMS
+    // the next window's records in flight; two windows per trip, so the loop carries no register copy of a window
+    // whose loads are in flight (a copy would wait for them)
+    Win wa = load(0);
+    for (int k0 = 0; k0 < total; k0 += 128) {
+        const Win wb = load(k0 + 64);
+        process(wa, k0);
+        if (k0 + 64 >= total) break;
+        wa = load(k0 + 128);
+        process(wb, k0 + 64);
     }
     if (lane == 0) {
         out[colI] = s;
@@ -1176,6 +1213,13 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
             atomicAdd(&w->dbg[15], static_cast<unsigned long long>(total));
             atomicAdd(&w->dbg[13], static_cast<unsigned long long>(fbs));
             atomicAdd(&w->dbg[12], static_cast<unsigned long long>(chained));
+            const unsigned long long t_all = __builtin_amdgcn_s_memtime() - t_begin;
+            atomicAdd(&w->dbg[16], t_all);
+            atomicMax(&w->dbg[17], t_all);
+            atomicAdd(&w->dbg[18], t_ch);
+            atomicAdd(&w->dbg[19], t_fs);
+            atomicAdd(&w->dbg[20], t_slow - t_ch - t_fs);
+            atomicAdd(&w->dbg[21], 1ull);
         }
 #endif
     }

@@ -454,7 +454,6 @@ __device__ __forceinline__ void walk_row(double& s, double& rec, double hx, doub
 template <int NT, int PT>
 __device__ __forceinline__ bool mono_sum_tx(const double (&x)[PT], int cnt, const double* s_x, MonoScratch<NT>& S,
                                             double& out, unsigned long long* stamps = nullptr) {
-    constexpr int NW = NT / kWave;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, base = tid * PT;
     // 1. approximate prefix (fp64): the prediction of each step's binade
     double run = 0.0;
@@ -681,11 +680,8 @@ namespace lo {
 // for each step.  Implemented across the chip for long columns below (k_mw_* in lo_exact.hip).
 // ---------------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int binade_abs(double v) {       // binade of |v| when it is a normal fp32 magnitude
-    const double a = fabs(v);
-    const uint64_t b = __builtin_bit_cast(uint64_t, a);
-    const int f = static_cast<int>((b >> 52) & 0x7FF);
-    const int e = f - 1023;
-    return (a > 0.0 && f != 0x7FF && e >= -120 && e <= 126) ? e : kExpNone;
+    const uint32_t f = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, v) >> 52) & 0x7FFu;   // biased exponent
+    return f - 903u <= 246u ? static_cast<int>(f) - 1023 : kExpNone;   // e in [-120, 126]: zero, subnormal, inf, NaN out
 }
 
 }  // namespace lo

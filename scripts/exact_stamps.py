@@ -32,14 +32,18 @@ def main():
     rows, stats, mrows = [], [], []
     for i in range(len(wl["scans"])):
         icp.optimize(None, wl["scans"][i], bench.pose12(wl["inits"][i]))
-        d = (C.c_ulonglong * 16)()
-        assert L.lo_debug_counters(icp.ctx, d) == 0
+        d = (C.c_ulonglong * 24)()
+        assert L.lo_debug_counters_ex(icp.ctx, d, 24) == 0
         if len(wl["scans"][i]) > 16384:                      # large scan: k_exact_sum43 walk statistics (cumulative)
             it = icp.get_last_stats().num_iterations
             print("scan %d: %d pts, %d iterations | sum43 cumulative: %d heads, %d segments term by term, %d chained "
                   "chunks | scale sums: %d / %d heads, %d / %d segments (%d / %d terms) term by term | mean walk %d cycles, "
                   "%d in its unrolled 64-head chains" % (i, len(wl["scans"][i]), it, d[15], d[13], d[12], d[5], d[8], d[6],
                                                          d[9], d[7], d[10], d[11], d[14]), flush=True)
+            if d[21]:
+                print("  sum43 walk cycles (cumulative, %d column walks): mean %.0f, slowest column %d | chained chunks "
+                      "%.0f, failed segments %.0f, head-by-head rest %.0f per column walk" %
+                      (d[21], d[16] / d[21], d[17], d[18] / d[21], d[19] / d[21], d[20] / d[21]), flush=True)
             continue
         if len(wl["scans"][i]) <= 8192:                       # one-launch path (k_exact_scale_c): 0 start, 12 sorted,
             mrows.append([d[12] - d[0], d[1] - d[12], d[4] - d[1], d[5] - d[4], d[6] - d[5], d[2] - d[6],   # 1 terms,
