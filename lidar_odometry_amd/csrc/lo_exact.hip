@@ -716,6 +716,7 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
 #define LO_MW_EDGE_BITS 10
 #endif
 constexpr int kMwEdgeBits = LO_MW_EDGE_BITS;
+constexpr int kMwChainAgain = 1;                              // the walk: failures per window followed by a chain
 static_assert(kMwEdgeBits >= 1 && kMwEdgeBits <= 11, "a 4096-term segment must fit the margin: 2^(23 - bits) > 2049");
 __device__ __forceinline__ int mw_n(int n_cap, const int* n_dev) { return n_dev ? *n_dev : n_cap; }
 
@@ -1107,7 +1108,7 @@ __global__ __launch_bounds__(256) void k_mw_compact(int n_cap, const int* n_dev,
 // The fast path adds the window's heads as a plain fp32 chain -- s += x (the head's own step), s += dq (its segment)
 // -- storing the sum right after head l's step to LDS (lane l reads it back); the 64 checks then run lane-parallel.  A
 // failed check at head f restarts from its recorded sum (exact: every earlier head passed), sums f's segment term by
-// term and takes the rest of the window head by head.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
+// term and chains the window's later heads again.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
 // term-by-term run.
 __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, int ld, int n_cap, const int* n_dev,
                                                 const DevState* st, MwBuf B, float* out, long long* stats) {
@@ -1135,8 +1136,10 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
 #define LO_WALK_TERMS(isch, expr) expr
 #endif
     // one window: the plain chain, the lane-parallel checks; from a failed check at head f: its segment term by term,
-    // then the rest of the window head by head (running the chain again over the rest measured slower: 498 against
-    // 547 scans/s on the C5 scans, same box)
+    // then, for the window's first failure, the chain over its later heads only, 8 at a time, and their checks; after
+    // that the rest head by head.  Same-box A/B on the C5 scans (scans/s): head by head after any failure 548, the
+    // chain again after the first 550, the first two 550, every failure 528 (failures cluster: a poorly predicted
+    // stretch fails head after head), a full 64-head chain again after every failure 498
     __shared__ float2 s_xd[64];                                // the window's (x, dq), read back as broadcasts
     __shared__ float s_rec[64 * 64];                           // [head l][lane]: the sum right after head l's step
     auto chain = [&]() -> float {
@@ -1154,44 +1157,74 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
         __syncthreads();
         return s_rec[lane * 64 + lane];
     };
+    // after a failure: the chain over heads [from, m) only, 8 at a time (the window's records below from are no-ops)
+    auto chain_from = [&](int from, int m) -> float {
+        __syncthreads();
+        for (int b = from & ~7; b < m; b += 8) {               // records up to 64 exist (pad: no-ops)
+            float2 xd[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xd[u] = s_xd[b + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s = s + xd[u].x;
+                s_rec[(b + u) * 64 + lane] = s;
+                s = s + xd[u].y;
+            }
+        }
+        __syncthreads();
+        return s_rec[lane * 64 + lane];
+    };
     auto process = [&](const Win& cur, int k0) {
         s_xd[lane] = make_float2(cur.x, cur.dq);
-        const float rec = chain();
-        const double d = static_cast<double>(rec);
-        const bool ok = cur.flag == 1 || (cur.flag == 0 && d >= cur.dlo && d <= cur.dhi);
-        const unsigned long long badm = __ballot(!ok);
-        if (!badm) return;                                     // uniform
+        float rec = chain();
+        const int m = min(64, total - k0);
+        int from = 0, nre = 0;                                 // heads below from are summed; nre: chains again
+        for (;;) {
+            const double d = static_cast<double>(rec);
+            const bool ok = lane < from || cur.flag == 1 || (cur.flag == 0 && d >= cur.dlo && d <= cur.dhi);
+            const unsigned long long badm = __ballot(!ok);
+            if (!badm) return;                                 // uniform
 #ifdef LO_EXACT_STAMPS
-        const unsigned long long t_s0 = __builtin_amdgcn_s_memtime();
+            const unsigned long long t_s0 = __builtin_amdgcn_s_memtime();
 #endif
-        const int f = __builtin_ctzll(badm);
-        s = rlf(rec, f);                                       // exact: every head before f passed
-        {
+            const int f = __builtin_ctzll(badm);
+            s = rlf(rec, f);                                   // exact: every head before f passed
             const int h = __builtin_amdgcn_readlane(cur.hi, f), end = __builtin_amdgcn_readlane(cur.end, f);
             const bool ch = __builtin_amdgcn_readlane(cur.flag, f) == kMwFail && end - h > 1;
             chained += ch ? 1 : 0;
             LO_WALK_TERMS(ch, s = walk_terms(col, h + 1, end, s));
             ++fbs;
-        }
-        const int m = min(64, total - k0);
-        for (int l = f + 1; l < m; ++l) {                      // the rest of the window head by head
-            const int h = __builtin_amdgcn_readlane(cur.hi, l), end = __builtin_amdgcn_readlane(cur.end, l);
-            s = s + rlf(cur.x, l);
-            const double dl = static_cast<double>(s);
-            const int fl = __builtin_amdgcn_readlane(cur.flag, l);
-            const bool okl = fl == 1 || (fl == 0 && dl >= rl64d(cur.dlo, l) && dl <= rl64d(cur.dhi, l));
-            if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) {
-                s = s + rlf(cur.dq, l);
-            } else {
-                const bool ch = fl == kMwFail && end - h > 1;
-                chained += ch ? 1 : 0;
-                LO_WALK_TERMS(ch, s = walk_terms(col, h + 1, end, s));
-                ++fbs;
-            }
-        }
+            from = f + 1;
+            if (from < m && nre < kMwChainAgain) {                // the chain again over the window's later heads
+                ++nre;
+                __syncthreads();
+                if (lane < from) s_xd[lane] = make_float2(-0.0f, -0.0f);
+                rec = chain_from(from, m);
 #ifdef LO_EXACT_STAMPS
-        t_slow += __builtin_amdgcn_s_memtime() - t_s0;
+                t_slow += __builtin_amdgcn_s_memtime() - t_s0;
 #endif
+                continue;
+            }
+            for (int l = from; l < m; ++l) {                   // the rest of the window head by head
+                const int hl = __builtin_amdgcn_readlane(cur.hi, l), el = __builtin_amdgcn_readlane(cur.end, l);
+                s = s + rlf(cur.x, l);
+                const double dl = static_cast<double>(s);
+                const int fl = __builtin_amdgcn_readlane(cur.flag, l);
+                const bool okl = fl == 1 || (fl == 0 && dl >= rl64d(cur.dlo, l) && dl <= rl64d(cur.dhi, l));
+                if (__builtin_amdgcn_readfirstlane(okl ? 1 : 0)) {
+                    s = s + rlf(cur.dq, l);
+                } else {
+                    const bool chl = fl == kMwFail && el - hl > 1;
+                    chained += chl ? 1 : 0;
+                    LO_WALK_TERMS(chl, s = walk_terms(col, hl + 1, el, s));
+                    ++fbs;
+                }
+            }
+#ifdef LO_EXACT_STAMPS
+            t_slow += __builtin_amdgcn_s_memtime() - t_s0;
+#endif
+            return;
+        }
     };
 #undef LO_WALK_TERMS
     // the next window's records in flight; two windows per trip, so the loop carries no register copy of a window
