@@ -18,28 +18,42 @@ constexpr int kExactTerms = 43;        // H (36, full: the reference's H is not 
 // LDLT<Matrix<float,6,6>> (Eigen ldlt_inplace<Lower>::unblocked with diagonal pivoting + LDLT::_solve_impl)
 __device__ inline void ldlt6_solve_f32(const float (&Hin)[36], const float (&b)[6], float (&x)[6]) {
     float m[6][6];
+#pragma unroll
     for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) m[r][c] = Hin[r * 6 + c];
     int transp[6];
     float temp[6];
     bool zero_all = false;
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         int big = k;
         float bv = fabsf(m[k][k]);
+#pragma unroll
         for (int i = k + 1; i < 6; ++i) if (fabsf(m[i][i]) > bv) { bv = fabsf(m[i][i]); big = i; }
         transp[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; ++j) { const float t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
-            for (int i = big + 1; i < 6; ++i) { const float t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
-            { const float t = m[k][k]; m[k][k] = m[big][big]; m[big][big] = t; }
-            for (int i = k + 1; i < big; ++i) { const float t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
+        // the symmetric pivot swap with compile-time indices only (one unrolled candidate per row): a runtime index
+        // into m would put the matrix in scratch memory
+#pragma unroll
+        for (int q = k + 1; q < 6; ++q) {
+            if (q != big) continue;
+#pragma unroll
+            for (int j = 0; j < k; ++j) { const float t = m[k][j]; m[k][j] = m[q][j]; m[q][j] = t; }
+#pragma unroll
+            for (int i = q + 1; i < 6; ++i) { const float t = m[i][k]; m[i][k] = m[i][q]; m[i][q] = t; }
+            { const float t = m[k][k]; m[k][k] = m[q][q]; m[q][q] = t; }
+#pragma unroll
+            for (int i = k + 1; i < q; ++i) { const float t = m[i][k]; m[i][k] = m[q][i]; m[q][i] = t; }
         }
         if (k > 0) {
+#pragma unroll
             for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
             float acc = 0.0f;
+#pragma unroll
             for (int j = 0; j < k; ++j) acc += m[k][j] * temp[j];
             m[k][k] -= acc;
+#pragma unroll
             for (int i = k + 1; i < 6; ++i) {
                 float a = 0.0f;
+#pragma unroll
                 for (int j = 0; j < k; ++j) a += m[i][j] * temp[j];
                 m[i][k] -= a;
             }
@@ -51,12 +65,23 @@ __device__ inline void ldlt6_solve_f32(const float (&Hin)[36], const float (&b)[
     }
     if (zero_all) { for (int i = 0; i < 6; ++i) x[i] = 0.0f; return; }
     float d[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) d[i] = b[i];
-    for (int k = 0; k < 6; ++k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int q = k + 1; q < 6; ++q) if (transp[k] == q) { const float t = d[k]; d[k] = d[q]; d[q] = t; }
+#pragma unroll
     for (int i = 0; i < 6; ++i) { float a = 0.0f; for (int j = 0; j < i; ++j) a += m[i][j] * d[j]; d[i] -= a; }
+#pragma unroll
     for (int i = 0; i < 6; ++i) d[i] = (fabsf(m[i][i]) > FLT_MIN) ? d[i] / m[i][i] : 0.0f;
+#pragma unroll
     for (int i = 5; i >= 0; --i) { float a = 0.0f; for (int j = i + 1; j < 6; ++j) a += m[j][i] * d[j]; d[i] -= a; }
-    for (int k = 5; k >= 0; --k) if (transp[k] != k) { const float t = d[k]; d[k] = d[transp[k]]; d[transp[k]] = t; }
+#pragma unroll
+    for (int k = 5; k >= 0; --k)
+#pragma unroll
+        for (int q = k + 1; q < 6; ++q) if (transp[k] == q) { const float t = d[k]; d[k] = d[q]; d[q] = t; }
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = d[i];
 }
 

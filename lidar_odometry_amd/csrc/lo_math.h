@@ -68,11 +68,13 @@ LO_HD inline Rot make_jacobi(float x, float y, float z) {
 // A row-major a[r][c]; U columns = left singular vectors, S descending.
 LO_HD inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], float Vout[3][3] = nullptr) {
     float scale = 0.0f;                                               // maxCoeff<PropagateNaN>
+#pragma unroll
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) {
         const float v = std::fabs(A[r][c]);
         scale = (std::isnan(v) || std::isnan(scale)) ? NAN : std::max(scale, v);
     }
     float W[3][3], V[3][3];
+#pragma unroll
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) { U[r][c] = V[r][c] = (r == c) ? 1.0f : 0.0f; }
     if (!std::isfinite(scale)) {
         S[0] = S[1] = S[2] = NAN;
@@ -80,13 +82,16 @@ LO_HD inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], fl
         return;
     }
     if (scale == 0.0f) scale = 1.0f;
+#pragma unroll
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) W[r][c] = A[r][c] / scale;
     float maxDiag = std::max(std::fabs(W[0][0]), std::max(std::fabs(W[1][1]), std::fabs(W[2][2])));
     const float prec = 2.0f * FLT_EPSILON;
     bool done = false;
     for (int sweep = 0; !done && sweep < 1000; ++sweep) {
         done = true;
+#pragma unroll
         for (int p = 1; p < 3; ++p) {
+#pragma unroll
             for (int q = 0; q < p; ++q) {
                 const float thr = std::max(FLT_MIN, prec * maxDiag);
                 if (!(std::fabs(W[p][q]) > thr || std::fabs(W[q][p]) > thr)) continue;
@@ -105,30 +110,41 @@ LO_HD inline void jacobi_svd3(const float A[3][3], float U[3][3], float S[3], fl
                 rotate(m01, m11, r1);
                 const Rot jr = make_jacobi(m00, m01, m11);
                 const Rot jl = rot_mul(r1, rot_t(jr));
+#pragma unroll
                 for (int i = 0; i < 3; ++i) rotate(W[p][i], W[q][i], jl);       // W.applyOnTheLeft(p,q,jl)
+#pragma unroll
                 for (int i = 0; i < 3; ++i) rotate(U[i][p], U[i][q], jl);       // U.applyOnTheRight(p,q,jl^T)
                 const Rot jrt = rot_t(jr);
+#pragma unroll
                 for (int i = 0; i < 3; ++i) rotate(W[i][p], W[i][q], jrt);      // W.applyOnTheRight(p,q,jr)
+#pragma unroll
                 for (int i = 0; i < 3; ++i) rotate(V[i][p], V[i][q], jrt);
                 maxDiag = std::max(maxDiag, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
             }
         }
     }
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float a = W[i][i];
         S[i] = std::fabs(a);
         if (a < 0.0f) for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
     }
+#pragma unroll
     for (int i = 0; i < 3; ++i) S[i] *= scale;
+#pragma unroll
     for (int i = 0; i < 3; ++i) {                                         // descending sort (first max)
         int pos = i;
+#pragma unroll
         for (int k = i + 1; k < 3; ++k) if (S[k] > S[pos]) pos = k;
         if (S[pos] == 0.0f) break;
-        if (pos != i) {
-            float tq = S[i]; S[i] = S[pos]; S[pos] = tq;
+#pragma unroll
+        for (int k = i + 1; k < 3; ++k) {                                  // swap with pos (compile-time indices:
+            if (k != pos) continue;                                        // no scratch copy of U / V on the device)
+            float tq = S[i]; S[i] = S[k]; S[k] = tq;
+#pragma unroll
             for (int r = 0; r < 3; ++r) {
-                tq = U[r][i]; U[r][i] = U[r][pos]; U[r][pos] = tq;
-                tq = V[r][i]; V[r][i] = V[r][pos]; V[r][pos] = tq;
+                tq = U[r][i]; U[r][i] = U[r][k]; U[r][k] = tq;
+                tq = V[r][i]; V[r][i] = V[r][k]; V[r][k] = tq;
             }
         }
     }
