@@ -716,6 +716,10 @@ __global__ __launch_bounds__(kExactSolveThreads) void k_exact_solve(KParams P, i
 #define LO_MW_EDGE_BITS 10
 #endif
 constexpr int kMwEdgeBits = LO_MW_EDGE_BITS;
+#ifndef LO_MW_REG_HEADS
+#define LO_MW_REG_HEADS 2
+#endif
+constexpr int kMwRegHeads = LO_MW_REG_HEADS;                  // classification: heads per thread kept in registers
 constexpr int kMwChainAgain = 1;                              // the walk: failures per window followed by a chain
 static_assert(kMwEdgeBits >= 1 && kMwEdgeBits <= 11, "a 4096-term segment must fit the margin: 2^(23 - bits) > 2049");
 __device__ __forceinline__ int mw_n(int n_cap, const int* n_dev) { return n_dev ? *n_dev : n_cap; }
@@ -931,15 +935,25 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
     };
     long long ql = 0;
     int nhl = 0;
+    // the first kMwRegHeads heads of the thread kept in registers: when no thread of the workgroup has more, the
+    // record pass below is skipped (same-box A/B, C5 exact scans/s: 0 / 1 / 2 / 3 heads -> 558 / 584 / 585 / 581;
+    // keeping them also ends the kernel's scratch spill)
+    int r_a[kMwRegHeads + 1], r_e[kMwRegHeads + 1], r_q[kMwRegHeads + 1];
+    double r_t[kMwRegHeads + 1];
     {
         double tl = 0.0;
         int ep = e_in, gp = g_in;
 #pragma unroll
         for (int a = 0; a < kMwPT; ++a) {
             tl += static_cast<double>(v[a]);
+            const double T = tex + tl;
             int E, G;
             long long qa;
-            nhl += classify(a, tex + tl, ep, gp, E, G, qa) ? 1 : 0;
+            const bool hd = classify(a, T, ep, gp, E, G, qa);
+#pragma unroll
+            for (int r = 0; r < kMwRegHeads; ++r)
+                if (hd && nhl == r) { r_a[r] = a; r_e[r] = E; r_q[r] = static_cast<int>(ql); r_t[r] = T; }
+            nhl += hd ? 1 : 0;
             ql += qa;
             ep = E;
             gp = G;
@@ -967,7 +981,11 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
         }
         return;
     }
-    {
+    if (kMwRegHeads > 0 && !__syncthreads_or(nhl > kMwRegHeads)) {   // uniform
+#pragma unroll
+        for (int r = 0; r < kMwRegHeads; ++r)
+            if (r < nhl) { S.h_idx[hbase + r] = base + r_a[r]; S.h_e[hbase + r] = r_e[r]; S.h_p[hbase + r] = pex + r_q[r]; S.h_t[hbase + r] = r_t[r]; }
+    } else {
         double tl = 0.0;
         int ep = e_in, gp = g_in, hk = hbase;
         long long prun = pex;
