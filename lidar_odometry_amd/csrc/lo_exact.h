@@ -13,6 +13,13 @@
 namespace lo {
 
 constexpr int kExactTerms = 43;        // H (36, full: the reference's H is not symmetrised), g (6), cost
+constexpr int kExactFactors = 14;      // per point: J (6), w J (6), w r, r (exact_point_factors)
+#ifndef LO_EXACT_FACTORED
+#define LO_EXACT_FACTORED 1
+#endif
+// long sums (term-major): k_exact_terms writes the 14 factor rows and the column sums form each term (1), or it writes
+// the 43 term columns (0, A/B)
+constexpr bool kExactFactored = LO_EXACT_FACTORED != 0;
 
 // ---- the reference's fp32 solve and pose update (restated exactly as the oracle states them) ----
 // LDLT<Matrix<float,6,6>> (Eigen ldlt_inplace<Lower>::unblocked with diagonal pivoting + LDLT::_solve_impl)

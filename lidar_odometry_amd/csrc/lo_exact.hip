@@ -606,8 +606,11 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
     const size_t os = P.ex_ld ? static_cast<size_t>(P.ex_ld) : 1;
     float* out = P.ex_terms + o0;
     const int s = P.slot[i];
+    // term-major (long sums): the point's 14 factor rows only -- the readers form each term as the same fp32 product
+    // (launch_mw_sums factored); row-major: the 43 products
+    const int nout = P.ex_ld && kExactFactored ? kExactFactors : kExactTerms;
     if (s < 0) {
-        for (int k = 0; k < kExactTerms; ++k) out[k * os] = 0.0f;
+        for (int k = 0; k < nout; ++k) out[k * os] = 0.0f;
         return;
     }
     float T[12];
@@ -627,6 +630,11 @@ __global__ __launch_bounds__(kBlock) void k_exact_terms(KParams P) {
     }
     float f[14];
     exact_point_factors(P, T, scale, dl, r64, px, py, pz, sl, f);
+    if (P.ex_ld && kExactFactored) {
+#pragma unroll
+        for (int k = 0; k < kExactFactors; ++k) out[k * os] = f[k];
+        return;
+    }
     for (int k = 0; k < kExactTerms; ++k) {
         int fa, fb;
         exact_term_factors(k, fa, fb);
@@ -723,7 +731,56 @@ constexpr int kMwRegHeads = LO_MW_REG_HEADS;                  // classification:
 constexpr int kMwChainAgain = 1;                              // the walk: failures per window followed by a chain
 static_assert(kMwEdgeBits >= 1 && kMwEdgeBits <= 11, "a 4096-term segment must fit the margin: 2^(23 - bits) > 2049");
 __device__ __forceinline__ int mw_n(int n_cap, const int* n_dev) { return n_dev ? *n_dev : n_cap; }
+// Column colI of the long sums, from term off on: a stored column (col0 + colI * ld), or (FAC) the fp32 product of
+// its two factor rows (exact_term_factors: the 43 terms are products of a point's 14 factors, so k_exact_terms writes
+// 14 rows instead of 43 columns and every reader forms the same product)
+template <bool FAC> struct MwCol {
+    const float* a;
+    const float* b;
+    __device__ __forceinline__ MwCol(const float* col0, int ld, int colI, int off) {
+        if constexpr (FAC) {
+            int fa, fb;
+            exact_term_factors(colI, fa, fb);
+            a = col0 + static_cast<size_t>(fa) * ld + off;
+            b = col0 + static_cast<size_t>(fb) * ld + off;
+        } else {
+            a = col0 + static_cast<size_t>(colI) * ld + off;
+            b = nullptr;
+        }
+    }
+    __device__ __forceinline__ float operator[](int j) const {
+        if constexpr (FAC) return a[j] * b[j];
+        else return a[j];
+    }
+    // terms base .. base + kMwPT - 1 (0 from lim on): 16-B loads when the run is whole and aligned (a thread's 16
+    // consecutive terms as 4 dwordx4 loads per row instead of 16 dword loads, each touching 64 lanes' lines)
+    __device__ __forceinline__ void load_run(int base, int lim, float (&v)[kMwPT]) const {
+        static_assert(kMwPT % 4 == 0, "whole float4s");
+        uintptr_t al = reinterpret_cast<uintptr_t>(a + base);
+        if constexpr (FAC) al |= reinterpret_cast<uintptr_t>(b + base);
+        if (base + kMwPT <= lim && (al & 15) == 0) {
+            const float4* pa = reinterpret_cast<const float4*>(a + base);
+#pragma unroll
+            for (int q = 0; q < kMwPT / 4; ++q) {
+                const float4 x = pa[q];
+                v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+            }
+            if constexpr (FAC) {
+                const float4* pb = reinterpret_cast<const float4*>(b + base);
+#pragma unroll
+                for (int q = 0; q < kMwPT / 4; ++q) {
+                    const float4 y = pb[q];
+                    v[4 * q] *= y.x; v[4 * q + 1] *= y.y; v[4 * q + 2] *= y.z; v[4 * q + 3] *= y.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kMwPT; ++q) v[q] = base + q < lim ? (*this)[base + q] : 0.0f;
+        }
+    }
+};
 
+template <bool FAC>
 __global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__ col0, int ld, int n_cap,
                                                        const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
@@ -731,7 +788,7 @@ __global__ __launch_bounds__(256) void k_mw_chunk_sums(const float* __restrict__
     const int c = blockIdx.x, colI = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
     if (mc <= 0) return;                                       // chunks past the end publish nothing
-    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    const MwCol<FAC> col(col0, ld, colI, c0);
     double v = 0.0, a = 0.0;
 #pragma unroll
     for (int k = 0; k < kMwChunk / 256; ++k) {                 // 16 terms per thread, coalesced
@@ -793,6 +850,7 @@ __device__ __forceinline__ double mw_drift_terms(const float (&v)[kMwPT], double
     return d;
 }
 
+template <bool FAC>
 __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict__ col0, int ld, int n_cap,
                                                         const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
@@ -801,13 +859,12 @@ __global__ __launch_bounds__(kMwThreads) void k_mw_drift(const float* __restrict
     const int n = mw_n(n_cap, n_dev), c0 = c * kMwChunk, mc = min(kMwChunk, n - c0);
     const size_t co = static_cast<size_t>(colI) * B.nchunks;
     if (mc <= 0) return;
-    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    const MwCol<FAC> col(col0, ld, colI, c0);
     double T0, A;
     mw_base<false>(B, co, c, s_w, T0, A);
     const int base = tid * kMwPT;
     float v[kMwPT];
-#pragma unroll
-    for (int a = 0; a < kMwPT; ++a) v[a] = base + a < mc ? col[base + a] : 0.0f;
+    col.load_run(base, mc, v);
     double run = 0.0;
 #pragma unroll
     for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
@@ -859,7 +916,7 @@ __device__ __forceinline__ void mw_block_sum2(double& x, double& y, double* s_w)
 // then its modelled drift the same way, then classifies -- k_mw_chunk_sums and k_mw_drift fold in.  The prediction
 // base is the same quantity summed in another order (T0 = chunk sums + drift corrections of the chunks before).
 // !FUSED: the three-launch path (LO_MW_SPLIT=1, A/B).
-template <bool FUSED>
+template <bool FUSED, bool FAC>
 __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __restrict__ col0, int ld, int n_cap,
                                                              const int* n_dev, const DevState* st, MwBuf B) {
     if (st && st->done) return;
@@ -871,11 +928,10 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
         if (tid == 0) B.nh[co + c] = 0;
         return;
     }
-    const float* col = col0 + static_cast<size_t>(colI) * ld + c0;
+    const MwCol<FAC> col(col0, ld, colI, c0);
     const int base = tid * kMwPT;
     float v[kMwPT];
-#pragma unroll
-    for (int a = 0; a < kMwPT; ++a) v[a] = base + a < mc ? col[base + a] : 0.0f;
+    col.load_run(base, mc, v);
     double run = 0.0;
 #pragma unroll
     for (int a = 0; a < kMwPT; ++a) run += static_cast<double>(v[a]);
@@ -1045,7 +1101,8 @@ __global__ __launch_bounds__(kMwThreads, 4) void k_mw_classify(const float* __re
 
 // s + col[j0] + ... + col[j1 - 1] term by term (one wave, wave-uniform).  The terms come in through scalar loads, 32 at a
 // time with the next 32 in flight, so the chain is one v_add_f32 per term with an SGPR operand (no readlane hazards).
-__device__ __forceinline__ float walk_terms(const float* __restrict__ col, int j0, int j1, float s) {
+template <bool FAC>
+__device__ __forceinline__ float walk_terms(const MwCol<FAC>& col, int j0, int j1, float s) {
     constexpr int kB = 32;
     j0 = __builtin_amdgcn_readfirstlane(j0);
     j1 = __builtin_amdgcn_readfirstlane(j1);
@@ -1128,12 +1185,13 @@ __global__ __launch_bounds__(256) void k_mw_compact(int n_cap, const int* n_dev,
 // failed check at head f restarts from its recorded sum (exact: every earlier head passed), sums f's segment term by
 // term and chains the window's later heads again.  stats (nullable, per column): heads, segments summed term by term, chunks that were one
 // term-by-term run.
+template <bool FAC>
 __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, int ld, int n_cap, const int* n_dev,
                                                 const DevState* st, MwBuf B, float* out, long long* stats) {
     if (st && st->done) return;
     const int lane = threadIdx.x, colI = blockIdx.x;
     const int n = mw_n(n_cap, n_dev);
-    const float* col = col0 + static_cast<size_t>(colI) * ld;
+    const MwCol<FAC> col(col0, ld, colI, 0);
     const size_t rb = static_cast<size_t>(colI) * B.cstride;
     const int total = n > 0 ? B.ntot[colI] : 0;
     struct Win { int hi, end, flag; float x, dq; double dlo, dhi; };
@@ -1278,21 +1336,31 @@ __global__ __launch_bounds__(64) void k_mw_walk(const float* __restrict__ col0, 
 
 // Host side: the fp32 sequential sums of ncol columns (col0 + k * ld, n terms each; n_dev: a device-side count <= n_cap
 // instead) into out[0, ncol), B sized for n_cap.  stats (nullable): 3 per column.
-void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
-                    float* out, long long* stats, hipStream_t s) {
+template <bool FAC>
+static void launch_mw_sums_t(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st,
+                             const MwBuf& B, float* out, long long* stats, hipStream_t s) {
     const int nc = (n_cap + kMwChunk - 1) / kMwChunk;
     static const bool split = std::getenv("LO_MW_SPLIT") != nullptr;   // A/B: the three-launch classification
     if (nc > 0) {
         if (split) {
-            hipLaunchKernelGGL(k_mw_chunk_sums, dim3(nc, ncol), dim3(256), 0, s, col0, ld, n_cap, n_dev, st, B);
-            hipLaunchKernelGGL(k_mw_drift, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
-            hipLaunchKernelGGL(k_mw_classify<false>, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL(k_mw_chunk_sums<FAC>, dim3(nc, ncol), dim3(256), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL(k_mw_drift<FAC>, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL((k_mw_classify<false, FAC>), dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev,
+                               st, B);
         } else {
-            hipLaunchKernelGGL(k_mw_classify<true>, dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev, st, B);
+            hipLaunchKernelGGL((k_mw_classify<true, FAC>), dim3(nc, ncol), dim3(kMwThreads), 0, s, col0, ld, n_cap, n_dev,
+                               st, B);
         }
         hipLaunchKernelGGL(k_mw_compact, dim3(nc, ncol), dim3(256), 0, s, n_cap, n_dev, st, B);
     }
-    hipLaunchKernelGGL(k_mw_walk, dim3(ncol), dim3(64), 0, s, col0, ld, n_cap, n_dev, st, B, out, stats);
+    hipLaunchKernelGGL(k_mw_walk<FAC>, dim3(ncol), dim3(64), 0, s, col0, ld, n_cap, n_dev, st, B, out, stats);
+}
+// factored: col0 holds the 14 factor rows of the exact terms (k_exact_terms, term-major) and column k is the product
+// of rows exact_term_factors(k); else ncol stored columns
+void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
+                    float* out, long long* stats, hipStream_t s, bool factored) {
+    if (factored) launch_mw_sums_t<true>(col0, ld, ncol, n_cap, n_dev, st, B, out, stats, s);
+    else launch_mw_sums_t<false>(col0, ld, ncol, n_cap, n_dev, st, B, out, stats, s);
 }
 // Bytes of an MwBuf for ncol columns of up to n_cap terms, and its layout in one allocation.
 size_t mw_bytes(int ncol, int n_cap) {

@@ -76,10 +76,13 @@ void launch_exact_scale_c(const KParams& P, hipStream_t s);
 void launch_exact_scale_m(const KParams& P, const uint64_t* runs, uint64_t* sorted, hipStream_t s);
 void launch_seq_sum_diag(const double* x, int n, double* sort, double* out, long long* stats, hipStream_t s);
 void launch_mw_sums(const float* col0, int ld, int ncol, int n_cap, const int* n_dev, const DevState* st, const MwBuf& B,
-                    float* out, long long* stats, hipStream_t s);
+                    float* out, long long* stats, hipStream_t s, bool factored);
 size_t mw_bytes(int ncol, int n_cap);
 MwBuf mw_layout(void* mem, int ncol, int n_cap);
 hipError_t mw_clear(const MwBuf& B, int ncol, hipStream_t s);
+#ifndef LO_EXACT_FACTORED
+#define LO_EXACT_FACTORED 1                                  // lo_exact.h kExactFactored
+#endif
 void launch_mwm_scale(KParams P, const double* sorted, const MwmBuf& B, hipStream_t s);
 size_t mwm_bytes(int n_cap);
 MwmBuf mwm_layout(void* mem, int n_cap);
@@ -1461,7 +1464,7 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
             LO_HIP(c, hipMalloc(&c->d_mwm, mwm_bytes(static_cast<int>(n))));
             c->mwm = mwm_layout(c->d_mwm, static_cast<int>(n));
         }
-        P.ex_ld = static_cast<int>(n);                     // term-major: one coalesced column per sum
+        P.ex_ld = static_cast<int>((n + 63) & ~static_cast<size_t>(63));   // term-major rows, 256-B aligned
         P.ex_tot = c->d_ex_tot;
         if (c->ex_res_cap < n) {
             if (c->d_ex_res) LO_HIP(c, hipFree(c->d_ex_res));
@@ -1513,7 +1516,7 @@ static void launch_exact_iteration(lo_ctx* c, const KParams& P, const KParams& P
     launch_pko(c, P, it);
     hipLaunchKernelGGL(k_exact_terms, dim3(P.nb), dim3(kBlock), 0, c->stream, P);
     if (P.ex_ld) {                                           // large scan: 43 parallel sequential-sum reproductions
-        launch_mw_sums(P.ex_terms, P.ex_ld, 43, P.n, P.n_dev, P.st, c->mw, P.ex_tot, nullptr, c->stream);
+        launch_mw_sums(P.ex_terms, P.ex_ld, 43, P.n, P.n_dev, P.st, c->mw, P.ex_tot, nullptr, c->stream, LO_EXACT_FACTORED != 0);
         hipLaunchKernelGGL(k_exact_finish, dim3(1), dim3(64), 0, c->stream, P, it);
     } else {
         hipLaunchKernelGGL(k_exact_solve, dim3(1), dim3(512), 0, c->stream, P, it);   // kExactSolveThreads
@@ -2296,7 +2299,7 @@ int lo_seq_sum_f32(lo_ctx* c, const float* x, size_t n, float* out_sum, long lon
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) {
         (void)hipEventRecord(e0, c->stream);
-        launch_mw_sums(d_x, ni, 1, ni, nullptr, nullptr, B, d_out, d_st, c->stream);
+        launch_mw_sums(d_x, ni, 1, ni, nullptr, nullptr, B, d_out, d_st, c->stream, false);
         (void)hipEventRecord(e1, c->stream);
         e = hipStreamSynchronize(c->stream);
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);

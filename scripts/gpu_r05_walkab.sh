@@ -3,7 +3,7 @@
 cd /root/repo && export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) echo "fatal rc $1 in $2"; exit 4;; esac; }
 for r in 1 2; do
-for L in icp_cf0 icp_cf1 icp_cf2 icp_cf64; do
+for L in icp icp_nf; do
   LO_ICP_LIB=lidar_odometry_amd/liblo_$L.so timeout -k 10 300 python bench.py --config patch1m --mode exact --no-cpu-baseline --pmc off --batch "" --sequences 0 --steps 40 --warmup 4 > gpurun_out/wab_${L}_$r.json 2> gpurun_out/wab_${L}_$r.log
   rc=$?; echo "$L $r rc $rc"; fatal $rc "bench $L"
 done
