@@ -233,14 +233,22 @@ private:
             out[r * 4 + 3] = t[r];
         }
     }
+    // The device's pose is the reference's current_transform bit for bit: its rotation already came out of
+    // SE3::operator*'s SO3(Matrix3f) projection (MathUtils.h:144-147).  SE3f(R, t) would run that JacobiSVD projection a
+    // second time (MathUtils.h:116-117, MathUtils.cpp:86-92), and the fp32 projection is not idempotent: re-projecting
+    // the exact mode's poses moves entries by up to ~3e-7 (tests/test_integration_adapter.py
+    // test_so3_reprojection_not_idempotent).  So the matrix is written into a default SE3f through the mutable accessors
+    // (MathUtils.h:75, :131, :140), which copy without projecting -- what `optimized_transform = current_transform`
+    // (:452) hands the caller.
     static SE3f from_row_major(const float T[12]) {
-        Eigen::Matrix3f R;
-        Eigen::Vector3f t;
+        SE3f out;
+        Eigen::Matrix3f& R = out.Rotation().Matrix();
+        Eigen::Vector3f& t = out.Translation();
         for (int r = 0; r < 3; ++r) {
             for (int c = 0; c < 3; ++c) R(r, c) = T[r * 4 + c];
             t[r] = T[r * 4 + 3];
         }
-        return SE3f(R, t);                                   // MathUtils.h:116 (R is already on SO(3))
+        return out;
     }
 
     ICPConfig m_config;

@@ -169,9 +169,9 @@ int lo_set_stream(lo_ctx* ctx, void* hip_stream);
  * and move the pose by 1e-4 .. 4e-4 (measured on the MID360-like and 1M-point workloads): NOT parity-safe.
  * LO_EXACT=0 in the environment starts contexts in the fast mode (A/B runs).
  * Device memory of the exact mode, allocated at the first scan that needs it and kept: up to 16384 points a fixed
- * ~1 MB; a larger scan adds ~0.95 KB per point of the largest such scan (the 43 fp32 term columns, 172 B, and the
- * sequential-sum head records, 2 x 1024 per 4096-term chunk of every column at 36 B, ~775 B) -- ~0.95 GB at 1M points,
- * ~3.8 GB at the 4M-point max_points.  An allocation failure there returns LO_ERR_HIP from that optimize call. */
+ * ~3 MB; a larger scan adds ~0.85 KB per point of the largest such scan (the 14 fp32 factor rows the 43 terms are
+ * formed from, 56 B, and the sequential-sum head records, 2 x 1024 per 4096-term chunk of every column at 36 B,
+ * ~775 B) -- ~0.85 GB at 1M points, ~3.4 GB at the 4M-point max_points.  An allocation failure there returns LO_ERR_HIP from that optimize call. */
 int lo_set_exact(lo_ctx* ctx, int enable);
 /* Scan pipeline (default on; LO_PIPE=0 in the environment turns it off at lo_create).  The reference's optimize
  * runs GN iterations until convergence (IterativeClosestPointOptimizer.cpp:281-449); the device loop enqueues all
@@ -221,6 +221,14 @@ int lo_icp_export_pose(lo_ctx* ctx, float* d_out16);
  * (lo_stage_span's clock: the first blocks' start to the last blocks' end; surfel correspondence only). */
 int lo_bench_kernel(lo_ctx* ctx, const float* d_pts, size_t n, const float T[12], double scale, double alpha,
                     int kernel_id, int reps, float* avg_ms);
+/* Timing harness for the out-of-cache correspondence roofline: `rounds` round-robin passes over `count` contexts,
+ * one correspondence launch per context per pass (d_pts[i], n[i] points at pose T[12 i .. 12 i + 11]), every launch
+ * back to back on ctxs[0]'s stream with no set-up pass, so each scan was last touched count - 1 launches earlier.  HIP
+ * events around the whole sequence: avg_ms = device time per launch, including the inter-launch gap of back-to-back
+ * dispatches (what a kernel trace's per-launch duration plus its dispatch gap adds up to).  Surfel contexts on one
+ * device; the caller's streams are not used. */
+int lo_bench_correspond_rr(lo_ctx* const* ctxs, const float* const* d_pts, const size_t* n, const float* T, int count,
+                           int rounds, float* avg_ms);
 
 /* ---- scan-parallel batch on one GPU ----
  * The north star's scan-parallel model (one independent scan stream per GPU, BASELINE.json configs[4]) applied

@@ -63,6 +63,10 @@ int           lo_odom_set_exact(lo_odometry* o, int enable);
 /* One raw scan (AoS float3, host memory) -> its world pose (row-major 3x4).  Returns LO_OK / LO_INSUFFICIENT
  * (the guess was kept, as :304-307) or a negative error. */
 int           lo_odom_process(lo_odometry* o, const float* raw_xyz, size_t n, float T_out[12], lo_odom_frame* info);
+/* Wait for the last keyframe's map update and report its status: LO_ERR_CAPACITY if it overflowed (an overflow at the
+ * final keyframe of a run is otherwise never read, since no later frame polls it).  Call before trusting the map after
+ * the last frame; lo_odom_destroy does not report. */
+int           lo_odom_flush(lo_odometry* o);
 size_t        lo_odom_keyframe_count(const lo_odometry* o);
 size_t        lo_odom_map_surfels(const lo_odometry* o);
 

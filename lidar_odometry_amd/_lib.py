@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "lo_device", "lo_get_config", "lo_map_set_surfels", "lo_map_surfel_count", "lo_map_set_points",
     "lo_map_point_count", "lo_icp_optimize", "lo_icp_optimize_raw_async", "lo_icp_optimize_raw", "lo_filtered_points",
     "lo_voxel_filter_gpu", "lo_icp_optimize_async", "lo_icp_optimize_loop", "lo_host_alloc", "lo_host_free",
-    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_set_pko_groups", "lo_update_config", "lo_map_sync_surfels", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
+    "lo_icp_result", "lo_sync", "lo_stream", "lo_set_stream", "lo_set_exact", "lo_set_pipeline", "lo_pipeline_status", "lo_set_pko_groups", "lo_update_config", "lo_map_sync_surfels", "lo_set_stage_timing", "lo_stage_time", "lo_pko_em_stats", "lo_icp_export_pose", "lo_bench_kernel", "lo_bench_correspond_rr", "lo_find_correspondences", "lo_knn_search", "lo_pko_scale_factor",
     "lo_build_normal_equations", "lo_pko_sample_indices", "lo_pko_sample_indices_host", "lo_debug_counters", "lo_debug_counters_ex", "lo_stage_span", "lo_seq_sum_f64", "lo_seq_sum_f32",
     "lo_batch_create", "lo_batch_destroy", "lo_batch_last_error", "lo_batch_size", "lo_batch_optimize_async",
     "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_status", "lo_devmap_status_async", "lo_devmap_status_poll", "lo_devmap_sync_points", "lo_kd_reruns", "lo_devmap_get_l0", "lo_devmap_get_l1",
     # include/lo_odometry.h
     "lo_odom_config_default_kitti", "lo_odom_create", "lo_odom_destroy", "lo_odom_last_error", "lo_odom_set_initial_pose",
-    "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact",
+    "lo_odom_process", "lo_odom_keyframe_count", "lo_odom_map_surfels", "lo_odom_set_exact", "lo_odom_flush",
     # include/lo_io.h
     "lo_load_kitti_bin", "lo_load_ply", "lo_kitti_pose_line", "lo_save_trajectory_kitti",
     # include/lo_pgo.h
@@ -147,6 +147,8 @@ def lib():
     L.lo_odom_map_surfels.restype = C.c_size_t
     L.lo_odom_map_surfels.argtypes = [vp]
     L.lo_odom_set_exact.argtypes = [vp, C.c_int]
+    L.lo_odom_flush.restype = C.c_int
+    L.lo_odom_flush.argtypes = [vp]
     L.lo_load_kitti_bin.restype = C.c_longlong
     L.lo_load_kitti_bin.argtypes = [C.c_char_p, fp, C.c_size_t]
     L.lo_load_ply.restype = C.c_longlong
@@ -211,6 +213,7 @@ def lib():
     L.lo_pko_em_stats.argtypes = [vp, C.POINTER(C.c_ulonglong), C.c_int]
     L.lo_icp_export_pose.argtypes = [vp, vp]
     L.lo_bench_kernel.argtypes = [vp, vp, C.c_size_t, fp, C.c_double, C.c_double, C.c_int, C.c_int, fp]
+    L.lo_bench_correspond_rr.argtypes = [C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_size_t), fp, C.c_int, C.c_int, fp]
     L.lo_find_correspondences.argtypes = [vp, fp, C.c_size_t, fp, u8p, dp]
     L.lo_knn_search.argtypes = [vp, fp, C.c_size_t, ip, fp]
     L.lo_pko_scale_factor.restype = C.c_double

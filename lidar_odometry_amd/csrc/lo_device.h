@@ -77,7 +77,8 @@ struct DevState {
     double g_out[6];
     double cost_out;
     double gmm_out[3 * kMaxK];
-    unsigned long long dbg[24];     // diagnostic build only (-DLO_PKO_STAMPS): phase timestamps / counters
+    unsigned long long dbg[24];     // diagnostic builds: phase timestamps / counters; product: [5] / [8] long-sum walk
+                                    // statistics, [23] the last one-workgroup exact scale's sort width (points)
     unsigned long long em_stat[3];  // with stage timing: EM s_memtime cycles, EM iterations, fits (lead workgroup)
     lo_iter_log logs[LO_MAX_ITERS];
 };

@@ -264,25 +264,27 @@ __device__ __forceinline__ KeyStat keystat_op(KeyStat a, KeyStat b) {
 }
 constexpr int kScaleC = 1024;                                // k_exact_scale_c threads
 template <int PT>
-__host__ __device__ constexpr int scale_c_bins() { return PT * kScaleC <= 4096 ? PT * kScaleC : 2048; }
+__host__ __device__ constexpr int scale_c_bins() { return PT * kScaleC <= 4096 ? PT * kScaleC : (PT <= 8 ? 2048 : 1024); }
 template <int PT>
 __host__ __device__ constexpr size_t scale_c_lds() {
     return static_cast<size_t>(PT) * kScaleC * sizeof(uint64_t) + 2 * static_cast<size_t>(scale_c_bins<PT>()) * sizeof(int);
 }
 
+// n: the scan's point count (<= PT * kScaleC); s_dyn: scale_c_lds<PT>() bytes; S / s_ks: the caller's static LDS (one
+// copy for every width the device-dispatching kernel inlines)
 template <int PT>
-__device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
+__device__ __forceinline__ void exact_scale_c_body(const KParams& P, int n, uint64_t* s_dyn, MonoScratch<kScaleC>& S,
+                                                   KeyStat* s_ks) {
     DevState* st = P.st;
-    if (st->done) return;
     constexpr int NT = kScaleC, N = PT * NT, NB = scale_c_bins<PT>();
-    extern __shared__ uint64_t s_dyn[];
     uint64_t* s_tmp = s_dyn;                                 // keys in bin order, then sorted (in place)
     int* s_cnt = reinterpret_cast<int*>(s_dyn + N);          // per-bin count
     int* s_end = s_cnt + NB;                                 // per-bin start, then end (after the scatter)
-    __shared__ MonoScratch<NT> S;
-    __shared__ KeyStat s_ks[NT / kWave];
     LO_XSTAMP(st, 0);
-    const int tid = threadIdx.x, n = scan_n(P);
+    const int tid = threadIdx.x;
+#ifndef LO_EXACT_STAMPS
+    if (tid == 0) st->dbg[23] = N;                           // the sort width this scan ran (lo_debug_counters_ex)
+#endif
     const int32_t* slot = P.slot;
     const double* res = P.kd_res ? P.kd_res : P.res_out;
     // the keys, coalesced: element e = q NT + tid (the accepted residual's bits, else +inf)
@@ -402,10 +404,43 @@ __device__ __forceinline__ void exact_scale_c_body(const KParams& P) {
     if (tid == 0) st->scale = sqrt(var) / 6.0;               // :313-315
 }
 template <int PT>
-__global__ __launch_bounds__(kScaleC) void k_exact_scale_c(KParams P) { exact_scale_c_body<PT>(P); }
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_c(KParams P) {
+    if (P.st->done) return;
+    extern __shared__ uint64_t s_dyn[];
+    __shared__ MonoScratch<kScaleC> S;
+    __shared__ KeyStat s_ks[kScaleC / kWave];
+    exact_scale_c_body<PT>(P, scan_n(P), s_dyn, S, s_ks);
+}
+// the widest sort out of line: its registers (it spills) stay out of the narrower widths' code in k_exact_scale_cd
+__device__ __noinline__ void exact_scale_c_body16(const KParams& P, int n, uint64_t* s_dyn, MonoScratch<kScaleC>& S,
+                                                  KeyStat* s_ks) {
+    exact_scale_c_body<16>(P, n, s_dyn, S, s_ks);
+}
+// A scan counted on the device (lo_icp_optimize_raw: the voxel filter's output count stays in HBM; the host knows only
+// the bound ceil(n_raw / stride)): the width is chosen from the count itself, so a 14k-point bound whose filtered scan
+// holds 4k points runs the 4k-point sort and sums.  Dynamic LDS: scale_c_lds<16>() (every narrower width fits in it).
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_cd(KParams P) {
+    if (P.st->done) return;
+    extern __shared__ uint64_t s_dyn[];
+    __shared__ MonoScratch<kScaleC> S;
+    __shared__ KeyStat s_ks[kScaleC / kWave];
+    const int n = min(scan_n(P), P.n);                       // the count never exceeds the bound the grid was sized for
+    if (n <= kScaleC) exact_scale_c_body<1>(P, n, s_dyn, S, s_ks);
+    else if (n <= 2 * kScaleC) exact_scale_c_body<2>(P, n, s_dyn, S, s_ks);
+    else if (n <= 4 * kScaleC) exact_scale_c_body<4>(P, n, s_dyn, S, s_ks);
+    else if (n <= 8 * kScaleC) exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
+    else exact_scale_c_body16(P, n, s_dyn, S, s_ks);
+}
 // batched (lo_batch_* over reference-exact contexts): one workgroup per job
 template <int PT>
-__global__ __launch_bounds__(kScaleC) void k_exact_scale_cb(const KParams* __restrict__ PB) { exact_scale_c_body<PT>(PB[blockIdx.x]); }
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_cb(const KParams* __restrict__ PB) {
+    const KParams& P = PB[blockIdx.x];
+    if (P.st->done) return;
+    extern __shared__ uint64_t s_dyn[];
+    __shared__ MonoScratch<kScaleC> S;
+    __shared__ KeyStat s_ks[kScaleC / kWave];
+    exact_scale_c_body<PT>(P, scan_n(P), s_dyn, S, s_ks);
+}
 template <int PT>
 static hipError_t scale_c_attr() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cb<PT>), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -414,8 +449,9 @@ static hipError_t scale_c_attr() {
                                static_cast<int>(scale_c_lds<PT>()));
 }
 hipError_t exact_scale_c_prepare() {
-    hipError_t e = hipSuccess;
-    for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>()})
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cd), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(scale_c_lds<16>()));
+    for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>(), scale_c_attr<16>()})
         if (e == hipSuccess) e = r;
     return e;
 }
@@ -427,12 +463,15 @@ void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t 
     else if (n_max <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<4>, g, b, scale_c_lds<4>(), s, PB);
     else hipLaunchKernelGGL(k_exact_scale_cb<8>, g, b, scale_c_lds<8>(), s, PB);
 }
-// the bound P.n (a device-counted scan: its upper bound) <= kExactMergeMax
+// P.n <= kExactScaleCMax; a device-counted scan (P.n_dev) chooses its width from the count on the device
 void launch_exact_scale_c(const KParams& P, hipStream_t s) {
-    if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
+    if (P.n_dev && P.n > kScaleC)
+        hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
+    else if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
     else if (P.n <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<2>, dim3(1), dim3(kScaleC), scale_c_lds<2>(), s, P);
     else if (P.n <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<4>, dim3(1), dim3(kScaleC), scale_c_lds<4>(), s, P);
-    else hipLaunchKernelGGL(k_exact_scale_c<8>, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
+    else if (P.n <= 8 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<8>, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
+    else hipLaunchKernelGGL(k_exact_scale_c<16>, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
 }
 
 constexpr int kScaleThreads = 256;                           // k_exact_scale_s: 4 waves, PT = padded size / 256

@@ -22,6 +22,7 @@
 
 #include "lo_ctx_internal.h"
 #include "lo_device.h"
+#include "lo_exact.h"
 #include "lo_kdorder.h"
 #include "lo_math.h"
 #include "lo_pko_tables.h"
@@ -149,7 +150,7 @@ struct lo_ctx {
     uint64_t cfg_gen = 0;           // bumped by lo_update_config and by (re)allocations of the PKO / candidate buffers: a
                                     //   batch's cached device KParams of this context are stale once it changes
     float* d_ex_terms = nullptr;
-    size_t ex_cap = 0;              //   rows of d_ex_terms
+    size_t ex_cap = 0;              //   floats in d_ex_terms
     float* d_ex_tot = nullptr;      //   large scans: the 43 sums (launch_mw_sums -> k_exact_finish)
     double* d_ex_rank = nullptr;    //   the iteration-0 residuals in sorted order (k_rank_sort, kExactMaxPoints), or
                                     //   up to kExactMergeMax points: the correspondence blocks' sorted runs
@@ -1228,10 +1229,12 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
 
 namespace lo {
 // ---- the same grid built on the device (ctx_grid_from_device: the device map's L0 centroids) ----
+// Every kernel here clamps the device count to the array's capacity: a corrupt or overflowing count is reported by the
+// host (out[6] carries the raw count) without a read past the array.
 __global__ __launch_bounds__(1024) void k_grid_bounds(const float* __restrict__ xyz, const int* __restrict__ d_count,
-                                                     float* __restrict__ out) {
+                                                     int cap, float* __restrict__ out) {
     __shared__ float s[6][16];
-    const int m = *d_count, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int m_raw = *d_count, m = min(max(m_raw, 0), cap), tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = tid; i < m; i += 1024)
         for (int a = 0; a < 3; ++a) { const float v = xyz[3 * i + a]; lo[a] = fminf(lo[a], v); hi[a] = fmaxf(hi[a], v); }
@@ -1244,7 +1247,7 @@ __global__ __launch_bounds__(1024) void k_grid_bounds(const float* __restrict__ 
         for (int w = 1; w < 16; ++w) r = tid < 3 ? fminf(r, s[tid][w]) : fmaxf(r, s[tid][w]);
         out[tid] = r;
     }
-    if (tid == 0) out[6] = __int_as_float(m);
+    if (tid == 0) out[6] = __int_as_float(m_raw);
 }
 struct GridGeom {
     float h;
@@ -1252,10 +1255,10 @@ struct GridGeom {
 };
 // grid_build's cell of a coordinate: floor(v / h) in fp32, as an int64 (the same operations)
 __device__ __forceinline__ long long grid_cell(float v, float h) { return static_cast<long long>(floorf(v / h)); }
-__global__ void k_grid_keys(const float* __restrict__ xyz, const int* __restrict__ d_count, GridGeom g,
+__global__ void k_grid_keys(const float* __restrict__ xyz, const int* __restrict__ d_count, int cap, GridGeom g,
                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *d_count) return;
+    if (i >= min(*d_count, cap)) return;
     const long long x = grid_cell(xyz[3 * i], g.h) - g.org[0], y = grid_cell(xyz[3 * i + 1], g.h) - g.org[1],
                     z = grid_cell(xyz[3 * i + 2], g.h) - g.org[2];
     const uint32_t lin = static_cast<uint32_t>((static_cast<unsigned long long>(z) * g.dim[1] + y) * g.dim[0] + x);
@@ -1263,10 +1266,10 @@ __global__ void k_grid_keys(const float* __restrict__ xyz, const int* __restrict
     vals[i] = static_cast<uint32_t>(i);
     atomicAdd(&counts[lin], 1u);
 }
-__global__ void k_grid_scatter(const float* __restrict__ xyz, const int* __restrict__ d_count,
+__global__ void k_grid_scatter(const float* __restrict__ xyz, const int* __restrict__ d_count, int cap,
                                const uint32_t* __restrict__ svals, float4* __restrict__ pts) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= *d_count) return;
+    if (p >= min(*d_count, cap)) return;
     const uint32_t i = svals[p];
     pts[p] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], __int_as_float(static_cast<int>(i)));
 }
@@ -1279,7 +1282,8 @@ int ctx_grid_from_device(lo_ctx* c, const float* d_xyz, const int* d_count, size
     DevGridScratch& S = c->gscr;
     if (!S.d_bounds) LO_HIP(c, hipMalloc(&S.d_bounds, 8 * sizeof(float)));
     if (!S.h_bounds) LO_HIP(c, hipHostMalloc(&S.h_bounds, 8 * sizeof(float), hipHostMallocDefault));
-    hipLaunchKernelGGL(k_grid_bounds, dim3(1), dim3(1024), 0, c->stream, d_xyz, d_count, S.d_bounds);
+    const int capi = static_cast<int>(std::min(cap, static_cast<size_t>(INT32_MAX)));
+    hipLaunchKernelGGL(k_grid_bounds, dim3(1), dim3(1024), 0, c->stream, d_xyz, d_count, capi, S.d_bounds);
     LO_HIP(c, hipMemcpyAsync(S.h_bounds, S.d_bounds, 8 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     LO_HIP(c, hipStreamSynchronize(c->stream));
     int mi = 0;
@@ -1336,11 +1340,11 @@ int ctx_grid_from_device(lo_ctx* c, const float* d_xyz, const int* d_count, size
     GridGeom g{h, {org[0], org[1], org[2]}, {dim[0], dim[1], dim[2]}};
     if (m > 0) {
         const dim3 grid((m + 255) / 256), blk(256);
-        hipLaunchKernelGGL(k_grid_keys, grid, blk, 0, c->stream, d_xyz, d_count, g, keys, vals, S.d_counts);
+        hipLaunchKernelGGL(k_grid_keys, grid, blk, 0, c->stream, d_xyz, d_count, capi, g, keys, vals, S.d_counts);
         size_t t = S.tmp_cap;
         LO_HIP(c, hipcub::DeviceRadixSort::SortPairs(S.d_tmp, t, keys, skeys, vals, svals, static_cast<int>(m), 0, bits,
                                                      c->stream));
-        hipLaunchKernelGGL(k_grid_scatter, grid, blk, 0, c->stream, d_xyz, d_count, svals, G.d_pts);
+        hipLaunchKernelGGL(k_grid_scatter, grid, blk, 0, c->stream, d_xyz, d_count, capi, svals, G.d_pts);
     }
     size_t t2 = S.tmp_cap;                               // start[cell] = points in the cells before it; start[ncell] = m
     LO_HIP(c, hipcub::DeviceScan::ExclusiveSum(S.d_tmp, t2, S.d_counts, G.d_start, static_cast<int>(ncell + 1), c->stream));
@@ -1430,11 +1434,15 @@ static void launch_correspond_first(lo_ctx* c, const KParams& P0, bool kd, int w
 // at most kExactMaxPoints sort in one workgroup (*n2 = n: registers + LDS, lo_seqsum.h); larger scans (*n2 = 0)
 // write their residuals out, sort them with hipCUB's radix sort and sum them across the chip (launch_mwm_scale).
 static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
-    if (!c->d_ex_terms || c->ex_cap < std::max(n, static_cast<size_t>(kExactMaxPoints))) {
+    // the term buffer: row-major [point][43] up to kExactMaxPoints (k_exact_terms + k_exact_solve), term-major rows of
+    // round_up(n, 64) beyond (the 14 factor rows, or the 43 term columns in the LO_EXACT_FACTORED=0 A/B build)
+    const size_t ex_need = std::max(static_cast<size_t>(kExactMaxPoints) * kExactTerms,
+                                    (kExactFactored ? kExactFactors : kExactTerms) * ((n + 63) & ~static_cast<size_t>(63)));
+    if (!c->d_ex_terms || c->ex_cap < ex_need) {
         if (c->d_ex_terms) LO_HIP(c, hipFree(c->d_ex_terms));
         c->d_ex_terms = nullptr;
-        c->ex_cap = std::max(n, static_cast<size_t>(kExactMaxPoints));
-        LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * 43 * sizeof(float)));
+        c->ex_cap = ex_need;
+        LO_HIP(c, hipMalloc(&c->d_ex_terms, c->ex_cap * sizeof(float)));
     }
     if (!c->d_ex_rank) LO_HIP(c, hipMalloc(&c->d_ex_rank, kExactMaxPoints * sizeof(double)));
     if (!c->ex_attr) {
@@ -1447,8 +1455,11 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
     P.scale_given = 1;
     // up to kExactMergeMax points the iteration-0 correspondence launch presorts its blocks (P0.presort, set by the
     // caller from ex_merge) and one workgroup merges and sums them
-    c->ex_merge = n <= static_cast<size_t>(kExactMergeMax);
-    c->ex_merge_presort = c->ex_merge && std::getenv("LO_EXACT_PRESORT") != nullptr;   // A/B: the presorted-runs path
+    // (r06: up to kExactMaxPoints; a device-counted scan -- the voxel filter's output -- picks its sort width from the
+    // count on the device, k_exact_scale_cd, instead of sizing the sort by the bound ceil(n_raw / stride))
+    c->ex_merge = n <= static_cast<size_t>(kExactMaxPoints);
+    c->ex_merge_presort = n <= static_cast<size_t>(kExactMergeMax) && std::getenv("LO_EXACT_PRESORT") != nullptr;   // A/B
+    if (std::getenv("LO_EXACT_RANKSORT")) c->ex_merge = c->ex_merge_presort = false;   // A/B: the chip-wide rank sort
     if (n > static_cast<size_t>(kExactMaxPoints)) {
         if (!c->d_ex_tot) LO_HIP(c, hipMalloc(&c->d_ex_tot, 64 * sizeof(float)));
         if (c->mw_n_cap < n) {                               // the column sums' head records
@@ -1489,7 +1500,7 @@ static int exact_prepare(lo_ctx* c, KParams& P, size_t n, int* n2) {
 // the iteration-0 scale of reference-exact mode (between the scan's first correspondence launch and its first PKO)
 static void launch_exact_scale_any(lo_ctx* c, const KParams& P, int n2, hipStream_t s) {
     if (c->ex_merge && !c->ex_merge_presort) {
-        launch_exact_scale_c(P, s);                          // counting sort + sums in one workgroup
+        launch_exact_scale_c(P, s);                          // counting sort + sums in one workgroup (<= 16384 points)
         return;
     }
     if (c->ex_merge) {
@@ -1580,7 +1591,8 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             // is final
             const int rc2 = pipe_alloc(c);
             if (rc2 != LO_OK) return rc2;
-            const uint32_t seq = ++c->pipe_seq;
+            if (++c->pipe_seq == 0) c->pipe_seq = 1;      // 0 is the fence word's reset value, never a scan's number
+            const uint32_t seq = c->pipe_seq;
             P.fin = P0.fin = c->d_fin;
             P.seq = P0.seq = seq;
             KParams Pt = P;                               // tail launches: leave once scan seq is final (the
@@ -1595,7 +1607,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
                 const bool tail = it >= c->pipe_main;
                 if (it == c->pipe_main)                   // bound 0: the test hook's forced timeout
                     hipLaunchKernelGGL(k_wait_seq, dim3(1), dim3(kWave), 0, c->s_tail, c->d_fin, seq, c->d_st, c->d_hbroken,
-                                       seq == c->pipe_fail_at ? 0ull : c->pipe_bound);
+                                       (c->pipe_fail_at != 0 && seq == c->pipe_fail_at) ? 0ull : c->pipe_bound);
                 const hipStream_t s = tail ? c->s_tail : c->stream;
                 const KParams& Pi = tail ? Pt : (it + 1 == c->pipe_main ? Ph : P);
                 launch_pko_spec(c, Pi, it, s);
@@ -2261,6 +2273,40 @@ int lo_bench_kernel(lo_ctx* c, const float* d_pts, size_t n, const float T[12], 
     return LO_OK;
 }
 
+int lo_bench_correspond_rr(lo_ctx* const* ctxs, const float* const* d_pts, const size_t* n, const float* T, int count,
+                           int rounds, float* avg_ms) {
+    if (!ctxs || !d_pts || !n || !T || !avg_ms || count < 1 || rounds < 1) return LO_ERR_ARG;
+    lo_ctx* c0 = ctxs[0];
+    if (!c0) return LO_ERR_ARG;
+    std::vector<KParams> P(count);
+    for (int i = 0; i < count; ++i) {
+        lo_ctx* c = ctxs[i];
+        if (!c || !d_pts[i] || n[i] == 0) return LO_ERR_ARG;
+        if (c->kd || c->device != c0->device) { c0->err = "lo_bench_correspond_rr: surfel contexts on one device"; return LO_ERR_STATE; }
+        if (n[i] > static_cast<size_t>(c->cfg.max_points)) { c0->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
+    }
+    LO_HIP(c0, hipSetDevice(c0->device));
+    for (int i = 0; i < count; ++i) {                       // every context's state on its own stream, then joined
+        lo_ctx* c = ctxs[i];
+        int rc = reset_state(c, T + 12 * i, 1.0, 0.1);
+        if (rc == LO_OK) rc = ensure_acc_part(c);
+        if (rc != LO_OK) { c0->err = c->err; return rc; }
+        P[i] = make_params(c, d_pts[i], static_cast<int>(n[i]));
+        LO_HIP(c0, hipStreamSynchronize(c->stream));
+    }
+    const hipStream_t s = c0->stream;
+    LO_HIP(c0, hipEventRecord(c0->ev0, s));
+    for (int r = 0; r < rounds; ++r)
+        for (int i = 0; i < count; ++i) hipLaunchKernelGGL(k_correspond, dim3(P[i].nb), dim3(kBlock), 0, s, P[i], 0);
+    LO_HIP(c0, hipEventRecord(c0->ev1, s));
+    LO_HIP(c0, hipGetLastError());
+    LO_HIP(c0, hipEventSynchronize(c0->ev1));
+    float ms = 0.0f;
+    LO_HIP(c0, hipEventElapsedTime(&ms, c0->ev0, c0->ev1));
+    *avg_ms = ms / (static_cast<float>(rounds) * count);
+    return LO_OK;
+}
+
 int lo_seq_sum_f64(lo_ctx* c, const double* x, size_t n, int sort, double* out_sum, long long stats[4]) {
     if (!c || !out_sum || (n > 0 && !x) || n > static_cast<size_t>(kExactMaxPoints)) return LO_ERR_ARG;
     LO_HIP(c, hipSetDevice(c->device));
@@ -2380,7 +2426,14 @@ struct lo_batch {
     std::vector<float> T_in;         // count x 12 (T_out of failed / skipped jobs)
     std::vector<int> act;            // active job -> job index
     std::vector<size_t> n;
-    struct Sig { const lo_ctx* ctx; uint64_t gen; const float* pts; int n; const Slot* tab; uint32_t log2cap; int exact; };
+    struct Sig {
+        const lo_ctx* ctx; uint64_t gen; const float* pts; int n; const Slot* tab; uint32_t log2cap; int exact;
+        // field by field: the padding after n is not initialised, so a byte compare could report a change every call
+        bool operator==(const Sig& o) const {
+            return ctx == o.ctx && gen == o.gen && pts == o.pts && n == o.n && tab == o.tab && log2cap == o.log2cap &&
+                   exact == o.exact;
+        }
+    };
     std::vector<Sig> sig;            // what d_P currently holds, per active slot
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_go = nullptr;      // reference-exact jobs: the batch's uploads done (their streams wait on it)
@@ -2417,6 +2470,9 @@ static int batch_alloc(lo_batch* b) {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxBlocks * sizeof(int))));
     LO_BHIP(b, hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_acc_b), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    static_cast<int>(kXcLdsBytes)));
+    // reference-exact jobs' iteration-0 scale (k_exact_scale_cb, up to 80 KB of dynamic LDS): a process that only
+    // batches must not depend on a single-context exact optimize having set the attribute first
+    LO_BHIP(b, exact_scale_c_prepare());
     b->T_in.assign(B * 12, 0.0f);
     b->n.assign(B, 0);
     return LO_OK;
@@ -2526,7 +2582,7 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
             }
             max_nb = std::max(max_nb, P.nb);
             const lo_batch::Sig sg{c, c->cfg_gen, pts, P.n, P.tab, P.log2cap, pass};
-            if (a >= static_cast<int>(b->sig.size()) || std::memcmp(&b->sig[a], &sg, sizeof(sg)) != 0) same = false;
+            if (a >= static_cast<int>(b->sig.size()) || !(b->sig[a] == sg)) same = false;
             if (!same) {
                 if (a < static_cast<int>(b->sig.size())) b->sig[a] = sg; else b->sig.push_back(sg);
             }
@@ -2584,7 +2640,10 @@ int lo_batch_optimize_async(lo_batch* b, const float* const* d_pts, const size_t
         const dim3 blk(kBlock);
         for (int it = 0; it < b->max_iters; ++it) {
             hipLaunchKernelGGL(k_correspond_b, dim3(max_nb, nact), blk, 0, b->stream, b->d_P, it == 0 ? 1 : 0, it == 0 ? 1 : 0);
-            if (it == 0 && nexl > 0) launch_exact_scale_cb(b->d_P + nfast, nexl, n_max_ex, b->stream);
+            if (it == 0 && nexl > 0) {
+                launch_exact_scale_cb(b->d_P + nfast, nexl, n_max_ex, b->stream);
+                LO_BHIP(b, hipGetLastError());                 // e.g. a dynamic-LDS launch the attribute did not allow
+            }
             if (nact >= b->one_wave_min)
                 hipLaunchKernelGGL((k_pko_tb<1, true>), dim3(1, nact), dim3(64), pre_bytes, b->stream, b->d_P, it);
             else

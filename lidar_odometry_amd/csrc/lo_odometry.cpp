@@ -209,6 +209,14 @@ int lo_odom_process(lo_odometry* o, const float* raw, size_t n, float T_out[12],
     return rc;
 }
 
+int lo_odom_flush(lo_odometry* o) {
+    if (!o) return LO_ERR_ARG;
+    if (!o->dmap) return LO_OK;                          // the host map reports inside lo_voxelmap_update
+    const int rc = lo_devmap_status(o->dmap);            // synchronous: the last update's error bits
+    if (rc != LO_OK) o->err = lo_devmap_last_error(o->dmap);
+    return rc;
+}
+
 size_t lo_odom_keyframe_count(const lo_odometry* o) { return o ? o->keyframes : 0; }
 size_t lo_odom_map_surfels(const lo_odometry* o) {
     if (!o) return 0;

@@ -76,6 +76,12 @@ class LidarOdometry:
         return T.reshape(3, 4), FrameInfo(info.status, bool(info.keyframe), info.icp_iterations, info.n_filtered,
                                           info.n_corr, info.device_ms, info.map_ms)
 
+    def flush(self):
+        """Wait for the last keyframe's map update; raise if it overflowed the device map (lo_odom_flush)."""
+        rc = lib().lo_odom_flush(self._o)
+        if rc < 0:
+            raise RuntimeError(f"lo_odom_flush error {rc}: {lib().lo_odom_last_error(self._o).decode()}")
+
     @property
     def keyframes(self) -> int:
         return int(lib().lo_odom_keyframe_count(self._o))

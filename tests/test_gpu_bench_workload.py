@@ -1,6 +1,7 @@
 """Parity on the bench's own workloads -- the exact inputs the `value` lines time: KITTI-07-like city map after 660
 frames (331 keyframes, 12.8k surfels, 120k L0 voxels) with its 20 measured scans (C2), the MID360-like rosette
-sequence (C3, 20 scans) and the synthetic 1M-point patch scans (C5, 4 scans), each with its perturbed initial poses.
+sequence (C3, 20 scans), the same city map through the KDTree correspondence variant (C4: 5-NN plane fits against its
+120k L0 centroids, 20 scans) and the synthetic 1M-point patch scans (C5, 4 scans), each with its perturbed initial poses.
 The PRODUCT DEFAULT (a context as lo_create makes it: reference-exact arithmetic) is bit-identical to the oracle at
 every iteration -- pose, alpha, correspondence count -- on all three, so it meets the north_star tolerance (1e-4 m /
 1e-4 rad per iteration) everywhere.  The opt-in fast mode (lo_set_exact(ctx, 0): fp64 tree sums) stays within the
@@ -16,7 +17,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["kitti", "mid360", "patch1m"])
+@pytest.fixture(scope="module", params=["kitti", "mid360", "kitti_kdtree", "patch1m"])
 def workload(request):
     wl = bench.WORKLOADS[request.param](0)
     wl["key"] = request.param
@@ -26,7 +27,7 @@ def workload(request):
     inits = [bench.pose12(T) for T in wl["inits"]]
     ref = []
     for pts, Ti in zip(wl["scans"], inits):
-        ok, To, _, logs = oracle.icp_optimize(m, pts, Ti)
+        ok, To, _, logs = oracle.icp_optimize(m, pts, Ti, kdtree=wl.get("kdtree", False))
         ref.append({"ok": ok, "T": np.asarray(To if ok else Ti, np.float32), "logs": logs})
     return wl, inits, ref
 
@@ -35,7 +36,8 @@ def _gpu_results(wl, inits, exact):
     """exact: True / False set the mode, None keeps the product default (lo_create's)."""
     from lidar_odometry_amd import AdaptiveMEstimatorConfig, ICPConfig, IterativeClosestPointOptimizer, MapGeometry
     from lidar_odometry_amd._lib import lib
-    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=True), AdaptiveMEstimatorConfig(),
+    o = IterativeClosestPointOptimizer(ICPConfig(use_surfel_correspondence=not wl.get("kdtree", False)),
+                                       AdaptiveMEstimatorConfig(),
                                        MapGeometry(voxel_size=wl["voxel"]),
                                        max_points=max(len(s) for s in wl["scans"]))   # as bench.py builds it
     try:
@@ -54,7 +56,7 @@ def _gpu_results(wl, inits, exact):
 
 def test_bench_workload_size(workload):
     wl, _, _ = workload
-    if wl["key"] == "kitti":
+    if wl["key"] in ("kitti", "kitti_kdtree"):
         assert len(wl["scans"]) == 20
         assert wl["vm"].surfel_count() > 10_000                 # 10^4-10^5 surfels
     elif wl["key"] == "patch1m":
@@ -73,11 +75,11 @@ def test_bench_workload_product_default_parity(workload):
 
 
 def test_bench_workload_fast_mode(workload):
-    """The opt-in fast mode: within 1e-4 on C2; on C3 / C5 bounded by 1e-3 (alpha near-ties resolve differently)."""
+    """The opt-in fast mode: within 1e-4 on C2 / C4; on C3 / C5 bounded by 1e-3 (alpha near-ties resolve differently)."""
     wl, inits, ref = workload
     p = bench.parity_vs_oracle(_gpu_results(wl, inits, exact=False), ref)
     assert p["status_equal"] == len(ref), p
-    if wl["key"] == "kitti":
+    if wl["key"] in ("kitti", "kitti_kdtree"):
         assert p["within_1e-4"], p
         assert p["iteration_count_equal"] == p["alpha_every_iteration_equal"] == len(ref), p
     else:

@@ -133,3 +133,68 @@ def test_exact_large_scan_bitwise(exact, n_points):
     exact.set_surfels(k, n, c)
     st = _bitwise(exact, m, pts, Ti)
     assert st.num_iterations >= 1
+
+
+def _scale_width(o):
+    """The sort width (points) the last one-workgroup exact scale ran with (DevState::dbg[23], product builds)."""
+    import ctypes as C
+    from lidar_odometry_amd._lib import lib
+    d = (C.c_ulonglong * 24)()
+    assert lib().lo_debug_counters_ex(o.ctx, d, 24) == 0
+    return int(d[23])
+
+
+def _bitwise_logs(st, ok_g, To_g, ref):
+    ok_o, To_o, it_o, logs_o = ref
+    assert ok_g == ok_o and st.num_iterations == it_o
+    for k, (lo, lg) in enumerate(zip(logs_o, st.iterations)):
+        for key in ("pose", "H", "g", "delta"):
+            np.testing.assert_array_equal(np.asarray(lg[key], np.float32).view(np.uint32),
+                                          np.asarray(lo[key], np.float32).view(np.uint32), err_msg=f"iter {k} {key}")
+        assert lg["scale"] == lo["scale"] and lg["alpha"] == lo["alpha"] and lg["n_corr"] == lo["n_corr"], k
+    np.testing.assert_array_equal(np.asarray(To_g, np.float32).reshape(12).view(np.uint32),
+                                  np.asarray(To_o, np.float32).reshape(12).view(np.uint32))
+
+
+@pytest.mark.parametrize("frame", [11, 25])
+def test_exact_raw_scan_sorts_by_device_count(exact, frame):
+    """A raw scan filtered on the device (lo_icp_optimize_raw) is sized on the host only by its bound ceil(n_raw /
+    stride) (~14k points here), while ~4k points survive the filter.  The iteration-0 scale picks its sort width from
+    the count on the device (k_exact_scale_cd): the one-workgroup path at <= 8192 points, not a 16k-wide sort.  Every
+    iteration bit-identical to the oracle run on the host-filtered scan (Estimator.cpp:561-589 -> optimize)."""
+    m, pts, Ti, _ = _data.kitti_case(frame)
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    raw = _data.kitti_scan(frame)
+    assert (len(raw) + 7) // 8 > 8192 >= len(pts)
+    ok_g, To_g = exact.optimize_raw(None, raw, Ti, stride=8, voxel_size=0.5)
+    _bitwise_logs(exact.get_last_stats(), ok_g, To_g, oracle.icp_optimize(m, pts, Ti))
+    w = _scale_width(exact)
+    assert len(pts) <= w <= 8192, w
+
+
+def test_exact_raw_scan_beyond_8192_filtered_points(exact):
+    """The device count above 8192 (a fine filter over a 14k-point raw scan): the widest one-workgroup sort (16384,
+    out of line in k_exact_scale_cd), still bitwise."""
+    m, pts, Ti, _ = _data.patch_case(n_points=14_000, seed=1003)
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    filt = oracle.voxel_filter(pts, 0.001, 1)
+    assert 8192 < len(filt) <= 16384
+    ok_g, To_g = exact.optimize_raw(None, pts, Ti, stride=1, voxel_size=0.001)
+    np.testing.assert_array_equal(exact.filtered_points().view(np.uint32), filt.view(np.uint32))
+    _bitwise_logs(exact.get_last_stats(), ok_g, To_g, oracle.icp_optimize(m, filt, Ti))
+    assert _scale_width(exact) == 16384
+
+
+@pytest.mark.parametrize("n_points", [12_000])
+def test_exact_mid_size_scan_both_sort_paths(exact, monkeypatch, n_points):
+    """8192 < n <= 16384 host-counted: the one-workgroup counting sort at width 16384 (default) and the chip-wide rank
+    sort (LO_EXACT_RANKSORT, the round-5 path) give the oracle's bits."""
+    m, pts, Ti, _ = _data.patch_case(n_points=n_points, seed=1001)
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    _bitwise(exact, m, pts, Ti)
+    assert _scale_width(exact) == 16384
+    monkeypatch.setenv("LO_EXACT_RANKSORT", "1")
+    _bitwise(exact, m, pts, Ti)

@@ -135,6 +135,31 @@ def test_map_overflow_reported_at_next_frame(monkeypatch):
         od.close()
 
 
+def test_map_overflow_at_last_keyframe_reported_by_flush(monkeypatch):
+    """An overflow at the run's final keyframe has no next frame to report it: lo_odom_flush waits for the update and
+    returns LO_ERR_CAPACITY."""
+    from lidar_odometry_amd import synth
+    from lidar_odometry_amd.odometry import LidarOdometry
+    from lidar_odometry_amd._lib import LO_ERR_CAPACITY
+    monkeypatch.setenv("LO_DEVMAP_MAX_L0", "64")
+    seq = synth.KittiLikeSequence(seed=7, n_frames=2)
+    od = LidarOdometry(initial_pose=seq.poses[0])
+    try:
+        _, info = od.process(seq.scan(0))
+        assert info.keyframe
+        with pytest.raises(RuntimeError, match=f"error {LO_ERR_CAPACITY}"):
+            od.flush()
+    finally:
+        od.close()
+    monkeypatch.delenv("LO_DEVMAP_MAX_L0")
+    od = LidarOdometry(initial_pose=seq.poses[0])
+    try:
+        od.process(seq.scan(0))
+        od.flush()                                        # a map within capacity: no error
+    finally:
+        od.close()
+
+
 def test_kdtree_frame_loop_device_map_matches_host_map(monkeypatch):
     """KDTree correspondences (use_surfel_correspondence = false): the frame loop on the device map -- the map update
     without surfel decisions (SetComputeSurfels(false), so no planarity erases) and RebuildKdTree as a device grid

@@ -162,3 +162,12 @@ def test_kernel_names_map_as_reference():
     assert got == list(range(6))
     assert L.lo_pko_kernel_from_name(b"Huber") == 1 and L.lo_pko_kernel_from_name(b"") == 1
     assert L.lo_pko_kernel_from_name(None) == 1
+
+
+def test_mutable_accessors_exist_for_unprojected_output(ref):
+    """from_row_major writes the device pose through SE3's non-const Rotation() / Translation() and SO3's non-const
+    Matrix() (no SO3(Matrix3f) projection on the output path, tests/test_adapter_pose.py): those accessors exist."""
+    mu = ref["util/MathUtils.h"]
+    assert re.search(r"\bSO3&\s+Rotation\(\)\s*\{", mu)
+    assert re.search(r"Eigen::Vector3f&\s+Translation\(\)\s*\{", mu)
+    assert re.search(r"Eigen::Matrix3f&\s+Matrix\(\)\s*\{", mu)
