@@ -411,25 +411,32 @@ __global__ __launch_bounds__(kScaleC) void k_exact_scale_c(KParams P) {
     __shared__ KeyStat s_ks[kScaleC / kWave];
     exact_scale_c_body<PT>(P, scan_n(P), s_dyn, S, s_ks);
 }
-// the widest sort out of line: its registers (it spills) stay out of the narrower widths' code in k_exact_scale_cd
-__device__ __noinline__ void exact_scale_c_body16(const KParams& P, int n, uint64_t* s_dyn, MonoScratch<kScaleC>& S,
-                                                  KeyStat* s_ks) {
-    exact_scale_c_body<16>(P, n, s_dyn, S, s_ks);
-}
 // A scan counted on the device (lo_icp_optimize_raw: the voxel filter's output count stays in HBM; the host knows only
 // the bound ceil(n_raw / stride)): the width is chosen from the count itself, so a 14k-point bound whose filtered scan
-// holds 4k points runs the 4k-point sort and sums.  Dynamic LDS: scale_c_lds<16>() (every narrower width fits in it).
+// holds 4k points runs the 4k-point sort and sums.  k_exact_scale_cd takes counts up to 8192 (dynamic LDS
+// scale_c_lds<8>(), every narrower width fits in it; no scratch), k_exact_scale_cw the rare count beyond (launched only
+// when the bound exceeds 8192; each leaves at once when the count is the other's).  One kernel for every width spilled:
+// the 16k-wide body's registers put ~1 KB of scratch per lane on the narrow paths too, 23 -> 46 us at KITTI size.
 __global__ __launch_bounds__(kScaleC) void k_exact_scale_cd(KParams P) {
     if (P.st->done) return;
     extern __shared__ uint64_t s_dyn[];
     __shared__ MonoScratch<kScaleC> S;
     __shared__ KeyStat s_ks[kScaleC / kWave];
     const int n = min(scan_n(P), P.n);                       // the count never exceeds the bound the grid was sized for
+    if (n > 8 * kScaleC) return;                             // k_exact_scale_cw's
     if (n <= kScaleC) exact_scale_c_body<1>(P, n, s_dyn, S, s_ks);
     else if (n <= 2 * kScaleC) exact_scale_c_body<2>(P, n, s_dyn, S, s_ks);
     else if (n <= 4 * kScaleC) exact_scale_c_body<4>(P, n, s_dyn, S, s_ks);
-    else if (n <= 8 * kScaleC) exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
-    else exact_scale_c_body16(P, n, s_dyn, S, s_ks);
+    else exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
+}
+__global__ __launch_bounds__(kScaleC) void k_exact_scale_cw(KParams P) {
+    if (P.st->done) return;
+    extern __shared__ uint64_t s_dyn[];
+    __shared__ MonoScratch<kScaleC> S;
+    __shared__ KeyStat s_ks[kScaleC / kWave];
+    const int n = min(scan_n(P), P.n);
+    if (n <= 8 * kScaleC) return;                            // k_exact_scale_cd's
+    exact_scale_c_body<16>(P, n, s_dyn, S, s_ks);
 }
 // batched (lo_batch_* over reference-exact contexts): one workgroup per job
 template <int PT>
@@ -450,7 +457,10 @@ static hipError_t scale_c_attr() {
 }
 hipError_t exact_scale_c_prepare() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cd), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(scale_c_lds<16>()));
+                                       static_cast<int>(scale_c_lds<8>()));
+    const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cw),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scale_c_lds<16>()));
+    if (e == hipSuccess) e = e2;
     for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>(), scale_c_attr<16>()})
         if (e == hipSuccess) e = r;
     return e;
@@ -465,9 +475,10 @@ void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t 
 }
 // P.n <= kExactScaleCMax; a device-counted scan (P.n_dev) chooses its width from the count on the device
 void launch_exact_scale_c(const KParams& P, hipStream_t s) {
-    if (P.n_dev && P.n > kScaleC)
-        hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
-    else if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
+    if (P.n_dev && P.n > kScaleC) {
+        hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
+        if (P.n > 8 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cw, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
+    } else if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
     else if (P.n <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<2>, dim3(1), dim3(kScaleC), scale_c_lds<2>(), s, P);
     else if (P.n <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<4>, dim3(1), dim3(kScaleC), scale_c_lds<4>(), s, P);
     else if (P.n <= 8 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<8>, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);

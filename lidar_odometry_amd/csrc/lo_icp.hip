@@ -172,6 +172,8 @@ struct lo_ctx {
     uint8_t* d_u8 = nullptr;
     DevState* d_st = nullptr;
     DevState* h_st = nullptr;       // pinned
+    int* h_nf = nullptr;            // pinned: the device-filtered scan's count, read back with the result
+    bool nf_valid = false;          //   h_nf holds the last device-filtered scan's count (lo_icp_result)
     // map
     Slot* d_tab = nullptr;
     size_t tab_cap = 0;             // allocated slots
@@ -596,6 +598,8 @@ static int ctx_alloc(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_st, sizeof(DevState)));
     LO_HIP(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
     std::memset(c->h_st, 0, sizeof(DevState));
+    LO_HIP(c, hipHostMalloc(&c->h_nf, sizeof(int), hipHostMallocDefault));
+    *c->h_nf = 0;
     LO_HIP(c, hipMemset(c->d_st, 0, sizeof(DevState)));
     // empty table (capacity 2) so a scan before any map upload finds nothing
     c->tab_cap = 2;
@@ -687,6 +691,7 @@ void lo_destroy(lo_ctx* c) {
     if (c->d_raw) (void)hipFree(c->d_raw);
     vf_free(c->vf);
     if (c->h_st) (void)hipHostFree(c->h_st);
+    if (c->h_nf) (void)hipHostFree(c->h_nf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (hipEvent_t e : c->st_ev) (void)hipEventDestroy(e);
@@ -1659,6 +1664,7 @@ int lo_icp_optimize_async(lo_ctx* c, const float* d_pts, size_t n, const float T
     if (n > static_cast<size_t>(c->cfg.max_points)) { c->err = "n exceeds max_points"; return LO_ERR_CAPACITY; }
     LO_HIP(c, hipSetDevice(c->device));
     c->last_dev_count = false;
+    c->nf_valid = false;
     return enqueue_optimize(c, d_pts, n, T_init);
 }
 
@@ -1668,6 +1674,10 @@ int lo_icp_result(lo_ctx* c, float T_out[12], lo_iter_log* logs, lo_stats* st) {
     // state header + the executed iterations' logs only
     const size_t bytes = offsetof(DevState, logs) + sizeof(lo_iter_log) * static_cast<size_t>(c->cfg.max_iterations);
     LO_HIP(c, hipMemcpyAsync(c->h_st, c->d_st, bytes, hipMemcpyDeviceToHost, c->stream));
+    // a device-filtered scan: its count comes back in the same sync (lo_filtered_points(ctx, NULL, 0) then reads it
+    // without another round trip -- the frame loop asks for it every frame)
+    c->nf_valid = c->last_dev_count && c->vf.n_out;
+    if (c->nf_valid) LO_HIP(c, hipMemcpyAsync(c->h_nf, c->vf.n_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     LO_HIP(c, hipStreamSynchronize(c->stream));
     c->pending = false;
     const DevState* hs = c->h_st;
@@ -1739,6 +1749,7 @@ int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12
     LO_HIP(c, hipSetDevice(c->device));
     if (n > 0) LO_HIP(c, hipMemcpyAsync(c->d_pts, pts, n * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     c->last_dev_count = false;
+    c->nf_valid = false;
     c->sync_call = true;
     int rc = enqueue_optimize(c, c->d_pts, n, T_init);
     c->sync_call = false;
@@ -1884,6 +1895,7 @@ int lo_icp_optimize_raw_async(lo_ctx* c, const float* d_raw, size_t n_raw, int s
     int m = 0;
     LO_HIP(c, vf_enqueue(c->vf, d_raw, n_raw, stride, voxel_size, c->d_pts, c->stream, m));
     c->last_dev_count = true;
+    c->nf_valid = false;
     return enqueue_optimize(c, c->d_pts, static_cast<size_t>(m), T_init, c->vf.n_out);
 }
 
@@ -1929,6 +1941,7 @@ int lo_icp_optimize_raw(lo_ctx* c, const float* raw, size_t n_raw, int stride, f
 long long lo_filtered_points(lo_ctx* c, float* out, size_t cap) {
     if (!c) return LO_ERR_ARG;
     if (!c->last_dev_count || !c->vf.n_out) { c->err = "no device-filtered scan"; return LO_ERR_STATE; }
+    if (!out && c->nf_valid && !c->pending) return *c->h_nf;   // read back with the scan's result (lo_icp_result)
     LO_HIP(c, hipSetDevice(c->device));
     int n = 0;
     LO_HIP(c, hipMemcpyAsync(&n, c->vf.n_out, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1951,6 +1964,7 @@ long long lo_voxel_filter_gpu(lo_ctx* c, const float* raw, size_t n_raw, float v
     int m = 0;
     LO_HIP(c, vf_enqueue(c->vf, c->d_raw, n_raw, stride, voxel_size, c->d_pts, c->stream, m));
     c->last_dev_count = true;
+    c->nf_valid = false;
     return lo_filtered_points(c, out, out_cap);
 }
 

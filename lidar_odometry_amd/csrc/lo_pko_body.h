@@ -838,7 +838,7 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
     exact_sums_wg(P, T, scale, cand_delta(P, c), dyn, s_tot);
 #ifdef LO_PKO_STAMPS
-    if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memtime() - c_t0);   // the slowest sums
+    if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memrealtime());   // the last candidate's sums end
 #endif
     if (tid == 0) {
         float tot[kExactTerms], pn[12], delta[6];
@@ -858,9 +858,10 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     __syncthreads();
     if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
 #ifdef LO_PKO_STAMPS
-    if (tid == 0 && c == 0) {                // diagnostic: candidate 0's cycles (dbg[7]); dbg[15]: the slowest sums
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        P.st->dbg[7] = __builtin_amdgcn_s_memtime() - c_t0;
+    if (tid == 0) {                          // diagnostic: candidate 0's cycles (dbg[7]); dbg[15] / [23]: the last
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // candidate's sums end / record end (s_memrealtime)
+        if (c == 0) P.st->dbg[7] = __builtin_amdgcn_s_memtime() - c_t0;
+        atomicMax(&P.st->dbg[23], __builtin_amdgcn_s_memrealtime());
     }
 #endif
 }
@@ -1243,6 +1244,9 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
         __syncthreads();
     }
     LO_STAMP(dbg, 6);
+#ifdef LO_PKO_STAMPS
+    if (dbg && tid == 0) dbg[22] = __builtin_amdgcn_s_memrealtime();   // the lead's JS end (100 MHz, chip-wide clock)
+#endif
 }
 
 // wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
@@ -1262,6 +1266,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
 #ifdef LO_PKO_STAMPS
     if (wg == 0) dbg = st->dbg;
     const unsigned long long t_launch = __builtin_amdgcn_s_memtime();   // dbg[0], stored by working launches only
+    const unsigned long long rt_launch = __builtin_amdgcn_s_memrealtime();   // dbg[21] (chip-wide clock)
 #endif
     // dynamic, nb ints: exclusive prefix of block counts (16-B aligned: the exact candidates read it with ds_read_b128,
     // and a misaligned 16-B LDS read is split -- the static part ends at a multiple of 8 only)
@@ -1302,7 +1307,7 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
     if (lead && tid == 0) st->n_corr = nc;
     if (!P.use_pko || nc == 0) return;                          // consumers use robust_loss_delta / 1.0
 #ifdef LO_PKO_STAMPS
-    if (dbg && tid == 0) dbg[0] = t_launch;
+    if (dbg && tid == 0) { dbg[0] = t_launch; dbg[21] = rt_launch; }
 #endif
     LO_STAMP(dbg, 1);
     pko_fit_js<NW, ONE_WAVE>(P, B, wg, G, nc, s_scale, pf, s_pre, s_wmask, L, dbg);

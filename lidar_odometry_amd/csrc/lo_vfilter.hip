@@ -32,6 +32,7 @@ constexpr int kVfHeadsBlock = 1024;
 constexpr int kVfSmall = 16;
 constexpr int kVfMid = 64;
 constexpr int kVfWideGrid = 64;
+constexpr int kVfBigSort = 1024;         // k_vf_wide: voxels up to this many members sort their bucket in LDS
 
 // computeMortonKey's per-axis cell.  The reference converts floor(x * inv) to int64 with static_cast; on
 // x86-64 (cvttss2si) every out-of-range value (|f| >= 2^63, inf) becomes INT64_MIN, which the clamp maps to 0.
@@ -163,6 +164,64 @@ __global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads(int m, const int32_t
     }
 }
 
+// Scans of at most kVfOneWg samples (a KITTI scan at stride 8: 14k): k_vf_heads + k_vf_place in ONE workgroup -- each
+// thread owns kVfPer consecutive samples, a thread-serial prefix and one block scan give every head its output slot and
+// bucket start (the same exclusive scan in index order as the multi-block pass, so the same slots), then the members are
+// appended to their buckets.  No inter-workgroup hand-off (the multi-block pass's agent-scope fences and last-block
+// scan cost ~14 us) and one launch fewer; loc holds global offsets and blk is zeroed, so k_vf_small / k_vf_wide read
+// them unchanged.
+constexpr int kVfPer = 16;
+constexpr int kVfOneWg = kVfHeadsBlock * kVfPer;
+__global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads_place(int m, const int32_t* __restrict__ sslot, VfSlot* tslot,
+                                                                  int2* __restrict__ loc, int2* __restrict__ blk, int nblk,
+                                                                  int32_t* __restrict__ bucket, VfCounters* ctr) {
+    __shared__ int2 s_w[kVfHeadsBlock / 64 + 1];
+    const int tid = threadIdx.x, j0 = tid * kVfPer;
+    uint32_t fq[kVfPer], cq[kVfPer];
+    {
+        int bq[kVfPer];
+#pragma unroll
+        for (int q = 0; q < kVfPer; ++q) bq[q] = j0 + q < m ? sslot[j0 + q] : -1;
+#pragma unroll
+        for (int q = 0; q < kVfPer; ++q) {
+            const int bb = bq[q] >= 0 ? bq[q] : 0;       // every load issued (clamped), the result masked
+            fq[q] = tslot[bb].first;
+            cq[q] = tslot[bb].cnt;
+            if (bq[q] < 0) { fq[q] = 0xFFFFFFFFu; cq[q] = 0u; }
+        }
+    }
+    int2 v = make_int2(0, 0);
+#pragma unroll
+    for (int q = 0; q < kVfPer; ++q)
+        if (fq[q] == static_cast<uint32_t>(j0 + q)) { v.x += 1; v.y += static_cast<int>(cq[q]); }
+    int2 tot;
+    int2 run = block_excl_scan2<kVfHeadsBlock>(v, tot, s_w);
+#pragma unroll
+    for (int q = 0; q < kVfPer; ++q) {
+        if (fq[q] == static_cast<uint32_t>(j0 + q)) {
+            loc[j0 + q] = run;
+            run.x += 1;
+            run.y += static_cast<int>(cq[q]);
+        }
+    }
+    for (int b = tid; b < nblk; b += kVfHeadsBlock) blk[b] = make_int2(0, 0);
+    if (tid == 0) {
+        ctr->n_out = tot.x;
+        ctr->arrive = 0u;
+        ctr->n_mid = 0;
+        ctr->n_big = 0;
+    }
+    __syncthreads();                                    // every head's loc is written (one workgroup: one L1)
+#pragma unroll
+    for (int q = 0; q < kVfPer; ++q) {
+        if (fq[q] == 0xFFFFFFFFu) continue;             // a non-finite point (or past the scan)
+        const int bb = sslot[j0 + q];
+        const int start = loc[fq[q]].y;
+        const unsigned r = atomicAdd(&tslot[bb].fill, 1u);
+        bucket[start + static_cast<int>(r)] = j0 + q;
+    }
+}
+
 __device__ __forceinline__ int2 vf_head_offsets(const int2* loc, const int2* blk, int h) {
     const int2 o = blk[h / kVfHeadsBlock], l = loc[h];
     return make_int2(o.x + l.x, o.y + l.y);            // (output slot, bucket start)
@@ -266,11 +325,11 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ samp,
             }
         float px = 0.0f, py = 0.0f, pz = 0.0f;
         if (lane < c) { const float* p = samp + 3 * v; px = p[0]; py = p[1]; pz = p[2]; }
-        float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // in index order = lane order
+        float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // in index order = lane order (c is wave-uniform: readlane)
         for (int t = 0; t < c; ++t) {
-            sx += __shfl(px, t, 64);
-            sy += __shfl(py, t, 64);
-            sz += __shfl(pz, t, 64);
+            sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), t));
+            sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), t));
+            sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz), t));
         }
         if (lane == 0) {
             const float inv = 1.0f / static_cast<float>(c);
@@ -280,15 +339,59 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ samp,
             vf_reset(tkey, tslot, b);
         }
     }
-    // ---- more than 64 members: one workgroup per voxel, ordered compaction of [first, last] ----
+    // ---- 65..kVfBigSort members: one workgroup per voxel sorts the voxel's bucket (its member indices) in LDS and
+    // wave 0 adds the members in index order; more: ordered compaction of the index range [first, last] ----
     __shared__ float s_p[256][3];
     __shared__ int s_wc[4];
+    __shared__ int s_srt[kVfBigSort];
     const int n_big = ctr->n_big;
     for (int q = blockIdx.x; q < n_big; q += gridDim.x) {
         const int j = big[q];
         const int b = sslot[j];
         const VfSlot s = tslot[b];
         const int2 o = vf_head_offsets(loc, blk, j);
+        const int c = static_cast<int>(s.cnt);
+        if (c <= kVfBigSort) {
+            // a voxel of a nearby surface is hit by several rings: its members span thousands of samples, so the range
+            // walk took ~18 dependent passes; the bucket holds exactly the members
+            for (int t = tid; t < kVfBigSort; t += 256) s_srt[t] = t < c ? bucket[o.y + t] : INT_MAX;
+            __syncthreads();
+            for (int k = 2; k <= kVfBigSort; k <<= 1) {                     // bitonic sort, ascending
+                for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                    for (int t = tid; t < kVfBigSort; t += 256) {
+                        const int l = t ^ jj;
+                        if (l > t) {
+                            const int a0 = s_srt[t], a1 = s_srt[l];
+                            const bool up = (t & k) == 0;
+                            if ((a0 > a1) == up) { s_srt[t] = a1; s_srt[l] = a0; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            if (wid == 0) {                             // wave 0: 64 members' points at a time, added in order
+                float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+                for (int t0 = 0; t0 < c; t0 += 64) {
+                    float px = 0.0f, py = 0.0f, pz = 0.0f;
+                    if (t0 + lane < c) { const float* p = samp + 3 * s_srt[t0 + lane]; px = p[0]; py = p[1]; pz = p[2]; }
+                    const int e = min(64, c - t0);
+                    for (int t = 0; t < e; ++t) {
+                        sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), t));
+                        sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), t));
+                        sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz), t));
+                    }
+                }
+                if (lane == 0) {
+                    const float inv = 1.0f / static_cast<float>(c);
+                    out[3 * o.x] = sx * inv;
+                    out[3 * o.x + 1] = sy * inv;
+                    out[3 * o.x + 2] = sz * inv;
+                    vf_reset(tkey, tslot, b);
+                }
+            }
+            __syncthreads();                            // s_srt is reused by this workgroup's next voxel
+            continue;
+        }
         float sx = 0.0f, sy = 0.0f, sz = 0.0f;         // thread 0's running sums
         for (int base = static_cast<int>(s.first); base <= static_cast<int>(s.last); base += 256) {
             const int jj = base + tid;
@@ -381,8 +484,13 @@ hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride
     const dim3 gh(static_cast<unsigned>((m + kVfHeadsBlock - 1) / kVfHeadsBlock)), th(kVfHeadsBlock);
     hipLaunchKernelGGL(k_vf_insert, g256, t256, 0, s, d_raw, stride, inv, mi, b.tkey, b.tslot,
                        static_cast<uint64_t>(b.tcap - 1), l2, b.sslot, b.samp);
-    hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.ctr);
-    hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.bucket);
+    if (mi <= kVfOneWg) {
+        hipLaunchKernelGGL(k_vf_heads_place, dim3(1), th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk,
+                           static_cast<int>((b.cap + kVfHeadsBlock - 1) / kVfHeadsBlock), b.bucket, b.ctr);
+    } else {
+        hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.ctr);
+        hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.bucket);
+    }
     hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, b.samp, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk,
                        b.bucket, b.mid, b.big, b.ctr, d_out);
     hipLaunchKernelGGL(k_vf_wide, dim3(kVfWideGrid), t256, 0, s, b.samp, b.sslot, b.tkey, b.tslot, b.loc,
