@@ -142,6 +142,39 @@ public:
         check(lo_map_sync_surfels(m_ctx, keys.data(), nrm.data(), ctr.data(), keys.size() / 3, &patched),
               "lo_map_sync_surfels");
         m_last_sync_patched = patched;
+        m_synced_once = true;
+    }
+    // The keyed sync: only the L1 voxels UpdateVoxelMap changed reach the device.  `changed` is what
+    // the two-line hook in VoxelMap::UpdateVoxelMap collects (INTEGRATION.md "Incremental map sync"): the parents of
+    // the pruned L0 voxels (:146-169) and every key of the touched loop (:187-261).  Each key's surfel is read with
+    // GetSurfelAtPoint at the voxel's centre (PointToVoxelKey(centre, 1) is the key itself, :50-58) and patched in
+    // place (lo_map_patch_surfels: upsert, or erase when the voxel has none) -- O(changed voxels) on the host, no walk
+    // over the whole surfel set and no key search.  The first sync, a table too full for the patch, or the KDTree
+    // configuration fall back to the full sync_map(vm).
+    void sync_map(const map::VoxelMap& vm, const std::vector<map::VoxelKey>& changed) {
+        if (!m_config.use_surfel_correspondence || !m_synced_once) { sync_map(vm); return; }
+        const float l1 = vm.GetVoxelSize() * static_cast<float>(vm.GetHierarchyFactor());
+        std::vector<int32_t> keys;
+        std::vector<float> nrm, ctr;
+        std::vector<uint8_t> present;
+        keys.reserve(3 * changed.size());
+        nrm.reserve(3 * changed.size());
+        ctr.reserve(3 * changed.size());
+        present.reserve(changed.size());
+        for (const map::VoxelKey& k : changed) {
+            const Eigen::Vector3f centre((static_cast<float>(k.x) + 0.5f) * l1, (static_cast<float>(k.y) + 0.5f) * l1,
+                                         (static_cast<float>(k.z) + 0.5f) * l1);
+            Eigen::Vector3f n = Eigen::Vector3f::Zero(), c = Eigen::Vector3f::Zero();
+            const bool has = vm.GetSurfelAtPoint(centre, n, c);
+            keys.insert(keys.end(), {k.x, k.y, k.z});
+            nrm.insert(nrm.end(), {n.x(), n.y(), n.z()});
+            ctr.insert(ctr.end(), {c.x(), c.y(), c.z()});
+            present.push_back(has ? 1 : 0);
+        }
+        const int rc = lo_map_patch_surfels(m_ctx, keys.data(), nrm.data(), ctr.data(), present.data(), present.size());
+        if (rc == LO_ERR_CAPACITY) { sync_map(vm); return; }   // tombstones: a full upload rebuilds the table
+        check(rc, "lo_map_patch_surfels");
+        m_last_sync_patched = static_cast<int>(present.size());
     }
     int last_sync_patched() const { return m_last_sync_patched; }   // records sent by the last sync_map (-1: full)
 
@@ -259,6 +292,7 @@ private:
     int m_max_points;
     OptimizationStats m_last_stats;
     int m_last_sync_patched = 0;
+    bool m_synced_once = false;                         // a whole-map sync_map ran (the keyed one patches on top)
     lo_ctx* m_ctx = nullptr;
 };
 

@@ -47,6 +47,21 @@ size_t       lo_voxelmap_surfel_count(const lo_voxelmap* m);
 /* L1 voxels with has_surfel, in L1 iteration order. Returns the number written. */
 size_t       lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys_xyz, float* normals, float* centroids,
                                      float* planarity, size_t cap);
+/* The L1 keys whose surfel the last lo_voxelmap_update may have changed -- created, refitted, lost its planarity or
+ * its children, erased by the radius prune or the planarity test (VoxelMap.cpp:146-169, :187-261) -- in the order the
+ * update met them (a key may repeat; an update that changed nothing gives none).  What the reference's UpdateVoxelMap
+ * collects with the two-line hook INTEGRATION.md shows, for the adapter's keyed sync_map (only these voxels patched:
+ * GetSurfelAtPoint at each key's centre, lo_map_patch_surfels).  After lo_voxelmap_apply_transform every key moved:
+ * none are listed, upload the whole map.  Returns the count; writes up to cap keys. */
+size_t       lo_voxelmap_changed_l1(const lo_voxelmap* m, int32_t* keys_xyz, size_t cap);
+/* GetSurfelAtPoint (VoxelMap.cpp:368-386): 1 and the normal / centroid of the surfel of p's L1 voxel
+ * (PointToVoxelKey(p, 1)) if it has one, else 0. */
+int          lo_voxelmap_surfel_at(const lo_voxelmap* m, const float p[3], float normal[3], float centroid[3]);
+/* The keyed sync's lookup loop in one call: for each of n L1 keys, GetSurfelAtPoint at the key's voxel centre
+ * ((k + 0.5) * voxel * factor per axis, fp32) -- present[i] = 1 and its normal / centroid, or 0 and zeros.  The
+ * arrays go straight to lo_map_patch_surfels.  Returns the number present. */
+size_t       lo_voxelmap_surfels_at_keys(const lo_voxelmap* m, const int32_t* keys_xyz, size_t n, float* normals,
+                                         float* centroids, uint8_t* present);
 /* GetPointCloud: L0 centroids in L0 iteration order. */
 size_t       lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap);
 /* Upload the map's surfels to an ICP context (lo_map_set_surfels). */

@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "lo_batch_result", "lo_batch_optimize", "lo_batch_bench_correspond",
     # include/lo_map.h
     "lo_voxelmap_create", "lo_voxelmap_destroy", "lo_voxelmap_update", "lo_voxelmap_l0_count",
-    "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0",
+    "lo_voxelmap_l1_count", "lo_voxelmap_surfel_count", "lo_voxelmap_get_surfels", "lo_voxelmap_get_l0", "lo_voxelmap_changed_l1", "lo_voxelmap_surfel_at", "lo_voxelmap_surfels_at_keys",
     "lo_map_set_from_voxelmap", "lo_map_sync_voxelmap", "lo_voxelmap_apply_transform", "lo_map_patch_surfels", "lo_voxel_filter",
     "lo_voxelmap_set_device_fit", "lo_devmap_create", "lo_devmap_destroy", "lo_devmap_last_error", "lo_devmap_update",
     "lo_devmap_update_from_scan", "lo_devmap_apply_transform", "lo_devmap_counts", "lo_devmap_status", "lo_devmap_status_async", "lo_devmap_status_poll", "lo_devmap_sync_points", "lo_kd_reruns", "lo_devmap_get_l0", "lo_devmap_get_l1",
@@ -251,6 +251,12 @@ def lib():
         getattr(L, f).argtypes = [vp]
     L.lo_voxelmap_get_surfels.restype = C.c_size_t
     L.lo_voxelmap_get_surfels.argtypes = [vp, ip, fp, fp, fp, C.c_size_t]
+    L.lo_voxelmap_changed_l1.restype = C.c_size_t
+    L.lo_voxelmap_changed_l1.argtypes = [vp, ip, C.c_size_t]
+    L.lo_voxelmap_surfel_at.restype = C.c_int
+    L.lo_voxelmap_surfel_at.argtypes = [vp, fp, fp, fp]
+    L.lo_voxelmap_surfels_at_keys.restype = C.c_size_t
+    L.lo_voxelmap_surfels_at_keys.argtypes = [vp, ip, C.c_size_t, fp, fp, vp]
     L.lo_voxelmap_get_l0.restype = C.c_size_t
     L.lo_voxelmap_get_l0.argtypes = [vp, fp, C.c_size_t]
     L.lo_map_set_from_voxelmap.argtypes = [vp, vp]

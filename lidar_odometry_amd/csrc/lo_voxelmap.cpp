@@ -210,6 +210,7 @@ struct HostVoxelMap {
     // changes when the journal restarts, which forces a full upload.
     std::vector<Key3> journal;
     uint64_t epoch = 1;
+    size_t changed_from = 0;                       // journal[changed_from:]: the keys the last update noted
     void note(const Key3& k) { journal.push_back(k); }
 
     // PointToVoxelKey for a whole cloud: floor(p / scale) per coordinate, one flat loop over the 3n floats
@@ -353,6 +354,7 @@ struct HostVoxelMap {
         }
         journal.clear();
         ++epoch;
+        changed_from = 0;                            // every key moved: a keyed sync cannot follow, upload it all
         if (!compute_surfels) return;
         std::vector<float> cs;
         for (size_t t = 0; t < l1.size(); ++t) {
@@ -373,7 +375,9 @@ struct HostVoxelMap {
 
     void update(const float* xyz, size_t n, const double sensor[3], double max_distance, bool keyframe) {
         resolve();
+        changed_from = journal.size();               // nothing changed unless this update changes it
         if (!xyz || n == 0 || !keyframe) return;
+        if (journal.size() > (size_t(1) << 22)) { journal.clear(); ++epoch; changed_from = 0; }
         const float sp[3] = {static_cast<float>(sensor[0]), static_cast<float>(sensor[1]), static_cast<float>(sensor[2])};
         const float rsq = static_cast<float>(max_distance * max_distance);
         std::vector<Key3> doomed;
@@ -387,7 +391,6 @@ struct HostVoxelMap {
         std::vector<Key3> empty1;
         for (size_t i = 0; i < l1.size(); ++i) if (l1.val_at(i).children.empty()) empty1.push_back(l1.key_at(i));
         for (const Key3& k : empty1) { note(k); l1.erase(k); }
-        if (journal.size() > (size_t(1) << 22)) { journal.clear(); ++epoch; }
 
         keys_of(xyz, n, voxel, k0);
         keys_of(xyz, n, voxel * static_cast<float>(factor), k1);
@@ -535,6 +538,64 @@ size_t lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys, float* norma
         ++c;
     }
     return c;
+}
+
+size_t lo_voxelmap_changed_l1(const lo_voxelmap* m, int32_t* keys, size_t cap) {
+    if (!m) return 0;
+    LO_MAP_LOCK(m);
+    const HostVoxelMap& h = resolved(m);
+    const size_t from = std::min(h.changed_from, h.journal.size());
+    const size_t cnt = h.journal.size() - from;
+    if (keys)
+        for (size_t i = 0; i < cnt && i < cap; ++i) {
+            const lo::Key3& k = h.journal[from + i];
+            keys[3 * i] = k.x; keys[3 * i + 1] = k.y; keys[3 * i + 2] = k.z;
+        }
+    return cnt;
+}
+
+// GetSurfelAtPoint (VoxelMap.cpp:368-386): PointToVoxelKey(p, 1) (:50-58: fp32 scale voxel * factor, floor of the
+// division), then the L1 voxel's surfel if it has one
+int lo_voxelmap_surfel_at(const lo_voxelmap* m, const float p[3], float normal[3], float centroid[3]) {
+    if (!m || !p) return 0;
+    LO_MAP_LOCK(m);
+    const HostVoxelMap& h = resolved(m);
+    const float scale = h.voxel * static_cast<float>(h.factor);
+    const lo::Key3 k{static_cast<int>(std::floor(p[0] / scale)), static_cast<int>(std::floor(p[1] / scale)),
+                 static_cast<int>(std::floor(p[2] / scale))};
+    const int64_t i = h.l1.find(k);
+    if (i < 0 || !h.l1.val_at(i).has_surfel) return 0;
+    const lo::L1& node = h.l1.val_at(i);
+    for (int a = 0; a < 3; ++a) {
+        if (normal) normal[a] = node.normal[a];
+        if (centroid) centroid[a] = node.centroid[a];
+    }
+    return 1;
+}
+
+size_t lo_voxelmap_surfels_at_keys(const lo_voxelmap* m, const int32_t* keys, size_t n, float* normals, float* centroids,
+                                   uint8_t* present) {
+    if (!m || (n > 0 && (!keys || !normals || !centroids || !present))) return 0;
+    LO_MAP_LOCK(m);
+    const HostVoxelMap& h = resolved(m);
+    const float l1 = h.voxel * static_cast<float>(h.factor);
+    size_t found = 0;
+    for (size_t i = 0; i < n; ++i) {
+        // GetSurfelAtPoint at the key's voxel centre: PointToVoxelKey(centre, 1) is the key itself
+        const float c[3] = {(static_cast<float>(keys[3 * i]) + 0.5f) * l1, (static_cast<float>(keys[3 * i + 1]) + 0.5f) * l1,
+                            (static_cast<float>(keys[3 * i + 2]) + 0.5f) * l1};
+        const lo::Key3 k{static_cast<int>(std::floor(c[0] / l1)), static_cast<int>(std::floor(c[1] / l1)),
+                         static_cast<int>(std::floor(c[2] / l1))};
+        const int64_t j = h.l1.find(k);
+        const bool has = j >= 0 && h.l1.val_at(j).has_surfel;
+        present[i] = has ? 1 : 0;
+        for (int a = 0; a < 3; ++a) {
+            normals[3 * i + a] = has ? h.l1.val_at(j).normal[a] : 0.0f;
+            centroids[3 * i + a] = has ? h.l1.val_at(j).centroid[a] : 0.0f;
+        }
+        found += has ? 1 : 0;
+    }
+    return found;
 }
 
 size_t lo_voxelmap_get_l0(const lo_voxelmap* m, float* xyz, size_t cap) {

@@ -197,6 +197,25 @@ class IterativeClosestPointOptimizer:
                                               len(k), C.byref(patched)))
         return int(patched.value)
 
+    def sync_changed(self, voxel_map, changed_keys) -> int:
+        """The keyed sync after UpdateVoxelMap (the adapter's sync_map(vm, changed)): only the L1 voxels the update
+        changed (``VoxelMap.changed_l1()``; in the reference, the keys the INTEGRATION.md hook collects) are looked up
+        with GetSurfelAtPoint at the key's voxel centre and patched in place (lo_map_patch_surfels): a surfel is
+        upserted, a voxel without one erased.  The map must have been uploaded whole before (set_surfels /
+        sync_surfels).  Returns the records sent."""
+        keys = np.ascontiguousarray(changed_keys, np.int32).reshape(-1, 3)
+        if len(keys) == 0:
+            return 0
+        n = np.zeros((len(keys), 3), np.float32)
+        c = np.zeros((len(keys), 3), np.float32)
+        pres = np.zeros(len(keys), np.uint8)
+        # the adapter's per-key GetSurfelAtPoint loop, in one call on this library's host map
+        lib().lo_voxelmap_surfels_at_keys(voxel_map.handle, keys.ctypes.data_as(C.POINTER(C.c_int32)), len(keys),
+                                          _fptr(n), _fptr(c), pres.ctypes.data)
+        self._check(lib().lo_map_patch_surfels(self._ctx, keys.ctypes.data, n.ctypes.data, c.ctypes.data,
+                                               pres.ctypes.data, len(keys)))
+        return len(keys)
+
     def update_config(self, config: ICPConfig, adaptive: AdaptiveMEstimatorConfig | None = None):
         """IterativeClosestPointOptimizer::update_config (IterativeClosestPointOptimizer.h:220): new parameters, same
         context -- the device map stays (lo_update_config).  adaptive: new PKO parameters too (the estimator's config)."""

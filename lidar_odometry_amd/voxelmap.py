@@ -91,6 +91,20 @@ class VoxelMap:
         got = lib().lo_voxelmap_get_surfels(self._h, k.ctypes.data_as(C.POINTER(C.c_int32)), _f(n), _f(c), _f(pl), m)
         return k[:got], n[:got], c[:got], pl[:got]
 
+    def changed_l1(self) -> np.ndarray:
+        """The L1 keys whose surfel the last update may have changed (lo_voxelmap_changed_l1), int32 [k, 3]."""
+        k = int(lib().lo_voxelmap_changed_l1(self._h, None, 0))
+        out = np.zeros((max(k, 1), 3), np.int32)
+        got = lib().lo_voxelmap_changed_l1(self._h, out.ctypes.data_as(C.POINTER(C.c_int32)), k)
+        return out[:min(got, k)]
+
+    def surfel_at(self, p):
+        """GetSurfelAtPoint (VoxelMap.cpp:368-386): (normal, centroid) of p's L1 voxel surfel, or None."""
+        q = np.ascontiguousarray(p, np.float32).reshape(3)
+        n = np.zeros(3, np.float32)
+        c = np.zeros(3, np.float32)
+        return (n, c) if lib().lo_voxelmap_surfel_at(self._h, _f(q), _f(n), _f(c)) else None
+
     def l0_cloud(self) -> np.ndarray:
         """VoxelMap::GetPointCloud (VoxelMap.cpp:388-403)."""
         m = self.l0_count()

@@ -10,3 +10,7 @@ timeout -k 10 600 python bench.py --config kitti_raw --no-cpu-baseline --pmc off
 rc=$?; echo "bench raw rc $rc"; fatal $rc raw
 timeout -k 10 600 python bench.py --config kitti_e2e --no-cpu-baseline --pmc off > gpurun_out/r06_bench_kitti_e2e_c.json 2> gpurun_out/r06_bench_kitti_e2e_c.log
 rc=$?; echo "bench e2e rc $rc"; fatal $rc e2e
+timeout -k 10 600 python -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_map_patch.py > gpurun_out/r06_t4b.log 2>&1
+rc=$?; echo "map tests rc $rc"; fatal $rc maptests
+timeout -k 10 600 python scripts/map_sync_timing.py 300 > gpurun_out/r06_map_sync_timing.txt 2>&1
+rc=$?; echo "map timing rc $rc"; fatal $rc maptiming

@@ -5,7 +5,9 @@ pruning radius 120 m; times per keyframe over the second half (the map at its st
 same map with device surfel fits (lo_voxelmap_set_device_fit: update without fits + patch + k_surfel_fit, the
 results applied at the next update).  Fourth: the reference-side sync (the adapter's sync_map ->
 lo_map_sync_surfels): the map's whole surfel set handed over each keyframe, diffed against the context's resident
-set, only the difference patched."""
+set, only the difference patched.  Fifth (r06): the adapter's keyed sync_map(vm, changed) -- only the L1 keys the
+update changed (the INTEGRATION.md hook's list, here lo_voxelmap_changed_l1), GetSurfelAtPoint at each key's centre,
+lo_map_patch_surfels; its host part is the Python mirror sync_changed (the C++ adapter does the same loop)."""
 import ctypes as C
 import os
 import sys
@@ -29,7 +31,9 @@ vd.set_device_fit(True)
 A, B = IterativeClosestPointOptimizer(max_points=1 << 16), IterativeClosestPointOptimizer(max_points=1 << 16)
 D = IterativeClosestPointOptimizer(max_points=1 << 16)
 E = IterativeClosestPointOptimizer(max_points=1 << 16)
+F = IterativeClosestPointOptimizer(max_points=1 << 16)
 t_upd, t_full, t_patch, kinds, t_dev, t_ref, sent = [], [], [], [], [], [], []
+t_key, sent_key = [], []
 patched = C.c_int(0)
 for k in range(0, n + 1, 2):
     T = seq.poses[k]
@@ -52,6 +56,16 @@ for k in range(0, n + 1, 2):
     sent.append(E.sync_surfels(keys, normals, cents))
     lib().lo_sync(E.ctx)
     t7 = time.perf_counter()
+    # the adapter's keyed sync_map(vm, changed): only the keys the update changed (the reference hook's list),
+    # GetSurfelAtPoint at each key's centre, lo_map_patch_surfels (C++ in the adapter; the Python mirror here)
+    t8 = time.perf_counter()
+    if k == 0:
+        F.set_surfels(keys, normals, cents)
+    else:
+        sent_key.append(F.sync_changed(vm, vm.changed_l1()))
+    lib().lo_sync(F.ctx)
+    t9 = time.perf_counter()
+    t_key.append(t9 - t8)
     t_upd.append(t1 - t0); t_full.append(t2 - t1); t_patch.append(t3 - t2); kinds.append(patched.value)
     t_dev.append(t5 - t4)
     t_ref.append(t7 - t6)
@@ -63,5 +77,7 @@ print(f"keyframes {len(t_upd)}, surfels {vm.surfel_count()}, L0 {vm.l0_count()}:
       f"full re-uploads in the second half {sum(p < 0 for p in kinds[h:])}; with device fits: update + sync "
       f"{ms(t_dev):.3f} ms (host fits: {ms(t_upd) + ms(t_patch):.3f} ms); reference-side sync_surfels of the full "
       f"surfel set {ms(t_ref):.3f} ms, {np.mean([x for x in sent[h:] if x >= 0]):.0f} records sent per keyframe "
-      f"(full uploads in the second half: {sum(x < 0 for x in sent[h:])})")
+      f"(full uploads in the second half: {sum(x < 0 for x in sent[h:])}); keyed sync of the changed keys "
+      f"{ms(t_key):.3f} ms, {np.mean(sent_key[h:]):.0f} keys per keyframe")
+assert F.surfel_count() == vm.surfel_count()
 assert vd.surfel_count() == vm.surfel_count()

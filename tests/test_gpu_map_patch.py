@@ -299,3 +299,34 @@ def test_update_config_keeps_the_device_map():
     finally:
         A.close()
         B.close()
+
+
+def test_keyed_sync_of_changed_voxels_matches_full_upload():
+    """The adapter's keyed sync_map(vm, changed), mirrored by sync_changed: after one whole upload,
+    each keyframe patches only the L1 keys the update changed (lo_voxelmap_changed_l1 = the reference hook's list),
+    each looked up with GetSurfelAtPoint at its voxel centre -- the device table answers every lookup as a full
+    upload does, across inserts, refits, planarity losses and the 60 m prune."""
+    from lidar_odometry_amd.voxelmap import VoxelMap, voxel_filter
+    seq = synth.KittiLikeSequence(seed=7, n_frames=62)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    A, B = _ctx(), _ctx()
+    try:
+        sent = []
+        for k in range(0, 61, 2):
+            T = seq.poses[k]
+            pts = voxel_filter(seq.scan(k), 0.5, 8)
+            vm.update(synth.transform(T, pts), T[:3, 3], 60.0, True)
+            if k == 0:
+                s = vm.surfels()
+                A.set_surfels(s[0], s[1], s[2])
+            else:
+                sent.append(A.sync_changed(vm, vm.changed_l1()))
+            _full(B, vm)
+            assert A.surfel_count() == B.surfel_count() == vm.surfel_count()
+            if k % 10 == 0:
+                f = k + 1
+                _same_lookups(A, B, voxel_filter(seq.scan(f), 0.5, 8), [seq.poses[f]])
+        assert 0 < np.mean(sent) < vm.surfel_count()
+    finally:
+        A.close()
+        B.close()

@@ -155,3 +155,44 @@ def test_deferred_fit_resolved_on_host_is_bitwise():
         if k % 4 == 0:
             _compare_maps(a, b)
     _compare_maps(a, b)
+
+
+def test_changed_l1_covers_every_surfel_change():
+    """lo_voxelmap_changed_l1 (the keys the reference's UpdateVoxelMap hook would collect): every L1 key
+    whose surfel appeared, changed or disappeared in an update is listed, and GetSurfelAtPoint at each listed key's voxel
+    centre gives the key's surfel after the update -- so the keyed sync (patch only these keys) rebuilds the full set.
+    Radius prune (60 m) and planarity erases included."""
+    seq = synth.KittiLikeSequence(seed=3, n_frames=24, ramp_s=2.0)
+    vm = VoxelMap(0.5, 3, 0.1, True)
+    l1 = np.float32(0.5) * np.float32(3)
+    mirror = {}
+    total = 0
+    for k in range(0, 24, 2):
+        T = seq.poses[k]
+        w = synth.transform(T, voxel_filter(seq.scan(k), 0.5, 8))
+        ka, na, ca, _ = vm.surfels()
+        before = {tuple(x): (tuple(n.view(np.uint32)), tuple(c.view(np.uint32))) for x, n, c in zip(ka, na, ca)}
+        vm.update(w, T[:3, 3], 60.0, True)
+        kb, nb, cb, _ = vm.surfels()
+        after = {tuple(x): (tuple(n.view(np.uint32)), tuple(c.view(np.uint32))) for x, n, c in zip(kb, nb, cb)}
+        diff = {key for key in set(before) | set(after) if before.get(key) != after.get(key)}
+        changed = {tuple(x) for x in vm.changed_l1()}
+        assert diff <= changed, (k, len(diff - changed))
+        total += len(diff)
+        # the keyed sync's lookups: the centre of each changed key finds exactly that key's surfel (or none)
+        for key in changed:
+            cen = ((np.asarray(key, np.float32) + np.float32(0.5)) * l1).astype(np.float32)
+            r = vm.surfel_at(cen)
+            if key in after:
+                assert r is not None
+                assert (tuple(r[0].view(np.uint32)), tuple(r[1].view(np.uint32))) == after[key]
+                mirror[key] = after[key]
+            else:
+                assert r is None
+                mirror.pop(key, None)
+        if k == 0:
+            mirror = dict(after)
+        assert mirror == after, k                          # patching only the changed keys rebuilds the set
+    assert total > 100
+    vm.update(np.zeros((0, 3), np.float32), np.zeros(3), 60.0, True)
+    assert len(vm.changed_l1()) == 0                       # an update that changes nothing lists nothing
