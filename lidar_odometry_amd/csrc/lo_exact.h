@@ -95,8 +95,9 @@ __device__ inline void ldlt6_solve_f32(const float (&Hin)[36], const float (&b)[
 __device__ inline float norm3e(const float* v) { return sqrtf(dot3e(v[0], v[1], v[2], v[0], v[1], v[2])); }
 
 // SO3::Exp (MathUtils.cpp:23-39, kEps 1e-6f) with the SO3(Matrix3f) re-projection of its result; sin / cos are
-// evaluated in fp64 and rounded (the correctly rounded fp32 value; glibc's sinf agrees with it for 99.6 % of the
-// floats in [1e-7, 0.8], cosf for 99.99 %)
+// glibc's sinf / cosf restated (lo_math.h sincosf_ref: bit-identical to the reference's std::sin / std::cos of a
+// float; r05 rounded the fp64 sin / cos instead, which differs from sinf in the last bit for 0.4 % of the floats in
+// [1e-7, 0.8], and its device sin / cos took ~4.5k cycles of the solve's ~21k)
 __device__ inline void so3_exp_exact(const float w[3], float R[3][3]) {
     const float theta = norm3e(w);
     float M[3][3];
@@ -107,8 +108,8 @@ __device__ inline void so3_exp_exact(const float w[3], float R[3][3]) {
         const float ti = 1.0f / theta;
         const float k[3] = {w[0] * ti, w[1] * ti, w[2] * ti};
         const float K[3][3] = {{0.0f, -k[2], k[1]}, {k[2], 0.0f, -k[0]}, {-k[1], k[0], 0.0f}};
-        const float s = static_cast<float>(sin(static_cast<double>(theta)));
-        const float omc = 1.0f - static_cast<float>(cos(static_cast<double>(theta)));
+        const float s = sincosf_ref(theta, 0);
+        const float omc = 1.0f - sincosf_ref(theta, 1);
         float sK[3][3], KK[3][3];
         for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) sK[r][c] = omc * K[r][c];
         mul33e(sK, K, KK);

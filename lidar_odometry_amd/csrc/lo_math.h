@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdint>
+#include <cstring>
 
 // The SVD / SO(3) restatements below also run on the device (lo_exact.hip): host-device under HIP.
 #if defined(__HIP__)
@@ -41,6 +43,55 @@ LO_HD inline double log_pos(double x) {
     const double r = dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
     const bool fin = x > 0.0 && x < INFINITY;
     return fin ? r : (x == 0.0 ? -INFINITY : (x > 0.0 ? x : NAN));
+}
+
+// ---------------------------------------------------------------------------------------------
+// sinf / cosf as glibc 2.35 computes them on x86-64 with FMA (the reference's std::sin(float) / std::cos(float) in
+// SO3::Exp, MathUtils.cpp:23-39): the optimized-routines algorithm (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c,
+// sincosf.h) -- |y| < pi/4 by the top 12 bits: the degree-7 odd / degree-8 even polynomials in double; |y| < 120:
+// reduce_fast by pi/2, the quadrant's sign and polynomial; the coefficients of __sincosf_table, the FMA build's
+// contractions (glibc selects its -mfma variant by ifunc on such CPUs), rounded once to float.  Bit-identical to
+// the host's sinf / cosf on every float in (1e-7, 120) (tests/test_sinf_restatement.py, exhaustive).  |y| >= 120,
+// inf and NaN (glibc's large-argument reduction) fall back to the fp64 sin / cos rounded to float.
+// ---------------------------------------------------------------------------------------------
+struct SinCosTab {
+    double c0, c1, s1, c2, s2, c3, s3, c4;
+};
+LO_HD inline uint32_t f32_top12(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return (u >> 20) & 0x7ffu;
+}
+LO_HD inline double sincosf_poly(double x, double x2, const SinCosTab& p, int n) {
+    if ((n & 1) == 0) {
+        const double x3 = x * x2, s1 = std::fma(x2, p.s3, p.s2), x7 = x3 * x2, s = std::fma(x3, p.s1, x);
+        return std::fma(x7, s1, s);
+    }
+    const double x4 = x2 * x2, c2 = std::fma(x2, p.c4, p.c3), c1 = std::fma(x2, p.c1, p.c0), x6 = x4 * x2;
+    const double c = std::fma(x4, p.c2, c1);
+    return std::fma(x6, c2, c);
+}
+// which = 0: sinf, 1: cosf
+LO_HD inline float sincosf_ref(float y, int which) {
+    constexpr SinCosTab t0{1.0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+                           0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16};
+    constexpr SinCosTab t1{-1.0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+                           0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16};
+    double x = y;
+    const uint32_t a = f32_top12(y);
+    if (a < f32_top12(0x1.921FB6p-1f)) {                          // |y| < pi/4
+        const double x2 = x * x;
+        if (a < f32_top12(0x1p-12f)) return which ? 1.0f : y;
+        return static_cast<float>(sincosf_poly(x, x2, t0, which));
+    }
+    if (a < f32_top12(120.0f)) {                                  // reduce_fast
+        const double r = x * 0x1.45F306DC9C883p+23;
+        const int n = (static_cast<int32_t>(r) + 0x800000) >> 24;
+        x = std::fma(-static_cast<double>(n), 0x1.921FB54442D18p0, x);
+        const double sg = ((n & 3) == 0 || (n & 3) == 3) ? 1.0 : -1.0;
+        return static_cast<float>(sincosf_poly(x * sg, x * x, (n & 2) ? t1 : t0, n ^ which));
+    }
+    return static_cast<float>(which ? std::cos(static_cast<double>(y)) : std::sin(static_cast<double>(y)));
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -212,14 +212,19 @@ __global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads_place(int m, const i
         ctr->n_big = 0;
     }
     __syncthreads();                                    // every head's loc is written (one workgroup: one L1)
+    // every sample's bucket start and fill ticket in flight together (16 independent round trips, not 16 in a row)
+    int st[kVfPer];
+    unsigned tk[kVfPer];
+#pragma unroll
+    for (int q = 0; q < kVfPer; ++q) st[q] = fq[q] != 0xFFFFFFFFu ? loc[fq[q]].y : 0;
 #pragma unroll
     for (int q = 0; q < kVfPer; ++q) {
-        if (fq[q] == 0xFFFFFFFFu) continue;             // a non-finite point (or past the scan)
-        const int bb = sslot[j0 + q];
-        const int start = loc[fq[q]].y;
-        const unsigned r = atomicAdd(&tslot[bb].fill, 1u);
-        bucket[start + static_cast<int>(r)] = j0 + q;
+        tk[q] = 0u;
+        if (fq[q] != 0xFFFFFFFFu) tk[q] = atomicAdd(&tslot[sslot[j0 + q]].fill, 1u);
     }
+#pragma unroll
+    for (int q = 0; q < kVfPer; ++q)
+        if (fq[q] != 0xFFFFFFFFu) bucket[st[q] + static_cast<int>(tk[q])] = j0 + q;   // non-finite points: no bucket
 }
 
 __device__ __forceinline__ int2 vf_head_offsets(const int2* loc, const int2* blk, int h) {
@@ -354,11 +359,13 @@ __global__ __launch_bounds__(256) void k_vf_wide(const float* __restrict__ samp,
         if (c <= kVfBigSort) {
             // a voxel of a nearby surface is hit by several rings: its members span thousands of samples, so the range
             // walk took ~18 dependent passes; the bucket holds exactly the members
-            for (int t = tid; t < kVfBigSort; t += 256) s_srt[t] = t < c ? bucket[o.y + t] : INT_MAX;
+            int np2 = 128;
+            while (np2 < c) np2 <<= 1;                  // the sort's width: the next power of two (block-uniform)
+            for (int t = tid; t < np2; t += 256) s_srt[t] = t < c ? bucket[o.y + t] : INT_MAX;
             __syncthreads();
-            for (int k = 2; k <= kVfBigSort; k <<= 1) {                     // bitonic sort, ascending
+            for (int k = 2; k <= np2; k <<= 1) {                            // bitonic sort, ascending
                 for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                    for (int t = tid; t < kVfBigSort; t += 256) {
+                    for (int t = tid; t < np2; t += 256) {
                         const int l = t ^ jj;
                         if (l > t) {
                             const int a0 = s_srt[t], a1 = s_srt[l];

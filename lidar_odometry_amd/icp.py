@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import LoBatchRec, LoConfig, LoIterLog, LoStats, lib
+from ._lib import LO_ERR_CAPACITY, LoBatchRec, LoConfig, LoIterLog, LoStats, lib
 
 
 @dataclass
@@ -212,8 +212,13 @@ class IterativeClosestPointOptimizer:
         # the adapter's per-key GetSurfelAtPoint loop, in one call on this library's host map
         lib().lo_voxelmap_surfels_at_keys(voxel_map.handle, keys.ctypes.data_as(C.POINTER(C.c_int32)), len(keys),
                                           _fptr(n), _fptr(c), pres.ctypes.data)
-        self._check(lib().lo_map_patch_surfels(self._ctx, keys.ctypes.data, n.ctypes.data, c.ctypes.data,
-                                               pres.ctypes.data, len(keys)))
+        rc = lib().lo_map_patch_surfels(self._ctx, keys.ctypes.data, n.ctypes.data, c.ctypes.data, pres.ctypes.data,
+                                        len(keys))
+        if rc == LO_ERR_CAPACITY:                 # tombstones: a whole upload rebuilds the table (as the adapter does)
+            s = voxel_map.surfels()
+            self.set_surfels(s[0], s[1], s[2])
+            return -1
+        self._check(rc)
         return len(keys)
 
     def update_config(self, config: ICPConfig, adaptive: AdaptiveMEstimatorConfig | None = None):

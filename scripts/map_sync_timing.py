@@ -78,6 +78,7 @@ print(f"keyframes {len(t_upd)}, surfels {vm.surfel_count()}, L0 {vm.l0_count()}:
       f"{ms(t_dev):.3f} ms (host fits: {ms(t_upd) + ms(t_patch):.3f} ms); reference-side sync_surfels of the full "
       f"surfel set {ms(t_ref):.3f} ms, {np.mean([x for x in sent[h:] if x >= 0]):.0f} records sent per keyframe "
       f"(full uploads in the second half: {sum(x < 0 for x in sent[h:])}); keyed sync of the changed keys "
-      f"{ms(t_key):.3f} ms, {np.mean(sent_key[h:]):.0f} keys per keyframe")
+      f"{ms(t_key):.3f} ms, {np.mean([x for x in sent_key[h:] if x >= 0]):.0f} keys per keyframe (full uploads "
+      f"in the second half: {sum(x < 0 for x in sent_key[h:])})")
 assert F.surfel_count() == vm.surfel_count()
 assert vd.surfel_count() == vm.surfel_count()

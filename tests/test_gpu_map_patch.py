@@ -326,7 +326,8 @@ def test_keyed_sync_of_changed_voxels_matches_full_upload():
             if k % 10 == 0:
                 f = k + 1
                 _same_lookups(A, B, voxel_filter(seq.scan(f), 0.5, 8), [seq.poses[f]])
-        assert 0 < np.mean(sent) < vm.surfel_count()
+        keyed = [x for x in sent if x >= 0]             # -1: a table full of tombstones was uploaded whole
+        assert len(keyed) > len(sent) // 2 and 0 < np.mean(keyed) < vm.surfel_count()
     finally:
         A.close()
         B.close()
