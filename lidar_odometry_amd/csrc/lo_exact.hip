@@ -411,32 +411,125 @@ __global__ __launch_bounds__(kScaleC) void k_exact_scale_c(KParams P) {
     __shared__ KeyStat s_ks[kScaleC / kWave];
     exact_scale_c_body<PT>(P, scan_n(P), s_dyn, S, s_ks);
 }
+// Device counts beyond 8192 (a fine filter over a large raw scan; never at the bench sizes): the same counting sort of
+// up to 16384 keys in LDS with the keys re-read from global memory in two register rounds (no 16-key arrays: the
+// one-kernel-for-every-width form spilled ~1 KB per lane and took 46 instead of 23 us on the narrow paths), then both
+// sums as the plain sequential chain (chain_sum_tx: the reference's own loop on one wave, ~0.15 ms) -- exact by
+// construction, no scratch.
+constexpr int kScaleWideNB = 1024;
+constexpr size_t kScaleWideLds = static_cast<size_t>(16) * kScaleC * sizeof(uint64_t) + 2 * kScaleWideNB * sizeof(int);
+__device__ __forceinline__ void exact_scale_c_wide(const KParams& P, int n, uint64_t* s_dyn, MonoScratch<kScaleC>& S,
+                                                KeyStat* s_ks) {
+    constexpr int NT = kScaleC, RT = 8, N = 2 * RT * NT, NB = kScaleWideNB;
+    DevState* st = P.st;
+    uint64_t* s_tmp = s_dyn;
+    int* s_cnt = reinterpret_cast<int*>(s_dyn + N);
+    int* s_end = s_cnt + NB;
+    const int tid = threadIdx.x;
+    if (tid == 0) st->dbg[23] = N;                           // the sort width this scan ran (lo_debug_counters_ex)
+    const int32_t* slot = P.slot;
+    const double* res = P.kd_res ? P.kd_res : P.res_out;
+    auto key_at = [&](int e) -> uint64_t {
+        const int ec = e < n ? e : 0;
+        const int sl = slot[ec];
+        const uint64_t r = static_cast<uint64_t>(__double_as_longlong(res[ec]));
+        return (e < n && sl >= 0) ? r : kInfKey;
+    };
+    KeyStat ks{~0ull, 0ull, 0, 0};
+    uint64_t nan_min = ~0ull;
+    for (int rd = 0; rd < 2; ++rd) {
+        uint64_t key[RT];
+#pragma unroll
+        for (int q = 0; q < RT; ++q) key[q] = key_at((rd * RT + q) * NT + tid);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            if (key[q] < kInfKey) { ks.mn = key[q] < ks.mn ? key[q] : ks.mn; ks.mx = key[q] > ks.mx ? key[q] : ks.mx; ++ks.cnt; }
+            if (key[q] > kInfKey) { ks.nan = 1; nan_min = key[q] < nan_min ? key[q] : nan_min; }
+        }
+    }
+    for (int b = tid; b < NB; b += NT) s_cnt[b] = 0;
+    KeyStat tot;
+    (void)block_excl_scan_dpp<NT>(ks, KeyStat{~0ull, 0ull, 0, 0}, keystat_op, s_ks, &tot);
+    const int cnt = tot.cnt;
+    if (cnt == 0) return;                                    // too few correspondences: the PKO launch reports it
+    if (tot.nan) {                                           // as exact_scale_c_body: the smallest NaN key's thread
+        if (nan_min != ~0ull) st->scale = sqrt(__longlong_as_double(static_cast<long long>(nan_min))) / 6.0;
+        return;
+    }
+    const uint64_t range = tot.mx - tot.mn;
+    const int bl = range ? 64 - __clzll(static_cast<long long>(range)) : 0;
+    int lb = 0;
+    while ((1 << (lb + 1)) <= NB) ++lb;
+    const int shift = bl > lb ? bl - lb : 0;
+    auto bin_of = [&](uint64_t k) { return static_cast<int>((k - tot.mn) >> shift); };
+    for (int rd = 0; rd < 2; ++rd) {                         // histogram
+        uint64_t key[RT];
+#pragma unroll
+        for (int q = 0; q < RT; ++q) key[q] = key_at((rd * RT + q) * NT + tid);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) if (key[q] < kInfKey) atomicAdd(&s_cnt[bin_of(key[q])], 1);
+    }
+    __syncthreads();
+    constexpr int BPT = NB / NT > 0 ? NB / NT : 1;
+    int bsum = 0;
+    for (int i = 0; i < BPT; ++i) bsum += tid * BPT + i < NB ? s_cnt[tid * BPT + i] : 0;
+    int bex = block_excl_scan_dpp<NT>(bsum, 0, [](int a, int c) { return a + c; }, S.wi);
+    for (int i = 0; i < BPT; ++i) if (tid * BPT + i < NB) { s_end[tid * BPT + i] = bex; bex += s_cnt[tid * BPT + i]; }
+    __syncthreads();
+    for (int rd = 0; rd < 2; ++rd) {                         // scatter into bin order
+        uint64_t key[RT];
+#pragma unroll
+        for (int q = 0; q < RT; ++q) key[q] = key_at((rd * RT + q) * NT + tid);
+#pragma unroll
+        for (int q = 0; q < RT; ++q) if (key[q] < kInfKey) s_tmp[atomicAdd(&s_end[bin_of(key[q])], 1)] = key[q];
+    }
+    __syncthreads();
+    uint64_t kk[2 * RT];                                     // each key's rank in its bin, then the moves
+    int pos[2 * RT];
+#pragma unroll
+    for (int i = 0; i < 2 * RT; ++i) {
+        const int p = tid + i * NT;
+        pos[i] = -1;
+        kk[i] = 0;
+        if (p < cnt) {
+            const uint64_t k = s_tmp[p];
+            const int b = bin_of(k), e = s_end[b], s0 = e - s_cnt[b];
+            int r = 0;
+            for (int q = s0; q < e; ++q) {
+                const uint64_t o = s_tmp[q];
+                r += (o < k || (o == k && q < p)) ? 1 : 0;
+            }
+            kk[i] = k;
+            pos[i] = s0 + r;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2 * RT; ++i) if (pos[i] >= 0) s_tmp[pos[i]] = kk[i];
+    __syncthreads();
+    double* s_x = reinterpret_cast<double*>(s_tmp);          // non-negative keys are their doubles' bits
+    const double sum = chain_sum_tx<NT>(s_x, cnt, S);        // std::accumulate, one rounding per add
+    const double mean = sum / cnt;
+    for (int p = tid; p < cnt; p += NT) { const double v = s_x[p]; s_x[p] = (v - mean) * (v - mean); }
+    __syncthreads();
+    double var = chain_sum_tx<NT>(s_x, cnt, S);
+    var /= cnt;
+    if (tid == 0) st->scale = sqrt(var) / 6.0;               // :313-315
+}
 // A scan counted on the device (lo_icp_optimize_raw: the voxel filter's output count stays in HBM; the host knows only
 // the bound ceil(n_raw / stride)): the width is chosen from the count itself, so a 14k-point bound whose filtered scan
-// holds 4k points runs the 4k-point sort and sums.  k_exact_scale_cd takes counts up to 8192 (dynamic LDS
-// scale_c_lds<8>(), every narrower width fits in it; no scratch), k_exact_scale_cw the rare count beyond (launched only
-// when the bound exceeds 8192; each leaves at once when the count is the other's).  One kernel for every width spilled:
-// the 16k-wide body's registers put ~1 KB of scratch per lane on the narrow paths too, 23 -> 46 us at KITTI size.
+// holds 4k points runs the 4k-point sort and sums.  Dynamic LDS: kScaleWideLds (every width fits in it).
 __global__ __launch_bounds__(kScaleC) void k_exact_scale_cd(KParams P) {
     if (P.st->done) return;
     extern __shared__ uint64_t s_dyn[];
     __shared__ MonoScratch<kScaleC> S;
     __shared__ KeyStat s_ks[kScaleC / kWave];
     const int n = min(scan_n(P), P.n);                       // the count never exceeds the bound the grid was sized for
-    if (n > 8 * kScaleC) return;                             // k_exact_scale_cw's
     if (n <= kScaleC) exact_scale_c_body<1>(P, n, s_dyn, S, s_ks);
     else if (n <= 2 * kScaleC) exact_scale_c_body<2>(P, n, s_dyn, S, s_ks);
     else if (n <= 4 * kScaleC) exact_scale_c_body<4>(P, n, s_dyn, S, s_ks);
-    else exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
-}
-__global__ __launch_bounds__(kScaleC) void k_exact_scale_cw(KParams P) {
-    if (P.st->done) return;
-    extern __shared__ uint64_t s_dyn[];
-    __shared__ MonoScratch<kScaleC> S;
-    __shared__ KeyStat s_ks[kScaleC / kWave];
-    const int n = min(scan_n(P), P.n);
-    if (n <= 8 * kScaleC) return;                            // k_exact_scale_cd's
-    exact_scale_c_body<16>(P, n, s_dyn, S, s_ks);
+    else if (n <= 8 * kScaleC) exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
+    else exact_scale_c_wide(P, n, s_dyn, S, s_ks);
 }
 // batched (lo_batch_* over reference-exact contexts): one workgroup per job
 template <int PT>
@@ -457,10 +550,7 @@ static hipError_t scale_c_attr() {
 }
 hipError_t exact_scale_c_prepare() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cd), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(scale_c_lds<8>()));
-    const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cw),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(scale_c_lds<16>()));
-    if (e == hipSuccess) e = e2;
+                                       static_cast<int>(std::max(kScaleWideLds, scale_c_lds<8>())));
     for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>(), scale_c_attr<16>()})
         if (e == hipSuccess) e = r;
     return e;
@@ -476,8 +566,8 @@ void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t 
 // P.n <= kExactScaleCMax; a device-counted scan (P.n_dev) chooses its width from the count on the device
 void launch_exact_scale_c(const KParams& P, hipStream_t s) {
     if (P.n_dev && P.n > kScaleC) {
-        hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
-        if (P.n > 8 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cw, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
+        const size_t lds = P.n > 8 * kScaleC ? std::max(kScaleWideLds, scale_c_lds<8>()) : scale_c_lds<8>();
+        hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), lds, s, P);
     } else if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
     else if (P.n <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<2>, dim3(1), dim3(kScaleC), scale_c_lds<2>(), s, P);
     else if (P.n <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<4>, dim3(1), dim3(kScaleC), scale_c_lds<4>(), s, P);

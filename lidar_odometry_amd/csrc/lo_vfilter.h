@@ -15,7 +15,7 @@ struct VfSlot {
 // Device counters of one filter pass (reset by the pass itself).
 struct VfCounters {
     int n_out;                   // voxels = output points (read by the ICP kernels as KParams::n_dev)
-    unsigned arrive;             // k_vf_heads last-block-done counter
+    unsigned arrive;             // (unused since r06: no last-block hand-off)
     int n_mid, n_big;            // voxels with 17..64 / more than 64 samples (k_vf_wide)
 };
 
@@ -27,7 +27,8 @@ struct VfBuffers {
     int32_t* sslot = nullptr;    // per sample: table slot, -1 = non-finite point
     float* samp = nullptr;       // per sample: its point (compact AoS float3; the raw scan is read once)
     int2* loc = nullptr;         // per head sample: (output slot, bucket start) inside its k_vf_heads block
-    int2* blk = nullptr;         // per k_vf_heads block: (heads, members), then their exclusive prefix
+    int2* blk = nullptr;         // per k_vf_heads block: (heads, members)
+    int2* blk_pre = nullptr;     // their exclusive prefix (+ the total), published by k_vf_place's block 0
     int32_t* bucket = nullptr;   // members of each voxel (bucket order = arrival order; sorted when summed)
     int32_t* mid = nullptr;      // head samples of voxels with 17..64 members
     int32_t* big = nullptr;      // head samples of voxels with more than 64 members

@@ -10,13 +10,15 @@
 //                sample index and a member count;
 //   k_vf_heads   a sample is its voxel's head iff it is the voxel's first index; a block scan of (head, members)
 //                gives each head its output slot (first-occurrence order) and bucket start inside the block, and
-//                the last block to finish turns the block totals into offsets (agent-scope fences: the XCDs'
-//                L2s are separate);
-//   k_vf_place   every sample appends its index to its voxel's bucket (arrival order);
+//                each block writes its totals (no inter-block hand-off: r06, the last-block pattern's agent-scope
+//                fences cost ~14 us);
+//   k_vf_place   every workgroup scans the block totals (one wave), block 0 publishes the prefix; every sample
+//                appends its index to its voxel's bucket (arrival order);
 //   k_vf_small   one lane per head with <= 16 members: register bitonic sort of the member indices, fp32 sums in
 //                index order, output, slot reset; larger voxels are listed for
-//   k_vf_wide    one wave per voxel with <= 64 members (wave bitonic sort, in-order sum over the lanes), one
-//                workgroup per larger voxel (ordered compaction of its index range), slot reset.
+//   k_vf_wide    one wave per voxel with <= 64 members (wave bitonic sort, in-order sum by readlane), one
+//                workgroup per larger voxel (up to 1024 members: its bucket sorted in LDS, wave 0 adds in order;
+//                beyond, an ordered compaction of its index range), slot reset.
 // The table slots are reset by the kernel that consumes them last, so the next pass starts from an empty table
 // without a memset.  The output count stays on the device (n_dev): the ICP kernels read it, no host round trip.
 #include "lo_device.h"
@@ -122,11 +124,13 @@ __device__ __forceinline__ int2 block_excl_scan2(int2 v, int2& tot, int2* s_w /*
     return ex;
 }
 
+// Every block writes its (heads, members) totals; the exclusive prefix over the blocks is formed by each consumer
+// workgroup itself (vf_block_prefix) -- r05's last-block-done hand-off needed agent-scope fences (an L2 write-back per
+// block) and cost ~14 us at KITTI size.
 __global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads(int m, const int32_t* __restrict__ sslot,
                                                             const VfSlot* __restrict__ tslot, int2* __restrict__ loc,
-                                                            int2* blk, VfCounters* ctr) {
+                                                            int2* blk) {
     __shared__ int2 s_w[kVfHeadsBlock / 64 + 1];
-    __shared__ int s_last;
     const int tid = threadIdx.x;
     const int j = blockIdx.x * kVfHeadsBlock + tid;
     int2 v = make_int2(0, 0);
@@ -141,90 +145,22 @@ __global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads(int m, const int32_t
     const int2 ex = block_excl_scan2<kVfHeadsBlock>(v, tot, s_w);
     if (v.x) loc[j] = ex;
     if (tid == 0) blk[blockIdx.x] = tot;
-    // last-block-done: block totals -> exclusive offsets (release at agent scope, count arrivals)
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) s_last = (atomicAdd(&ctr->arrive, 1u) == gridDim.x - 1) ? 1 : 0;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    const int nb = gridDim.x;
-    const int per = (nb + kVfHeadsBlock - 1) / kVfHeadsBlock;
-    const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
-    int2 loc_sum = make_int2(0, 0);
-    for (int q = b0; q < b1; ++q) { const int2 t = blk[q]; loc_sum.x += t.x; loc_sum.y += t.y; }
-    int2 all;
-    int2 run = block_excl_scan2<kVfHeadsBlock>(loc_sum, all, s_w);
-    for (int q = b0; q < b1; ++q) { const int2 t = blk[q]; blk[q] = run; run.x += t.x; run.y += t.y; }
-    if (tid == 0) {
-        ctr->n_out = all.x;
-        ctr->arrive = 0u;
-        ctr->n_mid = 0;
-        ctr->n_big = 0;
-    }
 }
 
-// Scans of at most kVfOneWg samples (a KITTI scan at stride 8: 14k): k_vf_heads + k_vf_place in ONE workgroup -- each
-// thread owns kVfPer consecutive samples, a thread-serial prefix and one block scan give every head its output slot and
-// bucket start (the same exclusive scan in index order as the multi-block pass, so the same slots), then the members are
-// appended to their buckets.  No inter-workgroup hand-off (the multi-block pass's agent-scope fences and last-block
-// scan cost ~14 us) and one launch fewer; loc holds global offsets and blk is zeroed, so k_vf_small / k_vf_wide read
-// them unchanged.
-constexpr int kVfPer = 16;
-constexpr int kVfOneWg = kVfHeadsBlock * kVfPer;
-__global__ __launch_bounds__(kVfHeadsBlock) void k_vf_heads_place(int m, const int32_t* __restrict__ sslot, VfSlot* tslot,
-                                                                  int2* __restrict__ loc, int2* __restrict__ blk, int nblk,
-                                                                  int32_t* __restrict__ bucket, VfCounters* ctr) {
-    __shared__ int2 s_w[kVfHeadsBlock / 64 + 1];
-    const int tid = threadIdx.x, j0 = tid * kVfPer;
-    uint32_t fq[kVfPer], cq[kVfPer];
-    {
-        int bq[kVfPer];
-#pragma unroll
-        for (int q = 0; q < kVfPer; ++q) bq[q] = j0 + q < m ? sslot[j0 + q] : -1;
-#pragma unroll
-        for (int q = 0; q < kVfPer; ++q) {
-            const int bb = bq[q] >= 0 ? bq[q] : 0;       // every load issued (clamped), the result masked
-            fq[q] = tslot[bb].first;
-            cq[q] = tslot[bb].cnt;
-            if (bq[q] < 0) { fq[q] = 0xFFFFFFFFu; cq[q] = 0u; }
-        }
+// The exclusive prefix of the heads blocks' totals into out[0 .. nb] (out[nb] = the grand total; LDS or global), by
+// wave 0 of the calling workgroup; the caller synchronises before reading LDS output.  nb = ceil(m / kVfHeadsBlock).
+__device__ __forceinline__ void vf_block_prefix(const int2* __restrict__ blk, int nb, int2* out) {
+    if ((threadIdx.x >> 6) != 0) return;
+    const int lane = threadIdx.x & 63;
+    int2 carry = make_int2(0, 0);
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int2 t = b0 + lane < nb ? blk[b0 + lane] : make_int2(0, 0);
+        const int2 inc = wave_incl_scan2(t);
+        if (b0 + lane < nb) out[b0 + lane] = make_int2(carry.x + inc.x - t.x, carry.y + inc.y - t.y);
+        carry.x += __shfl(inc.x, 63, 64);
+        carry.y += __shfl(inc.y, 63, 64);
     }
-    int2 v = make_int2(0, 0);
-#pragma unroll
-    for (int q = 0; q < kVfPer; ++q)
-        if (fq[q] == static_cast<uint32_t>(j0 + q)) { v.x += 1; v.y += static_cast<int>(cq[q]); }
-    int2 tot;
-    int2 run = block_excl_scan2<kVfHeadsBlock>(v, tot, s_w);
-#pragma unroll
-    for (int q = 0; q < kVfPer; ++q) {
-        if (fq[q] == static_cast<uint32_t>(j0 + q)) {
-            loc[j0 + q] = run;
-            run.x += 1;
-            run.y += static_cast<int>(cq[q]);
-        }
-    }
-    for (int b = tid; b < nblk; b += kVfHeadsBlock) blk[b] = make_int2(0, 0);
-    if (tid == 0) {
-        ctr->n_out = tot.x;
-        ctr->arrive = 0u;
-        ctr->n_mid = 0;
-        ctr->n_big = 0;
-    }
-    __syncthreads();                                    // every head's loc is written (one workgroup: one L1)
-    // every sample's bucket start and fill ticket in flight together (16 independent round trips, not 16 in a row)
-    int st[kVfPer];
-    unsigned tk[kVfPer];
-#pragma unroll
-    for (int q = 0; q < kVfPer; ++q) st[q] = fq[q] != 0xFFFFFFFFu ? loc[fq[q]].y : 0;
-#pragma unroll
-    for (int q = 0; q < kVfPer; ++q) {
-        tk[q] = 0u;
-        if (fq[q] != 0xFFFFFFFFu) tk[q] = atomicAdd(&tslot[sslot[j0 + q]].fill, 1u);
-    }
-#pragma unroll
-    for (int q = 0; q < kVfPer; ++q)
-        if (fq[q] != 0xFFFFFFFFu) bucket[st[q] + static_cast<int>(tk[q])] = j0 + q;   // non-finite points: no bucket
+    if (lane == 0) out[nb] = carry;
 }
 
 __device__ __forceinline__ int2 vf_head_offsets(const int2* loc, const int2* blk, int h) {
@@ -232,15 +168,44 @@ __device__ __forceinline__ int2 vf_head_offsets(const int2* loc, const int2* blk
     return make_int2(o.x + l.x, o.y + l.y);            // (output slot, bucket start)
 }
 
+// k_vf_place forms the block prefix in every workgroup (up to kVfMaxPre blocks, 2^20 samples, in LDS; beyond, each
+// sample sums the totals before its head's block), block 0 also publishes it (blk_pre, nb + 1 entries) and the pass's
+// counters for the later launches
+constexpr int kVfMaxPre = 1024;
 __global__ __launch_bounds__(256) void k_vf_place(int m, const int32_t* __restrict__ sslot, VfSlot* tslot,
                                                   const int2* __restrict__ loc, const int2* __restrict__ blk,
+                                                  int2* __restrict__ blk_pre, VfCounters* ctr,
                                                   int32_t* __restrict__ bucket) {
+    __shared__ int2 s_pre[kVfMaxPre + 1];
+    const int nb = (m + kVfHeadsBlock - 1) / kVfHeadsBlock;
     const int j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= m) return;
-    const int b = sslot[j];
-    if (b < 0) return;
-    const int h = static_cast<int>(tslot[b].first);
-    const int start = vf_head_offsets(loc, blk, h).y;
+    int b = -1, h = 0;
+    if (j < m) {                                     // the sample's loads go out before the prefix is formed
+        b = sslot[j];
+        if (b >= 0) h = static_cast<int>(tslot[b].first);
+    }
+    if (blockIdx.x == 0) {
+        vf_block_prefix(blk, nb, blk_pre);
+        if (threadIdx.x == 0) { ctr->n_mid = 0; ctr->n_big = 0; }
+    }
+    if (nb <= kVfMaxPre) {
+        vf_block_prefix(blk, nb, s_pre);
+        __syncthreads();
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctr->n_out = s_pre[nb].x;
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int tot = 0;
+        for (int q = 0; q < nb; ++q) tot += blk[q].x;
+        ctr->n_out = tot;
+    }
+    if (j >= m || b < 0) return;
+    int start;
+    if (nb <= kVfMaxPre) {
+        start = s_pre[h / kVfHeadsBlock].y + loc[h].y;
+    } else {
+        int o = 0;                                   // (beyond 2^20 samples only: C5 is 1M samples = 977 blocks)
+        for (int q = 0; q < h / kVfHeadsBlock; ++q) o += blk[q].y;
+        start = o + loc[h].y;
+    }
     const unsigned r = atomicAdd(&tslot[b].fill, 1u);
     bucket[start + static_cast<int>(r)] = j;
 }
@@ -440,7 +405,7 @@ hipError_t vf_reserve(VfBuffers& b, size_t m, hipStream_t s) {
         hipError_t e0 = hipStreamSynchronize(s);
         if (e0 != hipSuccess) return e0;
     }
-    void* old[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
+    void* old[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.blk_pre, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : old) if (p) (void)hipFree(p);
     b = VfBuffers{};
     const size_t cap = std::max<size_t>(m, 4096);
@@ -454,6 +419,7 @@ hipError_t vf_reserve(VfBuffers& b, size_t m, hipStream_t s) {
     if ((e = hipMalloc(&b.samp, cap * 3 * sizeof(float))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.loc, cap * sizeof(int2))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.blk, nb * sizeof(int2))) != hipSuccess) return e;
+    if ((e = hipMalloc(&b.blk_pre, (nb + 1) * sizeof(int2))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.bucket, cap * sizeof(int32_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.mid, cap * sizeof(int32_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&b.big, cap * sizeof(int32_t))) != hipSuccess) return e;
@@ -468,7 +434,7 @@ hipError_t vf_reserve(VfBuffers& b, size_t m, hipStream_t s) {
 }
 
 void vf_free(VfBuffers& b) {
-    void* all[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.bucket, b.mid, b.big, b.ctr};
+    void* all[] = {b.tkey, b.tslot, b.sslot, b.samp, b.loc, b.blk, b.blk_pre, b.bucket, b.mid, b.big, b.ctr};
     for (void* p : all) if (p) (void)hipFree(p);
     b = VfBuffers{};
 }
@@ -491,17 +457,12 @@ hipError_t vf_enqueue(VfBuffers& b, const float* d_raw, size_t n_raw, int stride
     const dim3 gh(static_cast<unsigned>((m + kVfHeadsBlock - 1) / kVfHeadsBlock)), th(kVfHeadsBlock);
     hipLaunchKernelGGL(k_vf_insert, g256, t256, 0, s, d_raw, stride, inv, mi, b.tkey, b.tslot,
                        static_cast<uint64_t>(b.tcap - 1), l2, b.sslot, b.samp);
-    if (mi <= kVfOneWg) {
-        hipLaunchKernelGGL(k_vf_heads_place, dim3(1), th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk,
-                           static_cast<int>((b.cap + kVfHeadsBlock - 1) / kVfHeadsBlock), b.bucket, b.ctr);
-    } else {
-        hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.ctr);
-        hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.bucket);
-    }
-    hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, b.samp, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk,
+    hipLaunchKernelGGL(k_vf_heads, gh, th, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk);
+    hipLaunchKernelGGL(k_vf_place, g256, t256, 0, s, mi, b.sslot, b.tslot, b.loc, b.blk, b.blk_pre, b.ctr, b.bucket);
+    hipLaunchKernelGGL(k_vf_small, g256, t256, 0, s, b.samp, mi, b.sslot, b.tkey, b.tslot, b.loc, b.blk_pre,
                        b.bucket, b.mid, b.big, b.ctr, d_out);
     hipLaunchKernelGGL(k_vf_wide, dim3(kVfWideGrid), t256, 0, s, b.samp, b.sslot, b.tkey, b.tslot, b.loc,
-                       b.blk, b.bucket, b.mid, b.big, b.ctr, d_out);
+                       b.blk_pre, b.bucket, b.mid, b.big, b.ctr, d_out);
     return hipGetLastError();
 }
 
