@@ -48,8 +48,8 @@ size_t       lo_voxelmap_surfel_count(const lo_voxelmap* m);
 size_t       lo_voxelmap_get_surfels(const lo_voxelmap* m, int32_t* keys_xyz, float* normals, float* centroids,
                                      float* planarity, size_t cap);
 /* The L1 keys whose surfel the last lo_voxelmap_update may have changed -- created, refitted, lost its planarity or
- * its children, erased by the radius prune or the planarity test (VoxelMap.cpp:146-169, :187-261) -- in the order the
- * update met them (a key may repeat; an update that changed nothing gives none).  What the reference's UpdateVoxelMap
+ * its children, erased by the radius prune or the planarity test (VoxelMap.cpp:146-169, :187-261) -- each key once,
+ * ordered by key (an update that changed nothing gives none).  What the reference's UpdateVoxelMap
  * collects with the two-line hook INTEGRATION.md shows, for the adapter's keyed sync_map (only these voxels patched:
  * GetSurfelAtPoint at each key's centre, lo_map_patch_surfels).  After lo_voxelmap_apply_transform every key moved:
  * none are listed, upload the whole map.  Returns the count; writes up to cap keys. */

@@ -941,23 +941,26 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     const int rc0 = reconcile_fit(c);
     if (rc0 != LO_OK) return rc0;
     // a key given more than once: its last record wins (as lo_map_set_surfels), the earlier ones are dropped, so the
-    // device patch (one thread per record) never races two records of one key
-    std::unordered_map<uint64_t, size_t> last;
-    last.reserve(2 * m);
+    // device patch (one thread per record) never races two records of one key.  keep[i]: record i is its key's last
+    // (a sort of (key, index) instead of a per-call hash map: the keyed sync hands over a few hundred keys per keyframe)
+    std::vector<std::pair<uint64_t, uint32_t>> ord(m);
     for (size_t i = 0; i < m; ++i) {
         for (int a = 0; a < 3; ++a) {
             const int32_t v = keys[3 * i + a];
             if (v < -(1 << 20) || v >= (1 << 20)) { c->err = "surfel key outside +-2^20"; return LO_ERR_ARG; }
         }
-        last[pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2])] = i;
+        ord[i] = {pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]), static_cast<uint32_t>(i)};
     }
+    std::sort(ord.begin(), ord.end());
+    std::vector<uint8_t> keep(m, 0), res_of(m, 0);
     size_t ins = 0, ers = 0;
-    for (size_t i = 0; i < m; ++i) {
-        const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
-        if (last[key] != i) continue;
-        const bool res = c->resident.count(key) != 0;
-        ins += (present[i] && !res) ? 1 : 0;
-        ers += (!present[i] && res) ? 1 : 0;
+    for (size_t r = 0; r < m; ++r) {
+        if (r + 1 < m && ord[r + 1].first == ord[r].first) continue;   // a later record of the key follows
+        const size_t i = ord[r].second;
+        keep[i] = 1;
+        res_of[i] = c->resident.count(ord[r].first) != 0 ? 1 : 0;
+        ins += (present[i] && !res_of[i]) ? 1 : 0;
+        ers += (!present[i] && res_of[i]) ? 1 : 0;
     }
     const size_t cap = size_t(1) << c->log2cap;
     if ((c->resident.size() + ins - ers) + (c->n_tomb + ers) > cap / 2) { c->err = "table full"; return LO_ERR_CAPACITY; }
@@ -978,9 +981,9 @@ int lo_map_patch_surfels(lo_ctx* c, const int32_t* keys, const float* normals, c
     MapPatchRec* r = static_cast<MapPatchRec*>(c->h_patch);
     int n_rec = 0;
     for (size_t i = 0; i < m; ++i) {
+        if (!keep[i]) continue;                            // superseded by a later record of the key
         const uint64_t key = pack_key_host(keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]);
-        if (last[key] != i) continue;                      // superseded by a later record of the key
-        const bool res = c->resident.count(key) != 0;
+        const bool res = res_of[i] != 0;
         if (!present[i] && !res) continue;                 // nothing on the device to remove
         MapPatchRec& q = r[n_rec++];
         q.key = key;

@@ -725,7 +725,7 @@ __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double sca
         const int c0 = __popcll(__ballot(sl_cur >= 0));
         if (lane == 0) s_cnt[r] = c0;                      // chunk 0's region counts (buffer 0)
     }
-    // consumer: lane k's factor rows (lanes >= 43 repeat term 0 and discard it)
+    // consumer: lane k's factor rows (lanes >= 43 are masked off in the add loop)
     int fa, fb;
     exact_term_factors(lane < kExactTerms ? lane : 0, fa, fb);
     __syncthreads();
@@ -769,7 +769,7 @@ __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double sca
 #if defined(LO_XC_EXP) && LO_XC_EXP == 2
         } else if (false) {                                // diagnostic: no adds (producers alone)
 #else
-        } else if (wid == 0 && ch > 0) {
+        } else if (wid == 0 && ch > 0 && lane < kExactTerms) {   // lanes 43-63 stay masked off: a third less LDS traffic
 #endif
             const float* base = s_f + ((ch - 1) & 1) * kXcBuf;
             const float4* A = reinterpret_cast<const float4*>(base + fa * kXcStride);
@@ -844,7 +844,18 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
         float tot[kExactTerms], pn[12], delta[6];
 #pragma unroll
         for (int k = 0; k < kExactTerms; ++k) tot[k] = s_tot[k];
+#ifdef LO_PKO_STAMPS
+        const unsigned long long sv0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const bool conv = exact_solve_step(tot, T, P.tol_t, P.tol_r, pn, delta);
+#ifdef LO_PKO_STAMPS
+        if (c == 0) {                        // diagnostic: candidate 0's solve in shader cycles (dbg[8]) and in
+            const float keep = pn[0] + delta[0];   // s_memrealtime ticks (dbg[9], 100 MHz): the launch's clock
+            asm volatile("" :: "v"(keep));
+            P.st->dbg[8] = __builtin_amdgcn_s_memtime() - sv0;
+            P.st->dbg[9] = __builtin_amdgcn_s_memrealtime() - sr0;
+        }
+#endif
 #pragma unroll
         for (int q = 0; q < 12; ++q) s_rec[q] = pn[q];
         s_rec[kCandCost] = tot[42];
@@ -1278,6 +1289,15 @@ __device__ __forceinline__ void pko_body(const KParams& P, const ScanBufs& B, in
 
     const int tid = threadIdx.x;
     const bool lead = wg == 0;
+    if constexpr (NW == 4 && !ONE_WAVE && XC) {
+        // reference-exact candidates need only the scale, which is given (iteration 0: k_exact_scale's, before this
+        // launch): they start their sums at once instead of after the prefix phase (~4k cycles).  Not in a tail launch,
+        // whose workgroups must see the scan still pending after the prefix (below) before they write anything.
+        if (wg >= G && P.scale_given && !P.tail) {
+            acc_candidate_exact(P, st->scale, wg - G, reinterpret_cast<float*>(s_pre));
+            return;
+        }
+    }
     // ---- 1. n_c, rank -> block prefix, iteration-0 scale ----
     int nc;
     double s_scale;

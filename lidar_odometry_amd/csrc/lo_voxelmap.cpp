@@ -545,12 +545,30 @@ size_t lo_voxelmap_changed_l1(const lo_voxelmap* m, int32_t* keys, size_t cap) {
     LO_MAP_LOCK(m);
     const HostVoxelMap& h = resolved(m);
     const size_t from = std::min(h.changed_from, h.journal.size());
-    const size_t cnt = h.journal.size() - from;
-    if (keys)
-        for (size_t i = 0; i < cnt && i < cap; ++i) {
-            const lo::Key3& k = h.journal[from + i];
-            keys[3 * i] = k.x; keys[3 * i + 1] = k.y; keys[3 * i + 2] = k.z;
+    // each key once (a voxel can be noted by the prune and by the touched loop), ordered by its packed bits
+    std::vector<uint64_t> u;
+    u.reserve(h.journal.size() - from);
+    for (size_t i = from; i < h.journal.size(); ++i) {
+        const lo::Key3& k = h.journal[i];
+        u.push_back((static_cast<uint64_t>(static_cast<uint32_t>(k.x)) << 42) ^
+                    (static_cast<uint64_t>(static_cast<uint32_t>(k.y)) << 21) ^ static_cast<uint32_t>(k.z));
+    }
+    std::vector<size_t> idx(u.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return u[a] < u[b] || (u[a] == u[b] && a < b); });
+    size_t cnt = 0;
+    for (size_t r = 0; r < idx.size(); ++r) {
+        if (r > 0 && u[idx[r]] == u[idx[r - 1]]) {
+            const lo::Key3& a = h.journal[from + idx[r]];
+            const lo::Key3& b = h.journal[from + idx[r - 1]];
+            if (a == b) continue;                                  // (the packing is not injective: compare keys)
         }
+        if (keys && cnt < cap) {
+            const lo::Key3& k = h.journal[from + idx[r]];
+            keys[3 * cnt] = k.x; keys[3 * cnt + 1] = k.y; keys[3 * cnt + 2] = k.z;
+        }
+        ++cnt;
+    }
     return cnt;
 }
 
