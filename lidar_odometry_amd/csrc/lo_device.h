@@ -146,8 +146,6 @@ struct KParams {
     float* cand_rec;          // nullable: each candidate's solved GN step [NA + 1][kCandWords] (pre-solved in the PKO
                               //   launch while the EM runs; k_pick_correspond / k_pick select one)
     unsigned* cand_cnt;       //   per-candidate arrivals of its W workgroups (the last one solves and re-zeroes it)
-    unsigned* cand_pick;      // nullable (reference-exact candidates): [0] the in-launch JS argmin's candidate + 1 (0:
-                              //   not yet known), [1] the JS workgroups' arrivals; both zeroed by every pick launch
     double* js;               // [NA+1] JS divergence per alpha (k_pko -> argmin in the consumers)
     double* res_dbg;          // nullable: per-point residual (parity entry point)
     unsigned long long* span; // nullable (timing, kSpanWords): start stamps of blocks 0-15, end stamps of the last 256

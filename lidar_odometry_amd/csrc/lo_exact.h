@@ -158,19 +158,12 @@ __device__ __forceinline__ void exact_term_factors(int k, int& fa, int& fb) {
 }
 
 // The reference's solve and right-update from the 43 sums (:417-448): pn = the new pose, delta, convergence.
-// pick (nullable, a candidate of the PKO launch): between the solve's stages the launch's in-launch pick is read (issued
-// a stage ahead), and a candidate other than self stops (*aborted = true, the outputs are then meaningless).
 __device__ inline bool exact_solve_step(const float (&tot)[kExactTerms], const float pose[12], double tol_t, double tol_r,
-                                        float (&pn)[12], float (&delta)[6], const unsigned* pick = nullptr,
-                                        int self = -1, bool* aborted = nullptr) {
-    auto chosen_other = [&](unsigned v) { return v != 0u && v != static_cast<unsigned>(self) + 1u; };
-    unsigned pk = pick ? Mem<true>::ld(pick) : 0u;             // in flight during the LDLT
+                                        float (&pn)[12], float (&delta)[6]) {
     float Hf[36], mg[6];
     for (int k = 0; k < 36; ++k) Hf[k] = tot[k];
     for (int j = 0; j < 6; ++j) mg[j] = -tot[36 + j];
     ldlt6_solve_f32(Hf, mg, delta);                            // :418
-    if (pick && chosen_other(pk)) { *aborted = true; return false; }
-    if (pick) pk = Mem<true>::ld(pick);                         // in flight during SO3::Exp
     const float dt[3] = {delta[0], delta[1], delta[2]}, dw[3] = {delta[3], delta[4], delta[5]};
     float Rd[3][3];
     if (norm3e(dw) < 1e-10f) {                                 // :427-431
@@ -179,7 +172,6 @@ __device__ inline bool exact_solve_step(const float (&tot)[kExactTerms], const f
     } else {
         so3_exp_exact(dw, Rd);
     }
-    if (pick && chosen_other(pk)) { *aborted = true; return false; }
     float R[3][3], t[3], M[3][3], Rn[3][3];
     for (int r = 0; r < 3; ++r) { for (int c = 0; c < 3; ++c) R[r][c] = pose[r * 4 + c]; t[r] = pose[r * 4 + 3]; }
     mul33e(R, Rd, M);                                           // SE3::operator* (MathUtils.h:144-147)

@@ -249,7 +249,6 @@ struct lo_ctx {
     bool pipe = true;
     int pipe_main = 2;
     int pko_groups = 0;             // EM workgroups per PKO launch (lo_set_pko_groups / LO_PKO_GROUPS; 0 = one per alpha)
-    bool cand_abort = true;         // LO_CAND_ABORT=0 (A/B): exact candidates run to the end even when not chosen
     bool pko_solo = false;          // LO_PKO_SOLO=1 (A/B): the speculative PKO launch asks for enough LDS that one
                                     //   workgroup holds a CU alone (no other launch's waves on its SIMDs)
     hipStream_t s_tail = nullptr;
@@ -335,8 +334,8 @@ static int ensure_acc_part(lo_ctx* c) {
     const size_t cand = static_cast<size_t>(c->cfg.num_alpha_segments) + 1;
     LO_HIP(c, hipMalloc(&c->d_acc_part, cand * kFuseMaxBlocks * kNE * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_cand_rec, cand * kCandWords * sizeof(float)));
-    LO_HIP(c, hipMalloc(&c->d_cand_cnt, (cand + 2) * sizeof(unsigned)));   // + KParams::cand_pick's two words
-    LO_HIP(c, hipMemset(c->d_cand_cnt, 0, (cand + 2) * sizeof(unsigned)));
+    LO_HIP(c, hipMalloc(&c->d_cand_cnt, cand * sizeof(unsigned)));
+    LO_HIP(c, hipMemset(c->d_cand_cnt, 0, cand * sizeof(unsigned)));
     ++c->cfg_gen;
     // the exact candidates' staging sits in the PKO launch's dynamic LDS (beyond the 64 KB default with the static part)
     LO_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pko_tx), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -652,7 +651,6 @@ lo_ctx* lo_create(const lo_config* cfg, int device, int* err) {
     if (const char* pf = std::getenv("LO_PIPE_FAIL_AT")) c->pipe_fail_at = static_cast<uint32_t>(std::max(0, std::atoi(pf)));
     if (const char* pg = std::getenv("LO_PKO_GROUPS")) c->pko_groups = std::max(0, std::atoi(pg));
     if (const char* ps = std::getenv("LO_PKO_SOLO")) c->pko_solo = std::atoi(ps) != 0;
-    if (const char* ca = std::getenv("LO_CAND_ABORT")) c->cand_abort = std::atoi(ca) != 0;
     if (const char* ex = std::getenv("LO_EXACT")) c->exact = std::atoi(ex) != 0;   // A/B runs: LO_EXACT=0 = fast mode
     rc = ctx_alloc(c);
     if (rc != LO_OK) {
@@ -1590,11 +1588,6 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             // small scans with PKO: the same launch sequence as the default mode, with the sorted-order scale after the
             // first correspondence launch and the PKO launch's candidates forming the reference's sequential sums
             P.exact_cand = P0.exact_cand = 1;
-            // the launch's last JS workgroup takes the argmin and publishes it; the candidates that were not chosen
-            // stop (between chunks of their sums, between the stages of their solve), so the launch lasts as long as
-            // the chosen candidate instead of the slowest one (LO_CAND_ABORT=0: off, A/B)
-            if (c->cand_abort)
-                P.cand_pick = P0.cand_pick = c->d_cand_cnt + (static_cast<size_t>(c->cfg.num_alpha_segments) + 1);
         }
         if (pipe_flagged(c)) {                            // an earlier scan's wait timed out: one stream from now on
             const int rc4 = pipe_recover(c);

@@ -278,9 +278,6 @@ template <bool CORR>
 __device__ __forceinline__ void pick_body(const KParams& P, int it) {
     DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    // the PKO launch before this one is over: its in-launch pick and arrival count are zeroed for the next one (every
-    // PKO launch of a scan is followed by a pick launch in stream order, done or not)
-    if (P.cand_pick && blk == 0 && tid == 0) { Mem<true>::st(P.cand_pick, 0u); Mem<true>::st(P.cand_pick + 1, 0u); }
     const int done = st->done || tail_gone(P);   // loaded with the points and the JS grid
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);

@@ -694,12 +694,7 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // addition, a chunk behind the producers (double-buffered, one barrier per chunk).  A zero pad row adds +0, which
 // leaves a running sum unchanged: the sums start at +0 and never become -0 (x + -x rounds to +0).  The consumer's loop
 // is uniform (no per-row test) with the next 16 rows' reads issued before the current 16 adds.
-// self >= 0 (a candidate of a launch with P.cand_pick): between chunks the workgroup checks whether the launch's
-// in-launch pick has chosen another candidate, and then stops (returns true: no sums).
-__device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double scale, float dl, float* dyn, float* s_tot,
-                              int self = -1) {
-    __shared__ int s_abort;
-    const bool poll = self >= 0 && P.cand_pick != nullptr;
+__device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double scale, float dl, float* dyn, float* s_tot) {
     float* s_f = dyn;                                      // [2][kXcFactors][kXcStride]
     int* s_cnt = reinterpret_cast<int*>(dyn + kXcCntOff);  // [4][kXcRegions]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = wid - 1;
@@ -730,7 +725,6 @@ __device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double sca
         const int c0 = __popcll(__ballot(sl_cur >= 0));
         if (lane == 0) s_cnt[r] = c0;                      // chunk 0's region counts (buffer 0)
     }
-    if (tid == 0) s_abort = 0;
     // consumer: lane k's factor rows (lanes >= 43 are masked off in the add loop)
     int fa, fb;
     exact_term_factors(lane < kExactTerms ? lane : 0, fa, fb);
@@ -743,8 +737,6 @@ __device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double sca
 #ifdef LO_PKO_STAMPS
         const unsigned long long t_c0 = __builtin_amdgcn_s_memtime();
 #endif
-        unsigned pk = 0;                                   // producer wave 1, lane 0: the in-launch pick, loaded at
-        if (poll && wid == 1 && lane == 0) pk = Mem<true>::ld(P.cand_pick);   // the chunk's start, read at its end
         if (wid > 0 && ch < nch) {
             float* buf = s_f + (ch & 1) * kXcBuf;
             const int* cn = s_cnt + (ch & 3) * kXcRegions;
@@ -805,7 +797,6 @@ __device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double sca
                 for (int q = 0; q < 4; ++q) { a[q] = an[q]; b[q] = bn[q]; }
             }
         }
-        if (poll && wid == 1 && lane == 0 && pk != 0u && pk != static_cast<unsigned>(self) + 1u) s_abort = 1;
 #ifdef LO_PKO_STAMPS
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const unsigned long long t_c1 = __builtin_amdgcn_s_memtime();
@@ -816,7 +807,6 @@ __device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double sca
 #else
         __syncthreads();
 #endif
-        if (poll && s_abort) return true;                 // another candidate was chosen: every wave leaves here
     }
 #ifdef LO_PKO_STAMPS
     // diagnostic sums over every exact candidate of the launch: dbg[16] calls, dbg[17] / [18] the consumer wave's add /
@@ -835,20 +825,12 @@ __device__ bool exact_sums_wg(const KParams& P, const float (&T)[12], double sca
 #endif
     if (wid == 0 && lane < kExactTerms) s_tot[lane] = sum;
     __syncthreads();
-    return false;
 }
 
 __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float* dyn) {
     if (c > P.NA) return;
 #ifdef LO_PKO_STAMPS
     const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
-#ifndef LO_PKO_SUMS_COUNTERS
-    if (threadIdx.x == 0) {                  // diagnostic: candidate 0's start (dbg[16]), the latest candidate start (dbg[18])
-        const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
-        if (c == 0) P.st->dbg[16] = r0;
-        atomicMax(&P.st->dbg[18], r0);
-    }
-#endif
 #endif
     float* s_tot = dyn + kXcTotOff;                        // [kExactTerms]
     float* s_rec = s_tot + kExactTerms;                    // [kCandWords]
@@ -856,15 +838,9 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
-    if (exact_sums_wg(P, T, scale, cand_delta(P, c), dyn, s_tot, c)) return;   // not the chosen candidate
+    exact_sums_wg(P, T, scale, cand_delta(P, c), dyn, s_tot);
 #ifdef LO_PKO_STAMPS
-    if (tid == 0) {
-        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
-        atomicMax(&P.st->dbg[15], r1);       // the last candidate's sums end
-#ifndef LO_PKO_SUMS_COUNTERS
-        if (c == 0) P.st->dbg[17] = r1;      // candidate 0's sums end
-#endif
-    }
+    if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memrealtime());   // the last candidate's sums end
 #endif
     if (tid == 0) {
         float tot[kExactTerms], pn[12], delta[6];
@@ -873,9 +849,7 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
 #ifdef LO_PKO_STAMPS
         const unsigned long long sv0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        bool aborted = false;
-        const bool conv = exact_solve_step(tot, T, P.tol_t, P.tol_r, pn, delta, P.cand_pick, c, &aborted);
-        s_rec[kCandConv + 1] = aborted ? 1.0f : 0.0f;     // (read below by thread 0 only)
+        const bool conv = exact_solve_step(tot, T, P.tol_t, P.tol_r, pn, delta);
 #ifdef LO_PKO_STAMPS
         if (c == 0) {                        // diagnostic: candidate 0's solve in shader cycles (dbg[8]) and in
             const float keep = pn[0] + delta[0];   // s_memrealtime ticks (dbg[9], 100 MHz): the launch's clock
@@ -892,10 +866,10 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
 #pragma unroll
         for (int j = 0; j < 6; ++j) { s_rec[kCandG + j] = tot[36 + j]; s_rec[kCandD + j] = delta[j]; }
         s_rec[kCandConv] = conv ? 1.0f : 0.0f;
+        s_rec[kCandConv + 1] = 0.0f;
     }
     __syncthreads();
-    if (s_rec[kCandConv + 1] != 0.0f) return;              // stopped inside the solve: another candidate was chosen
-    if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = tid == kCandConv + 1 ? 0.0f : s_rec[tid];
+    if (tid < kCandWords) P.cand_rec[static_cast<size_t>(c) * kCandWords + tid] = s_rec[tid];
 #ifdef LO_PKO_STAMPS
     if (tid == 0) {                          // diagnostic: candidate 0's cycles (dbg[7]); dbg[15] / [23]: the last
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // candidate's sums end / record end (s_memrealtime)
@@ -1275,9 +1249,7 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
 #pragma unroll
                     for (int q = 0; q < 20; ++q) vb[q] = vn[q];
                 }
-                const double jv = cnt == 0.0 ? DBL_MAX : cost / cnt;
-                if (P.cand_pick) Mem<true>::st(B.js + ai, jv);   // read in this launch by the last JS workgroup
-                else B.js[ai] = jv;
+                B.js[ai] = cnt == 0.0 ? DBL_MAX : cost / cnt;
             }
             if (!one_alpha) { L.az[tid] = nx_a; L.az[kJsPass + tid] = nx_z; }
             L.nan[tid] = 0;                                      // read above; the next pass counts after the barrier
@@ -1288,35 +1260,6 @@ __device__ __forceinline__ void pko_fit_js(const KParams& P, const ScanBufs& B, 
 #ifdef LO_PKO_STAMPS
     if (dbg && tid == 0) dbg[22] = __builtin_amdgcn_s_memrealtime();   // the lead's JS end (100 MHz, chip-wide clock)
 #endif
-    if (P.cand_pick && one_alpha) {
-        // in-launch pick (reference-exact candidates): each JS workgroup's value left write-through and drained, one
-        // agent-scope arrival each; the last arrival reads the grid past the caches, takes the same argmin the pick
-        // launch takes (pko_select_index: first strict minimum) and publishes its candidate, so the other candidates
-        // stop.  The pick launch still selects from js on its own; the published value only ends work early.
-        __shared__ int s_lastjs;
-        if (tid == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned old = __hip_atomic_fetch_add(P.cand_pick + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_lastjs = old + 1u == static_cast<unsigned>(G) ? 1 : 0;
-        }
-        __syncthreads();
-        if (s_lastjs && tid < kWave) {
-            double bv = DBL_MAX;
-            int bi = 0x7fffffff;
-            for (int i = 1 + tid; i <= P.NA; i += kWave) {
-                const double v = Mem<true>::ld(B.js + i);
-                if (v < bv) { bv = v; bi = i; }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const double ov = __shfl_xor(bv, o, 64);
-                const int oi = __shfl_xor(bi, o, 64);
-                if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-            }
-            const int b = bv < DBL_MAX ? bi : 0;
-            if (tid == 0) Mem<true>::st(P.cand_pick, static_cast<unsigned>((b > 0 ? b - 1 : P.NA) + 1));
-        }
-    }
 }
 
 // wg / G: this workgroup's index among the G workgroups working on the scan (the JS alpha slices); in the
