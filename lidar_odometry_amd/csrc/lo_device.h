@@ -35,6 +35,8 @@ constexpr int kMaxS = 256;
 constexpr int kMaxK = 4;
 constexpr int kMaxAlpha = 1000;
 constexpr int kKnnGroup = 16;       // KDTree k_knn: lanes per query (one DPP row)
+constexpr int kKnnAllMax = 8192;     // k_knn_all / k_inlier_all: points of a set searched whole from LDS (128 KB)
+constexpr int kAllThreads = 1024;    // k_knn_all / k_pick_knn_all / k_inlier_all: 16 queries (a wave each) per workgroup
 constexpr int kSpecBlocksPerWG = 16; // speculative normal equations: 256-point blocks per candidate workgroup
 constexpr int kCandWords = 48;      // a candidate's solved GN step: pose[12] | cost | H[21] | g[6] | delta[6] | conv | pad
 constexpr int kCandCost = 12, kCandH = 13, kCandG = 34, kCandD = 40, kCandConv = 46;
@@ -102,6 +104,7 @@ struct KParams {
     int kd_m;                         // map points
     int kd_org[3], kd_dim[3];         // grid origin (cell coords) and extent
     float kd_h;                       // grid cell edge
+    int kd_all;                       // kd_pts is a small set in index order searched whole from LDS (k_knn_all)
     int32_t* kd_nbr;                  // per point: 5 neighbour positions into kd_pts (-1: fewer than 5)
     int32_t* kd_unres;                // queries left to the brute-force pass
     double* kd_res;                   // per point fp64 point-to-plane distance (the reference's residual)

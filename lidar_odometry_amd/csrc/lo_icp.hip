@@ -39,6 +39,7 @@ __global__ void k_solve(KParams P, int it, int ne_only);
 __global__ void k_solve_pick(KParams P, int it);
 __global__ void k_solve_correspond(KParams P, int it);
 __global__ void k_solve_knn(KParams P, int it);
+__global__ void k_pick_knn(KParams P, int it);
 __global__ void k_pick_correspond(KParams P, int it);
 __global__ void k_pick(KParams P, int it);
 struct Pose12 { float v[12]; };
@@ -48,6 +49,10 @@ __global__ void k_wait_seq(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* 
 __global__ void k_wait_final(uint32_t* fin, uint32_t seq, DevState* st, uint32_t* hbroken, unsigned long long bound);
 __global__ void k_knn(KParams P);
 __global__ void k_knn_brute(KParams P);
+__global__ void k_knn_brute_w(KParams P);
+__global__ void k_knn_all(KParams P);
+__global__ void k_pick_knn_all(KParams P, int it);
+__global__ void k_inlier_all(KParams P);
 __global__ void k_knn_reset(KParams P);
 __global__ void k_plane(KParams P, int with_stats);
 __global__ void k_inlier(KParams P);
@@ -107,6 +112,7 @@ struct PointGrid {
     KdNode* d_nodes = nullptr;      //   and the tree's nodes (root = 0)
     size_t nodes_cap = 0;
     bool has_order = false;         // d_vpos / d_nodes hold the visit order of the current points
+    bool all = false;               // d_pts in index order, no cells (all_pairs_upload: k_knn_all / k_inlier_all)
     void* h_stage = nullptr;        // pinned upload staging (grid_build)
     size_t stage_cap = 0;
     int m = 0;
@@ -392,6 +398,7 @@ static void set_kd_params(lo_ctx* c, KParams& P, const PointGrid& G) {
     P.kd_m = G.m;
     for (int a = 0; a < 3; ++a) { P.kd_org[a] = G.org[a]; P.kd_dim[a] = G.dim[a]; }
     P.kd_h = G.h;
+    P.kd_all = G.all ? 1 : 0;
     P.kd_nbr = c->d_kd_nbr;
     P.kd_unres = c->d_kd_unres;
     P.kd_res = c->d_kd_res;
@@ -438,7 +445,7 @@ static KParams make_params(lo_ctx* c, const float* d_pts, int n) {
     P.blk_m2 = c->d_blk_m2;
     P.blk_part = c->d_blk_part;
     P.acc_part = c->d_acc_part;
-    P.cand_rec = (c->kd || !c->presolve) ? nullptr : c->d_cand_rec;   // surfel path: candidates pre-solve (k_pick*)
+    P.cand_rec = c->presolve ? c->d_cand_rec : nullptr;   // candidates pre-solve (k_pick*, KDTree: k_pick_knn)
     P.cand_cnt = c->d_cand_cnt;
     P.js = c->d_js;
     P.res_dbg = nullptr;
@@ -528,6 +535,9 @@ static int kd_alloc(lo_ctx* c) {
     LO_HIP(c, hipMalloc(&c->d_kd_unres, NB * kBlock * sizeof(int32_t)));
     LO_HIP(c, hipMalloc(&c->d_kd_res, NB * kBlock * sizeof(double)));
     LO_HIP(c, hipMalloc(&c->d_kd_plane, NB * kBlock * sizeof(Slot)));
+    for (const void* f : {reinterpret_cast<const void*>(&k_knn_all), reinterpret_cast<const void*>(&k_pick_knn_all),
+                          reinterpret_cast<const void*>(&k_inlier_all)})
+        LO_HIP(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kKnnAllMax * sizeof(float4)));
     for (PointGrid* G : {&c->grid, &c->lgrid}) {          // empty grid until a point set is uploaded
         LO_HIP(c, hipMalloc(&G->d_start, 2 * sizeof(uint32_t)));
         LO_HIP(c, hipMemset(G->d_start, 0, 2 * sizeof(uint32_t)));
@@ -1127,7 +1137,11 @@ static constexpr size_t kKdMaxCells = size_t(1) << 26;
 
 // with_order: also the reference kd-tree's visit order (the tie-break of equal distances); without it the kNN
 // kernels flag a deciding tie in DevState::kd_tie instead of ranking it (the loop-closure ICP then rebuilds with it).
-static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool with_order = true) {
+// min_per_cell > 0 (the loop-closure ICP's matched keyframe cloud): the cell edge doubles (up to 3 times) while the
+// occupied cells hold fewer than min_per_cell points on average -- a voxel-filtered, strided keyframe cloud is sparse
+// at 2 x voxel_size, so most queries would need the outer shells or the brute-force fallback.  The kNN result does
+// not depend on the edge (every answer is certified against the scanned cube); only the work per query does.
+static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool with_order = true, int min_per_cell = 0) {
     if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
     if (m > static_cast<size_t>(INT32_MAX / 2)) { c->err = "too many map points"; return LO_ERR_CAPACITY; }
     for (size_t i = 0; i < 3 * m; ++i)
@@ -1142,6 +1156,8 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
     float h = 2.0f * c->cfg.voxel_size;
     int org[3] = {0, 0, 0}, dim[3] = {1, 1, 1};
     auto cell = [&](float v) { return static_cast<int64_t>(std::floor(v / h)); };
+    std::vector<uint32_t> start, lin(m);
+    for (int grow = 0;; ++grow) {
     for (;;) {
         int64_t lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, hi[3] = {INT64_MIN, INT64_MIN, INT64_MIN};
         for (size_t i = 0; i < m; ++i)
@@ -1159,13 +1175,17 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
         h *= 2.0f;
     }
     const size_t ncell = static_cast<size_t>(dim[0]) * dim[1] * dim[2];
-    std::vector<uint32_t> start(ncell + 1, 0);
-    std::vector<uint32_t> lin(m);
+    start.assign(ncell + 1, 0);
+    size_t occupied = 0;
     for (size_t i = 0; i < m; ++i) {
         const int64_t x = cell(xyz[3 * i]) - org[0], y = cell(xyz[3 * i + 1]) - org[1], z = cell(xyz[3 * i + 2]) - org[2];
         lin[i] = static_cast<uint32_t>((static_cast<size_t>(z) * dim[1] + y) * dim[0] + x);
-        start[lin[i] + 1]++;
+        occupied += start[lin[i] + 1]++ == 0;
     }
+    if (min_per_cell > 0 && grow < 3 && m >= 64 && occupied * static_cast<size_t>(min_per_cell) > m) { h *= 2.0f; continue; }
+    break;
+    }
+    const size_t ncell = static_cast<size_t>(dim[0]) * dim[1] * dim[2];
     for (size_t k = 0; k < ncell; ++k) start[k + 1] += start[k];
     std::vector<float4> pts(std::max<size_t>(m, 1));
     std::vector<uint32_t> fill(start.begin(), start.end() - 1);
@@ -1228,8 +1248,46 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
     LO_HIP(c, hipMemcpyAsync(G.d_nodes, hs + b_pts + b_start + b_vpos, b_nodes, hipMemcpyHostToDevice, c->stream));
     G.m = static_cast<int>(m);
     G.has_order = with_order;
+    G.all = false;
     G.h = h;
     for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
+    return LO_OK;
+}
+
+// A small point set (<= kKnnAllMax) for the all-pairs kernels (k_knn_all, k_inlier_all): the points in index order as
+// float4 (x, y, z, index), one pinned staging copy, no cells and no visit order.
+static int all_pairs_upload(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
+    if (m > static_cast<size_t>(kKnnAllMax)) { c->err = "all_pairs_upload: too many points"; return LO_ERR_CAPACITY; }
+    if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
+    for (size_t i = 0; i < 3 * m; ++i)
+        if (!std::isfinite(xyz[i])) { c->err = "non-finite map point"; return LO_ERR_ARG; }
+    LO_HIP(c, hipSetDevice(c->device));
+    LO_HIP(c, hipStreamSynchronize(c->stream));          // the staging buffer's previous copy has retired
+    const size_t mm = std::max<size_t>(m, 1), bytes = mm * sizeof(float4);
+    if (mm > G.pts_cap) {
+        if (G.d_pts) LO_HIP(c, hipFree(G.d_pts));
+        G.d_pts = nullptr;
+        LO_HIP(c, hipMalloc(&G.d_pts, bytes));
+        G.pts_cap = mm;
+    }
+    if (bytes > G.stage_cap) {
+        if (G.h_stage) LO_HIP(c, hipHostFree(G.h_stage));
+        G.h_stage = nullptr;
+        G.stage_cap = 0;
+        LO_HIP(c, hipHostMalloc(&G.h_stage, 2 * bytes, hipHostMallocDefault));
+        G.stage_cap = 2 * bytes;
+    }
+    float4* hs = static_cast<float4*>(G.h_stage);
+    for (size_t i = 0; i < m; ++i) {
+        int32_t id = static_cast<int32_t>(i);
+        float w;
+        std::memcpy(&w, &id, sizeof(float));
+        hs[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], w);
+    }
+    if (m > 0) LO_HIP(c, hipMemcpyAsync(G.d_pts, hs, m * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    G.m = static_cast<int>(m);
+    G.has_order = false;
+    G.all = true;
     return LO_OK;
 }
 
@@ -1359,6 +1417,7 @@ int ctx_grid_from_device(lo_ctx* c, const float* d_xyz, const int* d_count, size
     LO_HIP(c, hipGetLastError());
     G.m = static_cast<int>(m);
     G.has_order = false;
+    G.all = false;
     G.h = h;
     for (int a = 0; a < 3; ++a) { G.org[a] = org[a]; G.dim[a] = dim[a]; }
     c->grid_dev = true;
@@ -1404,6 +1463,19 @@ size_t lo_map_point_count(const lo_ctx* c) { return c ? static_cast<size_t>(c->g
 // Correspondence stage of one GN iteration: surfel lookup, or (KDTree variant) grid kNN + brute-force
 // fallback + plane fit.  P0 carries init = 1 on a scan's first iteration.
 static constexpr int kBruteBlocks = 64;      // k_knn_brute workgroups (grid-strided over the unresolved list)
+static constexpr int kBruteWaveBlocks = 256; // k_knn_brute_w: 4 queries in flight per workgroup
+static constexpr int kBruteWaveMaxM = 16384; // k_knn_brute_w up to this many grid points (<= 256 per lane)
+
+// The unresolved queries: a wave per query (k_knn_brute_w) over a small grid without the kd visit order, else a
+// 1024-thread workgroup per query (k_knn_brute, which also ranks deciding ties in the visit order when it is built).
+static void launch_brute(lo_ctx* c, const KParams& P) {
+    if (!P.kd_nodes && P.kd_m <= kBruteWaveMaxM) hipLaunchKernelGGL(k_knn_brute_w, dim3(kBruteWaveBlocks), dim3(kBlock), 0, c->stream, P);
+    else hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, P);
+}
+
+static dim3 knn_grid(const KParams& P) { return dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock); }
+static size_t all_lds(const KParams& P) { return static_cast<size_t>((std::max(P.kd_m, 1) + 511) / 512 * 512) * sizeof(float4); }   // all_padded
+static dim3 all_grid(const KParams& P) { return dim3((std::max(P.n, 1) + kAllThreads / 64 - 1) / (kAllThreads / 64)); }
 
 static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool kd) {
     const dim3 grid(P.nb), blk(kBlock);
@@ -1413,9 +1485,35 @@ static void launch_correspond(lo_ctx* c, const KParams& P, int with_stats, bool 
     }
     KParams Pn = P;
     Pn.init = 0;
-    hipLaunchKernelGGL(k_knn, dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock), blk, 0, c->stream, P);
-    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, Pn);
+    if (P.kd_all) {                                      // a small set searched whole from LDS: no fallback pass
+        hipLaunchKernelGGL(k_knn_all, all_grid(P), dim3(kAllThreads), all_lds(P), c->stream, P);
+        hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
+        return;
+    }
+    hipLaunchKernelGGL(k_knn, knn_grid(P), blk, 0, c->stream, P);
+    launch_brute(c, Pn);
     hipLaunchKernelGGL(k_plane, grid, blk, 0, c->stream, Pn, with_stats);
+}
+
+// After a KDTree-variant PKO launch (small scans): the iteration's solve -- the selected candidate's record
+// (k_pick_knn) or its partial sums solved in every block (k_solve_knn) -- fused with the kNN search of it + 1, then
+// the unresolved queries and the plane stage.
+static void launch_pick_knn(lo_ctx* c, const KParams& P, int it) {
+    const dim3 knn = knn_grid(P), blk(kBlock);
+    if (P.kd_all) {
+        if (P.cand_rec) {
+            hipLaunchKernelGGL(k_pick_knn_all, all_grid(P), dim3(kAllThreads), all_lds(P), c->stream, P, it);
+        } else {
+            hipLaunchKernelGGL(k_solve_pick, dim3(1), blk, 0, c->stream, P, it);
+            hipLaunchKernelGGL(k_knn_all, all_grid(P), dim3(kAllThreads), all_lds(P), c->stream, P);
+        }
+        hipLaunchKernelGGL(k_plane, dim3(P.nb), blk, 0, c->stream, P, 0);
+        return;
+    }
+    if (P.cand_rec) hipLaunchKernelGGL(k_pick_knn, knn, blk, 0, c->stream, P, it);
+    else hipLaunchKernelGGL(k_solve_knn, knn, blk, 0, c->stream, P, it);
+    launch_brute(c, P);
+    hipLaunchKernelGGL(k_plane, dim3(P.nb), blk, 0, c->stream, P, 0);
 }
 
 static constexpr int kStageEvents = 1024;
@@ -1576,7 +1674,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
             P0.ex_terms = P.ex_terms;
             P0.scale_given = P.scale_given;
             if (c->ex_merge_presort) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
-            if (!(fused && P.cand_rec && !c->kd && n2 > 0)) {
+            if (!(fused && P.cand_rec && n2 > 0)) {
                 // reference-exact GN loop without candidates (lo_exact.hip): correspondences, (iteration 0) sorted-order
                 // scale, PKO, per-point fp32 terms, sequential sums + fp32 LDLT + SVD-projected update
                 for (int it = 0; it < g.max_iterations; ++it) launch_exact_iteration(c, P, P0, it, n2, c->kd);
@@ -1645,10 +1743,7 @@ static int enqueue_optimize(lo_ctx* c, const float* d_pts, size_t n, const float
                 if (P.cand_rec) hipLaunchKernelGGL(k_pick_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
                 else hipLaunchKernelGGL(k_solve_correspond, dim3(P.nb), dim3(kBlock), 0, c->stream, P, it);
             } else if (it + 1 < g.max_iterations) {
-                hipLaunchKernelGGL(k_solve_knn, dim3((static_cast<size_t>(P.n) * kKnnGroup + kBlock - 1) / kBlock),
-                                   dim3(kBlock), 0, c->stream, P, it);
-                hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, P);
-                hipLaunchKernelGGL(k_plane, dim3(P.nb), dim3(kBlock), 0, c->stream, P, 0);
+                launch_pick_knn(c, P, it);
             } else if (P.cand_rec) {
                 hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, c->stream, P, it);
             } else {
@@ -1767,6 +1862,7 @@ int lo_icp_optimize(lo_ctx* c, const float* pts, size_t n, const float T_init[12
 // checks, then the 1-NN inlier ratio (k_inlier) once converged.
 static constexpr int kLoopMaxIters = 100;                // :74
 static constexpr int kLoopChunk = 4;
+static constexpr int kLoopMinPerCell = 4;                // the matched cloud's grid: >= 4 points per occupied cell
 
 int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const float T_curr[12], const float* matched,
                          size_t n_matched, const float T_matched[12], float T_rel_out[12], float* inlier_ratio,
@@ -1785,7 +1881,8 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     // it only ranks exact distance ties that decide a query's five neighbours or their order, which keyframe
     // centroids rarely produce); a solve that met one is rerun with the order below
     bool with_order = false;
-    rc = grid_build(c, c->lgrid, lmap.data(), n_matched, with_order);
+    rc = n_matched <= static_cast<size_t>(kKnnAllMax) ? all_pairs_upload(c, c->lgrid, lmap.data(), n_matched)
+                                                      : grid_build(c, c->lgrid, lmap.data(), n_matched, with_order, kLoopMinPerCell);
     if (rc != LO_OK) return rc;
 retry:
     if (st) { std::memset(st, 0, sizeof(*st)); st->status = LO_INSUFFICIENT; }
@@ -1811,11 +1908,25 @@ retry:
     P0.init = 1;
     if (c->exact && c->ex_merge_presort) P0.presort = reinterpret_cast<uint64_t*>(c->d_ex_rank);
     std::memcpy(P0.T0, T_curr, sizeof(float) * 12);
+    // small clouds with PKO: the odometry path's launch sequence (candidates solved in the PKO launch, k_pick_knn
+    // taking the selected one fused with the next kNN search); reference-exact mode as there
+    const bool cand = spec_ok(P) && P.cand_rec && (!c->exact || n2 > 0);
+    if (cand && c->exact) { P.exact_cand = P0.exact_cand = 1; P0.ex_terms = P.ex_terms; }
     const dim3 blk(kBlock);
     LO_HIP(c, hipEventRecord(c->ev0, c->stream));
     const size_t head = offsetof(DevState, logs);
     for (int it = 0; it < kLoopMaxIters;) {
         for (int k = 0; k < kLoopChunk && it < kLoopMaxIters; ++k, ++it) {
+            if (cand) {
+                if (it == 0) {
+                    launch_correspond(c, P0, 1, true);
+                    if (c->exact) launch_exact_scale_any(c, P, n2, c->stream);
+                }
+                launch_pko_spec(c, P, it);
+                if (it + 1 < kLoopMaxIters) launch_pick_knn(c, P, it);
+                else hipLaunchKernelGGL(k_pick, dim3(1), blk, 0, c->stream, P, it);
+                continue;
+            }
             if (c->exact) {
                 launch_exact_iteration(c, P, P0, it, n2, true);
                 continue;
@@ -1829,7 +1940,8 @@ retry:
         if (c->h_st->done) break;                                 // converged, or too few correspondences
     }
     const bool converged = c->h_st->done && c->h_st->status == LO_OK;
-    if (converged) hipLaunchKernelGGL(k_inlier, dim3(P.nb), blk, 0, c->stream, P);
+    if (converged && P.kd_all) hipLaunchKernelGGL(k_inlier_all, all_grid(P), dim3(kAllThreads), all_lds(P), c->stream, P);
+    else if (converged) hipLaunchKernelGGL(k_inlier, dim3(P.nb), blk, 0, c->stream, P);
     LO_HIP(c, hipGetLastError());
     LO_HIP(c, hipEventRecord(c->ev1, c->stream));
     const size_t bytes = head + sizeof(lo_iter_log) * static_cast<size_t>(LO_MAX_ITERS);
@@ -1838,7 +1950,7 @@ retry:
     if (c->h_st->kd_tie && !with_order) {               // a deciding tie was ranked by index: redo with the order
         with_order = true;
         ++c->loop_reruns;
-        rc = grid_build(c, c->lgrid, lmap.data(), n_matched, true);
+        rc = grid_build(c, c->lgrid, lmap.data(), n_matched, true, kLoopMinPerCell);
         if (rc != LO_OK) return rc;
         goto retry;
     }
@@ -2028,7 +2140,7 @@ int lo_knn_search(lo_ctx* c, const float* q, size_t n, int32_t* idx, float* dist
     KParams Pn = P;
     Pn.init = 0;
     hipLaunchKernelGGL(k_knn, dim3((n * kKnnGroup + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, P);
-    hipLaunchKernelGGL(k_knn_brute, dim3(kBruteBlocks), dim3(1024), 0, c->stream, Pn);
+    launch_brute(c, Pn);
     hipLaunchKernelGGL(k_knn_reset, dim3(1), dim3(64), 0, c->stream, Pn);
     LO_HIP(c, hipGetLastError());
     std::vector<int32_t> nb(5 * n);

@@ -290,6 +290,19 @@ __global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
     knn_body(P, T);
 }
 
+// The KDTree counterpart of k_pick_correspond (reference-exact mode): the record of the candidate the PKO launch
+// selected (its reference-order sums and fp32 solve, acc_candidate_exact) is iteration it's pose, block 0 publishes
+// it, and every block searches its queries' five neighbours at that pose for iteration it + 1.
+__global__ __launch_bounds__(kBlock) void k_pick_knn(KParams P, int it) {
+    __shared__ float s_rec[kCandWords];
+    bool conv = false;
+    if (!pick_select(P, it, s_rec, &conv) || conv) return;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
+    knn_body(P, T);
+}
+
 // ====================================================================================================
 // k_knn_brute: unresolved queries, one 1024-thread workgroup each (grid-strided over the device-side list):
 // every lane scans a strided share of the map with 8 loads in flight, the 64 lanes of a wave merge with a
@@ -398,6 +411,190 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     }
 }
 
+// k_knn_brute_w: the same answers by one wave per unresolved query, for a grid of at most 16k points built without the
+// kd visit order (the loop-closure ICP's matched keyframe cloud, a device-built map grid): no LDS, no barrier and no
+// call into the visit-order walk (whose call frame puts k_knn_brute on scratch memory), so a launch with nothing to do
+// costs what an empty launch costs, and a few dozen queries run side by side.  A deciding tie is ranked by index and
+// flagged (DevState::kd_tie) for the host's rerun with the order, as k_knn_brute does without one.
+__global__ __launch_bounds__(kBlock) void k_knn_brute_w(KParams P) {
+    DevState* st = P.st;
+    if (st->done) return;
+    const unsigned nu = st->kd_unres_n;
+    constexpr int kWpb = kBlock / kWave;
+    const int lane = threadIdx.x & 63;
+    const unsigned w0 = blockIdx.x * kWpb + (threadIdx.x >> 6);
+    if (w0 >= nu) return;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    const KnnQ Q0{{0.0f, 0.0f, 0.0f}, nullptr, nullptr};
+    for (unsigned u = w0; u < nu; u += gridDim.x * kWpb) {
+        const int i = P.kd_unres[u];
+        float qx, qy, qz;
+        transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+        Top5 t;
+        top5_init(t);
+        for (int p0 = lane; p0 < P.kd_m; p0 += 8 * kWave) {
+            float4 v[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const int p = p0 + w * kWave;
+                v[w] = p < P.kd_m ? P.kd_pts[p] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const int p = p0 + w * kWave;
+                if (p < P.kd_m) top5_insert<false>(Q0, t, l2sq(qx, qy, qz, v[w]), __float_as_int(v[w].w), p);
+            }
+        }
+        t = group_merge<false>(Q0, t);
+        top5_merge_xor<false>(Q0, t, 16);
+        top5_merge_xor<false>(Q0, t, 32);
+        if (lane == 0) {
+            if ((t.n == 5 && t.tie <= t.d[4]) || (t.n < 5 && t.tie < __builtin_inff())) atomicOr(&st->kd_tie, 1u);
+            int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+            if (t.n < 5) out[0] = -1;
+            else for (int k = 0; k < 5; ++k) out[k] = t.pos[k];
+        }
+    }
+}
+
+// ====================================================================================================
+// Small point sets (the loop-closure ICP's matched keyframe cloud, <= kKnnAllMax points): every query against the
+// whole set, staged once per workgroup in LDS (index order, the original index in w).  One wave per query, 16
+// queries per 1024-thread workgroup (one LDS copy of the set per 16 queries, 4 waves per SIMD to hide the LDS and
+// VALU latency): lane l takes points l, l + 64, ... (a wave reads 64 consecutive points per ds_read_b128), keeps
+// its own top-5 list, and the wave merges the 64 lists (DPP rows, then across rows) -- the exact answer by
+// construction, no cells, no certification and no brute-force pass.  Fast order (distance, index) as k_knn; a
+// query whose five or their order rest on an equal distance is marked -3, k_plane flags it (DevState::kd_tie) and
+// the host reruns the solve on the grid with the kd visit order.
+// ====================================================================================================
+// The set in LDS, padded to a multiple of kAllBatch points with sentinels at +inf (their distance to any finite query
+// is +inf: never one of the five, never within 1 m), so the search loops read 8 points per lane with no bounds test.
+constexpr int kAllBatch = 8 * kWave;
+__device__ __forceinline__ int all_padded(int m) { return (m + kAllBatch - 1) / kAllBatch * kAllBatch; }
+__device__ __forceinline__ void stage_all(const KParams& P, float4* s_map) {
+    const int m = P.kd_m, mp = all_padded(m);
+    const float inf = __builtin_inff();
+#pragma unroll 4
+    for (int p = threadIdx.x; p < mp; p += kAllThreads) {
+        const float4 v = P.kd_pts[min(p, m - 1)];          // in bounds (m >= 1 when the set is searched)
+        s_map[p] = p < m ? v : make_float4(inf, inf, inf, __int_as_float(-1));
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ float wave_min(float f) {
+    f = fminf(f, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f), 0xB1, 0xf, 0xf, false)));
+    f = fminf(f, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f), 0x4E, 0xf, 0xf, false)));
+    f = fminf(f, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f), 0x141, 0xf, 0xf, false)));
+    f = fminf(f, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f), 0x140, 0xf, 0xf, false)));
+    f = fminf(f, __shfl_xor(f, 16, 64));
+    return fminf(f, __shfl_xor(f, 32, 64));
+}
+
+__device__ __forceinline__ void knn_all_body(const KParams& P, const float (&T)[12], const float4* s_map) {
+    const int i = blockIdx.x * (kAllThreads / kWave) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= scan_n(P)) return;                              // whole waves leave together
+    int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
+    float qx, qy, qz;
+    transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
+    if (!(isfinite(qx) && isfinite(qy) && isfinite(qz)) || P.kd_m < 5) { if (lane == 0) out[0] = -1; return; }
+    const KnnQ Q{{qx, qy, qz}, nullptr, nullptr};
+    const int mp = all_padded(P.kd_m);
+    Top5 t;
+    top5_init(t);
+    // thr: the smallest fifth distance over the wave's lanes so far -- every lane's five are points of the set, so the
+    // set's own fifth distance is <= thr, and a point farther than thr can neither be one of the five nor tie with
+    // the fifth: only points within thr reach the (branchy) insert, the rest cost a distance and a compare
+    float thr = __builtin_inff();
+    for (int p0 = lane; p0 < mp; p0 += kAllBatch) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = s_map[p0 + u * kWave];
+        float d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d[u] = l2sq(qx, qy, qz, v[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (d[u] <= thr) top5_insert<false>(Q, t, d[u], p0 + u * kWave, p0 + u * kWave);
+        thr = wave_min(t.n == 5 ? t.d[4] : __builtin_inff());
+    }
+    t = group_merge<false>(Q, t);                            // 16-lane rows
+    top5_merge_xor<false>(Q, t, 16);
+    top5_merge_xor<false>(Q, t, 32);                         // the wave's five
+    if (lane != 0) return;
+    if ((t.n == 5 && t.tie <= t.d[4]) || (t.n < 5 && t.tie < __builtin_inff())) { out[0] = -3; return; }
+    if (t.n < 5) { out[0] = -1; return; }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) out[k] = t.pos[k];
+}
+
+__global__ __launch_bounds__(kAllThreads) void k_knn_all(KParams P) {
+    extern __shared__ float4 s_map[];
+    if (!P.init && P.st->done) return;
+    float T[12];
+    scan_pose(P, P.init, blockIdx.x, T);
+    stage_all(P, s_map);
+    knn_all_body(P, T, s_map);
+}
+
+// k_pick_knn over a small set
+__global__ __launch_bounds__(kAllThreads) void k_pick_knn_all(KParams P, int it) {
+    extern __shared__ float4 s_map[];
+    __shared__ float s_rec[kCandWords];
+    bool conv = false;
+    if (!pick_select(P, it, s_rec, &conv) || conv) return;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
+    stage_all(P, s_map);
+    knn_all_body(P, T, s_map);
+}
+
+// k_inlier over a small set, a wave per point: its lanes take every 64th point until one lies within 1 m (an existence
+// test, so the order of the scan does not matter).  std::sqrt(sqdist) < 1.0f (:233) is sqdist < 1.0f: a correctly
+// rounded square root is monotone and exact at 1, and the largest float below 1 has its root rounded below 1.
+__global__ __launch_bounds__(kAllThreads) void k_inlier_all(KParams P) {
+    extern __shared__ float4 s_map[];
+    __shared__ unsigned s_hits[kAllThreads / kWave];
+    DevState* st = P.st;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = st->pose[k];
+    stage_all(P, s_map);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * (kAllThreads / kWave) + wid;
+    bool in = false;
+    if (i < scan_n(P)) {
+        const float px = P.pts[3 * i], py = P.pts[3 * i + 1], pz = P.pts[3 * i + 2];
+        const float q[3] = {T[3] + dot3f(T[0], T[1], T[2], px, py, pz), T[7] + dot3f(T[4], T[5], T[6], px, py, pz),
+                            T[11] + dot3f(T[8], T[9], T[10], px, py, pz)};
+        if (isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && P.kd_m > 0) {
+            const int mp = all_padded(P.kd_m);
+            for (int p0 = lane; p0 < mp; p0 += kAllBatch) {          // 8 LDS reads in flight
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = s_map[p0 + u * kWave];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float d0 = q[0] - v[u].x, d1 = q[1] - v[u].y, d2 = q[2] - v[u].z;
+                    in = in || (d0 * d0 + d1 * d1) + d2 * d2 < 1.0f;
+                }
+                if (__ballot(in)) break;                             // the wave found one
+            }
+        }
+    }
+    const bool hit = __ballot(in) != 0;
+    if (lane == 0) s_hits[wid] = hit ? 1u : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned h = 0;
+        for (int w = 0; w < kAllThreads / kWave; ++w) h += s_hits[w];
+        if (h) atomicAdd(&st->inliers, h);
+    }
+}
+
 // lo_knn_search (kNN without the plane stage): the unresolved-query counter k_plane would zero
 __global__ void k_knn_reset(KParams P) {
     if (threadIdx.x == 0) P.st->kd_unres_n = 0;
@@ -468,6 +665,7 @@ __global__ __launch_bounds__(kBlock) void k_plane(KParams P, int with_stats) {
     double dist = 0.0;
     if (i < scan_n(P)) {
         const int32_t* nb = P.kd_nbr + 5 * static_cast<size_t>(i);
+        if (nb[0] == -3) atomicOr(&st->kd_tie, 1u);                 // k_knn_all: a deciding tie (the host reruns)
         if (nb[0] >= 0) {
             double Pm[5][3];
 #pragma unroll

@@ -276,9 +276,7 @@ __device__ __forceinline__ void signal_main(const KParams& P) {
 
 template <bool CORR>
 __device__ __forceinline__ void pick_body(const KParams& P, int it) {
-    DevState* st = P.st;
     const int tid = threadIdx.x, blk = blockIdx.x;
-    const int done = st->done || tail_gone(P);   // loaded with the points and the JS grid
     const int i = blk * kBlock + tid;
     const int n = scan_n(P);
     float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -286,37 +284,8 @@ __device__ __forceinline__ void pick_body(const KParams& P, int it) {
     // may run after the caller has already taken the final result and reused or freed that buffer
     if (CORR && !P.tail && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
     __shared__ float s_rec[kCandWords];
-    __shared__ int s_skip;
-    __shared__ double s_alpha;
-    if (tid < kWave) {
-        const int bi = pko_select_index(P, P.js);
-        const int c = bi > 0 ? bi - 1 : P.NA;
-        if (tid < kCandWords) s_rec[tid] = P.cand_rec[static_cast<size_t>(c) * kCandWords + tid];
-        if (tid == 0) {                           // thread 0's view of the flag decides for the whole block
-            s_skip = done;
-            s_alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
-        }
-    }
-    __syncthreads();
-    if (s_skip) return;
-    const bool conv = s_rec[kCandConv] != 0.0f;
-    if (blk == 0 && tid == 0) {
-        lo_iter_log& L = st->logs[it];
-#pragma unroll
-        for (int q = 0; q < 12; ++q) { st->pose[q] = s_rec[q]; L.pose[q] = s_rec[q]; }
-        L.n_corr = st->n_corr;
-        L.scale = st->scale;
-        L.alpha = s_alpha;
-        L.cost = s_rec[kCandCost];
-#pragma unroll
-        for (int q = 0; q < 21; ++q) L.H[q] = s_rec[kCandH + q];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) { L.g[q] = s_rec[kCandG + q]; L.delta[q] = s_rec[kCandD + q]; }
-        st->alpha = s_alpha;
-        st->iter = it + 1;
-        if (conv) st->done = 1;
-        if (conv || it + 1 >= P.max_iters) publish_final(P);   // the scan's result is final (scan pipeline)
-    }
+    bool conv = false;
+    if (!pick_select(P, it, s_rec, &conv)) return;
     if (!CORR || conv) return;                    // converged: the later launches of the scan see DevState::done
     if (P.tail && i < n) { px = P.pts[3 * i]; py = P.pts[3 * i + 1]; pz = P.pts[3 * i + 2]; }
     float T[12];

@@ -245,4 +245,52 @@ __device__ inline bool solve_core(const KParams& P, int it, const double* tot, c
     return conv;
 }
 
+// The selection of GN iteration it among the candidates the PKO launch already solved (P.cand_rec; pko_select_index:
+// the reference's first strict JS minimum, AdaptiveMEstimator.cpp:256-275): the block's wave 0 loads the selected
+// 48-word record into s_rec, block 0's thread 0 publishes it as the iteration's pose, log and convergence test
+// (:417-448).  Returns false when the block has nothing to do (the scan already converged, or a tail launch whose
+// scan is final); otherwise s_rec holds the record and *conv its convergence flag.  Every thread calls it (one
+// barrier).  k_pick_correspond / k_pick (lo_kernels.hip) and k_pick_knn (lo_kdtree.hip).
+__device__ __forceinline__ bool pick_select(const KParams& P, int it, float* s_rec, bool* conv) {
+    DevState* st = P.st;
+    const int tid = threadIdx.x;
+    const int done = st->done || tail_gone(P);
+    __shared__ int s_skip;
+    __shared__ double s_alpha;
+    if (tid < kWave) {
+        const int bi = pko_select_index(P, P.js);
+        const int c = bi > 0 ? bi - 1 : P.NA;
+        if (tid < kCandWords) s_rec[tid] = P.cand_rec[static_cast<size_t>(c) * kCandWords + tid];
+        if (tid == 0) {                           // thread 0's view of the flag decides for the whole block
+            s_skip = done;
+            s_alpha = bi > 0 ? P.alphas[bi] : P.min_scale;
+        }
+    }
+    __syncthreads();
+    if (s_skip) return false;
+    *conv = s_rec[kCandConv] != 0.0f;
+    if (blockIdx.x == 0 && tid == 0) {
+        if (it < LO_MAX_ITERS) {                  // the loop-closure ICP runs up to 100
+            lo_iter_log& L = st->logs[it];
+#pragma unroll
+            for (int q = 0; q < 12; ++q) L.pose[q] = s_rec[q];
+            L.n_corr = st->n_corr;
+            L.scale = st->scale;
+            L.alpha = s_alpha;
+            L.cost = s_rec[kCandCost];
+#pragma unroll
+            for (int q = 0; q < 21; ++q) L.H[q] = s_rec[kCandH + q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) { L.g[q] = s_rec[kCandG + q]; L.delta[q] = s_rec[kCandD + q]; }
+        }
+#pragma unroll
+        for (int q = 0; q < 12; ++q) st->pose[q] = s_rec[q];
+        st->alpha = s_alpha;
+        st->iter = it + 1;
+        if (*conv) st->done = 1;
+        if (*conv || it + 1 >= P.max_iters) publish_final(P);   // the scan's result is final (scan pipeline)
+    }
+    return true;
+}
+
 }  // namespace lo

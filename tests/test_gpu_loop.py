@@ -136,8 +136,22 @@ def exact_icp():
 def test_loop_icp_exact_bitwise(exact_icp, fa, fb, seed):
     """Reference-exact mode (lo_set_exact): the loop ICP's every GN iteration bit-identical to the oracle (the same
     sequential fp32 normal equations, sorted-order scale, fp32 LDLT and SVD re-projection as the odometry ICP,
-    tests/test_gpu_exact.py), hence the same iteration count, T_rel and inlier count -- no alpha-flip allowance."""
+    tests/test_gpu_exact.py), hence the same iteration count, T_rel and inlier count -- no alpha-flip allowance.
+    These keyframe clouds (~3.7k points) take the all-pairs LDS search (k_knn_all, k_pick_knn_all, k_inlier_all)."""
     cur, Tc, mat, Tm, _ = _data.loop_case(fa, fb, seed)
+    _exact_loop_bitwise(exact_icp, cur, Tc, mat, Tm)
+
+
+def test_loop_icp_exact_bitwise_grid_path(exact_icp):
+    """A matched keyframe cloud beyond kKnnAllMax (8192) points: the cell grid (with the loop's adaptive cell edge),
+    the shell search and the wave-per-query brute-force pass instead of the all-pairs search -- still bit-identical."""
+    cur, Tc, _, Tm, _ = _data.loop_case(4, 7, 3)
+    mat = oracle.voxel_filter(_data.kitti_scan(4, 40), 0.3, 1)          # 11.6k points
+    assert len(mat) > 8192
+    _exact_loop_bitwise(exact_icp, cur, Tc, mat, Tm)
+
+
+def _exact_loop_bitwise(exact_icp, cur, Tc, mat, Tm):
     ok_o, conv_o, Tr_o, inl_o, it_o, logs_o = oracle.icp_optimize_loop(cur, Tc, mat, Tm)
     ok_g, Tr_g, inl_g = exact_icp.optimize_loop(cur, Tc, mat, Tm)
     st = exact_icp.get_last_stats()
