@@ -1255,15 +1255,16 @@ static int grid_build(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, bool 
 }
 
 // A small point set (<= kKnnAllMax) for the all-pairs kernels (k_knn_all, k_inlier_all): the points in index order as
-// float4 (x, y, z, index), one pinned staging copy, no cells and no visit order.
-static int all_pairs_upload(lo_ctx* c, PointGrid& G, const float* xyz, size_t m) {
+// float4 (x, y, z, index), no cells and no visit order; with q (nq points) also the query cloud into c->d_pts, both
+// through the grid's pinned staging buffer (two async copies, no pageable-memory copy).
+static int all_pairs_upload(lo_ctx* c, PointGrid& G, const float* xyz, size_t m, const float* q = nullptr, size_t nq = 0) {
     if (m > static_cast<size_t>(kKnnAllMax)) { c->err = "all_pairs_upload: too many points"; return LO_ERR_CAPACITY; }
     if (m > 0 && !xyz) { c->err = "null points"; return LO_ERR_ARG; }
     for (size_t i = 0; i < 3 * m; ++i)
         if (!std::isfinite(xyz[i])) { c->err = "non-finite map point"; return LO_ERR_ARG; }
     LO_HIP(c, hipSetDevice(c->device));
     LO_HIP(c, hipStreamSynchronize(c->stream));          // the staging buffer's previous copy has retired
-    const size_t mm = std::max<size_t>(m, 1), bytes = mm * sizeof(float4);
+    const size_t mm = std::max<size_t>(m, 1), bytes = mm * sizeof(float4) + nq * 3 * sizeof(float);
     if (mm > G.pts_cap) {
         if (G.d_pts) LO_HIP(c, hipFree(G.d_pts));
         G.d_pts = nullptr;
@@ -1285,6 +1286,11 @@ static int all_pairs_upload(lo_ctx* c, PointGrid& G, const float* xyz, size_t m)
         hs[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], w);
     }
     if (m > 0) LO_HIP(c, hipMemcpyAsync(G.d_pts, hs, m * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    if (nq > 0) {
+        float* hq = reinterpret_cast<float*>(hs + mm);
+        std::memcpy(hq, q, nq * 3 * sizeof(float));
+        LO_HIP(c, hipMemcpyAsync(c->d_pts, hq, nq * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    }
     G.m = static_cast<int>(m);
     G.has_order = false;
     G.all = true;
@@ -1881,14 +1887,15 @@ int lo_icp_optimize_loop(lo_ctx* c, const float* curr, size_t n_curr, const floa
     // it only ranks exact distance ties that decide a query's five neighbours or their order, which keyframe
     // centroids rarely produce); a solve that met one is rerun with the order below
     bool with_order = false;
-    rc = n_matched <= static_cast<size_t>(kKnnAllMax) ? all_pairs_upload(c, c->lgrid, lmap.data(), n_matched)
-                                                      : grid_build(c, c->lgrid, lmap.data(), n_matched, with_order, kLoopMinPerCell);
+    const bool all = n_matched <= static_cast<size_t>(kKnnAllMax);     // (the clouds' pinned upload, curr included)
+    rc = all ? all_pairs_upload(c, c->lgrid, lmap.data(), n_matched, curr, n_curr)
+             : grid_build(c, c->lgrid, lmap.data(), n_matched, with_order, kLoopMinPerCell);
     if (rc != LO_OK) return rc;
 retry:
     if (st) { std::memset(st, 0, sizeof(*st)); st->status = LO_INSUFFICIENT; }
     if (n_curr == 0 || n_matched == 0) return LO_INSUFFICIENT;       // empty clouds: 0 correspondences (:477-483)
     if ((rc = ensure_acc_part(c)) != LO_OK) return rc;
-    LO_HIP(c, hipMemcpyAsync(c->d_pts, curr, n_curr * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (!c->lgrid.all) LO_HIP(c, hipMemcpyAsync(c->d_pts, curr, n_curr * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     KParams P = make_params(c, c->d_pts, static_cast<int>(n_curr));
     set_kd_params(c, P, c->lgrid);
     P.loop = 1;

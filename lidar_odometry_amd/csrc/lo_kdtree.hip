@@ -493,7 +493,10 @@ __device__ __forceinline__ float wave_min(float f) {
     return fminf(f, __shfl_xor(f, 32, 64));
 }
 
-__device__ __forceinline__ void knn_all_body(const KParams& P, const float (&T)[12], const float4* s_map) {
+// seed (GN iterations after the first): the query's five neighbours of the previous iteration are five points of the
+// set, so the largest of their distances at the new pose bounds the fifth distance from above -- thr starts there and
+// only the few points within it reach the insert (without a seed, thr is the wave's smallest fifth distance so far).
+__device__ __forceinline__ void knn_all_body(const KParams& P, const float (&T)[12], const float4* s_map, bool seed) {
     const int i = blockIdx.x * (kAllThreads / kWave) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (i >= scan_n(P)) return;                              // whole waves leave together
     int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
@@ -508,6 +511,44 @@ __device__ __forceinline__ void knn_all_body(const KParams& P, const float (&T)[
     // set's own fifth distance is <= thr, and a point farther than thr can neither be one of the five nor tie with
     // the fifth: only points within thr reach the (branchy) insert, the rest cost a distance and a compare
     float thr = __builtin_inff();
+    if (seed) {
+        const int32_t* prev = P.kd_nbr + 5 * static_cast<size_t>(i);     // read before lane 0 rewrites it below
+        int pv[5];
+        bool ok = true;                                      // five distinct points of the set (else no seed)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            pv[k] = prev[k];
+            ok = ok && pv[k] >= 0 && pv[k] < P.kd_m;
+        }
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = a + 1; b < 5; ++b) ok = ok && pv[a] != pv[b];
+        if (ok) {
+            float s5 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) s5 = fmaxf(s5, l2sq(qx, qy, qz, s_map[pv[k]]));
+            thr = s5;
+        }
+    }
+    if (!(thr < __builtin_inff())) {
+        // no seed: a first pass takes each lane's nearest point; the fifth smallest of the 64 lane minima is the
+        // distance of five distinct points of the set, so it bounds the fifth distance from above (and equals it
+        // whenever the five nearest fall in five different lanes)
+        float mn = __builtin_inff();
+        for (int p0 = lane; p0 < mp; p0 += kAllBatch) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = s_map[p0 + u * kWave];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) mn = fminf(mn, l2sq(qx, qy, qz, v[u]));
+        }
+        for (int r = 0; r < 5; ++r) {                        // remove the wave minimum five times
+            thr = wave_min(mn);
+            const uint64_t b = __ballot(mn == thr);
+            if (b && lane == __builtin_ctzll(b)) mn = __builtin_inff();
+        }
+    }
     for (int p0 = lane; p0 < mp; p0 += kAllBatch) {
         float4 v[8];
 #pragma unroll
@@ -515,14 +556,21 @@ __device__ __forceinline__ void knn_all_body(const KParams& P, const float (&T)[
         float d[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) d[u] = l2sq(qx, qy, qz, v[u]);
+#if defined(LO_ALL_EXP) && LO_ALL_EXP == 1                 // diagnostic (scripts/knn_microbench): no inserts
+        if (p0 == lane) for (int u = 0; u < 5; ++u) top5_insert<false>(Q, t, d[u], p0 + u * kWave, p0 + u * kWave);
+        thr = fminf(thr, d[7]);
+#else
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (d[u] <= thr) top5_insert<false>(Q, t, d[u], p0 + u * kWave, p0 + u * kWave);
-        thr = wave_min(t.n == 5 ? t.d[4] : __builtin_inff());
+        thr = fminf(thr, wave_min(t.n == 5 ? t.d[4] : __builtin_inff()));
+#endif
     }
+#if !(defined(LO_ALL_EXP) && LO_ALL_EXP == 2)                // diagnostic: no merges
     t = group_merge<false>(Q, t);                            // 16-lane rows
     top5_merge_xor<false>(Q, t, 16);
     top5_merge_xor<false>(Q, t, 32);                         // the wave's five
+#endif
     if (lane != 0) return;
     if ((t.n == 5 && t.tie <= t.d[4]) || (t.n < 5 && t.tie < __builtin_inff())) { out[0] = -3; return; }
     if (t.n < 5) { out[0] = -1; return; }
@@ -536,7 +584,7 @@ __global__ __launch_bounds__(kAllThreads) void k_knn_all(KParams P) {
     float T[12];
     scan_pose(P, P.init, blockIdx.x, T);
     stage_all(P, s_map);
-    knn_all_body(P, T, s_map);
+    knn_all_body(P, T, s_map, !P.init);
 }
 
 // k_pick_knn over a small set
@@ -549,7 +597,7 @@ __global__ __launch_bounds__(kAllThreads) void k_pick_knn_all(KParams P, int it)
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
     stage_all(P, s_map);
-    knn_all_body(P, T, s_map);
+    knn_all_body(P, T, s_map, true);
 }
 
 // k_inlier over a small set, a wave per point: its lanes take every 64th point until one lies within 1 m (an existence

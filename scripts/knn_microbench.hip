@@ -80,6 +80,9 @@ int main() {
                     t_knn, t_in);
     };
     run("full", P);
+    KParams Pi = P;
+    Pi.init = 1;                                          // the scan's first search: no seed
+    run("first search (no seed)", Pi);
     KParams P0 = P;
     P0.n = 0;
     run("no queries (staging only)", P0);
