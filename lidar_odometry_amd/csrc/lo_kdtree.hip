@@ -151,21 +151,48 @@ __device__ __forceinline__ Top5 group_merge(const KnnQ& Q, const Top5& own) {
 // k_knn: grid shells.  kd_nbr[5i] = positions of the 5-NN, -1 = fewer than 5 (rejected), -2 = unresolved
 // ====================================================================================================
 // One candidate range of the kd_pts array (a run of cells of one grid row), scanned with 8 loads in flight.
+// thr: an upper bound on the query's fifth distance (seed_bound), or +inf: a point farther than it can neither be one
+// of the five nor tie with the fifth, so it skips the insert.
 __device__ __forceinline__ void scan_range8(const KParams& P, const KnnQ& Q, uint32_t s, uint32_t e, float qx, float qy,
-                                            float qz, Top5& t) {
+                                            float qz, float thr, Top5& t) {
     for (uint32_t p = s; p < e; p += 8) {
         float4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = (p + u < e) ? P.kd_pts[p + u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (p + u < e) top5_insert<false>(Q, t, l2sq(qx, qy, qz, v[u]), __float_as_int(v[u].w), static_cast<int>(p + u));
+        for (int u = 0; u < 8; ++u) {
+            const float d = l2sq(qx, qy, qz, v[u]);
+            if (p + u < e && d <= thr) top5_insert<false>(Q, t, d, __float_as_int(v[u].w), static_cast<int>(p + u));
+        }
     }
+}
+
+// The query's five neighbours of the previous GN iteration (kd_nbr, positions into kd_pts) are five distinct points
+// of the set, so the largest of their distances at the new pose bounds the fifth distance from above.  Any five
+// distinct positions would do (a stale record of an earlier call too); anything else gives +inf (no bound).
+__device__ __forceinline__ float seed_bound(const KParams& P, int i, float qx, float qy, float qz) {
+    const int32_t* prev = P.kd_nbr + 5 * static_cast<size_t>(i);
+    int pv[5];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        pv[k] = prev[k];
+        ok = ok && pv[k] >= 0 && pv[k] < P.kd_m;
+    }
+#pragma unroll
+    for (int a = 0; a < 5; ++a)
+#pragma unroll
+        for (int b = a + 1; b < 5; ++b) ok = ok && pv[a] != pv[b];
+    if (!ok) return __builtin_inff();
+    float s5 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s5 = fmaxf(s5, l2sq(qx, qy, qz, P.kd_pts[pv[k]]));
+    return s5;
 }
 
 constexpr int kKnnRowsMax = 4;          // rows of one round per lane: r = 3 has 49 rows over 16 lanes
 
-__device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12]) {
+__device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12], bool seed) {
     // kKnnGroup consecutive lanes (one DPP row) share one query: lane g takes rows g, g + 16, ... of each round.
     // The first round scans the whole 3x3x3 cube (the r = 0 cell alone almost never certifies: its faces are
     // < h / 2 away while the 5th neighbour of a surface sample is ~h); later rounds scan the shell r.  A lane's
@@ -188,6 +215,7 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
     const int ox = P.kd_org[0], oy = P.kd_org[1], oz = P.kd_org[2];
     const double q[3] = {qx, qy, qz};
     const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
+    const float thr = seed ? seed_bound(P, i, qx, qy, qz) : __builtin_inff();   // read before g == 0 rewrites it
     Top5 own, grp;
     top5_init(own);
     bool done = false;
@@ -216,7 +244,7 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12])
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, Q, rs[j], re[j], qx, qy, qz, own);
+            for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, Q, rs[j], re[j], qx, qy, qz, thr, own);
         }
         grp = group_merge<false>(Q, own);
         // every unscanned centroid lies outside the cube of cells [c - r, c + r]
@@ -252,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_knn(KParams P) {
     if (!P.init && P.st->done) return;
     float T[12];
     scan_pose(P, P.init, blockIdx.x, T);
-    knn_body(P, T);
+    knn_body(P, T, !P.init);
 }
 
 // The solve of GN iteration it fused with the kNN search of iteration it + 1 (small scans with PKO; the
@@ -287,7 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_solve_knn(KParams P, int it) {
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_T[k];
-    knn_body(P, T);
+    knn_body(P, T, true);
 }
 
 // The KDTree counterpart of k_pick_correspond (reference-exact mode): the record of the candidate the PKO launch
@@ -300,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void k_pick_knn(KParams P, int it) {
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = s_rec[k];
-    knn_body(P, T);
+    knn_body(P, T, true);
 }
 
 // ====================================================================================================

@@ -137,6 +137,24 @@ def test_batch_exact_jobs_bitwise_vs_single(pko_mode):
             o.close()
 
 
+def test_batch_only_exact_in_fresh_process():
+    """A process whose first exact work is a batch: exact jobs of 4096 < n <= 8192 points launch
+    k_exact_scale_cb with 80 KB of dynamic LDS, whose attribute batch_alloc now sets itself (before, only a single
+    exact optimize did, and in one pytest process an earlier test always had).  Every job equals its context's own
+    exact lo_icp_optimize bit for bit (tests/_batch_child.py, a child process so no earlier test has run)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = os.path.join(root, "tests", "_batch_child.py")
+    r = subprocess.run(["timeout", "-k", "10", "110", sys.executable, child], cwd=root, capture_output=True, text=True)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert all(4096 < n <= 8192 for n in out["n"]), out
+    assert all(out["equal"]), out
+
+
 def test_batch_follows_update_config():
     """lo_update_config on a context that belongs to a batch (IterativeClosestPointOptimizer::update_config): the next
     batch uses the new parameters -- a new alpha grid (the PKO tables and candidate buffers are re-made) and a new
