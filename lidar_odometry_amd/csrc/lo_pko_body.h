@@ -25,6 +25,8 @@
 #include "lo_solve.h"
 #include "lo_exact.h"
 
+#include <type_traits>
+
 #include <cfloat>
 
 namespace lo {
@@ -313,14 +315,19 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
     for (int q = 0; q < K; ++q)
 #pragma unroll
         for (int s = 0; s < SPL; ++s) pv[q][s] = s_p[q * kStride + 64 * s + lane];
-    int buf = 0;
     int n_em = 100;
 #if defined(LO_XC_EXP) && LO_XC_EXP == 3
     constexpr int kEmMax = 1;                              // diagnostic: one EM iteration (the launch without its EM)
 #else
     constexpr int kEmMax = 100;
 #endif
-    for (int em = 0; em < kEmMax; ++em) {
+    // One EM iteration with the double buffer's half as a compile-time constant (the loop below runs them in pairs):
+    // the next pdfs' LDS reads then sit at immediate offsets from one lane base (ds_read2st64_b64 pairs) instead of
+    // per-read address arithmetic on a runtime buffer index -- that arithmetic, and the split reads it brought, were
+    // the EM's 1092 -> 1152-cycle drift between rounds 3 and 5 (scripts/pko_em_isa.py, same source, different
+    // codegen).  Returns true when the change test ends the EM.
+    auto em_step = [&](auto bc, int em) -> bool {
+        constexpr int buf = decltype(bc)::value;
         double v[3] = {0.0, 0.0, 0.0};                     // N_j | sum r x | sum r d^2
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
@@ -374,8 +381,12 @@ __device__ __forceinline__ void gmm_fit_split(const double* s_sd, int S, const i
 #pragma unroll
         for (int q = 1; q < K; ++q) change += dmv[q];
         LO_COUNT(dbg, 8, em + 1);
-        if (change < 1e-6) { n_em = em + 1; break; }
-        buf ^= 1;
+        if (change < 1e-6) { n_em = em + 1; return true; }
+        return false;
+    };
+    for (int em = 0; em < kEmMax; em += 2) {
+        if (em_step(std::integral_constant<int, 0>{}, em)) break;
+        if (em + 1 >= kEmMax || em_step(std::integral_constant<int, 1>{}, em + 1)) break;
     }
     LO_STAMP(dbg, 5);
     if (emst && threadIdx.x == 0) {                        // wave 0 (component 0): the loop's own clock
