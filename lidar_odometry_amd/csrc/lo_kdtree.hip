@@ -53,7 +53,7 @@ struct KnnQ {
 // nanoflann visits original index a before b (both in the tree): descend while both vAcc_ positions fall on the
 // same side of a node's split; the node that separates them is entered on the query's side first
 // (searchLevel: (q - divlow) + (q - divhigh) < 0 -> child1, fp32 as nanoflann); one leaf: vAcc_ order.
-__device__ __noinline__ bool kd_visit_before(const KnnQ& Q, int a, int b) {
+__device__ __forceinline__ bool kd_visit_before(const KnnQ& Q, int a, int b) {
     const uint32_t pa = Q.vpos[a], pb = Q.vpos[b];
     int ni = 0;
     for (int depth = 0; depth < 64; ++depth) {
@@ -215,34 +215,38 @@ __device__ __forceinline__ void knn_body(const KParams& P, const float (&T)[12],
     const int ox = P.kd_org[0], oy = P.kd_org[1], oz = P.kd_org[2];
     const double q[3] = {qx, qy, qz};
     const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
+    // this lane's rows of round r from j0 on (kKnnRowsMax of them): their range bounds (up to 2 per row: a full row,
+    // or the shell's two end cells), loaded together
+    auto ranges = [&](int r, int j0, uint32_t (&rs)[2 * kKnnRowsMax], uint32_t (&re)[2 * kKnnRowsMax]) {
+        const int side = 2 * r + 1;
+#pragma unroll
+        for (int j = 0; j < kKnnRowsMax; ++j) {
+            rs[2 * j] = re[2 * j] = rs[2 * j + 1] = re[2 * j + 1] = 0;
+            const int k = j0 + g + j * kKnnGroup;
+            if (k >= side * side) continue;
+            const int dz = k / side - r, dy = k % side - r;
+            const int z = c[2] + dz - oz, y = c[1] + dy - oy;
+            if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
+            const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
+            if (r == 1 || dz == -r || dz == r || dy == -r || dy == r) {        // whole row of the cube / shell
+                const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
+                if (x0 <= x1) { rs[2 * j] = P.kd_start[row + x0]; re[2 * j] = P.kd_start[row + x1 + 1]; }
+            } else {                                                            // the two end cells
+                const int xa = c[0] - r - ox, xb = c[0] + r - ox;
+                if (xa >= 0 && xa < dimx) { rs[2 * j] = P.kd_start[row + xa]; re[2 * j] = P.kd_start[row + xa + 1]; }
+                if (xb >= 0 && xb < dimx) { rs[2 * j + 1] = P.kd_start[row + xb]; re[2 * j + 1] = P.kd_start[row + xb + 1]; }
+            }
+        }
+    };
     const float thr = seed ? seed_bound(P, i, qx, qy, qz) : __builtin_inff();   // read before g == 0 rewrites it
     Top5 own, grp;
     top5_init(own);
     bool done = false;
     for (int r = 1; r <= kKnnRMax && !done; ++r) {
         const int side = 2 * r + 1;
-        // this lane's rows of the round in chunks of kKnnRowsMax: the chunk's range bounds (up to 2 per row: a
-        // full row, or the shell's two end cells) are loaded together, then scanned
         for (int j0 = 0; j0 < side * side; j0 += kKnnRowsMax * kKnnGroup) {
             uint32_t rs[2 * kKnnRowsMax], re[2 * kKnnRowsMax];
-#pragma unroll
-            for (int j = 0; j < kKnnRowsMax; ++j) {
-                rs[2 * j] = re[2 * j] = rs[2 * j + 1] = re[2 * j + 1] = 0;
-                const int k = j0 + g + j * kKnnGroup;
-                if (k >= side * side) continue;
-                const int dz = k / side - r, dy = k % side - r;
-                const int z = c[2] + dz - oz, y = c[1] + dy - oy;
-                if (z < 0 || z >= dimz || y < 0 || y >= dimy) continue;
-                const size_t row = (static_cast<size_t>(z) * dimy + y) * dimx;
-                if (r == 1 || dz == -r || dz == r || dy == -r || dy == r) {        // whole row of the cube / shell
-                    const int x0 = max(c[0] - r - ox, 0), x1 = min(c[0] + r - ox, dimx - 1);
-                    if (x0 <= x1) { rs[2 * j] = P.kd_start[row + x0]; re[2 * j] = P.kd_start[row + x1 + 1]; }
-                } else {                                                            // the two end cells
-                    const int xa = c[0] - r - ox, xb = c[0] + r - ox;
-                    if (xa >= 0 && xa < dimx) { rs[2 * j] = P.kd_start[row + xa]; re[2 * j] = P.kd_start[row + xa + 1]; }
-                    if (xb >= 0 && xb < dimx) { rs[2 * j + 1] = P.kd_start[row + xb]; re[2 * j + 1] = P.kd_start[row + xb + 1]; }
-                }
-            }
+            ranges(r, j0, rs, re);
 #pragma unroll
             for (int j = 0; j < 2 * kKnnRowsMax; ++j) scan_range8(P, Q, rs[j], re[j], qx, qy, qz, thr, own);
         }
@@ -401,6 +405,43 @@ __device__ __forceinline__ Top5 brute_query(const KParams& P, const KnnQ& Q, flo
     return a;
 }
 
+// A deciding tie met by the fast order (a.n == 5, a.tie <= a.d[4]): the five in nanoflann's order.  The fifth distance
+// d5 does not depend on how ties are ranked, so the five are among the points within d5; the workgroup lists them in
+// LDS and one lane ranks them by (distance, visit order) -- the only place the visit-order walk is inlined, so the
+// kernel needs no call frame (no scratch memory: an empty launch costs what any empty launch costs).  A list longer
+// than kExCap (points equidistant by the thousand) is ranked by that lane over the whole set instead.
+constexpr int kExCap = 1024;
+__device__ __forceinline__ Top5 brute_query_ex(const KParams& P, const KnnQ& Q, float d5, float (&s_ed)[kExCap],
+                                               int (&s_ei)[kExCap], int (&s_ep)[kExCap], int& s_en) {
+    const int tid = threadIdx.x;
+    if (tid == 0) s_en = 0;
+    __syncthreads();
+    for (int p = tid; p < P.kd_m; p += kBruteThreads) {
+        const float4 v = P.kd_pts[p];
+        const float d = l2sq(Q.q[0], Q.q[1], Q.q[2], v);
+        if (d <= d5) {
+            const int k = atomicAdd(&s_en, 1);
+            if (k < kExCap) { s_ed[k] = d; s_ei[k] = __float_as_int(v.w); s_ep[k] = p; }
+        }
+    }
+    __syncthreads();
+    Top5 t;
+    top5_init(t);
+    if (tid == 0) {
+        const int ne = s_en;
+        if (ne <= kExCap) {
+            for (int k = 0; k < ne; ++k) top5_insert<true>(Q, t, s_ed[k], s_ei[k], s_ep[k]);
+        } else {
+            for (int p = 0; p < P.kd_m; ++p) {
+                const float4 v = P.kd_pts[p];
+                top5_insert<true>(Q, t, l2sq(Q.q[0], Q.q[1], Q.q[2], v), __float_as_int(v.w), p);
+            }
+        }
+    }
+    __syncthreads();
+    return t;
+}
+
 __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     DevState* st = P.st;
     if (st->done) return;
@@ -412,7 +453,10 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
     __shared__ int s_pos[kW][5];
     __shared__ int s_n[kW];
     __shared__ float s_tie[kW];
-    __shared__ int s_redo;
+    __shared__ int s_redo, s_five;
+    __shared__ float s_d5;
+    __shared__ float s_ed[kExCap];
+    __shared__ int s_ei[kExCap], s_ep[kExCap], s_en;
     const int tid = threadIdx.x;
     float T[12];
 #pragma unroll
@@ -423,13 +467,22 @@ __global__ __launch_bounds__(kBruteThreads) void k_knn_brute(KParams P) {
         transform_pt(T, P.pts[3 * i], P.pts[3 * i + 1], P.pts[3 * i + 2], qx, qy, qz);
         const KnnQ Q{{qx, qy, qz}, P.kd_vpos, P.kd_nodes};
         Top5 a = brute_query<false>(P, Q, s_d, s_id, s_pos, s_n, s_tie);
-        if (tid == 0) s_redo = (a.n == 5 && a.tie <= a.d[4]) || (a.n < 5 && a.tie < __builtin_inff());
+        if (tid == 0) {                                    // (a is thread 0's: the workgroup's five)
+            s_redo = (a.n == 5 && a.tie <= a.d[4]) || (a.n < 5 && a.tie < __builtin_inff());
+            s_five = a.n == 5;
+            s_d5 = a.d[4];
+        }
         __syncthreads();
-        const bool redo = s_redo != 0;
+        const bool redo = s_redo != 0, five = s_five != 0;
+        const float d5 = s_d5;
         __syncthreads();
         if (redo) {                                        // a deciding tie: nanoflann's visit order ranks it
-            if (P.kd_nodes) a = brute_query<true>(P, Q, s_d, s_id, s_pos, s_n, s_tie);
-            else if (tid == 0) atomicOr(&st->kd_tie, 1u);  // no visit order built: the host reruns with it
+            if (P.kd_nodes) {
+                // fewer than five: no five to rank (the answer is -1 whatever the order)
+                if (five) a = brute_query_ex(P, Q, d5, s_ed, s_ei, s_ep, s_en);   // uniform: every thread calls
+            } else if (tid == 0) {
+                atomicOr(&st->kd_tie, 1u);                 // no visit order built: the host reruns with it
+            }
         }
         if (tid == 0) {
             int32_t* out = P.kd_nbr + 5 * static_cast<size_t>(i);
