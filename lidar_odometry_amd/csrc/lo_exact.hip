@@ -551,7 +551,8 @@ static hipError_t scale_c_attr() {
 hipError_t exact_scale_c_prepare() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_exact_scale_cd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        static_cast<int>(std::max(kScaleWideLds, scale_c_lds<8>())));
-    for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<4>(), scale_c_attr<8>(), scale_c_attr<16>()})
+    for (hipError_t r : {scale_c_attr<1>(), scale_c_attr<2>(), scale_c_attr<3>(), scale_c_attr<4>(), scale_c_attr<5>(),
+                         scale_c_attr<6>(), scale_c_attr<8>(), scale_c_attr<16>()})
         if (e == hipSuccess) e = r;
     return e;
 }
@@ -560,7 +561,10 @@ void launch_exact_scale_cb(const KParams* PB, int njobs, int n_max, hipStream_t 
     const dim3 g(njobs), b(kScaleC);
     if (n_max <= kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<1>, g, b, scale_c_lds<1>(), s, PB);
     else if (n_max <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<2>, g, b, scale_c_lds<2>(), s, PB);
+    else if (n_max <= 3 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<3>, g, b, scale_c_lds<3>(), s, PB);
     else if (n_max <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<4>, g, b, scale_c_lds<4>(), s, PB);
+    else if (n_max <= 5 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<5>, g, b, scale_c_lds<5>(), s, PB);
+    else if (n_max <= 6 * kScaleC) hipLaunchKernelGGL(k_exact_scale_cb<6>, g, b, scale_c_lds<6>(), s, PB);
     else hipLaunchKernelGGL(k_exact_scale_cb<8>, g, b, scale_c_lds<8>(), s, PB);
 }
 // P.n <= kExactScaleCMax; a device-counted scan (P.n_dev) chooses its width from the count on the device
@@ -570,7 +574,12 @@ void launch_exact_scale_c(const KParams& P, hipStream_t s) {
         hipLaunchKernelGGL(k_exact_scale_cd, dim3(1), dim3(kScaleC), lds, s, P);
     } else if (P.n <= kScaleC) hipLaunchKernelGGL(k_exact_scale_c<1>, dim3(1), dim3(kScaleC), scale_c_lds<1>(), s, P);
     else if (P.n <= 2 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<2>, dim3(1), dim3(kScaleC), scale_c_lds<2>(), s, P);
+    // keys per thread = ceil(n / 1024) up to 6 (the kernel's time grows with the width: KITTI scans of 4-5k points
+    // took the 8-wide sort at 33 us against 22 us for the 4-wide one)
+    else if (P.n <= 3 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<3>, dim3(1), dim3(kScaleC), scale_c_lds<3>(), s, P);
     else if (P.n <= 4 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<4>, dim3(1), dim3(kScaleC), scale_c_lds<4>(), s, P);
+    else if (P.n <= 5 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<5>, dim3(1), dim3(kScaleC), scale_c_lds<5>(), s, P);
+    else if (P.n <= 6 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<6>, dim3(1), dim3(kScaleC), scale_c_lds<6>(), s, P);
     else if (P.n <= 8 * kScaleC) hipLaunchKernelGGL(k_exact_scale_c<8>, dim3(1), dim3(kScaleC), scale_c_lds<8>(), s, P);
     else hipLaunchKernelGGL(k_exact_scale_c<16>, dim3(1), dim3(kScaleC), scale_c_lds<16>(), s, P);
 }

@@ -187,6 +187,22 @@ def test_exact_raw_scan_beyond_8192_filtered_points(exact):
     assert _scale_width(exact) == 16384
 
 
+@pytest.mark.parametrize("extra,width", [(-800, 3072), (1000, 5120), (2200, 6144)])
+def test_exact_scale_widths_between_powers_of_two(exact, extra, width):
+    """The one-workgroup scale sorts ceil(n / 1024) keys per thread (r06: widths 3, 5 and 6 beside 1, 2, 4, 8, 16):
+    scans of ~2.9k, ~4.7k and ~5.9k points run the 3072-, 5120- and 6144-wide sorts, every iteration bit-identical."""
+    m, pts, Ti, _ = _data.kitti_case(11)
+    k, n, c = _data.surfels(m)
+    exact.set_surfels(k, n, c)
+    if extra < 0:
+        p = pts[: len(pts) + extra]
+    else:
+        p = np.concatenate([pts, pts[:extra] + np.float32(0.013)]).astype(np.float32)
+    assert width - 1024 < len(p) <= width
+    _bitwise(exact, m, p, Ti)
+    assert _scale_width(exact) == width
+
+
 @pytest.mark.parametrize("n_points", [12_000])
 def test_exact_mid_size_scan_both_sort_paths(exact, monkeypatch, n_points):
     """8192 < n <= 16384 host-counted: the one-workgroup counting sort at width 16384 (default) and the chip-wide rank
