@@ -527,7 +527,10 @@ __global__ __launch_bounds__(kScaleC) void k_exact_scale_cd(KParams P) {
     const int n = min(scan_n(P), P.n);                       // the count never exceeds the bound the grid was sized for
     if (n <= kScaleC) exact_scale_c_body<1>(P, n, s_dyn, S, s_ks);
     else if (n <= 2 * kScaleC) exact_scale_c_body<2>(P, n, s_dyn, S, s_ks);
+    else if (n <= 3 * kScaleC) exact_scale_c_body<3>(P, n, s_dyn, S, s_ks);
     else if (n <= 4 * kScaleC) exact_scale_c_body<4>(P, n, s_dyn, S, s_ks);
+    else if (n <= 5 * kScaleC) exact_scale_c_body<5>(P, n, s_dyn, S, s_ks);
+    else if (n <= 6 * kScaleC) exact_scale_c_body<6>(P, n, s_dyn, S, s_ks);
     else if (n <= 8 * kScaleC) exact_scale_c_body<8>(P, n, s_dyn, S, s_ks);
     else exact_scale_c_wide(P, n, s_dyn, S, s_ks);
 }
