@@ -33,7 +33,7 @@ D = IterativeClosestPointOptimizer(max_points=1 << 16)
 E = IterativeClosestPointOptimizer(max_points=1 << 16)
 F = IterativeClosestPointOptimizer(max_points=1 << 16)
 t_upd, t_full, t_patch, kinds, t_dev, t_ref, sent = [], [], [], [], [], [], []
-t_key, sent_key, t_key_host = [], [], []
+t_key, sent_key, t_key_host, t_key_list = [], [], [], []
 patched = C.c_int(0)
 for k in range(0, n + 1, 2):
     T = seq.poses[k]
@@ -59,15 +59,19 @@ for k in range(0, n + 1, 2):
     # the adapter's keyed sync_map(vm, changed): only the keys the update changed (the reference hook's list),
     # GetSurfelAtPoint at each key's centre, lo_map_patch_surfels (C++ in the adapter; the Python mirror here)
     t8 = time.perf_counter()
+    t8a = t8
     if k == 0:
         F.set_surfels(keys, normals, cents)
     else:
-        sent_key.append(F.sync_changed(vm, vm.changed_l1()))
+        ch = vm.changed_l1()                     # the hook's key list (a ctypes call + array here; a vector in C++)
+        t8a = time.perf_counter()
+        sent_key.append(F.sync_changed(vm, ch))
     t8b = time.perf_counter()                    # host work only: the patch is queued on the context stream
     lib().lo_sync(F.ctx)
     t9 = time.perf_counter()
     t_key.append(t9 - t8)
     t_key_host.append(t8b - t8)
+    t_key_list.append(t8a - t8)
     t_upd.append(t1 - t0); t_full.append(t2 - t1); t_patch.append(t3 - t2); kinds.append(patched.value)
     t_dev.append(t5 - t4)
     t_ref.append(t7 - t6)
@@ -81,7 +85,8 @@ print(f"keyframes {len(t_upd)}, surfels {vm.surfel_count()}, L0 {vm.l0_count()}:
       f"surfel set {ms(t_ref):.3f} ms, {np.mean([x for x in sent[h:] if x >= 0]):.0f} records sent per keyframe "
       f"(full uploads in the second half: {sum(x < 0 for x in sent[h:])}); keyed sync of the changed keys "
       f"{ms(t_key):.3f} ms incl. the stream sync, {ms(t_key_host):.3f} ms of host work (the patch queued on the "
-      f"stream), {np.mean([x for x in sent_key[h:] if x >= 0]):.0f} keys per keyframe (full uploads in the second "
+      f"stream; of it {ms(t_key_list):.3f} ms fetching the key list, {ms(t_key_host) - ms(t_key_list):.3f} ms the "
+      f"lookups + patch), {np.mean([x for x in sent_key[h:] if x >= 0]):.0f} keys per keyframe (full uploads in the second "
       f"half: {sum(x < 0 for x in sent_key[h:])})")
 assert F.surfel_count() == vm.surfel_count()
 assert vd.surfel_count() == vm.surfel_count()
