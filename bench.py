@@ -1028,7 +1028,7 @@ def main():
             else:                                     # RCCL on the side stream, off the critical path
                 L.lo_icp_export_pose(icp.ctx, C.c_void_p(gather.slot().data_ptr()))
             gather.launch()
-        if rec_log is not None:
+        if rec_log is not None and n_step[0] < rec_log.shape[0]:      # the warmup + timed steps (later passes: no log)
             L.lo_icp_export_pose(icp.ctx, C.c_void_p(rec_log[n_step[0]].data_ptr()))
         n_step[0] += 1
 
