@@ -704,7 +704,35 @@ __device__ void acc_candidate(const KParams& P, double scale, int wgi) {
 // staged row as fa * fb (the same fp32 product build_ne forms) and adds it to its running sum, one rounding per
 // addition, a chunk behind the producers (double-buffered, one barrier per chunk).  A zero pad row adds +0, which
 // leaves a running sum unchanged: the sums start at +0 and never become -0 (x + -x rounds to +0).  The consumer's loop
-// is uniform (no per-row test) with the next 16 rows' reads issued before the current 16 adds.
+// is uniform (no per-row test), three groups of 16 rows in flight (xc_add_mul).
+// The consumer's stages: XcRows = 16 staged rows of a lane's two factors, XcProd = their 16 fp32 products (each the
+// same separately rounded a * b; v_pk_mul_f32 rounds each half on its own).  xc_add_mul adds a group's products in row
+// order and places one packed product of the next group between every two adds (sched_barrier): the in-order wave
+// issues it in the dependent add's latency.  scripts/consumer_microbench.hip V5: 167 cycles per 16 rows against 199
+// for the read-ahead loop this replaces (floor 16 x 8.6 = 138, profiles/r06_consumer_microbench_v5.txt).
+typedef float xc_f2 __attribute__((ext_vector_type(2)));
+struct XcRows { float4 a[4], b[4]; };
+struct XcProd { xc_f2 v[8]; };
+__device__ __forceinline__ void xc_read(XcRows& r, const float4* A, const float4* B, int g) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { r.a[q] = A[4 * g + q]; r.b[q] = B[4 * g + q]; }
+}
+__device__ __forceinline__ xc_f2 xc_mul(const XcRows& c, int i) {   // products 2i, 2i + 1 of the group
+    const float4 a = c.a[i >> 1], b = c.b[i >> 1];
+    return (i & 1) ? xc_f2{a.z, a.w} * xc_f2{b.z, b.w} : xc_f2{a.x, a.y} * xc_f2{b.x, b.y};
+}
+__device__ __forceinline__ void xc_add_mul(float& sum, const XcProd& p, XcProd& pn, const XcRows& c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        sum += p.v[i].x;
+        __builtin_amdgcn_sched_barrier(0);
+        pn.v[i] = xc_mul(c, i);
+        __builtin_amdgcn_sched_barrier(0);
+        sum += p.v[i].y;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double scale, float dl, float* dyn, float* s_tot) {
     float* s_f = dyn;                                      // [2][kXcFactors][kXcStride]
     int* s_cnt = reinterpret_cast<int*>(dyn + kXcCntOff);  // [4][kXcRegions]
@@ -787,25 +815,30 @@ __device__ void exact_sums_wg(const KParams& P, const float (&T)[12], double sca
             const float4* B = reinterpret_cast<const float4*>(base + fb * kXcStride);
             const int* cn = s_cnt + ((ch - 1) & 3) * kXcRegions;
             const int ng = (cn[0] + cn[1] + cn[2] + kXcPad - 1) / kXcPad;   // groups of 16 rows (uniform)
-            float4 a[4], b[4];
             if (ng > 0) {
+                // three stages: the products of group g (p), the rows of group g + 1 (c), the reads of group g + 2;
+                // the products of g + 1 are formed one v_pk_mul_f32 between every two adds of g, in the adds' latency
+                // (two steps per trip with the register sets swapped, so no stage is copied and no read is waited
+                // for before its use; reads stay within the staged groups)
+                XcRows c0, c1;
+                XcProd p0, p1;
+                xc_read(c0, A, B, 0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { a[q] = A[q]; b[q] = B[q]; }
-            }
-            for (int g = 0; g < ng; ++g) {
-                float4 an[4], bn[4];
-                const int gn = g + 1 < ng ? g + 1 : g;     // the next group's rows (the last group re-reads itself)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) { an[q] = A[4 * gn + q]; bn[q] = B[4 * gn + q]; }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    sum += a[q].x * b[q].x;
-                    sum += a[q].y * b[q].y;
-                    sum += a[q].z * b[q].z;
-                    sum += a[q].w * b[q].w;
+                for (int i = 0; i < 8; ++i) p0.v[i] = xc_mul(c0, i);
+                xc_read(c0, A, B, ng > 1 ? 1 : 0);
+                // (whole trips only: products a break would leave unused get sunk past the break by the compiler,
+                // out of the adds' latency; an odd last group is added after the loop)
+                int g = 0;
+                for (; g + 2 <= ng; g += 2) {
+                    xc_read(c1, A, B, g + 2 < ng ? g + 2 : ng - 1);
+                    xc_add_mul(sum, p0, p1, c0);               // group g's adds, group g + 1's products
+                    xc_read(c0, A, B, g + 3 < ng ? g + 3 : ng - 1);
+                    xc_add_mul(sum, p1, p0, c1);               // group g + 1's adds, group g + 2's products
                 }
+                if (g < ng) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { a[q] = an[q]; b[q] = bn[q]; }
+                    for (int i = 0; i < 8; ++i) { sum += p0.v[i].x; sum += p0.v[i].y; }
+                }
             }
         }
 #ifdef LO_PKO_STAMPS
@@ -868,6 +901,16 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
             P.st->dbg[8] = __builtin_amdgcn_s_memtime() - sv0;
             P.st->dbg[9] = __builtin_amdgcn_s_memrealtime() - sr0;
         }
+#ifndef LO_PKO_SUMS_COUNTERS
+        {                                    // every candidate's solve: the largest (dbg[16]), the sum and count
+            const float keep = pn[1] + delta[1];   // (dbg[17] / [18], cumulative) in shader cycles
+            asm volatile("" :: "v"(keep));
+            const unsigned long long cyc = __builtin_amdgcn_s_memtime() - sv0;
+            atomicMax(&P.st->dbg[16], cyc);
+            atomicAdd(&P.st->dbg[17], cyc);
+            atomicAdd(&P.st->dbg[18], 1ull);
+        }
+#endif
 #endif
 #pragma unroll
         for (int q = 0; q < 12; ++q) s_rec[q] = pn[q];

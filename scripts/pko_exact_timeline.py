@@ -34,8 +34,7 @@ def main():
             assert L.lo_debug_counters_ex(icp.ctx, d, 24) == 0
             t0 = d[21]
             if rep == 1 and t0:
-                rows.append(((d[22] - t0) / 100.0, (d[15] - t0) / 100.0, (d[23] - t0) / 100.0, d[7], d[8], d[9],
-                             (d[16] - t0) / 100.0, (d[17] - t0) / 100.0, (d[18] - t0) / 100.0))
+                rows.append(((d[22] - t0) / 100.0, (d[15] - t0) / 100.0, (d[23] - t0) / 100.0, d[7], d[8], d[9]))
     a = np.array(rows)
     print(f"exact PKO launch (last working launch of {len(a)} scans), us from the lead workgroup's start:")
     print(f"  lead fit + JS end     mean {a[:, 0].mean():.1f}  median {np.median(a[:, 0]):.1f}  max {a[:, 0].max():.1f}")
@@ -44,8 +43,7 @@ def main():
     print(f"  candidate 0 cycles    mean {a[:, 3].mean():.0f}")
     print(f"  candidate 0's solve   mean {a[:, 4].mean():.0f} cycles = {a[:, 5].mean() / 100.0:.1f} us "
           f"(shader clock {a[:, 4].sum() / a[:, 5].sum() / 10.0:.2f} GHz)")
-    print(f"  candidate 0: start {a[:, 6].mean():.1f}, sums end {a[:, 7].mean():.1f} us; latest candidate start "
-          f"{a[:, 8].mean():.1f} us (max {a[:, 8].max():.1f})")
+    print(f"  every candidate's solve: mean {d[17] / max(d[18], 1):.0f} cycles over {d[18]} solves, largest {d[16]} cycles")
     print(f"  launches bound by the candidates: {int((a[:, 2] > a[:, 0]).sum())} of {len(a)}")
     for r in rows:
         print("   " + " ".join(f"{v:8.1f}" for v in r[:3]))
