@@ -910,6 +910,18 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
             atomicAdd(&P.st->dbg[17], cyc);
             atomicAdd(&P.st->dbg[18], 1ull);
         }
+        {                                    // the same solve again, now with its code in the instruction cache: the
+            float tot2[kExactTerms], pn2[12], delta2[6];   // largest (dbg[19]) and the sum (dbg[20]) of its cycles
+#pragma unroll
+            for (int k = 0; k < kExactTerms; ++k) { tot2[k] = tot[k]; asm volatile("" : "+v"(tot2[k])); }
+            const unsigned long long s2 = __builtin_amdgcn_s_memtime();
+            const bool conv2 = exact_solve_step(tot2, T, P.tol_t, P.tol_r, pn2, delta2);
+            const float keep = pn2[1] + delta2[1] + (conv2 ? 1.0f : 0.0f);
+            asm volatile("" :: "v"(keep));
+            const unsigned long long cyc = __builtin_amdgcn_s_memtime() - s2;
+            atomicMax(&P.st->dbg[19], cyc);
+            atomicAdd(&P.st->dbg[20], cyc);
+        }
 #endif
 #endif
 #pragma unroll

@@ -44,6 +44,7 @@ def main():
     print(f"  candidate 0's solve   mean {a[:, 4].mean():.0f} cycles = {a[:, 5].mean() / 100.0:.1f} us "
           f"(shader clock {a[:, 4].sum() / a[:, 5].sum() / 10.0:.2f} GHz)")
     print(f"  every candidate's solve: mean {d[17] / max(d[18], 1):.0f} cycles over {d[18]} solves, largest {d[16]} cycles")
+    print(f"  the same solve again (code cached): mean {d[20] / max(d[18], 1):.0f} cycles, largest {d[19]} cycles")
     print(f"  launches bound by the candidates: {int((a[:, 2] > a[:, 0]).sum())} of {len(a)}")
     for r in rows:
         print("   " + " ".join(f"{v:8.1f}" for v in r[:3]))
