@@ -882,6 +882,10 @@ __device__ void acc_candidate_exact(const KParams& P, double scale, int c, float
     float T[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) T[k] = P.st->pose[k];
+#ifdef LO_XC_PRIO
+    // A/B build: the candidate's adder wave and its solving lane at the highest issue priority
+    if (tid < kWave) __builtin_amdgcn_s_setprio(3);
+#endif
     exact_sums_wg(P, T, scale, cand_delta(P, c), dyn, s_tot);
 #ifdef LO_PKO_STAMPS
     if (tid == 0) atomicMax(&P.st->dbg[15], __builtin_amdgcn_s_memrealtime());   // the last candidate's sums end
